@@ -1,0 +1,571 @@
+// dpg_api.hip -- the extern "C" boundary (include/dpg_slam_c.h, include/dpg_icp_cov.h).
+//
+// Entry points replace (reference file:line):
+//   icp_cov_calculate     -> calculate_ICP_COV            src/icp_cov/cov_func_point_to_point.h:24
+//   dpg_run_icp           -> DpgSLAM::runIcp               src/dpg_slam/dpg_slam.cc:362-446
+//   dpg_icp_batch_*       -> the runIcp calls of reoptimize / updatePoseGraphObsConstraints
+//                            (dpg_slam.cc:85,101,263,295), batched
+//   dpg_optimize_graph    -> DpgSLAM::optimizeGraph        src/dpg_slam/dpg_slam.cc:316-329
+//   dpg_gn_*              -> the same solve, split for the edge-sharded multi-GPU driver
+// Host memory in, host memory out; device work is asynchronous on the context stream except
+// where a host value must be returned.  No fallback: without a usable GPU dpg_ctx_create returns
+// NULL and every call that needs one fails with DPG_ERR_HIP.
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/dpg_icp_cov.h"
+#include "../../include/dpg_slam_c.h"
+#include "dpg_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess) return fail(DPG_ERR_HIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+double now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int reserve(size_t n) {
+        if (n <= cap) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) return -1;
+        cap = n;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct dpg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    hipEvent_t ev[6] = {};
+    // scan store (batch form)
+    DevBuf<float> full, ds;
+    std::vector<int64_t> full_off, ds_off;
+    int64_t n_nodes = 0;
+    int32_t ratio = 1;
+    // staged edge batch
+    std::vector<dpg_icp_edge> h_edges;
+    DevBuf<dpg_icp_edge> edges;
+    DevBuf<dpg_icp_result> res;
+    DevBuf<double> hess;
+    DevBuf<int32_t> trace;
+    int64_t n_edges = 0;
+    int32_t max_src = 0, max_tgt = 0;
+    int32_t trace_iters = 0;
+    dpg_icp_kparams kp{};
+    bool have_cov = false;
+    // single-call scratch (dpg_run_icp / icp_cov_calculate)
+    DevBuf<float> s_pts;
+    DevBuf<dpg_icp_edge> s_edge;
+    DevBuf<dpg_icp_result> s_res;
+    DevBuf<double> s_hess;
+    // pose graph
+    dpg_gn_dev gn{};
+    bool gn_ready = false;
+    dpg_gn_params gp{};
+    float asm_ms = 0.f, solve_ms = 0.f;
+};
+
+namespace {
+
+int set_kparams(dpg_icp_kparams* kp, const dpg_icp_params* p) {
+    if (!p) return fail(DPG_ERR_ARG, "params is NULL");
+    if (!(p->icp_max_correspondence_distance > 0.0)) return fail(DPG_ERR_ARG, "icp_max_correspondence_distance must be > 0");
+    memset(kp, 0, sizeof(*kp));
+    const double r = p->icp_max_correspondence_distance;
+    kp->r2 = r * r;
+    float f = (float)kp->r2;
+    if ((double)f > kp->r2) f = nextafterf(f, 0.0f);
+    kp->r2_f = f;
+    kp->h_min = (float)(r * 1.05);
+    kp->eps = p->icp_maximum_transformation_epsilon;
+    kp->rot_thr = 1.0 - p->icp_maximum_transformation_epsilon;
+    kp->mse_abs = p->mse_threshold_absolute;
+    kp->max_iter = p->icp_maximum_iterations;
+    kp->min_corr = p->min_number_correspondences;
+    kp->reciprocal = p->icp_use_reciprocal_correspondences ? 1 : 0;
+    kp->cells_max = 4096;
+    return DPG_OK;
+}
+
+int32_t round_up(int32_t v, int32_t m) { return (v + m - 1) / m * m; }
+
+int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const dpg_icp_edge* edges_dev,
+                 int64_t ne, dpg_icp_kparams kp, int32_t max_src, int32_t max_tgt, dpg_icp_result* res_dev,
+                 double* hess_dev, int32_t* trace_dev, bool timed) {
+    kp.lds_tgt = round_up(std::max<int32_t>(max_tgt, 1), 64);
+    const int32_t maxp = std::max(max_src, max_tgt);
+    if (maxp > 4096) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 4096", maxp);
+    if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    int rc = dpg_launch_icp(ds_dev, edges_dev, ne, &kp, maxp, res_dev, trace_dev, c->stream);
+    if (rc) return fail(rc, "ICP kernel launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
+    if (timed) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if (hess_dev) {
+        rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->stream);
+        if (rc) return fail(rc, "covariance kernel launch failed");
+    }
+    if (timed) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    return DPG_OK;
+}
+
+void const_cov(const dpg_icp_params* p, double cov[9]) {
+    memset(cov, 0, 9 * sizeof(double));
+    cov[0] = (double)p->laser_x_variance;
+    cov[4] = (double)p->laser_y_variance;
+    cov[8] = (double)p->laser_theta_variance;
+}
+
+dpg_ctx* g_default_ctx = nullptr;
+
+}  // namespace
+
+extern "C" {
+
+const char* dpg_last_error(void) { return g_err.c_str(); }
+const char* dpg_version(void) { return "dpg-mi355x 0.1 (gfx950)"; }
+
+dpg_ctx* dpg_ctx_create(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        fail(DPG_ERR_HIP, "no HIP device available");
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        fail(DPG_ERR_ARG, "device %d out of range (%d devices)", device, n);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        fail(DPG_ERR_HIP, "hipSetDevice(%d) failed", device);
+        return nullptr;
+    }
+    dpg_ctx* c = new dpg_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        fail(DPG_ERR_HIP, "hipStreamCreate failed");
+        return nullptr;
+    }
+    c->own_stream = true;
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    dpg_gn_params_default(&c->gp);
+    return c;
+}
+
+void dpg_ctx_destroy(dpg_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->full.release(); c->ds.release(); c->edges.release(); c->res.release(); c->hess.release();
+    c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
+    if (c->gn_ready) dpg_gn_dev_free(&c->gn);
+    for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    if (c == g_default_ctx) g_default_ctx = nullptr;
+    delete c;
+}
+
+int dpg_ctx_set_stream(dpg_ctx* c, void* s) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->own_stream) (void)hipStreamDestroy(c->stream);
+    c->stream = reinterpret_cast<hipStream_t>(s);
+    c->own_stream = false;
+    return DPG_OK;
+}
+
+int dpg_ctx_synchronize(dpg_ctx* c) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+// ------------------------------------------------------------------ ICP, batched
+int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V, int32_t ratio) {
+    if (!c || !pts || !off || V <= 0) return fail(DPG_ERR_ARG, "dpg_scans_upload: bad arguments");
+    if (ratio < 1) ratio = 1;
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t total = off[V];
+    if (total >= ((int64_t)1 << 31)) return fail(DPG_ERR_SIZE, "too many points (%lld)", (long long)total);
+    c->full_off.assign(off, off + V + 1);
+    c->ds_off.assign((size_t)V + 1, 0);
+    for (int64_t v = 0; v < V; ++v) {
+        const int64_t n = off[v + 1] - off[v];
+        if (n < 0) return fail(DPG_ERR_ARG, "node offsets must be non-decreasing");
+        c->ds_off[(size_t)v + 1] = c->ds_off[(size_t)v] + (n + ratio - 1) / ratio;
+    }
+    std::vector<float> ds((size_t)(2 * std::max<int64_t>(c->ds_off[(size_t)V], 1)));
+    for (int64_t v = 0; v < V; ++v)   // R2 downsamplePointCloud, per node
+        dpg_downsample_cloud(pts + 2 * off[v], off[v + 1] - off[v], ratio, ds.data() + 2 * c->ds_off[(size_t)v]);
+    if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(ds.size()))
+        return fail(DPG_ERR_HIP, "out of device memory for scans");
+    HIP_TRY(hipMemcpyAsync(c->full.p, pts, sizeof(float) * 2 * (size_t)total, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->ds.p, ds.data(), sizeof(float) * ds.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->n_nodes = V;
+    c->ratio = ratio;
+    return DPG_OK;
+}
+
+int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
+    if (!c || (!edges && ne > 0) || !poses) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
+    if (c->n_nodes <= 0) return fail(DPG_ERR_STATE, "no scans uploaded");
+    if (p->downsample_icp_points_ratio != c->ratio && !(p->downsample_icp_points_ratio < 1 && c->ratio == 1))
+        return fail(DPG_ERR_STATE, "scans were uploaded with downsample ratio %d", c->ratio);
+    int rc = set_kparams(&c->kp, p);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    c->h_edges.resize((size_t)std::max<int64_t>(ne, 1));
+    int32_t ms = 0, mt = 0;
+    for (int64_t e = 0; e < ne; ++e) {
+        const int32_t t = edges[2 * e], s = edges[2 * e + 1];  // node_1 = target, node_2 = source
+        if (t < 0 || s < 0 || t >= c->n_nodes || s >= c->n_nodes)
+            return fail(DPG_ERR_ARG, "edge %lld references a missing node", (long long)e);
+        dpg_icp_edge& E = c->h_edges[(size_t)e];
+        E.src_ds_off = (int32_t)c->ds_off[(size_t)s];
+        E.n_src_ds = (int32_t)(c->ds_off[(size_t)s + 1] - c->ds_off[(size_t)s]);
+        E.tgt_ds_off = (int32_t)c->ds_off[(size_t)t];
+        E.n_tgt_ds = (int32_t)(c->ds_off[(size_t)t + 1] - c->ds_off[(size_t)t]);
+        E.src_full_off = (int32_t)c->full_off[(size_t)s];
+        E.n_src_full = (int32_t)(c->full_off[(size_t)s + 1] - c->full_off[(size_t)s]);
+        E.tgt_full_off = (int32_t)c->full_off[(size_t)t];
+        E.n_tgt_full = (int32_t)(c->full_off[(size_t)t + 1] - c->full_off[(size_t)t]);
+        dpg_icp_guess(poses + 3 * s, poses + 3 * t, E.guess);  // R3 (dpg_slam.cc:364-378)
+        ms = std::max(ms, E.n_src_ds);
+        mt = std::max(mt, E.n_tgt_ds);
+    }
+    if (c->edges.reserve((size_t)std::max<int64_t>(ne, 1)) || c->res.reserve((size_t)std::max<int64_t>(ne, 1)) ||
+        c->hess.reserve((size_t)(9 * std::max<int64_t>(ne, 1))))
+        return fail(DPG_ERR_HIP, "out of device memory for %lld edges", (long long)ne);
+    if (ne > 0)
+        HIP_TRY(hipMemcpyAsync(c->edges.p, c->h_edges.data(), sizeof(dpg_icp_edge) * (size_t)ne,
+                               hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->n_edges = ne;
+    c->max_src = ms;
+    c->max_tgt = mt;
+    return DPG_OK;
+}
+
+int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    dpg_icp_kparams kp = c->kp;
+    int32_t* tr = nullptr;
+    if (trace_iters > 0) {
+        const size_t n = (size_t)c->n_edges * (size_t)trace_iters * (size_t)std::max(c->max_src, 1);
+        if (c->trace.reserve(n)) return fail(DPG_ERR_HIP, "out of device memory for the trace");
+        HIP_TRY(hipMemsetAsync(c->trace.p, 0xff, n * sizeof(int32_t), c->stream));
+        kp.trace_iters = trace_iters;
+        kp.trace_stride = std::max(c->max_src, 1);
+        tr = c->trace.p;
+    }
+    c->trace_iters = trace_iters > 0 ? trace_iters : 0;
+    c->have_cov = compute_cov != 0;
+    return launch_batch(c, c->ds.p, c->full.p, c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
+                        compute_cov ? c->hess.p : nullptr, tr, true);
+}
+
+int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    HIP_TRY(hipSetDevice(c->device));
+    if (results && c->n_edges > 0)
+        HIP_TRY(hipMemcpyAsync(results, c->res.p, sizeof(dpg_icp_result) * (size_t)c->n_edges, hipMemcpyDeviceToHost,
+                               c->stream));
+    if (hess && c->n_edges > 0) {
+        if (!c->have_cov) return fail(DPG_ERR_STATE, "last batch ran without compute_cov");
+        HIP_TRY(hipMemcpyAsync(hess, c->hess.p, sizeof(double) * 9 * (size_t)c->n_edges, hipMemcpyDeviceToHost,
+                               c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t* max_src_out) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    if (max_src_out) *max_src_out = std::max(c->max_src, 1);
+    if (!trace) return DPG_OK;
+    if (c->trace_iters <= 0) return fail(DPG_ERR_STATE, "last batch ran without a trace");
+    const size_t n = (size_t)c->n_edges * (size_t)c->trace_iters * (size_t)std::max(c->max_src, 1);
+    HIP_TRY(hipMemcpyAsync(trace, c->trace.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+float dpg_icp_batch_kernel_ms(dpg_ctx* c) {
+    float ms = -1.f;
+    if (!c || hipEventSynchronize(c->ev[1]) != hipSuccess) return -1.f;
+    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) != hipSuccess) return -1.f;
+    return ms;
+}
+
+float dpg_cov_batch_kernel_ms(dpg_ctx* c) {
+    float ms = -1.f;
+    if (!c || hipEventSynchronize(c->ev[2]) != hipSuccess) return -1.f;
+    if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) != hipSuccess) return -1.f;
+    return ms;
+}
+
+double dpg_icp_batch_algorithmic_bytes(dpg_ctx* c) {
+    if (!c || c->n_edges <= 0) return 0.0;
+    std::vector<dpg_icp_result> r((size_t)c->n_edges);
+    if (hipMemcpy(r.data(), c->res.p, sizeof(dpg_icp_result) * r.size(), hipMemcpyDeviceToHost) != hipSuccess) return -1.0;
+    double bytes = 0.0;
+    for (int64_t e = 0; e < c->n_edges; ++e) {
+        const dpg_icp_edge& E = c->h_edges[(size_t)e];
+        // correspondence kernel per edge-iteration: 8N (source xy) + 8M (target xy) + 8N (idx + d^2)
+        bytes += (double)r[(size_t)e].iterations * (16.0 * E.n_src_ds + 8.0 * E.n_tgt_ds);
+    }
+    return bytes;
+}
+
+// ------------------------------------------------------------------ single alignment / covariance
+int dpg_run_icp(dpg_ctx* c, const float* src, int64_t ns, const float* tgt, int64_t nt, const float pose_src[3],
+                const float pose_tgt[3], const dpg_icp_params* p, dpg_icp_result* result, double cov_out[9],
+                double hess_out[9]) {
+    if (!c || !src || !tgt || ns < 0 || nt < 0 || !pose_src || !pose_tgt || !p || !result)
+        return fail(DPG_ERR_ARG, "dpg_run_icp: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    dpg_icp_kparams kp;
+    int rc = set_kparams(&kp, p);
+    if (rc) return rc;
+    const int32_t ratio = p->downsample_icp_points_ratio > 0 ? p->downsample_icp_points_ratio : 1;
+    const int64_t nsd = (ns + ratio - 1) / ratio, ntd = (nt + ratio - 1) / ratio;
+    // layout: [src full | tgt full | src ds | tgt ds]
+    std::vector<float> buf((size_t)(2 * (ns + nt + nsd + ntd) + 2));
+    memcpy(buf.data(), src, sizeof(float) * 2 * (size_t)ns);
+    memcpy(buf.data() + 2 * ns, tgt, sizeof(float) * 2 * (size_t)nt);
+    dpg_downsample_cloud(src, ns, ratio, buf.data() + 2 * (ns + nt));
+    dpg_downsample_cloud(tgt, nt, ratio, buf.data() + 2 * (ns + nt + nsd));
+    dpg_icp_edge E;
+    E.src_full_off = 0; E.n_src_full = (int32_t)ns;
+    E.tgt_full_off = (int32_t)ns; E.n_tgt_full = (int32_t)nt;
+    E.src_ds_off = (int32_t)(ns + nt); E.n_src_ds = (int32_t)nsd;
+    E.tgt_ds_off = (int32_t)(ns + nt + nsd); E.n_tgt_ds = (int32_t)ntd;
+    dpg_icp_guess(pose_src, pose_tgt, E.guess);
+    if (c->s_pts.reserve(buf.size()) || c->s_edge.reserve(1) || c->s_res.reserve(1) || c->s_hess.reserve(9))
+        return fail(DPG_ERR_HIP, "out of device memory");
+    HIP_TRY(hipMemcpyAsync(c->s_pts.p, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->s_edge.p, &E, sizeof(E), hipMemcpyHostToDevice, c->stream));
+    rc = launch_batch(c, c->s_pts.p, c->s_pts.p, c->s_edge.p, 1, kp, (int32_t)nsd, (int32_t)ntd, c->s_res.p,
+                      hess_out ? c->s_hess.p : nullptr, nullptr, false);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(result, c->s_res.p, sizeof(dpg_icp_result), hipMemcpyDeviceToHost, c->stream));
+    if (hess_out) HIP_TRY(hipMemcpyAsync(hess_out, c->s_hess.p, 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (cov_out) const_cov(p, cov_out);
+    return DPG_OK;
+}
+
+int icp_cov_calculate(dpg_ctx* c, const float* data, int64_t nd, const float* model, int64_t nm, const float T[16],
+                      float vx, float vy, float vth, double cov_out[9], double hess_out[9]) {
+    if (!cov_out || !T) return fail(DPG_ERR_ARG, "icp_cov_calculate: bad arguments");
+    // :572-575 -- ICP_COV.resize(3,3) << laser_x_variance, 0, 0, 0, laser_y_variance, ...
+    memset(cov_out, 0, 9 * sizeof(double));
+    cov_out[0] = (double)vx;
+    cov_out[4] = (double)vy;
+    cov_out[8] = (double)vth;
+    if (!hess_out) return DPG_OK;
+    if (!data || !model || nd < 0 || nm < 0) return fail(DPG_ERR_ARG, "icp_cov_calculate: bad clouds");
+    if (!c) {
+        if (!g_default_ctx) g_default_ctx = dpg_ctx_create(0);
+        c = g_default_ctx;
+        if (!c) return DPG_ERR_HIP;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<float> buf((size_t)(2 * (nd + nm) + 2));
+    memcpy(buf.data(), data, sizeof(float) * 2 * (size_t)nd);
+    memcpy(buf.data() + 2 * nd, model, sizeof(float) * 2 * (size_t)nm);
+    dpg_icp_edge E;
+    memset(&E, 0, sizeof(E));
+    E.src_full_off = 0; E.n_src_full = (int32_t)nd;
+    E.tgt_full_off = (int32_t)nd; E.n_tgt_full = (int32_t)nm;
+    dpg_icp_result R;
+    memset(&R, 0, sizeof(R));
+    R.T[0] = T[0]; R.T[1] = T[1]; R.T[2] = T[3];    // row-major 4x4 -> rows (T00 T01 T03 / T10 T11 T13)
+    R.T[3] = T[4]; R.T[4] = T[5]; R.T[5] = T[7];
+    if (c->s_pts.reserve(buf.size()) || c->s_edge.reserve(1) || c->s_res.reserve(1) || c->s_hess.reserve(9))
+        return fail(DPG_ERR_HIP, "out of device memory");
+    HIP_TRY(hipMemcpyAsync(c->s_pts.p, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->s_edge.p, &E, sizeof(E), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->s_res.p, &R, sizeof(R), hipMemcpyHostToDevice, c->stream));
+    int rc = dpg_launch_cov(c->s_pts.p, c->s_edge.p, 1, c->s_res.p, c->s_hess.p, c->stream);
+    if (rc) return fail(rc, "covariance kernel launch failed");
+    HIP_TRY(hipMemcpyAsync(hess_out, c->s_hess.p, 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+// ------------------------------------------------------------------ pose graph
+int dpg_gn_setup(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t b, int64_t e,
+                 const dpg_gn_params* gp) {
+    if (!c || !F || V <= 0 || nf < 0) return fail(DPG_ERR_ARG, "dpg_gn_setup: bad arguments");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->gn_ready) dpg_gn_dev_free(&c->gn);
+    c->gn_ready = false;
+    int rc = dpg_gn_dev_alloc(&c->gn, V, F, nf, b, e);
+    if (rc) return fail(rc, "pose-graph setup failed (invalid factor or out of memory)");
+    c->gn_ready = true;
+    if (gp) c->gp = *gp;
+    else dpg_gn_params_default(&c->gp);
+    return DPG_OK;
+}
+
+int dpg_gn_take_icp_measurements(dpg_ctx* c, int64_t first, int64_t count, int64_t n_always,
+                                 const dpg_icp_params* p) {
+    if (!c || !c->gn_ready || !p) return fail(DPG_ERR_STATE, "graph not set up");
+    if (count > c->n_edges) return fail(DPG_ERR_ARG, "only %lld ICP results available", (long long)c->n_edges);
+    int rc = dpg_gn_dev_icp_to_factors(&c->gn, c->res.p, first, count, n_always, 1.0 / (double)p->laser_x_variance,
+                                       1.0 / (double)p->laser_y_variance, 1.0 / (double)p->laser_theta_variance,
+                                       c->stream);
+    return rc ? fail(rc, "dpg_gn_take_icp_measurements failed") : DPG_OK;
+}
+
+int64_t dpg_gn_hb_size(dpg_ctx* c) { return (c && c->gn_ready) ? dpg_gn_dev_hb_size(&c->gn) : -1; }
+
+int dpg_gn_set_poses(dpg_ctx* c, const double* poses) {
+    if (!c || !c->gn_ready || !poses) return fail(DPG_ERR_STATE, "graph not set up");
+    HIP_TRY(hipMemcpyAsync(c->gn.poses, poses, sizeof(double) * 3 * (size_t)c->gn.n_nodes, hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+int dpg_gn_get_poses(dpg_ctx* c, double* poses) {
+    if (!c || !c->gn_ready || !poses) return fail(DPG_ERR_STATE, "graph not set up");
+    HIP_TRY(hipMemcpyAsync(poses, c->gn.poses, sizeof(double) * 3 * (size_t)c->gn.n_nodes, hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+int dpg_gn_assemble(dpg_ctx* c, double* hb_dev) {
+    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+    if (!hb_dev) hb_dev = c->gn.hb_own;
+    HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+    int rc = dpg_gn_dev_assemble(&c->gn, hb_dev, c->stream);
+    if (rc) return fail(rc, "assembly launch failed");
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    return DPG_OK;
+}
+
+int dpg_gn_solve_retract(dpg_ctx* c, const double* hb_dev, double* delta_inf, double* error, int32_t* pcg_iters) {
+    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+    if (!hb_dev) hb_dev = c->gn.hb_own;
+    int rc = dpg_gn_dev_solve(&c->gn, hb_dev, &c->gp, c->stream, delta_inf, error, pcg_iters);
+    if (rc) return fail(rc, "PCG solve failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+    float a = 0.f, s = 0.f;
+    if (hipEventSynchronize(c->ev[5]) == hipSuccess) {
+        (void)hipEventElapsedTime(&a, c->ev[3], c->ev[4]);
+        (void)hipEventElapsedTime(&s, c->ev[4], c->ev[5]);
+    }
+    c->asm_ms = a;
+    c->solve_ms = s;
+    return DPG_OK;
+}
+
+float dpg_gn_last_assemble_ms(dpg_ctx* c) { return c ? c->asm_ms : -1.f; }
+float dpg_gn_last_solve_ms(dpg_ctx* c) { return c ? c->solve_ms : -1.f; }
+
+static int read_error(dpg_ctx* c, double* err) {
+    HIP_TRY(hipMemcpyAsync(err, c->gn.hb_own + 9 * c->gn.nnzb_upper + 3 * c->gn.n_nodes, sizeof(double),
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+static int check_conv(const dpg_gn_params* gp, double cur, double nw) {
+    if (nw <= 0.0) return 1;
+    const double abs_dec = cur - nw;
+    const double rel_dec = abs_dec / cur;
+    return (gp->relative_error_tol != 0.0 && rel_dec <= gp->relative_error_tol) || (abs_dec <= gp->absolute_error_tol);
+}
+
+int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params* gp,
+                       dpg_gn_stats* st) {
+    const double t0 = now_ms();
+    dpg_gn_params P;
+    if (gp) P = *gp;
+    else dpg_gn_params_default(&P);
+    int rc = dpg_gn_setup(c, V, F, nf, 0, nf, &P);
+    if (rc) return rc;
+    if ((rc = dpg_gn_set_poses(c, poses))) return rc;
+    const double t1 = now_ms();
+    dpg_gn_stats S;
+    memset(&S, 0, sizeof(S));
+    if ((rc = dpg_gn_assemble(c, nullptr)) || (rc = read_error(c, &S.initial_error))) return rc;
+    double cur = S.initial_error, nw = cur, dinf = 0.0;
+    int it = 0;
+    if (!(cur <= 0.0) && P.max_iterations > 0) {
+        for (;;) {
+            double e_lin = 0.0;
+            int32_t pit = 0;
+            if ((rc = dpg_gn_solve_retract(c, nullptr, &dinf, &e_lin, &pit))) return rc;
+            S.pcg_iterations += pit;
+            ++it;
+            if ((rc = dpg_gn_assemble(c, nullptr)) || (rc = read_error(c, &nw))) return rc;
+            if (it >= P.max_iterations) break;
+            if (P.use_error_criteria) {
+                if (check_conv(&P, cur, nw) || !std::isfinite(cur)) break;
+            } else if (dinf < P.delta_tol) {
+                break;
+            }
+            cur = nw;
+        }
+    }
+    if ((rc = dpg_gn_get_poses(c, poses))) return rc;
+    const double t2 = now_ms();
+    S.iterations = it;
+    S.final_error = nw;
+    S.last_delta_inf = dinf;
+    S.ms_total = t2 - t0;
+    S.ms_per_iteration = it ? (t2 - t1) / it : 0.0;
+    if (st) *st = S;
+    return DPG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,542 @@
+// dpg_gn.hip -- pose-graph Gauss-Newton on gfx950: per-factor linearization + block-sparse
+// (H, b) assembly, block-Jacobi PCG in fp64, Pose2 retraction.
+//
+// Replaces DpgSLAM::optimizeGraph (src/dpg_slam/dpg_slam.cc:316-329) -> GTSAM
+// ISAM2/GaussNewtonOptimizer over PriorFactor<Pose2> / BetweenFactor<Pose2> (dpg_slam.cc:44-75,
+// 178-183,227-238,331-338), restated with GTSAM 4.x default semantics:
+//   Between: h = Xi^-1 Xj, e = Local(z, h) = z^-1 h as (x, y, theta); Jacobians of
+//            Pose2::between (H1 = -AdjointMap(h^-1) inlined, H2 = I) -- BetweenFactor without
+//            SLOW_BUT_CORRECT_BETWEENFACTOR applies no Local() Jacobian;
+//   Prior:   e = -Local(x, prior), H = I;
+//   whitened normal equations  H = sum A^T W A,  g = sum A^T W e,  solve H d = -g,
+//   retract X <- X * Pose2(d) (ChartAtOrigin, no Expmap).
+//
+// Assembly is a deterministic GATHER (no float atomics): one lane per upper 3x3 block walks the
+// factors that touch it in factor order.  The packed buffer [H upper | g | chi2] is exactly what
+// the multi-GPU path all-reduces (one RCCL call per GN iteration).
+// The solve: block-Jacobi preconditioned CG over the full BSR (two kernels per CG iteration,
+// deterministic fixed-order partial sums), then one retraction kernel.
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dpg_internal.h"
+
+namespace {
+
+constexpr int kRowThreads = 256;
+
+__device__ __forceinline__ void between_lin(const double* a, const double* b, double h[4], double H1[9]) {
+    const double c1 = cos(a[2]), s1 = sin(a[2]), c2 = cos(b[2]), s2 = sin(b[2]);
+    const double c = c1 * c2 + s1 * s2, s = -s1 * c2 + c1 * s2;
+    const double dx = b[0] - a[0], dy = b[1] - a[1];
+    h[0] = c1 * dx + s1 * dy;
+    h[1] = -s1 * dx + c1 * dy;
+    h[2] = c;
+    h[3] = s;
+    if (H1) {
+        const double dt1 = -s2 * dx + c2 * dy, dt2 = -c2 * dx - s2 * dy;
+        H1[0] = -c; H1[1] = -s; H1[2] = dt1;
+        H1[3] = s;  H1[4] = -c; H1[5] = dt2;
+        H1[6] = 0;  H1[7] = 0;  H1[8] = -1;
+    }
+}
+
+// error e and Jacobian A_i (A_j = I for Between, prior has only A_i = I)
+__device__ void linearize(const dpg_factor& f, const double* X, double e[3], double Ai[9]) {
+    double h[4];
+    if (f.kind == DPG_FACTOR_PRIOR) {
+        between_lin(X + 3 * f.i, f.z, h, nullptr);
+        e[0] = -h[0];
+        e[1] = -h[1];
+        e[2] = -atan2(h[3], h[2]);
+#pragma unroll
+        for (int q = 0; q < 9; ++q) Ai[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    between_lin(X + 3 * f.i, X + 3 * f.j, h, Ai);
+    const double cz = cos(f.z[2]), sz = sin(f.z[2]);
+    double ch = h[2], sh = h[3];
+    const double n = ch * ch + sh * sh;
+    if (fabs(n - 1.0) > 1e-10) { const double sc = 1.0 / sqrt(n); ch *= sc; sh *= sc; }
+    const double c = cz * ch + sz * sh, s = -sz * ch + cz * sh;
+    const double dx = h[0] - f.z[0], dy = h[1] - f.z[1];
+    e[0] = cz * dx + sz * dy;
+    e[1] = -sz * dx + cz * dy;
+    e[2] = atan2(s, c);
+}
+
+// C += A^T diag(w) B
+__device__ __forceinline__ void atwb_acc(const double* A, const double* w, const double* B, double* C) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc += A[3 * k + r] * w[k] * B[3 * k + c];
+            C[3 * r + c] += acc;
+        }
+}
+
+__global__ void assemble_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X,
+                                const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
+                                int64_t n_nodes, int64_t nnzb_upper, int64_t shard_begin, int64_t shard_end,
+                                double* __restrict__ hb, double* __restrict__ chi2_node) {
+    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nnzb_upper) return;
+    const bool is_diag = u < n_nodes;
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    double g[3] = {0, 0, 0};
+    double chi2 = 0.0;
+    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int32_t q = cptr[u]; q < cptr[u + 1]; ++q) {
+        const int32_t code = clist[q];
+        const int32_t fi = code >> 2, role = code & 3;
+        if (fi < shard_begin || fi >= shard_end) continue;
+        const dpg_factor f = F[fi];
+        double e[3], Ai[9];
+        linearize(f, X, e, Ai);
+        const double* w = f.info;
+        if (role == 0) {          // diag i
+            atwb_acc(Ai, w, Ai, H);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) g[r] += Ai[r] * w[0] * e[0] + Ai[3 + r] * w[1] * e[1] + Ai[6 + r] * w[2] * e[2];
+            chi2 += 0.5 * (w[0] * e[0] * e[0] + w[1] * e[1] * e[1] + w[2] * e[2] * e[2]);
+        } else if (role == 1) {   // diag j (A_j = I)
+            atwb_acc(I3, w, I3, H);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) g[r] += w[r] * e[r];
+        } else if (role == 2) {   // H(i, j) = A_i^T W A_j, i < j
+            atwb_acc(Ai, w, I3, H);
+        } else {                  // H(j, i) = A_j^T W A_i, j < i
+            atwb_acc(I3, w, Ai, H);
+        }
+    }
+    double* o = hb + 9 * u;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) o[q] = H[q];
+    if (is_diag) {
+        double* gb = hb + 9 * nnzb_upper + 3 * u;
+        gb[0] = g[0]; gb[1] = g[1]; gb[2] = g[2];
+        chi2_node[u] = chi2;
+    }
+}
+
+__device__ double block_sum(double v, double* red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_down(v, off, 64);
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0)
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w];
+    __syncthreads();
+    return s;
+}
+
+__global__ void chi2_kernel(const double* __restrict__ chi2_node, int64_t n, double* __restrict__ out) {
+    __shared__ double red[16];
+    double s = 0.0;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) s += chi2_node[k];
+    s = block_sum(s, red);
+    if (threadIdx.x == 0) *out = s;
+}
+
+// inverse of an SPD 3x3 block (adjugate / determinant)
+__device__ void inv3(const double* A, double* B) {
+    const double a = A[0], b = A[1], c = A[2], d = A[3], e = A[4], f = A[5], g = A[6], h = A[7], i = A[8];
+    const double C00 = e * i - f * h, C01 = -(d * i - f * g), C02 = d * h - e * g;
+    const double det = a * C00 + b * C01 + c * C02;
+    if (!(fabs(det) > 0.0)) {
+        for (int q = 0; q < 9; ++q) B[q] = (q % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    const double id = 1.0 / det;
+    B[0] = C00 * id; B[1] = -(b * i - c * h) * id; B[2] = (b * f - c * e) * id;
+    B[3] = C01 * id; B[4] = (a * i - c * g) * id;  B[5] = -(a * f - c * d) * id;
+    B[6] = C02 * id; B[7] = -(a * h - b * g) * id; B[8] = (a * e - b * d) * id;
+}
+
+__device__ __forceinline__ void mv3(const double* M, const double* x, double* y) {
+    y[0] = M[0] * x[0] + M[1] * x[1] + M[2] * x[2];
+    y[1] = M[3] * x[0] + M[4] * x[1] + M[5] * x[2];
+    y[2] = M[6] * x[0] + M[7] * x[1] + M[8] * x[2];
+}
+
+// expand the upper blocks into the full BSR, invert the diagonal, start PCG from x = 0
+__global__ void pcg_init_kernel(const double* __restrict__ hb, const int32_t* __restrict__ rowptr,
+                                const int32_t* __restrict__ src_up, int64_t n, int64_t nnzb_upper,
+                                double* __restrict__ bsr, double* __restrict__ minv, double* __restrict__ x,
+                                double* __restrict__ r, double* __restrict__ z, double* __restrict__ p0,
+                                double* __restrict__ part_rz, double* __restrict__ part_rr) {
+    __shared__ double red[16];
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double rz = 0.0, rr = 0.0;
+    if (v < n) {
+        for (int32_t s = rowptr[v]; s < rowptr[v + 1]; ++s) {
+            const int32_t su = src_up[s];
+            const double* U = hb + 9 * (int64_t)(su >= 0 ? su : -1 - su);
+            double* D = bsr + 9 * (int64_t)s;
+            if (su >= 0) {
+#pragma unroll
+                for (int q = 0; q < 9; ++q) D[q] = U[q];
+            } else {
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) D[3 * a + b] = U[3 * b + a];
+            }
+        }
+        double Mi[9];
+        inv3(hb + 9 * v, Mi);
+#pragma unroll
+        for (int q = 0; q < 9; ++q) minv[9 * v + q] = Mi[q];
+        const double* g = hb + 9 * nnzb_upper + 3 * v;
+        double rv[3] = {-g[0], -g[1], -g[2]}, zv[3];
+        mv3(Mi, rv, zv);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            x[3 * v + c] = 0.0;
+            r[3 * v + c] = rv[c];
+            z[3 * v + c] = zv[c];
+            p0[3 * v + c] = zv[c];
+            rz += rv[c] * zv[c];
+            rr += rv[c] * rv[c];
+        }
+    }
+    rz = block_sum(rz, red);
+    rr = block_sum(rr, red);
+    if (threadIdx.x == 0) { part_rz[blockIdx.x] = rz; part_rr[blockIdx.x] = rr; }
+}
+
+__device__ __forceinline__ double sum_partials(const double* __restrict__ p, int nb) {
+    double s = 0.0;
+    for (int k = 0; k < nb; ++k) s += p[k];
+    return s;
+}
+
+// K_A(it): rz_it = sum(part_rz); beta = rz_it / rz_{it-1} (it > 0); p_new = z + beta p_old
+// (redundantly for neighbour rows); q = H p_new; partial p_new . q
+__global__ void pcg_spmv_kernel(int it, const double* __restrict__ bsr, const int32_t* __restrict__ rowptr,
+                                const int32_t* __restrict__ colidx, int64_t n, const double* __restrict__ z,
+                                const double* __restrict__ p_old, double* __restrict__ p_new,
+                                double* __restrict__ q, const double* __restrict__ part_rz,
+                                const double* __restrict__ part_rr, double* __restrict__ part_pq,
+                                double* __restrict__ scal, int nb) {
+    __shared__ double red[16];
+    const double rz = sum_partials(part_rz, nb);
+    const double beta = it > 0 ? (scal[2 * (it - 1)] != 0.0 ? rz / scal[2 * (it - 1)] : 0.0) : 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        scal[2 * it] = rz;
+        scal[2 * it + 1] = sum_partials(part_rr, nb);
+    }
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double pq = 0.0;
+    if (v < n) {
+        double acc[3] = {0, 0, 0};
+        for (int32_t s = rowptr[v]; s < rowptr[v + 1]; ++s) {
+            const int64_t c = colidx[s];
+            double pc[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) pc[k] = it > 0 ? z[3 * c + k] + beta * p_old[3 * c + k] : p_old[3 * c + k];
+            const double* B = bsr + 9 * (int64_t)s;
+            acc[0] += B[0] * pc[0] + B[1] * pc[1] + B[2] * pc[2];
+            acc[1] += B[3] * pc[0] + B[4] * pc[1] + B[5] * pc[2];
+            acc[2] += B[6] * pc[0] + B[7] * pc[1] + B[8] * pc[2];
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double pv = it > 0 ? z[3 * v + k] + beta * p_old[3 * v + k] : p_old[3 * v + k];
+            p_new[3 * v + k] = pv;
+            q[3 * v + k] = acc[k];
+            pq += pv * acc[k];
+        }
+    }
+    pq = block_sum(pq, red);
+    if (threadIdx.x == 0) part_pq[blockIdx.x] = pq;
+}
+
+// K_B(it): alpha = rz_it / (p.q); x += alpha p; r -= alpha q; z = M^-1 r; partial rz, rr
+__global__ void pcg_update_kernel(int it, int64_t n, const double* __restrict__ minv,
+                                  const double* __restrict__ p, const double* __restrict__ q,
+                                  double* __restrict__ x, double* __restrict__ r, double* __restrict__ z,
+                                  const double* __restrict__ part_rz_in, const double* __restrict__ part_pq,
+                                  double* __restrict__ part_rz_out, double* __restrict__ part_rr, int nb) {
+    __shared__ double red[16];
+    const double rz = sum_partials(part_rz_in, nb);
+    const double pq = sum_partials(part_pq, nb);
+    const double alpha = pq != 0.0 ? rz / pq : 0.0;
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double rz_n = 0.0, rr = 0.0;
+    if (v < n) {
+        double rv[3], zv[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            x[3 * v + k] += alpha * p[3 * v + k];
+            rv[k] = r[3 * v + k] - alpha * q[3 * v + k];
+            r[3 * v + k] = rv[k];
+        }
+        mv3(minv + 9 * v, rv, zv);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            z[3 * v + k] = zv[k];
+            rz_n += rv[k] * zv[k];
+            rr += rv[k] * rv[k];
+        }
+    }
+    rz_n = block_sum(rz_n, red);
+    rr = block_sum(rr, red);
+    if (threadIdx.x == 0) { part_rz_out[blockIdx.x] = rz_n; part_rr[blockIdx.x] = rr; }
+}
+
+// X <- X * Pose2(d); partial max |d|
+__global__ void retract_kernel(double* __restrict__ X, const double* __restrict__ d, int64_t n,
+                               double* __restrict__ part_max) {
+    __shared__ double red[16];
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double m = 0.0;
+    if (v < n) {
+        const double c = cos(X[3 * v + 2]), s = sin(X[3 * v + 2]);
+        const double d0 = d[3 * v], d1 = d[3 * v + 1], d2 = d[3 * v + 2];
+        const double cd = cos(d2), sd = sin(d2);
+        const double nx = X[3 * v] + (c * d0 - s * d1);
+        const double ny = X[3 * v + 1] + (s * d0 + c * d1);
+        const double nc = c * cd - s * sd, ns = s * cd + c * sd;
+        X[3 * v] = nx;
+        X[3 * v + 1] = ny;
+        X[3 * v + 2] = atan2(ns, nc);
+        m = fmax(fabs(d0), fmax(fabs(d1), fabs(d2)));
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+    if (lane == 0) red[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double mm = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mm = fmax(mm, red[w]);
+        part_max[blockIdx.x] = mm;
+    }
+}
+
+// ICP results -> BetweenFactor measurement + diagonal information (dpg_slam.cc:331-338)
+__global__ void icp_to_factor_kernel(const dpg_icp_result* __restrict__ res, dpg_factor* __restrict__ F,
+                                     int64_t first, int64_t count, int64_t n_always, double ix, double iy,
+                                     double ith) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= count) return;
+    dpg_factor& f = F[first + e];
+    const dpg_icp_result r = res[e];
+    const bool keep = e < n_always || (r.converged && r.status == DPG_ICP_OK);
+    f.z[0] = r.z[0];
+    f.z[1] = r.z[1];
+    f.z[2] = r.z[2];
+    f.info[0] = keep ? ix : 0.0;
+    f.info[1] = keep ? iy : 0.0;
+    f.info[2] = keep ? ith : 0.0;
+}
+
+template <typename T>
+int dev_alloc(T** p, size_t n) {
+    if (n == 0) n = 1;
+    return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T)) == hipSuccess ? 0 : DPG_ERR_HIP;
+}
+
+template <typename T>
+int up(T* dst, const std::vector<T>& src) {
+    if (src.empty()) return 0;
+    return hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess ? 0 : DPG_ERR_HIP;
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + kRowThreads - 1) / kRowThreads); }
+
+}  // namespace
+
+extern "C" int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g) { return 9 * g->nnzb_upper + 3 * g->n_nodes + 2; }
+
+extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
+    void* ptrs[] = {g->factors, g->up_row, g->up_col, g->up_cptr, g->up_clist, g->node_fptr, g->node_flist,
+                    g->rowptr, g->colidx, g->src_up, g->bsr, g->minv, g->poses, g->x, g->r, g->z,
+                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    memset(g, 0, sizeof(*g));
+}
+
+extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, int64_t nf,
+                                int64_t shard_begin, int64_t shard_end) {
+    memset(g, 0, sizeof(*g));
+    if (n <= 0 || nf < 0 || n > (int64_t)1 << 28) return DPG_ERR_ARG;
+    // unique pairs (lo, hi) of Between factors
+    std::vector<std::pair<int64_t, int64_t>> pairs;
+    pairs.reserve((size_t)nf);
+    for (int64_t k = 0; k < nf; ++k) {
+        const dpg_factor& f = F[k];
+        if (f.kind == DPG_FACTOR_PRIOR) {
+            if (f.i < 0 || f.i >= n) return DPG_ERR_ARG;
+            continue;
+        }
+        if (f.kind != DPG_FACTOR_BETWEEN || f.i < 0 || f.j < 0 || f.i >= n || f.j >= n || f.i == f.j)
+            return DPG_ERR_ARG;
+        pairs.emplace_back(std::min<int64_t>(f.i, f.j), std::max<int64_t>(f.i, f.j));
+    }
+    std::sort(pairs.begin(), pairs.end());
+    pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
+    const int64_t P = (int64_t)pairs.size();
+    const int64_t nu = n + P;
+    auto pair_id = [&](int64_t lo, int64_t hi) {
+        return (int64_t)(std::lower_bound(pairs.begin(), pairs.end(), std::make_pair(lo, hi)) - pairs.begin());
+    };
+    // contribution lists per upper block (factor order)
+    std::vector<int32_t> cnt((size_t)nu + 1, 0);
+    for (int64_t k = 0; k < nf; ++k) {
+        const dpg_factor& f = F[k];
+        cnt[(size_t)f.i + 1]++;
+        if (f.kind == DPG_FACTOR_BETWEEN) {
+            cnt[(size_t)f.j + 1]++;
+            cnt[(size_t)(n + pair_id(std::min<int64_t>(f.i, f.j), std::max<int64_t>(f.i, f.j))) + 1]++;
+        }
+    }
+    for (int64_t u = 0; u < nu; ++u) cnt[(size_t)u + 1] += cnt[(size_t)u];
+    std::vector<int32_t> cptr = cnt, clist((size_t)cnt[(size_t)nu]);
+    std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
+    for (int64_t k = 0; k < nf; ++k) {
+        const dpg_factor& f = F[k];
+        clist[(size_t)cur[(size_t)f.i]++] = (int32_t)(k << 2 | 0);
+        if (f.kind == DPG_FACTOR_BETWEEN) {
+            clist[(size_t)cur[(size_t)f.j]++] = (int32_t)(k << 2 | 1);
+            const int64_t u = n + pair_id(std::min<int64_t>(f.i, f.j), std::max<int64_t>(f.i, f.j));
+            clist[(size_t)cur[(size_t)u]++] = (int32_t)(k << 2 | (f.i < f.j ? 2 : 3));
+        }
+    }
+    // full BSR rows
+    std::vector<std::vector<std::pair<int32_t, int32_t>>> rows((size_t)n);
+    for (int64_t v = 0; v < n; ++v) rows[(size_t)v].emplace_back((int32_t)v, (int32_t)v);
+    for (int64_t p = 0; p < P; ++p) {
+        const int64_t lo = pairs[(size_t)p].first, hi = pairs[(size_t)p].second;
+        rows[(size_t)lo].emplace_back((int32_t)hi, (int32_t)(n + p));
+        rows[(size_t)hi].emplace_back((int32_t)lo, (int32_t)(-1 - (n + p)));
+    }
+    std::vector<int32_t> rowptr((size_t)n + 1, 0), colidx, srcup;
+    colidx.reserve((size_t)(n + 2 * P));
+    srcup.reserve((size_t)(n + 2 * P));
+    for (int64_t v = 0; v < n; ++v) {
+        auto& rw = rows[(size_t)v];
+        std::sort(rw.begin(), rw.end());
+        for (auto& cs : rw) { colidx.push_back(cs.first); srcup.push_back(cs.second); }
+        rowptr[(size_t)v + 1] = (int32_t)colidx.size();
+    }
+    g->n_nodes = n;
+    g->n_factors = nf;
+    g->nnzb_upper = nu;
+    g->nnzb_full = (int64_t)colidx.size();
+    g->shard_begin = shard_begin < 0 ? 0 : shard_begin;
+    g->shard_end = shard_end > nf ? nf : shard_end;
+    g->n_blocks_rows = (int32_t)nblk(n);
+    int rc = 0;
+    rc |= dev_alloc(&g->factors, (size_t)nf);
+    rc |= dev_alloc(&g->up_cptr, cptr.size());
+    rc |= dev_alloc(&g->up_clist, clist.size());
+    rc |= dev_alloc(&g->rowptr, rowptr.size());
+    rc |= dev_alloc(&g->colidx, colidx.size());
+    rc |= dev_alloc(&g->src_up, srcup.size());
+    rc |= dev_alloc(&g->bsr, 9 * colidx.size());
+    rc |= dev_alloc(&g->minv, 9 * (size_t)n);
+    rc |= dev_alloc(&g->poses, 3 * (size_t)n);
+    rc |= dev_alloc(&g->x, 3 * (size_t)n);
+    rc |= dev_alloc(&g->r, 3 * (size_t)n);
+    rc |= dev_alloc(&g->z, 3 * (size_t)n);
+    rc |= dev_alloc(&g->p0, 3 * (size_t)n);
+    rc |= dev_alloc(&g->p1, 3 * (size_t)n);
+    rc |= dev_alloc(&g->q, 3 * (size_t)n);
+    rc |= dev_alloc(&g->partials, 6 * (size_t)g->n_blocks_rows + (size_t)n);
+    rc |= dev_alloc(&g->scal, 2 * (size_t)65536);
+    rc |= dev_alloc(&g->hb_own, (size_t)dpg_gn_dev_hb_size(g));
+    if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
+    if (nf && hipMemcpy(g->factors, F, (size_t)nf * sizeof(dpg_factor), hipMemcpyHostToDevice) != hipSuccess) rc = DPG_ERR_HIP;
+    rc |= up(g->up_cptr, cptr);
+    rc |= up(g->up_clist, clist);
+    rc |= up(g->rowptr, rowptr);
+    rc |= up(g->colidx, colidx);
+    rc |= up(g->src_up, srcup);
+    if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
+    return DPG_OK;
+}
+
+extern "C" int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* res, int64_t first, int64_t count,
+                                         int64_t n_always, double ix, double iy, double ith, void* stream) {
+    if (count <= 0) return DPG_OK;
+    if (first < 0 || first + count > g->n_factors) return DPG_ERR_ARG;
+    hipLaunchKernelGGL(icp_to_factor_kernel, dim3(nblk(count)), dim3(kRowThreads), 0,
+                       reinterpret_cast<hipStream_t>(stream), res, g->factors, first, count, n_always, ix, iy, ith);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    double* chi2_node = g->partials + 6 * (size_t)g->n_blocks_rows;
+    hipLaunchKernelGGL(assemble_kernel, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->factors, g->poses,
+                       g->up_cptr, g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, hb,
+                       chi2_node);
+    hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
+                       hb + 9 * g->nnzb_upper + 3 * g->n_nodes);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, void* stream,
+                                double* delta_inf, double* error, int32_t* pcg_iters) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nb = g->n_blocks_rows;
+    const int64_t n = g->n_nodes;
+    double* part_rz_a = g->partials;
+    double* part_rz_b = g->partials + nb;
+    double* part_rr = g->partials + 2 * (size_t)nb;
+    double* part_pq = g->partials + 3 * (size_t)nb;
+    double* part_max = g->partials + 4 * (size_t)nb;
+    hipLaunchKernelGGL(pcg_init_kernel, dim3(nb), dim3(kRowThreads), 0, s, hb, g->rowptr, g->src_up, n, g->nnzb_upper,
+                       g->bsr, g->minv, g->x, g->r, g->z, g->p0, part_rz_a, part_rr);
+    double host_scal[2] = {0, 0};
+    double rr0 = -1.0;
+    const int check = gp->pcg_check_every > 0 ? gp->pcg_check_every : 16;
+    const int max_it = std::min(gp->pcg_max_iterations > 0 ? gp->pcg_max_iterations : 20000, 65535);
+    const double tol2 = gp->pcg_rel_tol * gp->pcg_rel_tol;
+    int it = 0;
+    double* pbuf[2] = {g->p0, g->p1};
+    double* rzbuf[2] = {part_rz_a, part_rz_b};
+    double* xout = g->x;
+    for (; it < max_it; ++it) {
+        double* p_old = pbuf[it & 1];
+        double* p_new = pbuf[(it + 1) & 1];
+        hipLaunchKernelGGL(pcg_spmv_kernel, dim3(nb), dim3(kRowThreads), 0, s, it, g->bsr, g->rowptr, g->colidx, n,
+                           g->z, p_old, p_new, g->q, rzbuf[it & 1], part_rr, part_pq, g->scal, nb);
+        if (it % check == 0) {
+            if (hipMemcpyAsync(host_scal, g->scal + 2 * it, 2 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipStreamSynchronize(s) != hipSuccess)
+                return DPG_ERR_HIP;
+            if (rr0 < 0) rr0 = host_scal[1];
+            if (!(host_scal[1] > tol2 * rr0) || !(rr0 > 0)) break;   // converged (or zero rhs)
+        }
+        hipLaunchKernelGGL(pcg_update_kernel, dim3(nb), dim3(kRowThreads), 0, s, it, n, g->minv, p_new, g->q, g->x,
+                           g->r, g->z, rzbuf[it & 1], part_pq, rzbuf[(it + 1) & 1], part_rr, nb);
+    }
+    hipLaunchKernelGGL(retract_kernel, dim3(nb), dim3(kRowThreads), 0, s, g->poses, xout, n, part_max);
+    std::vector<double> pm((size_t)nb);
+    double chi2 = 0.0;
+    if (hipMemcpyAsync(pm.data(), part_max, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&chi2, hb + 9 * g->nnzb_upper + 3 * n, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return DPG_ERR_HIP;
+    double mx = 0.0;
+    for (double v : pm) mx = std::max(mx, v);
+    if (delta_inf) *delta_inf = mx;
+    if (error) *error = chi2;
+    if (pcg_iters) *pcg_iters = it;
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}

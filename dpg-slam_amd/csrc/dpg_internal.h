@@ -1,0 +1,93 @@
+/*
+ * dpg_internal.h -- private structures shared by the C-ABI layer (dpg_api.hip) and the HIP
+ * kernel translation units (dpg_icp.hip, dpg_gn.hip).  Not part of the public ABI.
+ */
+#ifndef DPG_INTERNAL_H
+#define DPG_INTERNAL_H
+
+#include <stdint.h>
+
+#include "../../include/dpg_slam_c.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* One ICP edge as the kernel sees it (48 B).  Offsets/counts are in points (float2). */
+typedef struct dpg_icp_edge {
+    int32_t src_ds_off, n_src_ds;    /* downsampled node_2 cloud (ICP source) */
+    int32_t tgt_ds_off, n_tgt_ds;    /* downsampled node_1 cloud (ICP target) */
+    int32_t src_full_off, n_src_full;  /* full node_2 cloud (covariance data_pi) */
+    int32_t tgt_full_off, n_tgt_full;  /* full node_1 cloud (covariance model_qi) */
+    float guess[6];                  /* runIcp transform_guess rows (dpg_slam.cc:374-378) */
+} dpg_icp_edge;
+
+/* Scalars of the ICP/convergence rule, precomputed on the host in double. */
+typedef struct dpg_icp_kparams {
+    double r2;          /* max_dist_sqr = d * d (determineReciprocalCorrespondences) */
+    double eps;         /* transformation_epsilon_ (translation threshold) */
+    double rot_thr;     /* 1 - transformation_epsilon_ (rotation threshold) */
+    double mse_abs;     /* mse_threshold_absolute_ */
+    float r2_f;         /* largest float <= r2: (double)d <= r2  <=>  d <= r2_f for float d */
+    float h_min;        /* smallest grid cell: 1.05 * r */
+    int32_t max_iter;
+    int32_t min_corr;
+    int32_t reciprocal;
+    int32_t cells_max;  /* LDS grid capacity */
+    int32_t lds_tgt;    /* LDS target capacity (points) */
+    int32_t trace_iters;
+    int32_t trace_stride;
+    int32_t pad;
+} dpg_icp_kparams;
+
+/* Launchers (defined in dpg_icp.hip).  Return 0 or a negative DPG_ERR_*. */
+int dpg_launch_icp(const float* ds_pts_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
+                   const dpg_icp_kparams* kp, int32_t max_points, dpg_icp_result* results_dev,
+                   int32_t* trace_dev, void* stream);
+int dpg_launch_cov(const float* full_pts_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
+                   const dpg_icp_result* results_dev, double* hess_dev, void* stream);
+size_t dpg_icp_lds_bytes(int32_t lds_tgt, int32_t cells_max);
+
+/* Pose-graph system on device (defined in dpg_gn.hip). */
+typedef struct dpg_gn_dev {
+    int64_t n_nodes, n_factors, nnzb_upper, nnzb_full;
+    int64_t shard_begin, shard_end;
+    /* factors and their per-block contribution lists */
+    dpg_factor* factors;           /* [n_factors] */
+    /* upper pattern: block u (0..nnzb_upper) = (row, col) with row <= col; diag blocks first */
+    int32_t* up_row;               /* [nnzb_upper] */
+    int32_t* up_col;
+    int32_t* up_cptr;              /* [nnzb_upper + 1] contribution list ptr */
+    int32_t* up_clist;             /* factor index << 2 | role (0: ii, 1: jj, 2: ij, 3: ji) */
+    int32_t* node_fptr;            /* [n_nodes + 1] factors whose FIRST key is the node (chi2/b) */
+    int32_t* node_flist;
+    /* full BSR for the solve */
+    int32_t* rowptr;               /* [n_nodes + 1] */
+    int32_t* colidx;               /* [nnzb_full] */
+    int32_t* src_up;               /* [nnzb_full] upper block feeding this block; < 0: transposed (-1-u) */
+    double* bsr;                   /* [nnzb_full][9] */
+    double* minv;                  /* [n_nodes][9] block-Jacobi inverses */
+    double* poses;                 /* [n_nodes][3] */
+    double* x, *r, *z, *p0, *p1, *q; /* PCG vectors [3 n_nodes] */
+    double* partials;              /* PCG per-block partial sums */
+    double* scal;                  /* PCG scalars */
+    double* hb_own;                /* packed [H upper | b | chi2] buffer for single-GPU solves */
+    int32_t n_blocks_rows;         /* grid size for row kernels */
+    int32_t pad;
+} dpg_gn_dev;
+
+int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n_nodes, const dpg_factor* factors, int64_t n_factors,
+                     int64_t shard_begin, int64_t shard_end);
+void dpg_gn_dev_free(dpg_gn_dev* g);
+int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g);
+int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb_dev, void* stream);
+int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb_dev, const dpg_gn_params* gp, void* stream,
+                     double* delta_inf, double* error, int32_t* pcg_iters);
+int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* results_dev, int64_t first,
+                              int64_t count, int64_t n_always, double info_x, double info_y,
+                              double info_th, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

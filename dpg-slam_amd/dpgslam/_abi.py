@@ -1,0 +1,212 @@
+"""ctypes view of the C ABI in include/dpg_slam_c.h and include/dpg_icp_cov.h.
+
+The shared library is dpg-slam_amd/lib/libdpg.so (built by `make -C dpg-slam_amd`, or
+`__graft_entry__.build()`).  There is no fallback implementation: if the library is missing,
+`lib()` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpg.so")
+
+DPG_OK = 0
+DPG_FACTOR_PRIOR = 0
+DPG_FACTOR_BETWEEN = 1
+DPG_ICP_OK = 0
+DPG_ICP_TOO_FEW_CORR = 1
+DPG_ICP_LANES = 256
+
+
+class IcpParams(C.Structure):
+    """dpg_icp_params -- PoseGraphParameters ICP fields (parameters.h:105-141)."""
+
+    _fields_ = [
+        ("icp_maximum_iterations", C.c_int32),
+        ("icp_use_reciprocal_correspondences", C.c_int32),
+        ("icp_maximum_transformation_epsilon", C.c_double),
+        ("icp_max_correspondence_distance", C.c_double),
+        ("ransac_iterations", C.c_int32),
+        ("downsample_icp_points_ratio", C.c_int32),
+        ("laser_x_variance", C.c_float),
+        ("laser_y_variance", C.c_float),
+        ("laser_theta_variance", C.c_float),
+        ("min_number_correspondences", C.c_int32),
+        ("mse_threshold_absolute", C.c_double),
+    ]
+
+
+class IcpResult(C.Structure):
+    _fields_ = [
+        ("T", C.c_float * 6),
+        ("z", C.c_float * 3),
+        ("converged", C.c_int32),
+        ("iterations", C.c_int32),
+        ("n_corr", C.c_int32),
+        ("status", C.c_int32),
+        ("pad", C.c_int32),
+        ("fitness", C.c_double),
+    ]
+
+
+class Factor(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("i", C.c_int32),
+        ("j", C.c_int32),
+        ("pad", C.c_int32),
+        ("z", C.c_double * 3),
+        ("info", C.c_double * 3),
+    ]
+
+
+class GnParams(C.Structure):
+    _fields_ = [
+        ("max_iterations", C.c_int32),
+        ("use_error_criteria", C.c_int32),
+        ("delta_tol", C.c_double),
+        ("relative_error_tol", C.c_double),
+        ("absolute_error_tol", C.c_double),
+        ("pcg_rel_tol", C.c_double),
+        ("pcg_max_iterations", C.c_int32),
+        ("pcg_check_every", C.c_int32),
+    ]
+
+
+class GnStats(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int32),
+        ("pcg_iterations", C.c_int32),
+        ("initial_error", C.c_double),
+        ("final_error", C.c_double),
+        ("last_delta_inf", C.c_double),
+        ("ms_total", C.c_double),
+        ("ms_per_iteration", C.c_double),
+    ]
+
+
+# numpy mirrors of the array-of-struct types (same layout as the C structs)
+RESULT_DTYPE = np.dtype(
+    [("T", "<f4", (6,)), ("z", "<f4", (3,)), ("converged", "<i4"), ("iterations", "<i4"),
+     ("n_corr", "<i4"), ("status", "<i4"), ("pad", "<i4"), ("fitness", "<f8")], align=True)
+FACTOR_DTYPE = np.dtype(
+    [("kind", "<i4"), ("i", "<i4"), ("j", "<i4"), ("pad", "<i4"), ("z", "<f8", (3,)),
+     ("info", "<f8", (3,))], align=True)
+assert RESULT_DTYPE.itemsize == C.sizeof(IcpResult) == 64
+assert FACTOR_DTYPE.itemsize == C.sizeof(Factor) == 64
+
+P = C.c_void_p
+F32P = C.POINTER(C.c_float)
+F64P = C.POINTER(C.c_double)
+I32P = C.POINTER(C.c_int32)
+I64P = C.POINTER(C.c_int64)
+
+# name -> (restype, argtypes); the full exported surface of include/*.h
+SIGNATURES = {
+    "dpg_last_error": (C.c_char_p, []),
+    "dpg_version": (C.c_char_p, []),
+    "dpg_icp_params_default": (None, [C.POINTER(IcpParams)]),
+    "dpg_gn_params_default": (None, [C.POINTER(GnParams)]),
+    "dpg_ctx_create": (P, [C.c_int]),
+    "dpg_ctx_destroy": (None, [P]),
+    "dpg_ctx_set_stream": (C.c_int, [P, P]),
+    "dpg_ctx_synchronize": (C.c_int, [P]),
+    "dpg_scan_to_cloud": (C.c_int64, [F32P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float,
+                                      C.c_float, C.c_float, F32P]),
+    "dpg_scans_to_clouds": (C.c_int64, [F32P, C.c_int64, C.c_int64, C.c_float, C.c_float, C.c_float,
+                                        C.c_float, C.c_float, C.c_float, F32P, I64P]),
+    "dpg_downsample_cloud": (C.c_int64, [F32P, C.c_int64, C.c_int32, F32P]),
+    "dpg_inverse_transform_point": (None, [F32P, F32P, F32P]),
+    "dpg_transform_point": (None, [F32P, F32P, F32P]),
+    "dpg_icp_guess": (None, [F32P, F32P, F32P]),
+    "dpg_odometry_factor": (C.c_int, [F32P, F32P, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float,
+                                      C.c_float, C.POINTER(Factor)]),
+    "dpg_icp_factor": (None, [C.POINTER(IcpResult), C.c_int32, C.c_int32, C.POINTER(IcpParams),
+                              C.POINTER(Factor)]),
+    "dpg_synth_world": (C.c_int64, [C.c_uint64, C.c_float, F32P, C.c_int64]),
+    "dpg_synth_trajectory": (C.c_int, [C.c_uint64, C.c_int64, F32P, C.c_int64, C.c_float, C.c_float, F64P]),
+    "dpg_synth_scans": (C.c_int, [F64P, C.c_int64, F32P, C.c_int64, C.c_int32, C.c_float, C.c_float,
+                                  C.c_float, C.c_float, C.c_float, C.c_float, C.c_float, C.c_uint64,
+                                  C.c_int32, F32P]),
+    "dpg_run_icp": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, F32P, C.POINTER(IcpParams),
+                              C.POINTER(IcpResult), F64P, F64P]),
+    "dpg_scans_upload": (C.c_int, [P, F32P, I64P, C.c_int64, C.c_int32]),
+    "dpg_icp_batch_prepare": (C.c_int, [P, I32P, C.c_int64, F32P, C.POINTER(IcpParams)]),
+    "dpg_icp_batch_run": (C.c_int, [P, C.c_int32, C.c_int32]),
+    "dpg_icp_batch_fetch": (C.c_int, [P, P, F64P]),
+    "dpg_icp_batch_fetch_trace": (C.c_int, [P, I32P, I64P]),
+    "dpg_icp_batch_kernel_ms": (C.c_float, [P]),
+    "dpg_cov_batch_kernel_ms": (C.c_float, [P]),
+    "dpg_icp_batch_algorithmic_bytes": (C.c_double, [P]),
+    "dpg_optimize_graph": (C.c_int, [P, F64P, C.c_int64, P, C.c_int64, C.POINTER(GnParams),
+                                     C.POINTER(GnStats)]),
+    "dpg_gn_setup": (C.c_int, [P, C.c_int64, P, C.c_int64, C.c_int64, C.c_int64, C.POINTER(GnParams)]),
+    "dpg_gn_take_icp_measurements": (C.c_int, [P, C.c_int64, C.c_int64, C.c_int64, C.POINTER(IcpParams)]),
+    "dpg_gn_hb_size": (C.c_int64, [P]),
+    "dpg_gn_set_poses": (C.c_int, [P, F64P]),
+    "dpg_gn_get_poses": (C.c_int, [P, F64P]),
+    "dpg_gn_assemble": (C.c_int, [P, P]),
+    "dpg_gn_solve_retract": (C.c_int, [P, P, F64P, F64P, I32P]),
+    "dpg_gn_last_assemble_ms": (C.c_float, [P]),
+    "dpg_gn_last_solve_ms": (C.c_float, [P]),
+    "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,
+                                    C.c_float, F64P, F64P]),
+}
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load libdpg.so (raises OSError/RuntimeError when it is not built -- no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is not built; run `make -C dpg-slam_amd` or __graft_entry__.build()")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def ptr(a: np.ndarray, ctype):
+    """Pointer to a contiguous numpy array (None for None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def vptr(a: np.ndarray):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return C.c_void_p(a.ctypes.data)
+
+
+class DpgError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = "dpg call"):
+    if rc != DPG_OK:
+        msg = lib().dpg_last_error()
+        raise DpgError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def default_icp_params() -> IcpParams:
+    p = IcpParams()
+    lib().dpg_icp_params_default(C.byref(p))
+    return p
+
+
+def default_gn_params() -> GnParams:
+    p = GnParams()
+    lib().dpg_gn_params_default(C.byref(p))
+    return p

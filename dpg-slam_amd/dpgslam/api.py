@@ -1,0 +1,276 @@
+"""Python mirror of the reference's hot-path interface, over the C ABI (libdpg.so).
+
+Reference interface (file:line)                         this module
+------------------------------------------------------  ---------------------------------------
+calculate_ICP_COV(data_pi, model_qi, T, ICP_COV, vx,     calculate_ICP_COV(data, model, T, vx, vy,
+  vy, vth)  src/icp_cov/cov_func_point_to_point.h:24        vth) -> (ICP_COV, hessian block)
+DpgSLAM::runIcp(node_1, node_2, icp_results) -> bool     Context.run_icp(node_1, node_2, params)
+  src/dpg_slam/dpg_slam.cc:362-446                          -> (converged, ((x, y), theta), cov)
+DpgSLAM::optimizeGraph(init_estimates)                   Context.optimize_graph(poses, factors)
+  src/dpg_slam/dpg_slam.cc:316-329
+batched runIcp calls of reoptimize (dpg_slam.cc:85-106)  Context.upload_scans / icp_batch
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import (FACTOR_DTYPE, RESULT_DTYPE, F32P, F64P, I32P, I64P, check, lib, ptr, vptr)
+
+
+@dataclass
+class Node:
+    """The part of DpgNode (src/dpg_slam/dpg_node.h:30-36) the hot path reads: the estimated pose
+    and the cached base_link cloud (getCachedPointCloudFromNode, dpg_node.cc:8-25)."""
+
+    pose: np.ndarray   # float32 (x, y, theta)
+    cloud: np.ndarray  # float32 [n, 2]
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _f64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+# ------------------------------------------------------------------------- host helpers (R1-R3)
+def scan_to_cloud(ranges, angle_min, angle_max, range_max, laser=(0.2, 0.0, 0.0)) -> np.ndarray:
+    r = _f32(ranges)
+    out = np.empty((max(r.size, 1), 2), np.float32)
+    n = lib().dpg_scan_to_cloud(ptr(r, C.c_float), r.size, angle_min, angle_max, range_max,
+                                laser[0], laser[1], laser[2], ptr(out, C.c_float))
+    return out[:n].copy()
+
+
+def scans_to_clouds(ranges, angle_min, angle_max, range_max, laser=(0.2, 0.0, 0.0)):
+    r = _f32(ranges)
+    V, nb = r.shape
+    pts = np.empty((V * nb, 2), np.float32)
+    offs = np.empty(V + 1, np.int64)
+    tot = lib().dpg_scans_to_clouds(ptr(r, C.c_float), V, nb, angle_min, angle_max, range_max,
+                                    laser[0], laser[1], laser[2], ptr(pts, C.c_float), ptr(offs, C.c_int64))
+    return pts[:tot].copy(), offs
+
+
+def downsample(cloud, ratio: int) -> np.ndarray:
+    c = _f32(cloud)
+    out = np.empty((max(len(c), 1), 2), np.float32)
+    n = lib().dpg_downsample_cloud(ptr(c, C.c_float), len(c), ratio, ptr(out, C.c_float))
+    return out[:n].copy()
+
+
+def inverse_transform_point(a, b) -> np.ndarray:
+    a, b, o = _f32(a), _f32(b), np.empty(3, np.float32)
+    lib().dpg_inverse_transform_point(ptr(a, C.c_float), ptr(b, C.c_float), ptr(o, C.c_float))
+    return o
+
+
+def transform_point(p, frame) -> np.ndarray:
+    p, f, o = _f32(p), _f32(frame), np.empty(3, np.float32)
+    lib().dpg_transform_point(ptr(p, C.c_float), ptr(f, C.c_float), ptr(o, C.c_float))
+    return o
+
+
+def icp_guess(pose_src, pose_tgt) -> np.ndarray:
+    a, b, o = _f32(pose_src), _f32(pose_tgt), np.empty(6, np.float32)
+    lib().dpg_icp_guess(ptr(a, C.c_float), ptr(b, C.c_float), ptr(o, C.c_float))
+    return o
+
+
+def odometry_factor(odom_prev, odom_cur, i_prev, i_cur, motion=(0.4, 0.4, 0.4, 0.4)):
+    a, b = _f32(odom_prev), _f32(odom_cur)
+    f = _abi.Factor()
+    rc = lib().dpg_odometry_factor(ptr(a, C.c_float), ptr(b, C.c_float), i_prev, i_cur, *motion, C.byref(f))
+    check(rc, "dpg_odometry_factor")
+    return f
+
+
+def prior_factor(node: int, pose=(0.0, 0.0, 0.0), sigmas=(0.2, 0.2, 0.15)) -> np.ndarray:
+    """PriorFactor<Pose2> with Diagonal::Sigmas (dpg_slam.cc:44-49); sigmas are the float
+    parameters new_pass_{x,y,theta}_std_dev_ (parameters.h:264-274) widened to double."""
+    f = np.zeros(1, FACTOR_DTYPE)
+    f["kind"] = _abi.DPG_FACTOR_PRIOR
+    f["i"] = node
+    f["z"] = pose
+    s = np.asarray(sigmas, np.float32).astype(np.float64)
+    f["info"] = 1.0 / (s * s)
+    return f
+
+
+def between_factor(i, j, z, sigmas=None, info=None) -> np.ndarray:
+    f = np.zeros(1, FACTOR_DTYPE)
+    f["kind"] = _abi.DPG_FACTOR_BETWEEN
+    f["i"], f["j"], f["z"] = i, j, z
+    if info is None:
+        s = np.asarray(sigmas, np.float64)
+        info = 1.0 / (s * s)
+    f["info"] = info
+    return f
+
+
+def calculate_ICP_COV(data_pi, model_qi, transform, laser_x_variance=0.5, laser_y_variance=0.5,
+                      laser_theta_variance=0.3, ctx: "Context | None" = None, with_hessian=True):
+    """calculate_ICP_COV (cov_func_point_to_point.h:24): returns (ICP_COV 3x3, [x,y,yaw] Hessian
+    block or None).  transform: 4x4 (row-major) homogeneous matrix."""
+    d, m = _f32(data_pi).reshape(-1, 2), _f32(model_qi).reshape(-1, 2)
+    T = _f32(transform).reshape(4, 4)
+    cov = np.zeros(9, np.float64)
+    hess = np.zeros(9, np.float64) if with_hessian else None
+    rc = lib().icp_cov_calculate(ctx.handle if ctx else None, ptr(d, C.c_float), len(d), ptr(m, C.c_float),
+                                 len(m), ptr(T, C.c_float), laser_x_variance, laser_y_variance,
+                                 laser_theta_variance, ptr(cov, C.c_double), ptr(hess, C.c_double))
+    check(rc, "icp_cov_calculate")
+    return cov.reshape(3, 3), (hess.reshape(3, 3) if hess is not None else None)
+
+
+def results_array(n: int) -> np.ndarray:
+    return np.zeros(n, RESULT_DTYPE)
+
+
+# ------------------------------------------------------------------------- GPU context
+class Context:
+    """One dpg_ctx (one GPU, one HIP stream).  Creating it without a usable GPU raises."""
+
+    def __init__(self, device: int = 0):
+        self.handle = lib().dpg_ctx_create(device)
+        if not self.handle:
+            raise _abi.DpgError("dpg_ctx_create failed: " + (lib().dpg_last_error() or b"").decode())
+        self.device = device
+        self.n_edges = 0
+        self.V = 0
+
+    def close(self):
+        if self.handle:
+            lib().dpg_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream_handle: int):
+        check(lib().dpg_ctx_set_stream(self.handle, C.c_void_p(stream_handle)), "dpg_ctx_set_stream")
+
+    def synchronize(self):
+        check(lib().dpg_ctx_synchronize(self.handle), "dpg_ctx_synchronize")
+
+    # ---- runIcp ----
+    def run_icp(self, node_1: Node, node_2: Node, params=None, with_hessian=False):
+        """DpgSLAM::runIcp(node_1, node_2, icp_results): node_1 = target, node_2 = source.
+        Returns (converged, ((tx, ty), theta), ICP_COV, result, hessian_block)."""
+        p = params or _abi.default_icp_params()
+        s, t = _f32(node_2.cloud).reshape(-1, 2), _f32(node_1.cloud).reshape(-1, 2)
+        ps, pt = _f32(node_2.pose), _f32(node_1.pose)
+        res = _abi.IcpResult()
+        cov = np.zeros(9, np.float64)
+        hess = np.zeros(9, np.float64) if with_hessian else None
+        rc = lib().dpg_run_icp(self.handle, ptr(s, C.c_float), len(s), ptr(t, C.c_float), len(t),
+                               ptr(ps, C.c_float), ptr(pt, C.c_float), C.byref(p), C.byref(res),
+                               ptr(cov, C.c_double), ptr(hess, C.c_double))
+        check(rc, "dpg_run_icp")
+        ok = bool(res.converged) and res.status == _abi.DPG_ICP_OK
+        z = ((float(res.z[0]), float(res.z[1])), float(res.z[2]))
+        return ok, z, cov.reshape(3, 3), res, (hess.reshape(3, 3) if hess is not None else None)
+
+    # ---- batched ICP ----
+    def upload_scans(self, pts: np.ndarray, offsets: np.ndarray, ratio: int = 5):
+        pts, offs = _f32(pts).reshape(-1, 2), np.ascontiguousarray(offsets, np.int64)
+        check(lib().dpg_scans_upload(self.handle, ptr(pts, C.c_float), ptr(offs, C.c_int64), len(offs) - 1,
+                                     ratio), "dpg_scans_upload")
+        self.V = len(offs) - 1
+
+    def icp_prepare(self, edges: np.ndarray, poses: np.ndarray, params=None):
+        p = params or _abi.default_icp_params()
+        e = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
+        ps = _f32(poses).reshape(-1, 3)
+        check(lib().dpg_icp_batch_prepare(self.handle, ptr(e, C.c_int32), len(e), ptr(ps, C.c_float), C.byref(p)),
+              "dpg_icp_batch_prepare")
+        self.n_edges = len(e)
+
+    def icp_run(self, compute_cov=True, trace_iters=0):
+        check(lib().dpg_icp_batch_run(self.handle, int(compute_cov), int(trace_iters)), "dpg_icp_batch_run")
+
+    def icp_fetch(self, with_hessian=True):
+        res = results_array(self.n_edges)
+        hess = np.zeros((self.n_edges, 9), np.float64) if with_hessian else None
+        check(lib().dpg_icp_batch_fetch(self.handle, vptr(res), ptr(hess, C.c_double)), "dpg_icp_batch_fetch")
+        return res, (hess.reshape(-1, 3, 3) if hess is not None else None)
+
+    def icp_fetch_trace(self, iters: int) -> np.ndarray:
+        ms = C.c_int64(0)
+        check(lib().dpg_icp_batch_fetch_trace(self.handle, None, C.byref(ms)), "trace size")
+        tr = np.empty((self.n_edges, iters, ms.value), np.int32)
+        check(lib().dpg_icp_batch_fetch_trace(self.handle, ptr(tr, C.c_int32), C.byref(ms)), "trace fetch")
+        return tr
+
+    def icp_batch(self, edges, poses, params=None, compute_cov=True, trace_iters=0):
+        self.icp_prepare(edges, poses, params)
+        self.icp_run(compute_cov, trace_iters)
+        return self.icp_fetch(compute_cov)
+
+    def icp_kernel_ms(self) -> float:
+        return float(lib().dpg_icp_batch_kernel_ms(self.handle))
+
+    def cov_kernel_ms(self) -> float:
+        return float(lib().dpg_cov_batch_kernel_ms(self.handle))
+
+    def icp_algorithmic_bytes(self) -> float:
+        return float(lib().dpg_icp_batch_algorithmic_bytes(self.handle))
+
+    # ---- optimizeGraph ----
+    def optimize_graph(self, poses: np.ndarray, factors: np.ndarray, params=None):
+        """Batch Gauss-Newton to convergence; returns (poses [V,3] float64, stats)."""
+        X = _f64(poses).reshape(-1, 3).copy()
+        F = np.ascontiguousarray(factors, FACTOR_DTYPE)
+        gp = params or _abi.default_gn_params()
+        st = _abi.GnStats()
+        check(lib().dpg_optimize_graph(self.handle, ptr(X, C.c_double), len(X), vptr(F), len(F), C.byref(gp),
+                                       C.byref(st)), "dpg_optimize_graph")
+        return X, st
+
+    # ---- sharded GN step API ----
+    def gn_setup(self, V: int, factors: np.ndarray, shard=(0, None), params=None):
+        F = np.ascontiguousarray(factors, FACTOR_DTYPE)
+        b, e = shard[0], (len(F) if shard[1] is None else shard[1])
+        gp = params or _abi.default_gn_params()
+        check(lib().dpg_gn_setup(self.handle, V, vptr(F), len(F), b, e, C.byref(gp)), "dpg_gn_setup")
+        return int(lib().dpg_gn_hb_size(self.handle))
+
+    def gn_take_icp(self, first: int, count: int, n_always: int, params=None):
+        p = params or _abi.default_icp_params()
+        check(lib().dpg_gn_take_icp_measurements(self.handle, first, count, n_always, C.byref(p)),
+              "dpg_gn_take_icp_measurements")
+
+    def gn_set_poses(self, poses):
+        X = _f64(poses).reshape(-1, 3)
+        check(lib().dpg_gn_set_poses(self.handle, ptr(X, C.c_double)), "dpg_gn_set_poses")
+
+    def gn_get_poses(self, V: int) -> np.ndarray:
+        X = np.empty((V, 3), np.float64)
+        check(lib().dpg_gn_get_poses(self.handle, ptr(X, C.c_double)), "dpg_gn_get_poses")
+        return X
+
+    def gn_assemble(self, hb_dev_ptr: int | None = None):
+        check(lib().dpg_gn_assemble(self.handle, C.c_void_p(hb_dev_ptr) if hb_dev_ptr else None), "dpg_gn_assemble")
+
+    def gn_solve_retract(self, hb_dev_ptr: int | None = None):
+        d, e, it = C.c_double(0), C.c_double(0), C.c_int32(0)
+        check(lib().dpg_gn_solve_retract(self.handle, C.c_void_p(hb_dev_ptr) if hb_dev_ptr else None, C.byref(d),
+                                         C.byref(e), C.byref(it)), "dpg_gn_solve_retract")
+        return d.value, e.value, it.value
+
+    def gn_times_ms(self):
+        return float(lib().dpg_gn_last_assemble_ms(self.handle)), float(lib().dpg_gn_last_solve_ms(self.handle))

@@ -1,0 +1,192 @@
+"""Seeded synthetic workloads for BASELINE.json's configs.
+
+config 1: two 360-beam scans, one alignment (ratio 5, and a ratio-1 variant)
+config 2: 500-node odometry chain, 499 successive ICP edges, no loop closures
+config 3: 2000 nodes, 1999 successive ICP edges + 200 loop closures (|i-j| >= 50, <= 2 m)
+config 4: 5000 nodes, 4999 successive + 15001 loop-closure ICP edges (<= 5 m, nearest pairs
+          first), 4999 odometry factors, 1 prior -> 25000 factors
+
+World, trajectory and scans come from the C generator (dpg_synth.c).  Node estimated poses (the
+values runIcp reads, dpg_slam.cc:364-368, and the GN initial values, dpg_slam.cc:111-118) are the
+ground truth in node 0's frame plus Gaussian noise, as after an earlier optimisation; odometry
+(odom_only_estimates_) is the ground-truth motion plus per-step noise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from ._abi import FACTOR_DTYPE, lib, ptr
+from . import api
+
+ANGLE_MIN = -math.pi
+ANGLE_MAX = math.pi
+RANGE_MAX = 30.0
+LASER = (0.2, 0.0, 0.0)   # parameters.h:319-339
+
+
+@dataclass
+class SynthConfig:
+    name: str
+    n_nodes: int
+    n_beams: int = 5000
+    seed: int = 4
+    world_size: float = 40.0
+    downsample: int = 5
+    n_loop_closures: int = 0
+    lc_max_dist: float = 5.0
+    lc_min_sep: int = 2
+    range_noise: float = 0.01
+    est_noise: tuple = (0.05, 0.02)
+    odom_noise: tuple = (0.05, 0.01)
+    threads: int = 0
+
+
+CONFIGS = {
+    "config1": SynthConfig("config1", n_nodes=2, n_beams=360, seed=1, world_size=20.0),
+    "config2": SynthConfig("config2", n_nodes=500, seed=2),
+    "config3": SynthConfig("config3", n_nodes=2000, seed=3, n_loop_closures=200, lc_max_dist=2.0, lc_min_sep=50),
+    "config4": SynthConfig("config4", n_nodes=5000, seed=4, n_loop_closures=15001, lc_max_dist=5.0, lc_min_sep=2),
+}
+
+
+@dataclass
+class Workload:
+    cfg: SynthConfig
+    segs: np.ndarray            # world segments [S,4]
+    gt: np.ndarray              # ground truth (world frame) [V,3] f64
+    ranges: np.ndarray          # [V, n_beams] f32
+    pts: np.ndarray             # concatenated full base_link clouds [P,2] f32
+    offsets: np.ndarray         # [V+1] i64
+    est: np.ndarray             # node estimated poses [V,3] f32 (node-0 frame)
+    odom: np.ndarray            # odom_only_estimates_ [V,3] f32
+    edges: np.ndarray           # ICP edges [E,2] = (node_1 target, node_2 source)
+    n_successive: int
+    base_factors: np.ndarray = field(default=None)   # prior + odometry factors
+    icp_factor_first: int = 0
+
+    @property
+    def V(self) -> int:
+        return len(self.gt)
+
+    @property
+    def E(self) -> int:
+        return len(self.edges)
+
+    def cloud(self, v: int) -> np.ndarray:
+        return self.pts[self.offsets[v]:self.offsets[v + 1]]
+
+    def node(self, v: int) -> api.Node:
+        return api.Node(pose=self.est[v], cloud=self.cloud(v))
+
+    def factors_with_icp(self, results: np.ndarray, params=None) -> np.ndarray:
+        """Full factor list: base factors, then one BetweenFactor per ICP edge in edge order;
+        successive edges always count, loop closures only when converged (zero information
+        otherwise -- same H, g and error as leaving the factor out)."""
+        p = params or _abi.default_icp_params()
+        F = np.zeros(len(self.base_factors) + self.E, FACTOR_DTYPE)
+        F[:len(self.base_factors)] = self.base_factors
+        k = len(self.base_factors)
+        F["kind"][k:] = _abi.DPG_FACTOR_BETWEEN
+        F["i"][k:] = self.edges[:, 0]
+        F["j"][k:] = self.edges[:, 1]
+        F["z"][k:] = results["z"].astype(np.float64)
+        keep = np.ones(self.E, bool)
+        keep[self.n_successive:] = (results["converged"][self.n_successive:] != 0) & (
+            results["status"][self.n_successive:] == _abi.DPG_ICP_OK)
+        info = np.array([1.0 / float(np.float32(p.laser_x_variance)), 1.0 / float(np.float32(p.laser_y_variance)),
+                         1.0 / float(np.float32(p.laser_theta_variance))])
+        F["info"][k:] = np.where(keep[:, None], info[None, :], 0.0)
+        return F
+
+    def factors_placeholder(self) -> np.ndarray:
+        """Factor list with the ICP slots present (measurements filled on device)."""
+        F = np.zeros(len(self.base_factors) + self.E, FACTOR_DTYPE)
+        F[:len(self.base_factors)] = self.base_factors
+        k = len(self.base_factors)
+        F["kind"][k:] = _abi.DPG_FACTOR_BETWEEN
+        F["i"][k:] = self.edges[:, 0]
+        F["j"][k:] = self.edges[:, 1]
+        return F
+
+
+def _relative(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """pose a in frame b (double)."""
+    c, s = np.cos(b[..., 2]), np.sin(b[..., 2])
+    dx, dy = a[..., 0] - b[..., 0], a[..., 1] - b[..., 1]
+    th = np.arctan2(np.sin(a[..., 2] - b[..., 2]), np.cos(a[..., 2] - b[..., 2]))
+    return np.stack([c * dx + s * dy, -s * dx + c * dy, th], -1)
+
+
+def _compose(a: np.ndarray, d: np.ndarray) -> np.ndarray:
+    c, s = math.cos(a[2]), math.sin(a[2])
+    th = a[2] + d[2]
+    return np.array([a[0] + c * d[0] - s * d[1], a[1] + s * d[0] + c * d[1], math.atan2(math.sin(th), math.cos(th))])
+
+
+def loop_closure_pairs(est: np.ndarray, n: int, max_dist: float, min_sep: int) -> np.ndarray:
+    """Reference distance rule (dpg_slam.cc:91-98): pairs (j, i), j < i - 1 (|i - j| >= min_sep),
+    float32 ||p_j - p_i|| <= threshold; the n nearest pairs first (ties by (i, j))."""
+    if n <= 0:
+        return np.zeros((0, 2), np.int32)
+    from scipy.spatial import cKDTree
+    xy = est[:, :2].astype(np.float64)
+    pairs = cKDTree(xy).query_pairs(max_dist * 1.0001, output_type="ndarray")
+    if len(pairs) == 0:
+        return np.zeros((0, 2), np.int32)
+    j = np.minimum(pairs[:, 0], pairs[:, 1])
+    i = np.maximum(pairs[:, 0], pairs[:, 1])
+    sel = (i - j) >= max(min_sep, 2)
+    i, j = i[sel], j[sel]
+    d = est[j, :2].astype(np.float32) - est[i, :2].astype(np.float32)
+    dist = np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]).astype(np.float32)
+    ok = dist <= np.float32(max_dist)
+    i, j, dist = i[ok], j[ok], dist[ok]
+    order = np.lexsort((j, i, dist))[:n]
+    return np.stack([j[order], i[order]], 1).astype(np.int32)
+
+
+def generate(cfg: SynthConfig | str) -> Workload:
+    if isinstance(cfg, str):
+        cfg = CONFIGS[cfg]
+    L = lib()
+    segs = np.zeros((4096, 4), np.float32)
+    ns = L.dpg_synth_world(cfg.seed, cfg.world_size, ptr(segs, C.c_float), len(segs))
+    segs = np.ascontiguousarray(segs[:ns])
+    V = cfg.n_nodes
+    gt = np.zeros((V, 3), np.float64)
+    _abi.check(L.dpg_synth_trajectory(cfg.seed, V, ptr(segs, C.c_float), ns, cfg.world_size, 1.0,
+                                      ptr(gt, C.c_double)), "dpg_synth_trajectory")
+    ranges = np.zeros((V, cfg.n_beams), np.float32)
+    threads = cfg.threads or min(16, os.cpu_count() or 1)
+    _abi.check(L.dpg_synth_scans(ptr(gt, C.c_double), V, ptr(segs, C.c_float), ns, cfg.n_beams, ANGLE_MIN,
+                                 ANGLE_MAX, RANGE_MAX, LASER[0], LASER[1], LASER[2], cfg.range_noise,
+                                 cfg.seed * 7919 + 1, threads, ptr(ranges, C.c_float)), "dpg_synth_scans")
+    pts, offs = api.scans_to_clouds(ranges, ANGLE_MIN, ANGLE_MAX, RANGE_MAX, LASER)
+    rng = np.random.default_rng(cfg.seed)
+    rel = _relative(gt, gt[0])
+    est = rel + np.concatenate([rng.normal(0, cfg.est_noise[0], (V, 2)), rng.normal(0, cfg.est_noise[1], (V, 1))], 1)
+    est[0] = 0.0   # createNewPassFirstNode: (0, 0, 0)
+    est = est.astype(np.float32)
+    odom = np.zeros((V, 3), np.float64)
+    for v in range(1, V):
+        d = _relative(gt[v], gt[v - 1])
+        d = d + np.array([rng.normal(0, cfg.odom_noise[0]), rng.normal(0, cfg.odom_noise[0]),
+                          rng.normal(0, cfg.odom_noise[1])])
+        odom[v] = _compose(odom[v - 1], d)
+    odom = odom.astype(np.float32)
+    succ = np.stack([np.arange(V - 1), np.arange(1, V)], 1).astype(np.int32)
+    lc = loop_closure_pairs(est, cfg.n_loop_closures, cfg.lc_max_dist, cfg.lc_min_sep)
+    edges = np.ascontiguousarray(np.concatenate([succ, lc], 0), np.int32)
+    base = [api.prior_factor(0)]
+    for v in range(1, V):
+        f = api.odometry_factor(odom[v - 1], odom[v], v - 1, v)
+        base.append(np.frombuffer(bytes(f), FACTOR_DTYPE).copy())
+    base = np.concatenate(base).astype(FACTOR_DTYPE)
+    return Workload(cfg=cfg, segs=segs, gt=gt, ranges=ranges, pts=pts, offsets=offs, est=est, odom=odom,
+                    edges=edges, n_successive=len(succ), base_factors=base, icp_factor_first=len(base))

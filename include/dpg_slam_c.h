@@ -1,0 +1,230 @@
+/*
+ * dpg_slam_c.h -- C ABI of the MI355X-native DPG-SLAM hot path.
+ *
+ * This library replaces the numerically hot part of BharathMasetty/DPG-SLAM:
+ *   - DpgSLAM::runIcp            (src/dpg_slam/dpg_slam.cc:362-446, decl dpg_slam.h:630)
+ *     which wraps pcl::IterativeClosestPoint<PointXYZ,PointXYZ>::align (dpg_slam.cc:387-416)
+ *     and calculate_ICP_COV (src/icp_cov/cov_func_point_to_point.h:24, see dpg_icp_cov.h);
+ *   - DpgSLAM::optimizeGraph     (src/dpg_slam/dpg_slam.cc:316-329, decl dpg_slam.h:464)
+ *     which runs GTSAM ISAM2 / Gauss-Newton over PriorFactor<Pose2> / BetweenFactor<Pose2>
+ *     built at dpg_slam.cc:44-75,178-183,227-238,331-338.
+ *
+ * All entry points are extern "C", take plain pointers + sizes, and return an int status
+ * (0 = OK, negative = error; dpg_last_error() gives the message).  Buffers are caller-owned
+ * HOST memory unless the parameter name ends in _dev (device memory on the context's GPU).
+ * A context is thread-compatible (one per thread), not thread-safe -- the reference calls
+ * all of these from the single ros::spin thread (dpg_slam_main.cc:328).
+ */
+#ifndef DPG_SLAM_C_H
+#define DPG_SLAM_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DPG_OK 0
+#define DPG_ERR_ARG (-1)
+#define DPG_ERR_HIP (-2)
+#define DPG_ERR_STATE (-3)
+#define DPG_ERR_SIZE (-4)
+#define DPG_ERR_NUMERIC (-5)
+
+/* Fixed reduction geometry of the ICP rigid fit (part of the algorithm's definition so that
+ * CPU oracle and GPU agree bit for bit): lane l accumulates source points l, l+256, ... in
+ * increasing order (fp64); each 64-lane wave folds acc[k] += acc[k + off], off = 32 ... 1, and
+ * the four wave totals combine as (W0 + W1) + (W2 + W3). */
+#define DPG_ICP_LANES 256
+
+/* ICP parameters: field names follow PoseGraphParameters (src/dpg_slam/parameters.h:105-141,
+ * defaults :146,159,173,191,201,374,385,396,402) plus the PCL defaults the reference inherits
+ * (Registration::min_number_correspondences_ = 3, DefaultConvergenceCriteria mse abs 1e-12). */
+typedef struct dpg_icp_params {
+    int32_t icp_maximum_iterations;              /* 500 */
+    int32_t icp_use_reciprocal_correspondences;  /* 1 */
+    double icp_maximum_transformation_epsilon;   /* 5e-9 */
+    double icp_max_correspondence_distance;      /* 0.6 */
+    int32_t ransac_iterations;                   /* 50 -- inert, as in PCL ICP */
+    int32_t downsample_icp_points_ratio;         /* 5 */
+    float laser_x_variance;                      /* 0.5 */
+    float laser_y_variance;                      /* 0.5 */
+    float laser_theta_variance;                  /* 0.3 */
+    int32_t min_number_correspondences;          /* 3 (pcl::Registration default) */
+    double mse_threshold_absolute;               /* 1e-12 (pcl DefaultConvergenceCriteria) */
+} dpg_icp_params;
+
+/* Per-edge ICP outcome (runIcp's out-param + return value, dpg_slam.cc:433-445). */
+typedef struct dpg_icp_result {
+    float T[6];          /* final transformation, rows: T00 T01 T03 / T10 T11 T13 (z row = e3) */
+    float z[3];          /* measurement (T03, T13, atan2(T10, T00)) -- dpg_slam.cc:434-439 */
+    int32_t converged;   /* icp.hasConverged() (max iterations counts as converged, as in PCL) */
+    int32_t iterations;  /* nr_iterations_ */
+    int32_t n_corr;      /* correspondences of the last iteration */
+    int32_t status;      /* DPG_ICP_* below */
+    int32_t pad;
+    double fitness;      /* MSE of the last iteration's correspondences */
+} dpg_icp_result;
+
+#define DPG_ICP_OK 0
+#define DPG_ICP_TOO_FEW_CORR 1   /* fewer than min_number_correspondences -> converged = 0 */
+#define DPG_ICP_NON_PLANAR 2     /* est_transform(2,2) != 1 (dpg_slam.cc:422-426); never produced by
+                                    the planar closed form, kept for ABI parity */
+
+/* Factors (R9/R10).  info = diagonal information (1/sigma^2 for noiseModel::Diagonal::Sigmas,
+ * 1/variance for noiseModel::Gaussian::Covariance of a diagonal matrix, dpg_slam.cc:335). */
+#define DPG_FACTOR_PRIOR 0
+#define DPG_FACTOR_BETWEEN 1
+typedef struct dpg_factor {
+    int32_t kind;      /* DPG_FACTOR_PRIOR | DPG_FACTOR_BETWEEN */
+    int32_t i;         /* first key (prior: the key) */
+    int32_t j;         /* second key (between) */
+    int32_t pad;
+    double z[3];       /* measured Pose2 (x, y, theta): prior mean or between measurement */
+    double info[3];    /* diagonal information */
+} dpg_factor;          /* 64 bytes */
+
+typedef struct dpg_gn_params {
+    int32_t max_iterations;      /* 100 (GaussNewtonParams.maxIterations, dpg_slam_main.cc:262) */
+    int32_t use_error_criteria;  /* 1: GTSAM checkConvergence on the error; 0: stop on max|delta| */
+    double delta_tol;            /* 1e-10: batch-GN target */
+    double relative_error_tol;   /* 1e-5 (GaussNewtonParams.relativeErrorTol) */
+    double absolute_error_tol;   /* 1e-5 (NonlinearOptimizerParams default) */
+    double pcg_rel_tol;          /* 1e-12: PCG stops when |r| <= tol * |b| */
+    int32_t pcg_max_iterations;  /* 20000 */
+    int32_t pcg_check_every;     /* PCG iterations between host convergence checks (GPU only) */
+} dpg_gn_params;
+
+typedef struct dpg_gn_stats {
+    int32_t iterations;
+    int32_t pcg_iterations;      /* total over all GN iterations */
+    double initial_error;        /* 0.5 * sum ||e||^2_info at the initial values */
+    double final_error;
+    double last_delta_inf;
+    double ms_total;
+    double ms_per_iteration;
+} dpg_gn_stats;
+
+typedef struct dpg_ctx dpg_ctx;
+
+/* ---- library / context ---- */
+const char* dpg_last_error(void);
+const char* dpg_version(void);
+void dpg_icp_params_default(dpg_icp_params* p);
+void dpg_gn_params_default(dpg_gn_params* p);
+/* device = HIP device ordinal; returns NULL (and sets dpg_last_error) when no GPU is usable. */
+dpg_ctx* dpg_ctx_create(int device);
+void dpg_ctx_destroy(dpg_ctx* ctx);
+/* Run all work of this context on an external hipStream_t (e.g. torch's current stream). */
+int dpg_ctx_set_stream(dpg_ctx* ctx, void* hip_stream);
+int dpg_ctx_synchronize(dpg_ctx* ctx);
+
+/* ---- host-side data path helpers (R1-R3, no GPU) ---- */
+/* MeasurementPoint + createNode + getCachedPointCloudFromNode (dpg_measurement.h:41-46,102-104,
+ * dpg_slam.cc:488-513, dpg_node.cc:8-25): polar scan -> base_link cloud, MAX_RANGE dropped.
+ * Returns the number of points written to xy_out (capacity n_ranges points). */
+int64_t dpg_scan_to_cloud(const float* ranges, int64_t n_ranges, float angle_min, float angle_max,
+                          float range_max, float laser_x, float laser_y, float laser_theta,
+                          float* xy_out);
+/* R1 over a scan set: ranges[V][n_beams] -> concatenated clouds, offsets_out[V+1] (capacity
+ * V * n_beams points).  Returns the total number of points. */
+int64_t dpg_scans_to_clouds(const float* ranges, int64_t n_nodes, int64_t n_beams, float angle_min,
+                            float angle_max, float range_max, float laser_x, float laser_y,
+                            float laser_theta, float* xy_out, int64_t* offsets_out);
+/* downsamplePointCloud (dpg_slam.cc:346-360). Returns the number of points written. */
+int64_t dpg_downsample_cloud(const float* xy, int64_t n, int32_t ratio, float* xy_out);
+/* math_utils::inverseTransformPoint (math_utils.cc:21-35): pose of a in b's frame. */
+void dpg_inverse_transform_point(const float a[3], const float b[3], float out[3]);
+/* math_utils::transformPoint (math_utils.cc:6-19). */
+void dpg_transform_point(const float p[3], const float frame[3], float out[3]);
+/* runIcp guess (dpg_slam.cc:364-378): 2x3 float matrix rows (c,-s,tx / s,c,ty). */
+void dpg_icp_guess(const float pose_src[3], const float pose_tgt[3], float guess_out[6]);
+/* R9 factor builders: odometry BetweenFactor with the motion-model sigmas (dpg_slam.cc:53-75),
+ * ICP BetweenFactor with the calculate_ICP_COV diagonal (dpg_slam.cc:331-338). */
+int dpg_odometry_factor(const float odom_prev[3], const float odom_cur[3], int32_t i_prev, int32_t i_cur,
+                        float transl_from_transl, float transl_from_rot, float rot_from_transl,
+                        float rot_from_rot, dpg_factor* out);
+void dpg_icp_factor(const dpg_icp_result* r, int32_t from_node, int32_t to_node,
+                    const dpg_icp_params* p, dpg_factor* out);
+
+/* ---- synthetic workload generator (seeded, deterministic) ---- */
+/* World: axis-aligned rooms + random boxes in [0, world_size]^2; segments [n][4] (x0,y0,x1,y1). */
+int64_t dpg_synth_world(uint64_t seed, float world_size, float* segs_out, int64_t max_segs);
+/* Ground-truth trajectory: 1 m steps with heading noise, collision-free w.r.t. the world. */
+int dpg_synth_trajectory(uint64_t seed, int64_t n_nodes, const float* segs, int64_t n_segs,
+                         float world_size, float step, double* gt_out /*[n][3]*/);
+/* Ray-cast laser scans (laser pose in base_link), Gaussian range noise, >= range_max kept as
+ * range_max (MAX_RANGE).  ranges_out[n_nodes][n_beams]. */
+int dpg_synth_scans(const double* gt, int64_t n_nodes, const float* segs, int64_t n_segs,
+                    int32_t n_beams, float angle_min, float angle_max, float range_max,
+                    float laser_x, float laser_y, float laser_theta, float noise_sigma,
+                    uint64_t seed, int32_t n_threads, float* ranges_out);
+
+/* ---- ICP (runIcp) ---- */
+/* One alignment, mirroring DpgSLAM::runIcp(node_1 = target, node_2 = source, ...).
+ * src_xy / tgt_xy are the FULL base_link clouds of node_2 / node_1 (the ICP downsamples them
+ * by params->downsample_icp_points_ratio; the covariance uses the full clouds, dpg_slam.cc:430).
+ * pose_src / pose_tgt: estimated poses (x, y, theta) of node_2 / node_1.
+ * cov_out (3x3 row-major) receives ICP_COV; hess_out (nullable) the diagnostic [x,y,yaw] block.
+ * Returns DPG_OK; the boolean runIcp result is result->converged && status == DPG_ICP_OK. */
+int dpg_run_icp(dpg_ctx* ctx, const float* src_xy, int64_t n_src, const float* tgt_xy, int64_t n_tgt,
+                const float pose_src[3], const float pose_tgt[3], const dpg_icp_params* params,
+                dpg_icp_result* result, double cov_out[9], double hess_out[9]);
+
+/* Batched, device-resident form (the GPU entry point).
+ * 1) upload all node clouds once: pts_xy = concatenated full clouds, node_offsets[V+1]. */
+int dpg_scans_upload(dpg_ctx* ctx, const float* pts_xy, const int64_t* node_offsets, int64_t n_nodes,
+                     int32_t downsample_ratio);
+/* 2) stage an edge batch: edges[e] = {node_1 (target), node_2 (source)}, poses[V][3] float. */
+int dpg_icp_batch_prepare(dpg_ctx* ctx, const int32_t* edges, int64_t n_edges, const float* poses,
+                          const dpg_icp_params* params);
+/* 3) run ICP (+ covariance block when compute_cov) over the staged edges, asynchronously on the
+ * context stream.  trace_iters > 0 records the per-iteration correspondence indices of every
+ * edge (test mode; see dpg_icp_batch_fetch_trace). */
+int dpg_icp_batch_run(dpg_ctx* ctx, int32_t compute_cov, int32_t trace_iters);
+/* 4) copy results back (any pointer may be NULL). */
+int dpg_icp_batch_fetch(dpg_ctx* ctx, dpg_icp_result* results, double* hess /*[E][9]*/);
+int dpg_icp_batch_fetch_trace(dpg_ctx* ctx, int32_t* trace /*[E][trace_iters][max_src]*/,
+                              int64_t* max_src_out);
+/* Device time of the last ICP / covariance kernels (ms, HIP events on the context stream). */
+float dpg_icp_batch_kernel_ms(dpg_ctx* ctx);
+float dpg_cov_batch_kernel_ms(dpg_ctx* ctx);
+/* Sum over edges of iterations x (8N + 8M + 8N) -- algorithmic bytes of the correspondence
+ * search for the last run, computed on device and copied back. */
+double dpg_icp_batch_algorithmic_bytes(dpg_ctx* ctx);
+
+/* ---- pose-graph Gauss-Newton (optimizeGraph) ---- */
+/* Single call, batch GN to convergence.  poses_inout[V][3] double. */
+int dpg_optimize_graph(dpg_ctx* ctx, double* poses_inout, int64_t n_nodes, const dpg_factor* factors,
+                       int64_t n_factors, const dpg_gn_params* params, dpg_gn_stats* stats);
+
+/* Step API for the edge-sharded multi-GPU solve (one RCCL all-reduce of the packed [H|b|chi2]
+ * buffer per iteration, done by the caller between assemble and solve).
+ * factors: ALL factors of the graph (the sparsity pattern is global); this rank assembles only
+ * factors[shard_begin, shard_end). */
+int dpg_gn_setup(dpg_ctx* ctx, int64_t n_nodes, const dpg_factor* factors, int64_t n_factors,
+                 int64_t shard_begin, int64_t shard_end, const dpg_gn_params* params);
+/* Overwrite the measurement/information of factors [first, first+count) with the ICP batch
+ * results of edges [0, count) of the last dpg_icp_batch_run (device to device).  Edges
+ * [0, n_always) always become factors (successive scans, dpg_slam.cc:85-89); the others only when
+ * the alignment converged (loop closures, dpg_slam.cc:101-104) -- a dropped edge keeps its slot
+ * with zero information, which adds nothing to H, g or the error. */
+int dpg_gn_take_icp_measurements(dpg_ctx* ctx, int64_t first_factor, int64_t count, int64_t n_always,
+                                 const dpg_icp_params* params);
+int64_t dpg_gn_hb_size(dpg_ctx* ctx);   /* doubles in the packed buffer */
+int dpg_gn_set_poses(dpg_ctx* ctx, const double* poses);
+int dpg_gn_get_poses(dpg_ctx* ctx, double* poses);
+/* Linearize the local shard at the current poses into hb_dev (overwritten, not accumulated). */
+int dpg_gn_assemble(dpg_ctx* ctx, double* hb_dev);
+/* Solve (sum of all shards in hb_dev) with PCG and retract.  Blocking: returns max|delta| and
+ * the error 0.5*chi2 at the linearization point. */
+int dpg_gn_solve_retract(dpg_ctx* ctx, const double* hb_dev, double* delta_inf, double* error,
+                         int32_t* pcg_iterations);
+float dpg_gn_last_assemble_ms(dpg_ctx* ctx);
+float dpg_gn_last_solve_ms(dpg_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPG_SLAM_C_H */

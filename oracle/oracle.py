@@ -1,0 +1,194 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes loader for the CPU oracle (oracle/build/liboracle.so).
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the CHECKER (and the
+timed CPU baseline, kind "port"); never by the product path.  See dpg_oracle.h for what is
+pinned by the reference's own known answers and what is unpinned (PCL / GTSAM arithmetic).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+
+NN_BRUTE = 0
+NN_GRID = 1
+
+_L = None
+
+
+def build():
+    subprocess.run(["make", "-C", _HERE], check=True, stdout=subprocess.DEVNULL)
+
+
+def lib():
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        from dpgslam import _abi
+        L = C.CDLL(LIB_PATH)
+        F32P, F64P, I32P, I64P, P = _abi.F32P, _abi.F64P, _abi.I32P, _abi.I64P, C.c_void_p
+        sig = {
+            "oracle_scan_to_cloud": (C.c_int64, [F32P, C.c_int64, C.c_float, C.c_float, C.c_float, C.c_float,
+                                                 C.c_float, C.c_float, F32P]),
+            "oracle_downsample": (C.c_int64, [F32P, C.c_int64, C.c_int32, F32P]),
+            "oracle_inverse_transform_point": (None, [F32P, F32P, F32P]),
+            "oracle_transform_point": (None, [F32P, F32P, F32P]),
+            "oracle_icp_guess": (None, [F32P, F32P, F32P]),
+            "oracle_icp_align": (C.c_int, [F32P, C.c_int64, F32P, C.c_int64, F32P, C.POINTER(_abi.IcpParams),
+                                           C.c_int, C.POINTER(_abi.IcpResult), I32P, C.c_int32]),
+            "oracle_icp_cov": (None, [F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float, C.c_float,
+                                      F64P, F64P]),
+            "oracle_cov_block_literal": (None, [F32P, C.c_int64, F32P, C.c_int64, F32P, F64P]),
+            "oracle_run_icp": (C.c_int, [F32P, C.c_int64, F32P, C.c_int64, F32P, F32P, C.POINTER(_abi.IcpParams),
+                                         C.c_int, C.POINTER(_abi.IcpResult), F64P, F64P]),
+            "oracle_icp_batch": (C.c_int, [F32P, I64P, C.c_int64, I32P, C.c_int64, F32P, C.POINTER(_abi.IcpParams),
+                                           C.c_int, C.c_int, P, F64P]),
+            "oracle_linearize": (None, [P, F64P, F64P, F64P, F64P]),
+            "oracle_graph_error": (C.c_double, [F64P, P, C.c_int64]),
+            "oracle_optimize_graph": (C.c_int, [F64P, C.c_int64, P, C.c_int64, C.POINTER(_abi.GnParams),
+                                                C.POINTER(_abi.GnStats)]),
+            "oracle_gn_delta": (C.c_int, [F64P, C.c_int64, P, C.c_int64, F64P, F64P]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _L = L
+    return _L
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(C.POINTER(t))
+
+
+def _f32(a):
+    return np.ascontiguousarray(np.asarray(a, np.float32))
+
+
+def scan_to_cloud(ranges, amin, amax, rmax, laser=(0.2, 0.0, 0.0)):
+    r = _f32(ranges)
+    out = np.empty((max(r.size, 1), 2), np.float32)
+    n = lib().oracle_scan_to_cloud(_p(r, C.c_float), r.size, amin, amax, rmax, *laser, _p(out, C.c_float))
+    return out[:n].copy()
+
+
+def downsample(cloud, ratio):
+    c = _f32(cloud).reshape(-1, 2)
+    out = np.empty((max(len(c), 1), 2), np.float32)
+    n = lib().oracle_downsample(_p(c, C.c_float), len(c), ratio, _p(out, C.c_float))
+    return out[:n].copy()
+
+
+def inverse_transform_point(a, b):
+    a, b, o = _f32(a), _f32(b), np.empty(3, np.float32)
+    lib().oracle_inverse_transform_point(_p(a, C.c_float), _p(b, C.c_float), _p(o, C.c_float))
+    return o
+
+
+def transform_point(p, f):
+    p, f, o = _f32(p), _f32(f), np.empty(3, np.float32)
+    lib().oracle_transform_point(_p(p, C.c_float), _p(f, C.c_float), _p(o, C.c_float))
+    return o
+
+
+def icp_guess(ps, pt):
+    a, b, o = _f32(ps), _f32(pt), np.empty(6, np.float32)
+    lib().oracle_icp_guess(_p(a, C.c_float), _p(b, C.c_float), _p(o, C.c_float))
+    return o
+
+
+def icp_align(src_ds, tgt_ds, guess, params=None, nn=NN_BRUTE, trace_iters=0):
+    """PCL ICP align on downsampled clouds. Returns (IcpResult, trace [iters, n_src] or None)."""
+    from dpgslam import _abi
+    p = params or _abi.default_icp_params()
+    s, t, g = _f32(src_ds).reshape(-1, 2), _f32(tgt_ds).reshape(-1, 2), _f32(guess)
+    res = _abi.IcpResult()
+    tr = np.full((trace_iters, len(s)), -1, np.int32) if trace_iters else None
+    lib().oracle_icp_align(_p(s, C.c_float), len(s), _p(t, C.c_float), len(t), _p(g, C.c_float), C.byref(p), nn,
+                           C.byref(res), _p(tr, C.c_int32), trace_iters)
+    return res, tr
+
+
+def icp_cov(data, model, T6, vx=0.5, vy=0.5, vth=0.3, literal=False):
+    d, m, T = _f32(data).reshape(-1, 2), _f32(model).reshape(-1, 2), _f32(T6)
+    cov, hess = np.zeros(9), np.zeros(9)
+    if literal:
+        lib().oracle_cov_block_literal(_p(d, C.c_float), len(d), _p(m, C.c_float), len(m), _p(T, C.c_float),
+                                       _p(hess, C.c_double))
+        return None, hess.reshape(3, 3)
+    lib().oracle_icp_cov(_p(d, C.c_float), len(d), _p(m, C.c_float), len(m), _p(T, C.c_float), vx, vy, vth,
+                         _p(cov, C.c_double), _p(hess, C.c_double))
+    return cov.reshape(3, 3), hess.reshape(3, 3)
+
+
+def run_icp(src_full, tgt_full, pose_src, pose_tgt, params=None, nn=NN_GRID):
+    from dpgslam import _abi
+    p = params or _abi.default_icp_params()
+    s, t = _f32(src_full).reshape(-1, 2), _f32(tgt_full).reshape(-1, 2)
+    a, b = _f32(pose_src), _f32(pose_tgt)
+    res = _abi.IcpResult()
+    cov, hess = np.zeros(9), np.zeros(9)
+    lib().oracle_run_icp(_p(s, C.c_float), len(s), _p(t, C.c_float), len(t), _p(a, C.c_float), _p(b, C.c_float),
+                         C.byref(p), nn, C.byref(res), _p(cov, C.c_double), _p(hess, C.c_double))
+    return res, cov.reshape(3, 3), hess.reshape(3, 3)
+
+
+def icp_batch(pts, offsets, edges, poses, params=None, nn=NN_GRID, threads=1):
+    from dpgslam import _abi
+    p = params or _abi.default_icp_params()
+    pts, offs = _f32(pts).reshape(-1, 2), np.ascontiguousarray(offsets, np.int64)
+    e = np.ascontiguousarray(edges, np.int32).reshape(-1, 2)
+    ps = _f32(poses).reshape(-1, 3)
+    res = np.zeros(len(e), _abi.RESULT_DTYPE)
+    hess = np.zeros((len(e), 9))
+    lib().oracle_icp_batch(_p(pts, C.c_float), _p(offs, C.c_int64), len(offs) - 1, _p(e, C.c_int32), len(e),
+                           _p(ps, C.c_float), C.byref(p), nn, threads, C.c_void_p(res.ctypes.data),
+                           _p(hess, C.c_double))
+    return res, hess.reshape(-1, 3, 3)
+
+
+def linearize(factor, poses):
+    from dpgslam import _abi
+    f = np.ascontiguousarray(np.asarray(factor, _abi.FACTOR_DTYPE).reshape(1))
+    X = np.ascontiguousarray(poses, np.float64)
+    e, Ai, Aj = np.zeros(3), np.zeros(9), np.zeros(9)
+    lib().oracle_linearize(C.c_void_p(f.ctypes.data), _p(X, C.c_double), _p(e, C.c_double), _p(Ai, C.c_double),
+                           _p(Aj, C.c_double))
+    return e, Ai.reshape(3, 3), Aj.reshape(3, 3)
+
+
+def graph_error(poses, factors):
+    from dpgslam import _abi
+    X = np.ascontiguousarray(poses, np.float64)
+    F = np.ascontiguousarray(factors, _abi.FACTOR_DTYPE)
+    return lib().oracle_graph_error(_p(X, C.c_double), C.c_void_p(F.ctypes.data), len(F))
+
+
+def optimize_graph(poses, factors, params=None):
+    from dpgslam import _abi
+    X = np.ascontiguousarray(poses, np.float64).reshape(-1, 3).copy()
+    F = np.ascontiguousarray(factors, _abi.FACTOR_DTYPE)
+    gp = params or _abi.default_gn_params()
+    st = _abi.GnStats()
+    rc = lib().oracle_optimize_graph(_p(X, C.c_double), len(X), C.c_void_p(F.ctypes.data), len(F), C.byref(gp),
+                                     C.byref(st))
+    if rc:
+        raise RuntimeError(f"oracle_optimize_graph failed ({rc})")
+    return X, st
+
+
+def gn_delta(poses, factors):
+    from dpgslam import _abi
+    X = np.ascontiguousarray(poses, np.float64).reshape(-1, 3)
+    F = np.ascontiguousarray(factors, _abi.FACTOR_DTYPE)
+    d, err = np.zeros(X.size), C.c_double(0)
+    rc = lib().oracle_gn_delta(_p(X, C.c_double), len(X), C.c_void_p(F.ctypes.data), len(F), _p(d, C.c_double),
+                               C.byref(err))
+    if rc:
+        raise RuntimeError(f"oracle_gn_delta failed ({rc})")
+    return d.reshape(-1, 3), err.value
