@@ -1,0 +1,116 @@
+"""Edge-sharded multi-GPU driver: one process per GPU, torch.distributed (RCCL over xGMI on the
+"nccl" backend) for the single collective of the path.
+
+  ICP:  edges are independent -> rank r aligns its contiguous, cost-balanced edge range; no
+        collective (every rank holds all scans).
+  GN:   every rank holds the whole factor list (the sparsity pattern is global) but linearizes
+        only its shard: rank 0 the prior + odometry factors and its ICP edges, rank r > 0 its ICP
+        edges.  Per GN iteration ONE all-reduce(sum, fp64) of the packed [H upper | g | chi2]
+        buffer, then every rank runs the identical deterministic PCG + retraction (replicated
+        solve), so poses stay bitwise consistent without a broadcast.
+
+The GN loop is written against a small backend protocol so the orchestration can be exercised on
+CPU with the gloo backend (tests/test_dist_cpu.py); the GPU backend is `DeviceBackend`.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def shard_ranges(n: int, world: int, weights: np.ndarray | None = None) -> list[tuple[int, int]]:
+    """Contiguous ranges [b, e) covering [0, n), balanced by cumulative weight."""
+    if world <= 1 or n == 0:
+        return [(0, n)] + [(n, n)] * max(0, world - 1)
+    w = np.ones(n) if weights is None else np.asarray(weights, np.float64)
+    c = np.concatenate([[0.0], np.cumsum(w)])
+    cuts = [0]
+    for r in range(1, world):
+        cuts.append(int(np.searchsorted(c, c[-1] * r / world, side="left")))
+    cuts.append(n)
+    cuts = np.maximum.accumulate(np.clip(cuts, 0, n))
+    return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
+
+
+@dataclass
+class ShardPlan:
+    rank: int
+    world: int
+    edge_range: tuple[int, int]      # ICP edges of this rank
+    factor_range: tuple[int, int]    # factors this rank linearizes
+    n_always_local: int              # successive edges among this rank's edges
+
+
+def plan(rank: int, world: int, n_edges: int, n_successive: int, icp_factor_first: int,
+         edge_cost: np.ndarray | None = None) -> ShardPlan:
+    er = shard_ranges(n_edges, world, edge_cost)[rank]
+    fb = 0 if rank == 0 else icp_factor_first + er[0]
+    fe = icp_factor_first + er[1]
+    n_alw = int(np.clip(n_successive - er[0], 0, er[1] - er[0]))
+    return ShardPlan(rank, world, er, (fb, fe), n_alw)
+
+
+def check_convergence(rel_tol: float, abs_tol: float, cur: float, new: float) -> bool:
+    """GTSAM checkConvergence with errorTol = 0 (NonlinearOptimizer.cpp)."""
+    if new <= 0.0:
+        return True
+    dec = cur - new
+    return (rel_tol != 0.0 and dec / cur <= rel_tol) or dec <= abs_tol
+
+
+def gn_loop(backend, allreduce, params) -> dict:
+    """Batch Gauss-Newton with one all-reduce per iteration (mirrors dpg_optimize_graph).
+
+    backend: assemble(hb), chi2(hb) -> float, solve_retract(hb) -> (dinf, err, pcg_it), new_hb()
+    allreduce(hb): in-place sum over ranks (identity for one rank)."""
+    hb = backend.new_hb()
+    backend.assemble(hb)
+    allreduce(hb)
+    cur = backend.chi2(hb)
+    stats = {"iterations": 0, "pcg_iterations": 0, "initial_error": cur, "final_error": cur, "last_delta_inf": 0.0}
+    if cur <= 0.0 or params.max_iterations <= 0:
+        return stats
+    it = 0
+    while True:
+        dinf, _, pit = backend.solve_retract(hb)
+        it += 1
+        stats["pcg_iterations"] += pit
+        backend.assemble(hb)
+        allreduce(hb)
+        new = backend.chi2(hb)
+        stats.update(iterations=it, final_error=new, last_delta_inf=dinf)
+        if it >= params.max_iterations:
+            break
+        if params.use_error_criteria:
+            if check_convergence(params.relative_error_tol, params.absolute_error_tol, cur, new) or not np.isfinite(cur):
+                break
+        elif dinf < params.delta_tol:
+            break
+        cur = new
+    return stats
+
+
+class DeviceBackend:
+    """GN backend on one GPU: libdpg step API + a torch-owned packed buffer (so torch.distributed
+    can all-reduce it in place with RCCL)."""
+
+    def __init__(self, ctx, hb_size: int, chi2_index: int, device):
+        import torch
+        self.ctx = ctx
+        self.n = hb_size
+        self.chi2_index = chi2_index
+        self.device = device
+        self.torch = torch
+
+    def new_hb(self):
+        return self.torch.zeros(self.n, dtype=self.torch.float64, device=self.device)
+
+    def assemble(self, hb):
+        self.ctx.gn_assemble(hb.data_ptr())
+
+    def chi2(self, hb) -> float:
+        return float(hb[self.chi2_index].item())
+
+    def solve_retract(self, hb):
+        return self.ctx.gn_solve_retract(hb.data_ptr())

@@ -933,3 +933,31 @@ int oracle_optimize_graph(double* X, int64_t n, const dpg_factor* f, int64_t nf,
     sys_free(&S);
     return rc;
 }
+
+/* Symbolic statistics of the block Cholesky (min-degree): out = {nnz blocks of L (off-diagonal),
+ * max column count, flop estimate, elimination-tree height}. Diagnostics for solver design. */
+int oracle_symbolic_stats(int64_t n, const dpg_factor* f, int64_t nf, double out[4]) {
+    sym_t Y;
+    if (sym_analyze(&Y, n, f, nf)) return -1;
+    double flops = 0.0;
+    int64_t mx = 0;
+    int64_t* height = (int64_t*)calloc((size_t)n, sizeof(int64_t));
+    int64_t hmax = 0;
+    for (int64_t p = 0; p < n; ++p) {
+        int64_t c = Y.cptr[p + 1] - Y.cptr[p];
+        if (c > mx) mx = c;
+        flops += 27.0 * (double)(c + 1) * (double)(c + 1);
+        if (c > 0) {   /* parent = first row of the column */
+            int64_t par = Y.pos[Y.crow[Y.cptr[p]]];
+            if (height[p] + 1 > height[par]) height[par] = height[p] + 1;
+        }
+        if (height[p] > hmax) hmax = height[p];
+    }
+    out[0] = (double)Y.cptr[n];
+    out[1] = (double)mx;
+    out[2] = flops;
+    out[3] = (double)hmax;
+    free(height);
+    sym_free(&Y);
+    return 0;
+}
