@@ -1,0 +1,226 @@
+// dpg_chol_sym.cpp -- symbolic analysis of the block-sparse pose-graph system for the GPU
+// supernodal multifrontal Cholesky (the CHOLESKY linear solver GTSAM runs inside
+// ISAM2 / GaussNewtonOptimizer).  Host code, run once per sparsity pattern
+// (dpg_gn_setup); the numeric factorization and solves are in dpg_chol.hip.
+//
+//   1. fill-reducing order: minimum degree on the 3x3-block graph (bitset elimination graphs,
+//      ties -> lowest node index)
+//   2. column structure of L and the elimination tree
+//   3. fundamental supernodes, merged further while the added explicit zeros stay small
+//      (relaxed amalgamation), and the supernodal elimination tree
+//   4. level schedule (leaves = level 0) and the maps the GPU kernels need: original H blocks
+//      -> front positions, child update matrix rows -> parent front rows
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "dpg_chol.h"
+
+namespace {
+
+// Minimum-degree ordering over the block graph.  adjacency: CSR of the symmetric graph without
+// self loops.  Returns perm (elimination order) and the L column patterns (later nodes, by pos).
+void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<int32_t>& adj,
+                std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pattern) {
+    const int64_t W = (n + 63) / 64;
+    std::vector<uint64_t> bits((size_t)(n * W), 0ull);
+    for (int64_t v = 0; v < n; ++v)
+        for (int64_t q = aptr[v]; q < aptr[v + 1]; ++q) {
+            const int32_t u = adj[(size_t)q];
+            bits[(size_t)(v * W + u / 64)] |= 1ull << (u % 64);
+        }
+    std::vector<int32_t> deg((size_t)n);
+    for (int64_t v = 0; v < n; ++v) deg[(size_t)v] = (int32_t)(aptr[v + 1] - aptr[v]);
+    std::vector<char> done((size_t)n, 0);
+    perm.assign((size_t)n, -1);
+    pattern.assign((size_t)n, {});
+    std::vector<int32_t> nb;
+    nb.reserve(1024);
+    // degree buckets would be faster; n is a few thousand, a linear scan is fine (once per pattern)
+    for (int64_t p = 0; p < n; ++p) {
+        int32_t v = -1, best = INT32_MAX;
+        for (int64_t u = 0; u < n; ++u)
+            if (!done[(size_t)u] && deg[(size_t)u] < best) { best = deg[(size_t)u]; v = (int32_t)u; }
+        done[(size_t)v] = 1;
+        perm[(size_t)p] = v;
+        nb.clear();
+        const uint64_t* bv = &bits[(size_t)(v * W)];
+        for (int64_t w = 0; w < W; ++w) {
+            uint64_t b = bv[w];
+            while (b) {
+                const int t = __builtin_ctzll(b);
+                b &= b - 1;
+                nb.push_back((int32_t)(w * 64 + t));
+            }
+        }
+        pattern[(size_t)p] = nb;   // node ids; converted to positions after the ordering is known
+        for (int32_t u : nb) {
+            uint64_t* bu = &bits[(size_t)(u * W)];
+            for (int64_t w = 0; w < W; ++w) bu[w] |= bv[w];
+            bu[u / 64] &= ~(1ull << (u % 64));
+            bu[v / 64] &= ~(1ull << (v % 64));
+        }
+        for (int32_t u : nb) {
+            const uint64_t* bu = &bits[(size_t)(u * W)];
+            int32_t d = 0;
+            for (int64_t w = 0; w < W; ++w) d += __builtin_popcountll(bu[w]);
+            deg[(size_t)u] = d;
+        }
+        memset(&bits[(size_t)(v * W)], 0, sizeof(uint64_t) * (size_t)W);
+    }
+}
+
+}  // namespace
+
+int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                      const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    if (n <= 0) return -1;
+    // ---- graph
+    std::vector<int64_t> aptr((size_t)n + 1, 0);
+    for (int64_t p = 0; p < n_pairs; ++p) { aptr[(size_t)pair_lo[p] + 1]++; aptr[(size_t)pair_hi[p] + 1]++; }
+    for (int64_t v = 0; v < n; ++v) aptr[(size_t)v + 1] += aptr[(size_t)v];
+    std::vector<int32_t> adj((size_t)aptr[(size_t)n]);
+    {
+        std::vector<int64_t> cur(aptr.begin(), aptr.end() - 1);
+        for (int64_t p = 0; p < n_pairs; ++p) {
+            adj[(size_t)cur[(size_t)pair_lo[p]]++] = pair_hi[p];
+            adj[(size_t)cur[(size_t)pair_hi[p]]++] = pair_lo[p];
+        }
+    }
+    // ---- ordering + column patterns (in positions)
+    std::vector<int32_t> perm;
+    std::vector<std::vector<int32_t>> pat;
+    min_degree(n, aptr, adj, perm, pat);
+    std::vector<int32_t> pos((size_t)n);
+    for (int64_t p = 0; p < n; ++p) pos[(size_t)perm[(size_t)p]] = (int32_t)p;
+    for (int64_t p = 0; p < n; ++p) {
+        for (int32_t& u : pat[(size_t)p]) u = pos[(size_t)u];
+        std::sort(pat[(size_t)p].begin(), pat[(size_t)p].end());
+    }
+    std::vector<int32_t> parent((size_t)n, -1), nchild((size_t)n, 0);
+    for (int64_t p = 0; p < n; ++p)
+        if (!pat[(size_t)p].empty()) { parent[(size_t)p] = pat[(size_t)p][0]; nchild[(size_t)parent[(size_t)p]]++; }
+    // ---- fundamental supernodes, then relaxed merging of chains
+    // column p+1 joins p's supernode when p's only parent is p+1, p is p+1's only child and the
+    // patterns nest (fundamental), or when the explicit zeros added stay within the budget.
+    std::vector<int32_t> sn_first;   // first column of each supernode
+    std::vector<int32_t> sn_of((size_t)n);
+    const int32_t max_cols = opts && opts->max_supernode_cols > 0 ? opts->max_supernode_cols : 64;
+    const double relax = opts ? opts->relax_fraction : 0.0;
+    {
+        int32_t s = -1;
+        int64_t zeros = 0, cols = 0;
+        for (int64_t p = 0; p < n; ++p) {
+            bool join = false;
+            if (p > 0 && s >= 0) {
+                const int64_t q = p - 1;
+                const bool chain = parent[(size_t)q] == (int32_t)p && nchild[(size_t)p] == 1;
+                const int64_t cq = (int64_t)pat[(size_t)q].size(), cp = (int64_t)pat[(size_t)p].size();
+                const int64_t ncols = p - sn_first[(size_t)s] + 1;
+                if (chain && ncols <= max_cols) {
+                    if (cq == cp + 1) join = true;   // fundamental
+                    else if (relax > 0.0) {
+                        // every earlier column of the supernode would carry p's pattern: the rows
+                        // of pat[p] missing from pat[q] \ {p} become explicit zeros in them
+                        const int64_t add = std::max<int64_t>(0, cp - (cq - 1)) * cols;
+                        if ((double)(zeros + add) <= relax * (double)((cols + 1) * (cp + 1))) { join = true; zeros += add; }
+                    }
+                }
+            }
+            if (!join) { sn_first.push_back((int32_t)p); ++s; zeros = 0; cols = 0; }
+            sn_of[(size_t)p] = s;
+            ++cols;
+        }
+    }
+    const int32_t ns = (int32_t)sn_first.size();
+    sn_first.push_back((int32_t)n);
+    // ---- supernode row sets: union of its columns' patterns beyond its last column
+    S->n = n;
+    S->ns = ns;
+    S->perm.assign(perm.begin(), perm.end());
+    S->pos.assign(pos.begin(), pos.end());
+    S->sn_c0.assign(sn_first.begin(), sn_first.end());
+    S->sn_rows_ptr.assign((size_t)ns + 1, 0);
+    S->sn_rows.clear();
+    S->sn_parent.assign((size_t)ns, -1);
+    for (int32_t s = 0; s < ns; ++s) {
+        const int32_t c0 = sn_first[(size_t)s], c1 = sn_first[(size_t)s + 1];
+        std::vector<int32_t> rows;
+        for (int32_t c = c0; c < c1; ++c)
+            for (int32_t r : pat[(size_t)c])
+                if (r >= c1) rows.push_back(r);
+        std::sort(rows.begin(), rows.end());
+        rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
+        S->sn_rows.insert(S->sn_rows.end(), rows.begin(), rows.end());
+        S->sn_rows_ptr[(size_t)s + 1] = (int64_t)S->sn_rows.size();
+        if (!rows.empty()) S->sn_parent[(size_t)s] = sn_of[(size_t)rows[0]];
+    }
+    S->sn_of.assign(sn_of.begin(), sn_of.end());
+    // ---- levels
+    S->sn_level.assign((size_t)ns, 0);
+    for (int32_t s = 0; s < ns; ++s) {   // children precede parents in elimination order
+        const int32_t p = S->sn_parent[(size_t)s];
+        if (p >= 0) S->sn_level[(size_t)p] = std::max(S->sn_level[(size_t)p], S->sn_level[(size_t)s] + 1);
+    }
+    int32_t nl = 0;
+    for (int32_t s = 0; s < ns; ++s) nl = std::max(nl, S->sn_level[(size_t)s] + 1);
+    S->n_levels = nl;
+    S->level_ptr.assign((size_t)nl + 1, 0);
+    for (int32_t s = 0; s < ns; ++s) S->level_ptr[(size_t)S->sn_level[(size_t)s] + 1]++;
+    for (int32_t l = 0; l < nl; ++l) S->level_ptr[(size_t)l + 1] += S->level_ptr[(size_t)l];
+    S->level_list.assign((size_t)ns, 0);
+    {
+        std::vector<int32_t> cur(S->level_ptr.begin(), S->level_ptr.end() - 1);
+        for (int32_t s = 0; s < ns; ++s) S->level_list[(size_t)cur[(size_t)S->sn_level[(size_t)s]]++] = s;
+    }
+    // ---- children lists and relative maps (child update rows -> parent front index)
+    S->child_ptr.assign((size_t)ns + 1, 0);
+    for (int32_t s = 0; s < ns; ++s)
+        if (S->sn_parent[(size_t)s] >= 0) S->child_ptr[(size_t)S->sn_parent[(size_t)s] + 1]++;
+    for (int32_t s = 0; s < ns; ++s) S->child_ptr[(size_t)s + 1] += S->child_ptr[(size_t)s];
+    S->child_list.assign((size_t)S->child_ptr[(size_t)ns], 0);
+    {
+        std::vector<int64_t> cur(S->child_ptr.begin(), S->child_ptr.end() - 1);
+        for (int32_t s = 0; s < ns; ++s)
+            if (S->sn_parent[(size_t)s] >= 0) S->child_list[(size_t)cur[(size_t)S->sn_parent[(size_t)s]]++] = s;
+    }
+    S->relmap.assign(S->sn_rows.size(), 0);
+    for (int32_t s = 0; s < ns; ++s) {
+        const int32_t p = S->sn_parent[(size_t)s];
+        if (p < 0) continue;
+        const int32_t pc0 = sn_first[(size_t)p], pk = sn_first[(size_t)p + 1] - pc0;
+        const int32_t* prow = S->sn_rows.data() + S->sn_rows_ptr[(size_t)p];
+        const int64_t pr = S->sn_rows_ptr[(size_t)p + 1] - S->sn_rows_ptr[(size_t)p];
+        for (int64_t t = S->sn_rows_ptr[(size_t)s]; t < S->sn_rows_ptr[(size_t)s + 1]; ++t) {
+            const int32_t row = S->sn_rows[(size_t)t];
+            int32_t li;
+            if (row < pc0 + pk) {
+                li = row - pc0;
+                if (li < 0) return -2;   // child rows must lie in the parent's front
+            } else {
+                const int32_t* it = std::lower_bound(prow, prow + pr, row);
+                if (it == prow + pr || *it != row) return -2;
+                li = pk + (int32_t)(it - prow);
+            }
+            S->relmap[(size_t)t] = li;
+        }
+    }
+    // ---- front offsets (doubles), stats
+    S->front_off.assign((size_t)ns + 1, 0);
+    double flops = 0.0;
+    int32_t maxm = 0;
+    for (int32_t s = 0; s < ns; ++s) {
+        const int64_t k = sn_first[(size_t)s + 1] - sn_first[(size_t)s];
+        const int64_t r = S->sn_rows_ptr[(size_t)s + 1] - S->sn_rows_ptr[(size_t)s];
+        const int64_t m3 = 3 * (k + r);
+        S->front_off[(size_t)s + 1] = S->front_off[(size_t)s] + m3 * m3;
+        maxm = std::max<int32_t>(maxm, (int32_t)(k + r));
+        const double k3 = 3.0 * (double)k, r3 = 3.0 * (double)r;
+        flops += k3 * k3 * k3 / 3.0 + k3 * k3 * r3 + k3 * r3 * r3;
+    }
+    S->max_front = maxm;
+    S->flops = flops;
+    return 0;
+}

@@ -296,15 +296,17 @@ __global__ void pcg_update_kernel(int it, int64_t n, const double* __restrict__ 
     if (threadIdx.x == 0) { part_rz_out[blockIdx.x] = rz_n; part_rr[blockIdx.x] = rr; }
 }
 
-// X <- X * Pose2(d); partial max |d|
+// X <- X * Pose2(d); partial max |d|.  d is indexed by node, or by elimination position when
+// pos != NULL (the Cholesky's solution vector).
 __global__ void retract_kernel(double* __restrict__ X, const double* __restrict__ d, int64_t n,
-                               double* __restrict__ part_max) {
+                               const int32_t* __restrict__ pos, double* __restrict__ part_max) {
     __shared__ double red[16];
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double m = 0.0;
     if (v < n) {
+        const int64_t di = 3 * (int64_t)(pos ? pos[v] : v);
         const double c = cos(X[3 * v + 2]), s = sin(X[3 * v + 2]);
-        const double d0 = d[3 * v], d1 = d[3 * v + 1], d2 = d[3 * v + 2];
+        const double d0 = d[di], d1 = d[di + 1], d2 = d[di + 2];
         const double cd = cos(d2), sd = sin(d2);
         const double nx = X[3 * v] + (c * d0 - s * d1);
         const double ny = X[3 * v + 1] + (s * d0 + c * d1);
@@ -367,6 +369,7 @@ extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
                     g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (g->chol) dpg_chol_destroy(g->chol);
     memset(g, 0, sizeof(*g));
 }
 
@@ -467,6 +470,11 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     rc |= up(g->colidx, colidx);
     rc |= up(g->src_up, srcup);
     if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
+    // symbolic analysis + device structures of the supernodal Cholesky (once per pattern)
+    std::vector<int32_t> plo((size_t)P), phi((size_t)P);
+    for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)pairs[(size_t)p].first; phi[(size_t)p] = (int32_t)pairs[(size_t)p].second; }
+    rc = dpg_chol_create(&g->chol, n, plo.data(), phi.data(), P);
+    if (rc) g->chol = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
     return DPG_OK;
 }
 
@@ -490,6 +498,8 @@ extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
+static int pcg_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, hipStream_t s);
+
 extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, void* stream,
                                 double* delta_inf, double* error, int32_t* pcg_iters) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -500,6 +510,47 @@ extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_pa
     double* part_rr = g->partials + 2 * (size_t)nb;
     double* part_pq = g->partials + 3 * (size_t)nb;
     double* part_max = g->partials + 4 * (size_t)nb;
+    int it = 0;
+    const double* xout = g->x;
+    const int32_t* xpos = nullptr;
+    int32_t chol_status = 0;
+    if (gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol) {
+        const int rc = dpg_chol_solve(g->chol, hb, stream);
+        if (rc) return rc;
+        xout = dpg_chol_x_dev(g->chol);
+        xpos = dpg_chol_pos_dev(g->chol);
+        if (hipMemcpyAsync(&chol_status, dpg_chol_status_dev(g->chol), sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+            return DPG_ERR_HIP;
+    } else {
+        it = pcg_solve(g, hb, gp, s);
+        if (it < 0) return DPG_ERR_HIP;
+    }
+    hipLaunchKernelGGL(retract_kernel, dim3(nb), dim3(kRowThreads), 0, s, g->poses, xout, n, xpos, part_max);
+    std::vector<double> pm((size_t)nb);
+    double chi2 = 0.0;
+    if (hipMemcpyAsync(pm.data(), part_max, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&chi2, hb + 9 * g->nnzb_upper + 3 * n, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return DPG_ERR_HIP;
+    if (chol_status) return DPG_ERR_NUMERIC;   // H not positive definite
+    double mx = 0.0;
+    for (double v : pm) mx = std::max(mx, v);
+    if (delta_inf) *delta_inf = mx;
+    if (error) *error = chi2;
+    if (pcg_iters) *pcg_iters = it;
+    (void)part_rz_a; (void)part_rz_b; (void)part_rr; (void)part_pq;
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+// block-Jacobi PCG on the full BSR; returns the iteration count (< 0 on a HIP error)
+static int pcg_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, hipStream_t s) {
+    const int nb = g->n_blocks_rows;
+    const int64_t n = g->n_nodes;
+    double* part_rz_a = g->partials;
+    double* part_rz_b = g->partials + nb;
+    double* part_rr = g->partials + 2 * (size_t)nb;
+    double* part_pq = g->partials + 3 * (size_t)nb;
     hipLaunchKernelGGL(pcg_init_kernel, dim3(nb), dim3(kRowThreads), 0, s, hb, g->rowptr, g->src_up, n, g->nnzb_upper,
                        g->bsr, g->minv, g->x, g->r, g->z, g->p0, part_rz_a, part_rr);
     double host_scal[2] = {0, 0};
@@ -510,7 +561,6 @@ extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_pa
     int it = 0;
     double* pbuf[2] = {g->p0, g->p1};
     double* rzbuf[2] = {part_rz_a, part_rz_b};
-    double* xout = g->x;
     for (; it < max_it; ++it) {
         double* p_old = pbuf[it & 1];
         double* p_new = pbuf[(it + 1) & 1];
@@ -519,24 +569,12 @@ extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_pa
         if (it % check == 0) {
             if (hipMemcpyAsync(host_scal, g->scal + 2 * it, 2 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess)
-                return DPG_ERR_HIP;
+                return -1;
             if (rr0 < 0) rr0 = host_scal[1];
             if (!(host_scal[1] > tol2 * rr0) || !(rr0 > 0)) break;   // converged (or zero rhs)
         }
         hipLaunchKernelGGL(pcg_update_kernel, dim3(nb), dim3(kRowThreads), 0, s, it, n, g->minv, p_new, g->q, g->x,
                            g->r, g->z, rzbuf[it & 1], part_pq, rzbuf[(it + 1) & 1], part_rr, nb);
     }
-    hipLaunchKernelGGL(retract_kernel, dim3(nb), dim3(kRowThreads), 0, s, g->poses, xout, n, part_max);
-    std::vector<double> pm((size_t)nb);
-    double chi2 = 0.0;
-    if (hipMemcpyAsync(pm.data(), part_max, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&chi2, hb + 9 * g->nnzb_upper + 3 * n, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipStreamSynchronize(s) != hipSuccess)
-        return DPG_ERR_HIP;
-    double mx = 0.0;
-    for (double v : pm) mx = std::max(mx, v);
-    if (delta_inf) *delta_inf = mx;
-    if (error) *error = chi2;
-    if (pcg_iters) *pcg_iters = it;
-    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+    return it;
 }

@@ -72,9 +72,20 @@ typedef struct dpg_gn_dev {
     double* partials;              /* PCG per-block partial sums */
     double* scal;                  /* PCG scalars */
     double* hb_own;                /* packed [H upper | b | chi2] buffer for single-GPU solves */
+    void* chol;                    /* supernodal Cholesky (dpg_chol.hip), NULL if analysis failed */
     int32_t n_blocks_rows;         /* grid size for row kernels */
     int32_t pad;
 } dpg_gn_dev;
+
+/* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip). */
+int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+void dpg_chol_destroy(void* chol);
+/* factor H (upper blocks of hb) and solve H x = -g; x (block positions) stays on device */
+int dpg_chol_solve(void* chol, const double* hb, void* stream);
+const int32_t* dpg_chol_pos_dev(void* chol);
+const double* dpg_chol_x_dev(void* chol);
+const int32_t* dpg_chol_status_dev(void* chol);
+void dpg_chol_stats(void* chol, double out[6]);
 
 int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n_nodes, const dpg_factor* factors, int64_t n_factors,
                      int64_t shard_begin, int64_t shard_end);

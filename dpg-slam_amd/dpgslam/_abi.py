@@ -74,7 +74,13 @@ class GnParams(C.Structure):
         ("pcg_rel_tol", C.c_double),
         ("pcg_max_iterations", C.c_int32),
         ("pcg_check_every", C.c_int32),
+        ("linear_solver", C.c_int32),
+        ("pad", C.c_int32),
     ]
+
+
+DPG_SOLVER_CHOLESKY = 0
+DPG_SOLVER_PCG = 1
 
 
 class GnStats(C.Structure):

@@ -94,7 +94,12 @@ typedef struct dpg_gn_params {
     double pcg_rel_tol;          /* 1e-12: PCG stops when |r| <= tol * |b| */
     int32_t pcg_max_iterations;  /* 20000 */
     int32_t pcg_check_every;     /* PCG iterations between host convergence checks (GPU only) */
+    int32_t linear_solver;       /* DPG_SOLVER_CHOLESKY (default, GTSAM's CHOLESKY) | DPG_SOLVER_PCG */
+    int32_t pad;
 } dpg_gn_params;
+
+#define DPG_SOLVER_CHOLESKY 0    /* supernodal multifrontal Cholesky on the GPU */
+#define DPG_SOLVER_PCG 1         /* block-Jacobi preconditioned CG on the GPU */
 
 typedef struct dpg_gn_stats {
     int32_t iterations;

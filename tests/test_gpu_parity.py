@@ -112,9 +112,12 @@ def test_gtsam_test_graph_gpu():
             assert np.abs(pose_diff(X, X_opt)).max() < 1e-9, (crit, X)
 
 
+@pytest.mark.parametrize("solver", [0, 1], ids=["cholesky", "pcg"])
 @pytest.mark.parametrize("name", ["config2", "config3"])
-def test_gn_matches_oracle(ctx, workload, name):
-    """Batch GN on the GPU (PCG) vs the oracle's block-sparse Cholesky GN: poses within 1e-6."""
+def test_gn_matches_oracle(ctx, workload, name, solver):
+    """Batch GN on the GPU (supernodal Cholesky, or PCG) vs the oracle's block-sparse Cholesky GN:
+    poses within 1e-6."""
+    from dpgslam import _abi
     O = _oracle()
     w = workload(name)
     p = _params()
@@ -122,7 +125,9 @@ def test_gn_matches_oracle(ctx, workload, name):
     res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
     F = w.factors_with_icp(res, p)
     X0 = w.est.astype(np.float64)
-    Xg, sg = ctx.optimize_graph(X0, F)
+    gp = _abi.default_gn_params()
+    gp.linear_solver = solver
+    Xg, sg = ctx.optimize_graph(X0, F, gp)
     Xo, so = O.optimize_graph(X0, F)
     assert sg.iterations < 100 and so.iterations < 100
     err = np.abs(pose_diff(Xg, Xo)).max()
