@@ -80,12 +80,17 @@ struct dpg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
-    hipEvent_t ev[6] = {};
+    hipEvent_t ev[8] = {};
+    int32_t icp_variant = DPG_ICP_KDTREE;
     // scan store (batch form)
     DevBuf<float> full, ds;
+    DevBuf<int64_t> ds_off_dev;
+    DevBuf<float> tree_pts;        // per-node k-d trees over the downsampled clouds
+    DevBuf<uint16_t> tree_idx;
     std::vector<int64_t> full_off, ds_off;
     int64_t n_nodes = 0;
     int32_t ratio = 1;
+    int32_t max_ds = 0;
     // staged edge batch
     std::vector<dpg_icp_edge> h_edges;
     DevBuf<dpg_icp_edge> edges;
@@ -102,6 +107,9 @@ struct dpg_ctx {
     DevBuf<dpg_icp_edge> s_edge;
     DevBuf<dpg_icp_result> s_res;
     DevBuf<double> s_hess;
+    DevBuf<int64_t> s_off;
+    DevBuf<float> s_tree_pts;
+    DevBuf<uint16_t> s_tree_idx;
     // pose graph
     dpg_gn_dev gn{};
     bool gn_ready = false;
@@ -133,14 +141,27 @@ int set_kparams(dpg_icp_kparams* kp, const dpg_icp_params* p) {
 
 int32_t round_up(int32_t v, int32_t m) { return (v + m - 1) / m * m; }
 
-int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const dpg_icp_edge* edges_dev,
-                 int64_t ne, dpg_icp_kparams kp, int32_t max_src, int32_t max_tgt, dpg_icp_result* res_dev,
-                 double* hess_dev, int32_t* trace_dev, bool timed) {
-    kp.lds_tgt = round_up(std::max<int32_t>(max_tgt, 1), 64);
+// Trees: built over `n_tree_nodes` clouds (offsets ds_off_dev) when the k-d variant runs.
+int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const int64_t* ds_off_dev,
+                 int64_t n_tree_nodes, int32_t max_node_pts, float* tree_pts, uint16_t* tree_idx,
+                 const dpg_icp_edge* edges_dev, int64_t ne, dpg_icp_kparams kp, int32_t max_src,
+                 int32_t max_tgt, dpg_icp_result* res_dev, double* hess_dev, int32_t* trace_dev, bool timed) {
     const int32_t maxp = std::max(max_src, max_tgt);
     if (maxp > 4096) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 4096", maxp);
+    int rc = 0;
+    if (timed) HIP_TRY(hipEventRecord(c->ev[6], c->stream));
+    if (c->icp_variant == DPG_ICP_KDTREE) {
+        rc = dpg_launch_kdtree_build(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, c->stream);
+        if (rc) return fail(rc, "k-d tree build launch failed (%d)", rc);
+    }
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    int rc = dpg_launch_icp(ds_dev, edges_dev, ne, &kp, maxp, res_dev, trace_dev, c->stream);
+    if (c->icp_variant == DPG_ICP_KDTREE) {
+        kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 64);
+        rc = dpg_launch_icp_kd(ds_dev, tree_pts, tree_idx, edges_dev, ne, &kp, maxp, res_dev, trace_dev, c->stream);
+    } else {
+        kp.lds_tgt = round_up(std::max<int32_t>(max_tgt, 1), 64);
+        rc = dpg_launch_icp(ds_dev, edges_dev, ne, &kp, maxp, res_dev, trace_dev, c->stream);
+    }
     if (rc) return fail(rc, "ICP kernel launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
     if (timed) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     if (hess_dev) {
@@ -200,6 +221,8 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     c->full.release(); c->ds.release(); c->edges.release(); c->res.release(); c->hess.release();
     c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
+    c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release();
+    c->s_off.release(); c->s_tree_pts.release(); c->s_tree_idx.release();
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -239,13 +262,20 @@ int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V
     std::vector<float> ds((size_t)(2 * std::max<int64_t>(c->ds_off[(size_t)V], 1)));
     for (int64_t v = 0; v < V; ++v)   // R2 downsamplePointCloud, per node
         dpg_downsample_cloud(pts + 2 * off[v], off[v + 1] - off[v], ratio, ds.data() + 2 * c->ds_off[(size_t)v]);
-    if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(ds.size()))
+    int64_t mx = 0;
+    for (int64_t v = 0; v < V; ++v) mx = std::max(mx, c->ds_off[(size_t)v + 1] - c->ds_off[(size_t)v]);
+    if (mx > 4096) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 4096)", (long long)mx);
+    if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(ds.size()) ||
+        c->ds_off_dev.reserve((size_t)V + 1) || c->tree_pts.reserve(ds.size()) || c->tree_idx.reserve(ds.size() / 2))
         return fail(DPG_ERR_HIP, "out of device memory for scans");
     HIP_TRY(hipMemcpyAsync(c->full.p, pts, sizeof(float) * 2 * (size_t)total, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->ds.p, ds.data(), sizeof(float) * ds.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->ds_off_dev.p, c->ds_off.data(), sizeof(int64_t) * ((size_t)V + 1), hipMemcpyHostToDevice,
+                           c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_nodes = V;
     c->ratio = ratio;
+    c->max_ds = (int32_t)mx;
     return DPG_OK;
 }
 
@@ -304,8 +334,22 @@ int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
     }
     c->trace_iters = trace_iters > 0 ? trace_iters : 0;
     c->have_cov = compute_cov != 0;
-    return launch_batch(c, c->ds.p, c->full.p, c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
+    return launch_batch(c, c->ds.p, c->full.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
+                        c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
                         compute_cov ? c->hess.p : nullptr, tr, true);
+}
+
+int dpg_ctx_set_icp_variant(dpg_ctx* c, int32_t variant) {
+    if (!c || (variant != DPG_ICP_KDTREE && variant != DPG_ICP_GRID)) return fail(DPG_ERR_ARG, "bad ICP variant");
+    c->icp_variant = variant;
+    return DPG_OK;
+}
+
+float dpg_kdtree_build_ms(dpg_ctx* c) {
+    float ms = -1.f;
+    if (!c || hipEventSynchronize(c->ev[0]) != hipSuccess) return -1.f;
+    if (hipEventElapsedTime(&ms, c->ev[6], c->ev[0]) != hipSuccess) return -1.f;
+    return ms;
 }
 
 int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
@@ -382,14 +426,20 @@ int dpg_run_icp(dpg_ctx* c, const float* src, int64_t ns, const float* tgt, int6
     dpg_icp_edge E;
     E.src_full_off = 0; E.n_src_full = (int32_t)ns;
     E.tgt_full_off = (int32_t)ns; E.n_tgt_full = (int32_t)nt;
-    E.src_ds_off = (int32_t)(ns + nt); E.n_src_ds = (int32_t)nsd;
-    E.tgt_ds_off = (int32_t)(ns + nt + nsd); E.n_tgt_ds = (int32_t)ntd;
+    // downsampled clouds (and their trees) are addressed relative to the ds part of the buffer
+    E.src_ds_off = 0; E.n_src_ds = (int32_t)nsd;
+    E.tgt_ds_off = (int32_t)nsd; E.n_tgt_ds = (int32_t)ntd;
     dpg_icp_guess(pose_src, pose_tgt, E.guess);
-    if (c->s_pts.reserve(buf.size()) || c->s_edge.reserve(1) || c->s_res.reserve(1) || c->s_hess.reserve(9))
+    const int64_t offs[3] = {0, nsd, nsd + ntd};
+    if (c->s_pts.reserve(buf.size()) || c->s_edge.reserve(1) || c->s_res.reserve(1) || c->s_hess.reserve(9) ||
+        c->s_off.reserve(3) || c->s_tree_pts.reserve((size_t)(2 * (nsd + ntd) + 2)) ||
+        c->s_tree_idx.reserve((size_t)(nsd + ntd + 1)))
         return fail(DPG_ERR_HIP, "out of device memory");
     HIP_TRY(hipMemcpyAsync(c->s_pts.p, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->s_edge.p, &E, sizeof(E), hipMemcpyHostToDevice, c->stream));
-    rc = launch_batch(c, c->s_pts.p, c->s_pts.p, c->s_edge.p, 1, kp, (int32_t)nsd, (int32_t)ntd, c->s_res.p,
+    HIP_TRY(hipMemcpyAsync(c->s_off.p, offs, sizeof(offs), hipMemcpyHostToDevice, c->stream));
+    rc = launch_batch(c, c->s_pts.p + 2 * (ns + nt), c->s_pts.p, c->s_off.p, 2, (int32_t)std::max(nsd, ntd),
+                      c->s_tree_pts.p, c->s_tree_idx.p, c->s_edge.p, 1, kp, (int32_t)nsd, (int32_t)ntd, c->s_res.p,
                       hess_out ? c->s_hess.p : nullptr, nullptr, false);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(result, c->s_res.p, sizeof(dpg_icp_result), hipMemcpyDeviceToHost, c->stream));

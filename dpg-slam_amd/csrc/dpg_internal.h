@@ -47,6 +47,13 @@ int dpg_launch_icp(const float* ds_pts_dev, const dpg_icp_edge* edges_dev, int64
 int dpg_launch_cov(const float* full_pts_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
                    const dpg_icp_result* results_dev, double* hess_dev, void* stream);
 size_t dpg_icp_lds_bytes(int32_t lds_tgt, int32_t cells_max);
+/* k-d tree variant (dpg_icp_kd.hip): per-node trees over the downsampled clouds, then ICP. */
+int dpg_launch_kdtree_build(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
+                            int32_t max_points, float* tree_pts_dev, uint16_t* tree_idx_dev, void* stream);
+int dpg_launch_icp_kd(const float* ds_pts_dev, const float* tree_pts_dev, const uint16_t* tree_idx_dev,
+                      const dpg_icp_edge* edges_dev, int64_t n_edges, const dpg_icp_kparams* kp,
+                      int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* stream);
+size_t dpg_icp_kd_lds_bytes(int32_t cap);
 
 /* Pose-graph system on device (defined in dpg_gn.hip). */
 typedef struct dpg_gn_dev {

@@ -167,6 +167,14 @@ class Context:
     def synchronize(self):
         check(lib().dpg_ctx_synchronize(self.handle), "dpg_ctx_synchronize")
 
+    def set_icp_variant(self, variant: str):
+        """'kdtree' (default) or 'grid' -- nearest-neighbour machinery; results are identical."""
+        v = {"kdtree": 2, "grid": 1}[variant]
+        check(lib().dpg_ctx_set_icp_variant(self.handle, v), "dpg_ctx_set_icp_variant")
+
+    def kdtree_build_ms(self) -> float:
+        return float(lib().dpg_kdtree_build_ms(self.handle))
+
     # ---- runIcp ----
     def run_icp(self, node_1: Node, node_2: Node, params=None, with_hessian=False):
         """DpgSLAM::runIcp(node_1, node_2, icp_results): node_1 = target, node_2 = source.
