@@ -81,12 +81,13 @@ struct dpg_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev[8] = {};
-    int32_t icp_variant = DPG_ICP_KDTREE;
+    int32_t icp_variant = DPG_ICP_ANGULAR;
     // scan store (batch form)
     DevBuf<float> full, ds;
     DevBuf<int64_t> ds_off_dev;
-    DevBuf<float> tree_pts;        // per-node k-d trees over the downsampled clouds
+    DevBuf<float> tree_pts;        // per-node index over the downsampled clouds (k-d tree or angle order)
     DevBuf<uint16_t> tree_idx;
+    DevBuf<uint16_t> buckets;      // angle variant: [V][B+1] bucket starts
     std::vector<int64_t> full_off, ds_off;
     int64_t n_nodes = 0;
     int32_t ratio = 1;
@@ -110,6 +111,7 @@ struct dpg_ctx {
     DevBuf<int64_t> s_off;
     DevBuf<float> s_tree_pts;
     DevBuf<uint16_t> s_tree_idx;
+    DevBuf<uint16_t> s_buckets;
     // pose graph
     dpg_gn_dev gn{};
     bool gn_ready = false;
@@ -141,11 +143,13 @@ int set_kparams(dpg_icp_kparams* kp, const dpg_icp_params* p) {
 
 int32_t round_up(int32_t v, int32_t m) { return (v + m - 1) / m * m; }
 
-// Trees: built over `n_tree_nodes` clouds (offsets ds_off_dev) when the k-d variant runs.
+// Per-node indexes (k-d trees / angle order) are built over `n_tree_nodes` clouds (offsets
+// ds_off_dev) before the ICP kernel of those variants.
 int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const int64_t* ds_off_dev,
                  int64_t n_tree_nodes, int32_t max_node_pts, float* tree_pts, uint16_t* tree_idx,
-                 const dpg_icp_edge* edges_dev, int64_t ne, dpg_icp_kparams kp, int32_t max_src,
-                 int32_t max_tgt, dpg_icp_result* res_dev, double* hess_dev, int32_t* trace_dev, bool timed) {
+                 uint16_t* buckets, const dpg_icp_edge* edges_dev, int64_t ne, dpg_icp_kparams kp,
+                 int32_t max_src, int32_t max_tgt, dpg_icp_result* res_dev, double* hess_dev, int32_t* trace_dev,
+                 bool timed) {
     const int32_t maxp = std::max(max_src, max_tgt);
     if (maxp > 4096) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 4096", maxp);
     int rc = 0;
@@ -153,9 +157,17 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     if (c->icp_variant == DPG_ICP_KDTREE) {
         rc = dpg_launch_kdtree_build(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, c->stream);
         if (rc) return fail(rc, "k-d tree build launch failed (%d)", rc);
+    } else if (c->icp_variant == DPG_ICP_ANGULAR) {
+        rc = dpg_launch_angle_index(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, buckets,
+                                    c->stream);
+        if (rc) return fail(rc, "angle index build launch failed (%d)", rc);
     }
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    if (c->icp_variant == DPG_ICP_KDTREE) {
+    if (c->icp_variant == DPG_ICP_ANGULAR) {
+        kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 64);
+        rc = dpg_launch_icp_ang(ds_dev, tree_pts, tree_idx, buckets, edges_dev, ne, &kp, maxp, res_dev, trace_dev,
+                                c->stream);
+    } else if (c->icp_variant == DPG_ICP_KDTREE) {
         kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 64);
         rc = dpg_launch_icp_kd(ds_dev, tree_pts, tree_idx, edges_dev, ne, &kp, maxp, res_dev, trace_dev, c->stream);
     } else {
@@ -223,6 +235,7 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
     c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release();
     c->s_off.release(); c->s_tree_pts.release(); c->s_tree_idx.release();
+    c->buckets.release(); c->s_buckets.release();
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -266,7 +279,8 @@ int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V
     for (int64_t v = 0; v < V; ++v) mx = std::max(mx, c->ds_off[(size_t)v + 1] - c->ds_off[(size_t)v]);
     if (mx > 4096) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 4096)", (long long)mx);
     if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(ds.size()) ||
-        c->ds_off_dev.reserve((size_t)V + 1) || c->tree_pts.reserve(ds.size()) || c->tree_idx.reserve(ds.size() / 2))
+        c->ds_off_dev.reserve((size_t)V + 1) || c->tree_pts.reserve(ds.size()) || c->tree_idx.reserve(ds.size() / 2) ||
+        c->buckets.reserve((size_t)V * (size_t)(dpg_angle_buckets() + 1)))
         return fail(DPG_ERR_HIP, "out of device memory for scans");
     HIP_TRY(hipMemcpyAsync(c->full.p, pts, sizeof(float) * 2 * (size_t)total, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->ds.p, ds.data(), sizeof(float) * ds.size(), hipMemcpyHostToDevice, c->stream));
@@ -294,6 +308,9 @@ int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const fl
         if (t < 0 || s < 0 || t >= c->n_nodes || s >= c->n_nodes)
             return fail(DPG_ERR_ARG, "edge %lld references a missing node", (long long)e);
         dpg_icp_edge& E = c->h_edges[(size_t)e];
+        memset(&E, 0, sizeof(E));
+        E.src_node = s;
+        E.tgt_node = t;
         E.src_ds_off = (int32_t)c->ds_off[(size_t)s];
         E.n_src_ds = (int32_t)(c->ds_off[(size_t)s + 1] - c->ds_off[(size_t)s]);
         E.tgt_ds_off = (int32_t)c->ds_off[(size_t)t];
@@ -335,12 +352,13 @@ int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
     c->trace_iters = trace_iters > 0 ? trace_iters : 0;
     c->have_cov = compute_cov != 0;
     return launch_batch(c, c->ds.p, c->full.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
-                        c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
+                        c->buckets.p, c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
                         compute_cov ? c->hess.p : nullptr, tr, true);
 }
 
 int dpg_ctx_set_icp_variant(dpg_ctx* c, int32_t variant) {
-    if (!c || (variant != DPG_ICP_KDTREE && variant != DPG_ICP_GRID)) return fail(DPG_ERR_ARG, "bad ICP variant");
+    if (!c || (variant != DPG_ICP_ANGULAR && variant != DPG_ICP_KDTREE && variant != DPG_ICP_GRID))
+        return fail(DPG_ERR_ARG, "bad ICP variant");
     c->icp_variant = variant;
     return DPG_OK;
 }
@@ -424,6 +442,9 @@ int dpg_run_icp(dpg_ctx* c, const float* src, int64_t ns, const float* tgt, int6
     dpg_downsample_cloud(src, ns, ratio, buf.data() + 2 * (ns + nt));
     dpg_downsample_cloud(tgt, nt, ratio, buf.data() + 2 * (ns + nt + nsd));
     dpg_icp_edge E;
+    memset(&E, 0, sizeof(E));
+    E.src_node = 0;
+    E.tgt_node = 1;
     E.src_full_off = 0; E.n_src_full = (int32_t)ns;
     E.tgt_full_off = (int32_t)ns; E.n_tgt_full = (int32_t)nt;
     // downsampled clouds (and their trees) are addressed relative to the ds part of the buffer
@@ -433,13 +454,13 @@ int dpg_run_icp(dpg_ctx* c, const float* src, int64_t ns, const float* tgt, int6
     const int64_t offs[3] = {0, nsd, nsd + ntd};
     if (c->s_pts.reserve(buf.size()) || c->s_edge.reserve(1) || c->s_res.reserve(1) || c->s_hess.reserve(9) ||
         c->s_off.reserve(3) || c->s_tree_pts.reserve((size_t)(2 * (nsd + ntd) + 2)) ||
-        c->s_tree_idx.reserve((size_t)(nsd + ntd + 1)))
+        c->s_tree_idx.reserve((size_t)(nsd + ntd + 1)) || c->s_buckets.reserve((size_t)(2 * (dpg_angle_buckets() + 1))))
         return fail(DPG_ERR_HIP, "out of device memory");
     HIP_TRY(hipMemcpyAsync(c->s_pts.p, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->s_edge.p, &E, sizeof(E), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->s_off.p, offs, sizeof(offs), hipMemcpyHostToDevice, c->stream));
     rc = launch_batch(c, c->s_pts.p + 2 * (ns + nt), c->s_pts.p, c->s_off.p, 2, (int32_t)std::max(nsd, ntd),
-                      c->s_tree_pts.p, c->s_tree_idx.p, c->s_edge.p, 1, kp, (int32_t)nsd, (int32_t)ntd, c->s_res.p,
+                      c->s_tree_pts.p, c->s_tree_idx.p, c->s_buckets.p, c->s_edge.p, 1, kp, (int32_t)nsd, (int32_t)ntd, c->s_res.p,
                       hess_out ? c->s_hess.p : nullptr, nullptr, false);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(result, c->s_res.p, sizeof(dpg_icp_result), hipMemcpyDeviceToHost, c->stream));

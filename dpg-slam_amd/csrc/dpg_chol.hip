@@ -26,7 +26,7 @@
 namespace {
 
 constexpr int kT = 256;     // threads per front workgroup
-constexpr int kNB = 16;     // factorization panel width (scalar columns)
+constexpr int kNB = 32;     // factorization panel width (scalar columns)
 constexpr int kSB = 64;     // triangular-solve diagonal block
 
 struct SnDev {
@@ -81,42 +81,79 @@ __global__ __launch_bounds__(kT) void chol_factor_level(const int32_t* __restric
         }
         __syncthreads();
     }
-    // blocked right-looking partial Cholesky of the first k3 columns
+    // blocked right-looking partial Cholesky of the first k3 columns:
+    //   panel (R x w, R = rows from j0 down) in LDS, factored Crout-style (2 barriers / column),
+    //   then the trailing lower triangle updated by 4x4 register tiles (lower-triangle tiles only).
     for (int j0 = 0; j0 < k3; j0 += kNB) {
         const int w = min(kNB, k3 - j0), R = m3 - j0;
         for (int e = tid; e < w * R; e += kT) {
-            const int t = e / R, i = e % R;
+            const int t = e / R, i = e - t * R;
             P[e] = F[(j0 + t) * m3 + j0 + i];
         }
         __syncthreads();
         for (int t = 0; t < w; ++t) {
+            // column t: subtract the contributions of the panel's earlier columns (rows i >= t)
+            if (t > 0) {
+                for (int i = t + tid; i < R; i += kT) {
+                    double acc = 0.0;
+                    for (int s2 = 0; s2 < t; ++s2) acc += P[s2 * R + i] * P[s2 * R + t];
+                    P[t * R + i] -= acc;
+                }
+                __syncthreads();
+            }
             double piv = P[t * R + t];
-            __syncthreads();
             if (!(piv > 0.0)) {
                 if (tid == 0) atomicExch(status, 1);
                 piv = 1.0;
             }
             piv = sqrt(piv);
-            for (int i = t + tid; i < R; i += kT) P[t * R + i] = (i == t) ? piv : P[t * R + i] / piv;
-            __syncthreads();
-            const int nl = w - t - 1;
-            for (int e = tid; e < nl * R; e += kT) {
-                const int l = t + 1 + e / R, i = e % R;
-                if (i >= l) P[l * R + i] -= P[t * R + i] * P[t * R + l];
-            }
+            const double inv = 1.0 / piv;
+            __syncthreads();   // everyone has read the pivot before row t is overwritten
+            for (int i = t + tid; i < R; i += kT) P[t * R + i] = (i == t) ? piv : P[t * R + i] * inv;
             __syncthreads();
         }
         for (int e = tid; e < w * R; e += kT) {
-            const int t = e / R, i = e % R;
+            const int t = e / R, i = e - t * R;
             if (i >= t) F[(j0 + t) * m3 + j0 + i] = P[e];
         }
-        const int T = m3 - j0 - w;
-        for (int e = tid; e < T * T; e += kT) {
-            const int i = w + e % T, l = w + e / T;
-            if (i < l) continue;
-            double acc = 0.0;
-            for (int t = 0; t < w; ++t) acc += P[t * R + i] * P[t * R + l];
-            F[(j0 + l) * m3 + j0 + i] -= acc;
+        // trailing update: F(i, l) -= sum_t P(i, t) P(l, t) for w <= l <= i < R (panel-local)
+        const int T = R - w;
+        const int nt = (T + 3) >> 2;
+        const int ntiles = nt * (nt + 1) / 2;
+        for (int q = tid; q < ntiles; q += kT) {
+            int ti = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+            while (ti * (ti + 1) / 2 > q) --ti;
+            while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
+            const int tl = q - ti * (ti + 1) / 2;
+            const int i0 = w + 4 * ti, l0 = w + 4 * tl;
+            double acc[4][4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
+            for (int t = 0; t < w; ++t) {
+                const double* Pt = P + t * R;
+                double a[4], b[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) a[r] = (i0 + r < R) ? Pt[i0 + r] : 0.0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) b[c] = (l0 + c < R) ? Pt[l0 + c] : 0.0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[r][c] += a[r] * b[c];
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int l = l0 + c;
+                if (l >= R) continue;
+                double* col = F + (int64_t)(j0 + l) * m3 + j0;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = i0 + r;
+                    if (i < R && i >= l) col[i] -= acc[r][c];
+                }
+            }
         }
         __syncthreads();
     }

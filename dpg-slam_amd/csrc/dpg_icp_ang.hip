@@ -1,0 +1,417 @@
+// dpg_icp_ang.hip -- ICP scan matching, angular-index variant (the default batched ICP kernel).
+//
+// Same semantics and bit-exact results as the grid / k-d kernels (PCL IterativeClosestPoint with
+// reciprocal KdTreeFLANN correspondences, dpg_slam.cc:387-416), with a neighbour index built for
+// laser scans: a scan is uniform in ANGLE, not in space (near the sensor its points are a few mm
+// apart, far away tens of cm), so every cloud is indexed by the angle of its points around the
+// node origin:
+//   angle_index_kernel: per node, points sorted by atan2 (bitonic sort in LDS) + a table of the
+//     first sorted position of each of B uniform angle buckets.
+//   exactness: every point p with |p - q| <= rho satisfies |angle(p) - angle(q)| <= asin(rho/|q|)
+//     (|q| > rho), so a query scans the contiguous sorted range of the buckets covering
+//     [angle(q) -+ (asin(rho'/|q|) + margin)]; the bucket map is the same monotone float function
+//     at build and query time; queries within rho' of the origin scan everything.
+//   icp_ang_kernel (one workgroup per edge, all iterations resident in LDS):
+//     forward 1-NN: radius = distance to the previous iteration's match (r when unseeded), the
+//       window scan keeps the exact (distance, lowest index) argmin;
+//     reciprocal test: radius query in the SOURCE index (source node frame, static) around
+//       F_k^-1 t_j with radius sqrt(d_ij) + drift_k, candidates re-checked in exact float on their
+//       CURRENT coordinates (see dpg_icp_kd.hip for the drift argument);
+//     rigid fit + convergence exactly as the other variants (fp64 256-lane fixed tree).
+// Built with -ffp-contract=off.
+
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "dpg_internal.h"
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kW = kT / 64;
+constexpr int kSums = 10;
+constexpr int kB = 512;                         // angle buckets per cloud
+constexpr float kPi = 3.14159265358979323846f;
+constexpr float kBucketScale = (float)kB / (2.0f * 3.14159265358979323846f);
+
+__device__ __forceinline__ int bucket_of(float th) {
+    int b = (int)floorf((th + kPi) * kBucketScale);
+    return min(max(b, 0), kB - 1);
+}
+
+__device__ __forceinline__ uint32_t orderable(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// one workgroup per node: points sorted by angle + bucket starts
+__global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restrict__ ds_pts,
+                                                         const int64_t* __restrict__ ds_off,
+                                                         float2* __restrict__ idx_pts,
+                                                         uint16_t* __restrict__ idx_orig,
+                                                         uint16_t* __restrict__ buckets /* [V][kB+1] */) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int v = blockIdx.x, tid = threadIdx.x;
+    const int64_t off = ds_off[v];
+    const int N = (int)(ds_off[v + 1] - off);
+    uint16_t* bk = buckets + (size_t)v * (kB + 1);
+    if (N <= 0) {
+        for (int b = tid; b <= kB; b += kT) bk[b] = 0;
+        return;
+    }
+    int P = 1;
+    while (P < N) P <<= 1;
+    uint64_t* key = reinterpret_cast<uint64_t*>(smem);   // [P]: orderable(angle) << 32 | index
+    for (int s = tid; s < P; s += kT) {
+        if (s < N) {
+            const float2 p = ds_pts[off + s];
+            key[s] = ((uint64_t)orderable(atan2f(p.y, p.x)) << 32) | (uint32_t)s;
+        } else {
+            key[s] = ~0ull;
+        }
+    }
+    __syncthreads();
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int q = tid; q < P / 2; q += kT) {
+                const int i = 2 * q - (q & (j - 1));
+                const int l = i + j;
+                const bool up = (i & k) == 0;
+                const uint64_t a = key[i], b = key[l];
+                if ((a > b) == up) { key[i] = b; key[l] = a; }
+            }
+            __syncthreads();
+        }
+    }
+    for (int s = tid; s < N; s += kT) {
+        const int o = (int)(key[s] & 0xffffffffu);
+        const float2 p = ds_pts[off + o];
+        idx_pts[off + s] = p;
+        idx_orig[off + s] = (uint16_t)o;
+        const int b = bucket_of(atan2f(p.y, p.x));
+        int bp = -1;
+        if (s > 0) {
+            const float2 pp = ds_pts[off + (int)(key[s - 1] & 0xffffffffu)];
+            bp = bucket_of(atan2f(pp.y, pp.x));
+        }
+        for (int bb = bp + 1; bb <= b; ++bb) bk[bb] = (uint16_t)s;   // first sorted position >= bucket
+        if (s == N - 1)
+            for (int bb = b + 1; bb <= kB; ++bb) bk[bb] = (uint16_t)N;
+    }
+}
+
+struct Lds {
+    float2* tp;       // target points sorted by angle
+    float2* sp;       // source points sorted by angle (source node frame)
+    float2* sc;       // current (moved) source points, original order
+    uint16_t* ti;     // target sorted -> original index
+    uint16_t* si;     // source sorted -> original index
+    uint16_t* tb;     // target bucket starts [kB+1]
+    uint16_t* sb;     // source bucket starts [kB+1]
+    double* wpart;    // [kW][kSums + 2]
+};
+
+__device__ __forceinline__ size_t a16(size_t x) { return (x + 15) & ~size_t(15); }
+
+__device__ Lds carve(unsigned char* base, int cap) {
+    Lds L;
+    size_t o = 0;
+    L.tp = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
+    L.sp = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
+    L.sc = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
+    L.ti = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
+    L.si = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
+    L.tb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
+    L.sb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
+    L.wpart = reinterpret_cast<double*>(base + o);
+    return L;
+}
+
+__device__ __forceinline__ float sqd(float ax, float ay, float bx, float by) {
+    const float dx = ax - bx, dy = ay - by;
+    return dx * dx + dy * dy;
+}
+
+// sorted-position ranges of the points that can lie within `rad` of q (angle window); returns
+// the number of ranges (1 or 2), or 0 meaning "scan everything".
+__device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int r0[2], int r1[2]) {
+    const float rq = sqrtf(qx * qx + qy * qy);
+    const float ratio = rad / rq;
+    if (!(ratio < 0.7f)) return 0;
+    const float half = asinf(ratio) * 1.0001f + 2e-4f;
+    const float th = atan2f(qy, qx);
+    float lo = th - half, hi = th + half;
+    if (lo < -kPi) {
+        r0[0] = bk[bucket_of(lo + 2.0f * kPi)]; r1[0] = n;
+        r0[1] = 0; r1[1] = bk[bucket_of(hi) + 1];
+        return 2;
+    }
+    if (hi > kPi) {
+        r0[0] = bk[bucket_of(lo)]; r1[0] = n;
+        r0[1] = 0; r1[1] = bk[bucket_of(hi - 2.0f * kPi) + 1];
+        return 2;
+    }
+    r0[0] = bk[bucket_of(lo)];
+    r1[0] = bk[bucket_of(hi) + 1];
+    return 1;
+}
+
+template <int PPT>
+__global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ ds_pts,
+                                                     const float2* __restrict__ idx_pts,
+                                                     const uint16_t* __restrict__ idx_orig,
+                                                     const uint16_t* __restrict__ buckets,
+                                                     const dpg_icp_edge* __restrict__ edges,
+                                                     dpg_icp_kparams kp, dpg_icp_result* __restrict__ results,
+                                                     int32_t* __restrict__ trace) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int e = blockIdx.x;
+    const dpg_icp_edge E = edges[e];
+    const int N = E.n_src_ds, M = E.n_tgt_ds;
+    const int vt = E.tgt_node, vs = E.src_node;
+    Lds L = carve(smem, kp.lds_tgt);
+    for (int i = t; i < M; i += kT) {
+        L.tp[i] = idx_pts[E.tgt_ds_off + i];
+        L.ti[i] = idx_orig[E.tgt_ds_off + i];
+    }
+    for (int i = t; i < N; i += kT) {
+        L.sp[i] = idx_pts[E.src_ds_off + i];
+        L.si[i] = idx_orig[E.src_ds_off + i];
+    }
+    for (int b = t; b <= kB; b += kT) {
+        L.tb[b] = buckets[(size_t)vt * (kB + 1) + b];
+        L.sb[b] = buckets[(size_t)vs * (kB + 1) + b];
+    }
+    float F[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) F[q] = E.guess[q];
+    float sx[PPT], sy[PPT];
+    int seed[PPT];
+#pragma unroll
+    for (int m = 0; m < PPT; ++m) {
+        const int i = t + kT * m;
+        seed[m] = -1;
+        sx[m] = 0.f;
+        sy[m] = 0.f;
+        if (i < N) {
+            const float2 p = ds_pts[E.src_ds_off + i];
+            sx[m] = (F[0] * p.x + F[1] * p.y) + F[2];
+            sy[m] = (F[3] * p.x + F[4] * p.y) + F[5];
+            L.sc[i] = make_float2(sx[m], sy[m]);
+        }
+    }
+    __syncthreads();
+
+    const float r2f = kp.r2_f;
+    const float rmax = sqrtf(r2f) * 1.0001f + 1e-5f;
+    double prev_mse = DBL_MAX, last_mse = 0.0;
+    int k = 0, converged = 0, status = DPG_ICP_OK, last_cnt = 0;
+    for (;;) {
+        const double det = (double)F[0] * (double)F[4] - (double)F[1] * (double)F[3];
+        const double i00 = (double)F[4] / det, i01 = -(double)F[1] / det;
+        const double i10 = -(double)F[3] / det, i11 = (double)F[0] / det;
+        const float drift = 1e-4f + 5e-5f * (float)(k + 1);
+        double acc[kSums];
+#pragma unroll
+        for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            const int i = t + kT * m;
+            if (i >= N) continue;
+            const float qx = sx[m], qy = sy[m];
+            // ---- forward 1-NN (target index), seeded radius ----
+            float bd = r2f;
+            int bi = 0x7fffffff, bp = -1;
+            float rad = rmax;
+            if (seed[m] >= 0) {
+                const float2 s0 = L.tp[seed[m]];
+                const float d = sqd(qx, qy, s0.x, s0.y);
+                if (d <= r2f) {
+                    bd = d; bi = L.ti[seed[m]]; bp = seed[m];
+                    rad = sqrtf(d) * 1.0001f + 1e-6f;
+                }
+            }
+            {
+                int r0[2], r1[2];
+                int nr = window(L.tb, M, qx, qy, rad, r0, r1);
+                if (nr == 0) { nr = 1; r0[0] = 0; r1[0] = M; }
+                for (int w = 0; w < nr; ++w) {
+                    for (int s = r0[w]; s < r1[w]; ++s) {
+                        const float2 tq = L.tp[s];
+                        const float d = sqd(qx, qy, tq.x, tq.y);
+                        if (d <= bd) {
+                            const int j = L.ti[s];
+                            if (d < bd || j < bi) { bd = d; bi = j; bp = s; }
+                        }
+                    }
+                }
+            }
+            seed[m] = bp;
+            bool ok = bp >= 0;
+            // ---- reciprocal test in the static source index ----
+            if (ok && kp.reciprocal) {
+                const float2 tj = L.tp[bp];
+                const double ux = (double)tj.x - (double)F[2], uy = (double)tj.y - (double)F[5];
+                const float px = (float)(i00 * ux + i01 * uy), py = (float)(i10 * ux + i11 * uy);
+                const float rho = sqrtf(bd) * 1.0001f + drift;
+                int r0[2], r1[2];
+                int nr = window(L.sb, N, px, py, rho, r0, r1);
+                if (nr == 0) { nr = 1; r0[0] = 0; r1[0] = N; }
+                for (int w = 0; w < nr && ok; ++w) {
+                    for (int s = r0[w]; s < r1[w]; ++s) {
+                        const int kk = L.si[s];
+                        if (kk == i) continue;
+                        const float2 c = L.sc[kk];
+                        const float d = sqd(c.x, c.y, tj.x, tj.y);
+                        if (d < bd || (d == bd && kk < i)) { ok = false; break; }
+                    }
+                }
+            }
+            if (trace && k < kp.trace_iters) trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
+            if (ok) {
+                const float2 tq = L.tp[bp];
+                const double px = qx, py = qy, tx = tq.x, ty = tq.y;
+                acc[0] = acc[0] + 1.0;
+                acc[1] = acc[1] + (double)bd;
+                acc[2] = acc[2] + px;
+                acc[3] = acc[3] + py;
+                acc[4] = acc[4] + tx;
+                acc[5] = acc[5] + ty;
+                acc[6] = acc[6] + px * tx;
+                acc[7] = acc[7] + px * ty;
+                acc[8] = acc[8] + py * tx;
+                acc[9] = acc[9] + py * ty;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+            for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + __shfl_down(acc[q], off, 64);
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
+        }
+        __syncthreads();
+        double S[kSums];
+#pragma unroll
+        for (int q = 0; q < kSums; ++q)
+            S[q] = (L.wpart[0 * (kSums + 2) + q] + L.wpart[1 * (kSums + 2) + q]) +
+                   (L.wpart[2 * (kSums + 2) + q] + L.wpart[3 * (kSums + 2) + q]);
+        const int cnt = (int)S[0];
+        last_cnt = cnt;
+        if (cnt < kp.min_corr) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
+        const double n = S[0];
+        const double a = (S[6] + S[9]) - (S[2] * S[4] + S[3] * S[5]) / n;
+        const double b = (S[7] - S[8]) - (S[2] * S[5] - S[3] * S[4]) / n;
+        const double hh = sqrt(a * a + b * b);
+        double c = 1.0, s = 0.0;
+        if (hh > 0.0) { c = a / hh; s = b / hh; }
+        const double mpx = S[2] / n, mpy = S[3] / n, mqx = S[4] / n, mqy = S[5] / n;
+        const double txd = mqx - (c * mpx - s * mpy);
+        const double tyd = mqy - (s * mpx + c * mpy);
+        const float cf = (float)c, sf = (float)s, txf = (float)txd, tyf = (float)tyd;
+        const float nsf = -sf;
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            const int i = t + kT * m;
+            const float x = sx[m], y = sy[m];
+            sx[m] = (cf * x + nsf * y) + txf;
+            sy[m] = (sf * x + cf * y) + tyf;
+            if (i < N) L.sc[i] = make_float2(sx[m], sy[m]);
+        }
+        float Nf[6];
+        Nf[0] = cf * F[0] + nsf * F[3];
+        Nf[1] = cf * F[1] + nsf * F[4];
+        Nf[2] = (cf * F[2] + nsf * F[5]) + txf;
+        Nf[3] = sf * F[0] + cf * F[3];
+        Nf[4] = sf * F[1] + cf * F[4];
+        Nf[5] = (sf * F[2] + cf * F[5]) + tyf;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) F[q] = Nf[q];
+        ++k;
+        const double mse = S[1] / S[0];
+        last_mse = mse;
+        __syncthreads();
+        if (k >= kp.max_iter) { converged = 1; break; }
+        const float tr = ((cf + cf) + 1.0f) - 1.0f;
+        const double cos_angle = 0.5 * (double)tr;
+        const double tsq = (double)(txf * txf + tyf * tyf);
+        if (cos_angle >= kp.rot_thr && tsq <= kp.eps) { converged = 1; break; }
+        if (fabs(mse - prev_mse) < kp.mse_abs) { converged = 1; break; }
+        prev_mse = mse;
+    }
+    if (t == 0) {
+        dpg_icp_result R;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) R.T[q] = F[q];
+        R.z[0] = F[2];
+        R.z[1] = F[5];
+        R.z[2] = (float)atan2((double)F[3], (double)F[0]);
+        R.converged = converged;
+        R.iterations = k;
+        R.n_corr = last_cnt;
+        R.status = status;
+        R.pad = 0;
+        R.fitness = last_mse;
+        results[e] = R;
+    }
+}
+
+}  // namespace
+
+extern "C" int32_t dpg_angle_buckets(void) { return kB; }
+
+extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) {
+    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+    size_t o = 0;
+    o = al(o + 8 * (size_t)cap);
+    o = al(o + 8 * (size_t)cap);
+    o = al(o + 8 * (size_t)cap);
+    o = al(o + 2 * (size_t)cap);
+    o = al(o + 2 * (size_t)cap);
+    o = al(o + 2 * (size_t)(kB + 1));
+    o = al(o + 2 * (size_t)(kB + 1));
+    o += sizeof(double) * kW * (kSums + 2);
+    return al(o);
+}
+
+extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
+                                      int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
+                                      uint16_t* buckets_dev, void* stream) {
+    if (n_nodes <= 0) return DPG_OK;
+    int cap = 1;
+    while (cap < max_points) cap <<= 1;
+    if (cap > 4096) return DPG_ERR_SIZE;
+    hipLaunchKernelGGL(angle_index_kernel, dim3((unsigned)n_nodes), dim3(kT), 8 * (size_t)cap,
+                       reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(ds_pts_dev), ds_off_dev,
+                       reinterpret_cast<float2*>(idx_pts_dev), idx_orig_dev, buckets_dev);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_dev, const uint16_t* idx_orig_dev,
+                                  const uint16_t* buckets_dev, const dpg_icp_edge* edges_dev, int64_t n_edges, const dpg_icp_kparams* kp,
+                                  int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* stream) {
+    if (n_edges <= 0) return DPG_OK;
+    if (max_points > kp->lds_tgt || kp->lds_tgt > 4096) return DPG_ERR_SIZE;
+    const size_t lds = dpg_icp_ang_lds_bytes(kp->lds_tgt);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const dim3 grid((unsigned)n_edges), block(kT);
+    const float2* ds = reinterpret_cast<const float2*>(ds_pts_dev);
+    const float2* ip = reinterpret_cast<const float2*>(idx_pts_dev);
+    const int ppt = (max_points + kT - 1) / kT;
+#define DPG_ANG_LAUNCH(P)                                                                                     \
+    hipLaunchKernelGGL(icp_ang_kernel<P>, grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, edges_dev, \
+                       *kp, results_dev, trace_dev)
+    if (ppt <= 1) DPG_ANG_LAUNCH(1);
+    else if (ppt <= 2) DPG_ANG_LAUNCH(2);
+    else if (ppt <= 4) DPG_ANG_LAUNCH(4);
+    else if (ppt <= 8) DPG_ANG_LAUNCH(8);
+    else if (ppt <= 16) DPG_ANG_LAUNCH(16);
+    else return DPG_ERR_SIZE;
+#undef DPG_ANG_LAUNCH
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}

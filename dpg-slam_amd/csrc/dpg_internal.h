@@ -13,13 +13,15 @@
 extern "C" {
 #endif
 
-/* One ICP edge as the kernel sees it (48 B).  Offsets/counts are in points (float2). */
+/* One ICP edge as the kernel sees it (64 B).  Offsets/counts are in points (float2). */
 typedef struct dpg_icp_edge {
     int32_t src_ds_off, n_src_ds;    /* downsampled node_2 cloud (ICP source) */
     int32_t tgt_ds_off, n_tgt_ds;    /* downsampled node_1 cloud (ICP target) */
     int32_t src_full_off, n_src_full;  /* full node_2 cloud (covariance data_pi) */
     int32_t tgt_full_off, n_tgt_full;  /* full node_1 cloud (covariance model_qi) */
     float guess[6];                  /* runIcp transform_guess rows (dpg_slam.cc:374-378) */
+    int32_t src_node, tgt_node;      /* cloud ids (angle-index bucket tables) */
+    int32_t pad[2];
 } dpg_icp_edge;
 
 /* Scalars of the ICP/convergence rule, precomputed on the host in double. */
@@ -54,6 +56,16 @@ int dpg_launch_icp_kd(const float* ds_pts_dev, const float* tree_pts_dev, const 
                       const dpg_icp_edge* edges_dev, int64_t n_edges, const dpg_icp_kparams* kp,
                       int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* stream);
 size_t dpg_icp_kd_lds_bytes(int32_t cap);
+/* angular-index variant (dpg_icp_ang.hip, the default): per-node angle-sorted clouds + buckets. */
+int32_t dpg_angle_buckets(void);
+int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
+                           int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
+                           uint16_t* buckets_dev, void* stream);
+int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_dev, const uint16_t* idx_orig_dev,
+                       const uint16_t* buckets_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
+                       const dpg_icp_kparams* kp, int32_t max_points, dpg_icp_result* results_dev,
+                       int32_t* trace_dev, void* stream);
+size_t dpg_icp_ang_lds_bytes(int32_t cap);
 
 /* Pose-graph system on device (defined in dpg_gn.hip). */
 typedef struct dpg_gn_dev {

@@ -168,8 +168,8 @@ class Context:
         check(lib().dpg_ctx_synchronize(self.handle), "dpg_ctx_synchronize")
 
     def set_icp_variant(self, variant: str):
-        """'kdtree' (default) or 'grid' -- nearest-neighbour machinery; results are identical."""
-        v = {"kdtree": 2, "grid": 1}[variant]
+        """'angular' (default), 'kdtree' or 'grid' -- nearest-neighbour machinery; results are identical."""
+        v = {"angular": 3, "kdtree": 2, "grid": 1}[variant]
         check(lib().dpg_ctx_set_icp_variant(self.handle, v), "dpg_ctx_set_icp_variant")
 
     def kdtree_build_ms(self) -> float:

@@ -195,10 +195,11 @@ int dpg_icp_batch_fetch_trace(dpg_ctx* ctx, int32_t* trace /*[E][trace_iters][ma
 /* Device time of the last ICP / covariance kernels (ms, HIP events on the context stream). */
 float dpg_icp_batch_kernel_ms(dpg_ctx* ctx);
 float dpg_cov_batch_kernel_ms(dpg_ctx* ctx);
-/* Device time of the per-node k-d tree build that precedes the ICP kernel (k-d variant). */
+/* Device time of the per-node index build (k-d trees / angle index) that precedes the ICP kernel. */
 float dpg_kdtree_build_ms(dpg_ctx* ctx);
-/* Nearest-neighbour machinery of the ICP kernel; both give bit-identical results. */
-#define DPG_ICP_KDTREE 2   /* per-node k-d trees, seeded search, static-frame reciprocal test (default) */
+/* Nearest-neighbour machinery of the ICP kernel; all give bit-identical results. */
+#define DPG_ICP_ANGULAR 3  /* per-node angle-sorted clouds + buckets, windowed scans (default) */
+#define DPG_ICP_KDTREE 2   /* per-node k-d trees, seeded search, static-frame reciprocal test */
 #define DPG_ICP_GRID 1     /* uniform LDS grid, all-pairs reverse keys by LDS atomics */
 int dpg_ctx_set_icp_variant(dpg_ctx* ctx, int32_t variant);
 /* Sum over edges of iterations x (8N + 8M + 8N) -- algorithmic bytes of the correspondence

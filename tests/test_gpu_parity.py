@@ -56,10 +56,10 @@ def test_config1_single_alignment_bit_exact(ctx, workload, ratio):
     np.testing.assert_array_equal(tr[:n, :len(src_ds)], ref_tr[:n])
 
 
-@pytest.mark.parametrize("variant", ["kdtree", "grid"])
+@pytest.mark.parametrize("variant", ["angular", "kdtree", "grid"])
 def test_icp_batch_config2_bit_exact(ctx, workload, variant):
     """config 2: all 499 successive edges of the 500-node chain, full ICP outcome bit-exact and the
-    first 40 iterations' correspondence indices bit-exact on 16 edges (both NN variants)."""
+    first 40 iterations' correspondence indices bit-exact on 16 edges (every NN variant)."""
     O = _oracle()
     w = workload("config2")
     p = _params()
@@ -77,7 +77,7 @@ def test_icp_batch_config2_bit_exact(ctx, workload, variant):
         r1, rt = O.icp_align(sd, td, api.icp_guess(w.est[s], w.est[t]), p, O.NN_BRUTE, trace_iters=40)
         n = min(r1.iterations, 40)
         np.testing.assert_array_equal(tr[e, :n, :len(sd)], rt[:n], err_msg=f"edge {e}")
-    ctx.set_icp_variant("kdtree")
+    ctx.set_icp_variant("angular")
 
 
 def test_icp_cov_calculate_constant(ctx, workload):
