@@ -1,12 +1,16 @@
 // dpg_chol.hip -- supernodal multifrontal Cholesky of the pose-graph normal equations on gfx950.
 //
 // The CHOLESKY solve that GTSAM runs inside GaussNewtonOptimizer / ISAM2 as a
-// level-scheduled GPU factorization: the symbolic analysis (dpg_chol_sym.cpp) runs once per
-// sparsity pattern; each GN iteration then runs, per elimination-tree level, ONE kernel launch
-// for all fronts of that level (one 256-thread workgroup per front):
-//   factor: zero the dense front, scatter the original 3x3 blocks of H, extend-add the
-//           children's update matrices (in child order: deterministic, no atomics), partial
-//           Cholesky of the pivot columns in LDS panels, Schur complement left in place;
+// level-scheduled GPU factorization: the symbolic analysis (dpg_chol_sym.cpp) and the per-level
+// task lists run once per sparsity pattern; each GN iteration then runs, per elimination-tree
+// level, task-list kernels over all fronts of the level (dense fronts are column-major in HBM):
+//   assemble: one workgroup per (front, 32-column tile): zero, scatter the original 3x3 blocks
+//             of H, extend-add the children's update matrices (in child order: deterministic,
+//             no atomics);
+//   then per 32-column panel step:
+//     panel:  one workgroup per front, one panel row per thread in registers, right-looking;
+//     update: one workgroup per 32x32 tile of every front's trailing lower triangle (SYRK),
+//             so a large front's Schur complement is spread over many CUs;
 //   forward:  L y = -g  (children's pending row updates gathered, diagonal blocks solved by one
 //             wave from LDS, L21 y passed up);
 //   backward: L^T x = y (ancestors' x gathered by row position).
@@ -15,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -28,6 +33,8 @@ namespace {
 constexpr int kT = 256;     // threads per front workgroup
 constexpr int kNB = 32;     // factorization panel width (scalar columns)
 constexpr int kSB = 64;     // triangular-solve diagonal block
+constexpr int kCT = 32;     // assembly column tile
+constexpr int kUT = 32;     // trailing-update tile (rows and columns)
 
 struct SnDev {
     int32_t c0, k, r, nchild;   // k, r in 3x3 blocks
@@ -45,117 +52,139 @@ struct OEnt {                   // one upper 3x3 block of H -> its front positio
     int32_t tr, pad;            // 1: the front wants H(lo,hi)^T
 };
 
-__global__ __launch_bounds__(kT) void chol_factor_level(const int32_t* __restrict__ level_sn,
-                                                        const SnDev* __restrict__ sns,
-                                                        const OEnt* __restrict__ omap,
-                                                        const double* __restrict__ hb,
-                                                        const int32_t* __restrict__ child_list,
-                                                        const int32_t* __restrict__ relmap,
-                                                        double* __restrict__ fronts, int32_t* __restrict__ status) {
-    extern __shared__ __attribute__((aligned(16))) double P[];
+// ---- numeric factorization: three task-list kernels per elimination-tree level ----
+// (task lists are built once per sparsity pattern in dpg_chol_create)
+
+// assembly: one workgroup per (front, kCT-column tile) -- zero the lower part of the tile's
+// columns, scatter the original H blocks, then extend-add the children's update matrices in child
+// order (a barrier between children: every element is summed in the same order on every run).
+// The omap range and each child's column range [ja, jb) for the tile are precomputed on the host.
+struct AsmTask {
+    int32_t s, c0;              // front, first column of the tile
+    int32_t om_b, om_e;         // omap entries whose block column meets the tile
+    int32_t ch_off, ch_cnt;     // into AsmChild
+};
+struct AsmChild { int32_t c, ja, jb, pad; };
+
+__global__ __launch_bounds__(kT) void chol_assemble(const AsmTask* __restrict__ tasks,
+                                                    const AsmChild* __restrict__ tchild,
+                                                    const SnDev* __restrict__ sns,
+                                                    const OEnt* __restrict__ omap, const double* __restrict__ hb,
+                                                    const int32_t* __restrict__ relmap, double* __restrict__ fronts) {
     const int tid = threadIdx.x;
-    const int s = level_sn[blockIdx.x];
-    const SnDev S = sns[s];
-    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k;
+    const AsmTask tk = tasks[blockIdx.x];
+    const SnDev S = sns[tk.s];
+    const int m3 = 3 * (S.k + S.r);
+    const int c0 = tk.c0, c1 = min(c0 + kCT, m3);
     double* F = fronts + S.front_off;
-    for (int e = tid; e < m3 * m3; e += kT) F[e] = 0.0;
+    for (int j = c0; j < c1; ++j)
+        for (int i = j + tid; i < m3; i += kT) F[(int64_t)j * m3 + i] = 0.0;
     __syncthreads();
-    for (int q = tid; q < S.omap_n * 9; q += kT) {
-        const OEnt o = omap[S.omap_off + q / 9];
+    for (int q = tid; q < (tk.om_e - tk.om_b) * 9; q += kT) {
+        const OEnt o = omap[tk.om_b + q / 9];
         const int ii = (q % 9) / 3, jj = q % 3;
+        const int row = 3 * o.a + ii, col = 3 * o.b + jj;
+        if (col < c0 || col >= c1 || row < col) continue;
         const double* B = hb + 9 * (int64_t)o.u;
-        F[(3 * o.b + jj) * m3 + 3 * o.a + ii] = o.tr ? B[3 * jj + ii] : B[3 * ii + jj];
+        F[(int64_t)col * m3 + row] = o.tr ? B[3 * jj + ii] : B[3 * ii + jj];
+    }
+    for (int q = 0; q < tk.ch_cnt; ++q) {
+        __syncthreads();
+        const AsmChild ch = tchild[tk.ch_off + q];
+        const SnDev C = sns[ch.c];
+        const int r3c = 3 * C.r, k3c = 3 * C.k, m3c = 3 * (C.k + C.r);
+        const int32_t* rm = relmap + C.rows_off;
+        const double* Fc = fronts + C.front_off;
+        const int nj = ch.jb - ch.ja;
+        for (int e = tid; e < nj * r3c; e += kT) {   // all (column, row) pairs in flight at once
+            const int j = ch.ja + e / r3c, i = e - (e / r3c) * r3c;
+            if (i < j) continue;
+            const int pj = 3 * rm[j / 3] + j % 3, pi = 3 * rm[i / 3] + i % 3;
+            F[(int64_t)pj * m3 + pi] += Fc[(int64_t)(k3c + j) * m3c + k3c + i];
+        }
+    }
+}
+
+// panel: one workgroup per front, one panel row per thread in registers (NT >= rows), right-
+// looking, two barriers per column (the pivot, then the column's first w entries, broadcast
+// through LDS).  The trailing matrix is left to chol_update.
+template <int NT>
+__global__ __launch_bounds__(NT) void chol_panel(const int2* __restrict__ tasks, const SnDev* __restrict__ sns,
+                                                   double* __restrict__ fronts, int32_t* __restrict__ status) {
+    __shared__ double s_col[kNB];
+    __shared__ double s_piv;
+    const int i = threadIdx.x;
+    const int2 tk = tasks[blockIdx.x];
+    const SnDev S = sns[tk.x];
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k;
+    const int j0 = tk.y, w = min(kNB, k3 - j0), R = m3 - j0;
+    double* F = fronts + S.front_off + (int64_t)j0 * m3 + j0;
+    double p[kNB];
+#pragma unroll
+    for (int c = 0; c < kNB; ++c) p[c] = (i < R && c < w && c <= i) ? F[(int64_t)c * m3 + i] : 0.0;
+#pragma unroll
+    for (int t = 0; t < kNB; ++t) {
+        if (t >= w) continue;
+        if (i == t) {
+            double d = p[t];
+            if (!(d > 0.0)) {
+                atomicExch(status, 1);
+                d = 1.0;
+            }
+            s_piv = sqrt(d);
+        }
+        __syncthreads();
+        const double piv = s_piv, inv = 1.0 / piv;
+        if (i == t) p[t] = piv;
+        else if (i > t && i < R) {
+            p[t] *= inv;
+            if (i < w) s_col[i] = p[t];
+        }
+        __syncthreads();
+        if (i > t && i < R) {
+            const double lt = p[t];
+#pragma unroll
+            for (int c = t + 1; c < kNB; ++c)
+                if (c < w && c <= i) p[c] -= lt * s_col[c];
+        }
+    }
+    if (i < R) {
+#pragma unroll
+        for (int c = 0; c < kNB; ++c)
+            if (c < w && c <= i) F[(int64_t)c * m3 + i] = p[c];
+    }
+}
+
+// update: one workgroup per 32x32 tile (rows i0.., cols l0..) of a front's trailing lower
+// triangle: F(i, l) -= sum_c L(i, j0 + c) L(l, j0 + c) over the panel's w columns.
+__global__ __launch_bounds__(kT) void chol_update(const int4* __restrict__ tasks, const SnDev* __restrict__ sns,
+                                                  double* __restrict__ fronts) {
+    __shared__ double A[kNB][33], B[kNB][33];
+    const int tid = threadIdx.x;
+    const int4 tk = tasks[blockIdx.x];
+    const SnDev S = sns[tk.x];
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k;
+    const int j0 = tk.y, w = min(kNB, k3 - j0), i0 = tk.z, l0 = tk.w;
+    double* F = fronts + S.front_off;
+    for (int e = tid; e < kNB * 32; e += kT) {
+        const int c = e >> 5, rr = e & 31;
+        A[c][rr] = (c < w && i0 + rr < m3) ? F[(int64_t)(j0 + c) * m3 + i0 + rr] : 0.0;
+        B[c][rr] = (c < w && l0 + rr < m3) ? F[(int64_t)(j0 + c) * m3 + l0 + rr] : 0.0;
     }
     __syncthreads();
-    for (int ci = 0; ci < S.nchild; ++ci) {   // extend-add, one child at a time
-        const int c = child_list[S.child_off + ci];
-        const SnDev C = sns[c];
-        const int r3c = 3 * C.r, k3c = 3 * C.k, m3c = 3 * (C.k + C.r);
-        const double* Fc = fronts + C.front_off;
-        const int32_t* rm = relmap + C.rows_off;
-        for (int e = tid; e < r3c * r3c; e += kT) {
-            const int i = e % r3c, j = e / r3c;
-            if (i < j) continue;
-            const int pi = 3 * rm[i / 3] + i % 3, pj = 3 * rm[j / 3] + j % 3;
-            F[pj * m3 + pi] += Fc[(k3c + j) * m3c + k3c + i];
-        }
-        __syncthreads();
+    const int tx = tid & 31, ty = tid >> 5;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int c = 0; c < w; ++c) {
+        const double a = A[c][tx];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[q] += a * B[c][4 * ty + q];
     }
-    // blocked right-looking partial Cholesky of the first k3 columns:
-    //   panel (R x w, R = rows from j0 down) in LDS, factored Crout-style (2 barriers / column),
-    //   then the trailing lower triangle updated by 4x4 register tiles (lower-triangle tiles only).
-    for (int j0 = 0; j0 < k3; j0 += kNB) {
-        const int w = min(kNB, k3 - j0), R = m3 - j0;
-        for (int e = tid; e < w * R; e += kT) {
-            const int t = e / R, i = e - t * R;
-            P[e] = F[(j0 + t) * m3 + j0 + i];
-        }
-        __syncthreads();
-        for (int t = 0; t < w; ++t) {
-            // column t: subtract the contributions of the panel's earlier columns (rows i >= t)
-            if (t > 0) {
-                for (int i = t + tid; i < R; i += kT) {
-                    double acc = 0.0;
-                    for (int s2 = 0; s2 < t; ++s2) acc += P[s2 * R + i] * P[s2 * R + t];
-                    P[t * R + i] -= acc;
-                }
-                __syncthreads();
-            }
-            double piv = P[t * R + t];
-            if (!(piv > 0.0)) {
-                if (tid == 0) atomicExch(status, 1);
-                piv = 1.0;
-            }
-            piv = sqrt(piv);
-            const double inv = 1.0 / piv;
-            __syncthreads();   // everyone has read the pivot before row t is overwritten
-            for (int i = t + tid; i < R; i += kT) P[t * R + i] = (i == t) ? piv : P[t * R + i] * inv;
-            __syncthreads();
-        }
-        for (int e = tid; e < w * R; e += kT) {
-            const int t = e / R, i = e - t * R;
-            if (i >= t) F[(j0 + t) * m3 + j0 + i] = P[e];
-        }
-        // trailing update: F(i, l) -= sum_t P(i, t) P(l, t) for w <= l <= i < R (panel-local)
-        const int T = R - w;
-        const int nt = (T + 3) >> 2;
-        const int ntiles = nt * (nt + 1) / 2;
-        for (int q = tid; q < ntiles; q += kT) {
-            int ti = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
-            while (ti * (ti + 1) / 2 > q) --ti;
-            while ((ti + 1) * (ti + 2) / 2 <= q) ++ti;
-            const int tl = q - ti * (ti + 1) / 2;
-            const int i0 = w + 4 * ti, l0 = w + 4 * tl;
-            double acc[4][4];
+    const int i = i0 + tx;
+    if (i >= m3) return;
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) acc[r][c] = 0.0;
-            for (int t = 0; t < w; ++t) {
-                const double* Pt = P + t * R;
-                double a[4], b[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) a[r] = (i0 + r < R) ? Pt[i0 + r] : 0.0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) b[c] = (l0 + c < R) ? Pt[l0 + c] : 0.0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) acc[r][c] += a[r] * b[c];
-            }
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int l = l0 + c;
-                if (l >= R) continue;
-                double* col = F + (int64_t)(j0 + l) * m3 + j0;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = i0 + r;
-                    if (i < R && i >= l) col[i] -= acc[r][c];
-                }
-            }
-        }
-        __syncthreads();
+    for (int q = 0; q < 4; ++q) {
+        const int l = l0 + 4 * ty + q;
+        if (l < m3 && i >= l) F[(int64_t)l * m3 + i] -= acc[q];
     }
 }
 
@@ -303,8 +332,17 @@ struct CholDev {
     double* xsol = nullptr;
     int32_t* status = nullptr;
     std::vector<int32_t> level_ptr;
-    std::vector<size_t> lds_factor, lds_solve;   // per level
+    std::vector<size_t> lds_solve;   // per level
     int64_t nnzb_upper = 0;
+    // factorization task lists (device) and the per-level launch plan (host)
+    AsmTask* asm_tasks = nullptr;
+    AsmChild* asm_child = nullptr;
+    int2* panel_tasks = nullptr;
+    int4* upd_tasks = nullptr;
+    struct Step { int32_t panel_off, panel_cnt, rpt /* panel rows / kT, rounded up */, max_rows, upd_off, upd_cnt; };
+    struct Level { int32_t asm_off, asm_cnt; std::vector<Step> steps; };
+    std::vector<Level> plan;
+    int64_t n_launches = 0;
 };
 
 }  // namespace
@@ -313,7 +351,7 @@ extern "C" void dpg_chol_destroy(void* h) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!c) return;
     void* ptrs[] = {c->sns, c->omap, c->child_list, c->relmap, c->rows, c->level_list, c->perm, c->pos,
-                    c->fronts, c->acc, c->ysol, c->xsol, c->status};
+                    c->fronts, c->acc, c->ysol, c->xsol, c->status, c->asm_tasks, c->asm_child, c->panel_tasks, c->upd_tasks};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -357,6 +395,8 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
         per[(size_t)s].push_back(OEnt{(int32_t)(n + q), (int16_t)a, (int16_t)b, plo > phi ? 0 : 1, 0});
     }
+    for (auto& v : per)
+        std::sort(v.begin(), v.end(), [](const OEnt& x, const OEnt& y) { return x.b != y.b ? x.b < y.b : x.a < y.a; });
     std::vector<OEnt> omap;
     std::vector<SnDev> sns((size_t)S.ns);
     int64_t acc_total = 0;
@@ -377,18 +417,73 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         omap.insert(omap.end(), per[(size_t)s].begin(), per[(size_t)s].end());
     }
     c->level_ptr = S.level_ptr;
-    c->lds_factor.assign((size_t)S.n_levels, 0);
     c->lds_solve.assign((size_t)S.n_levels, 0);
+    std::vector<AsmTask> asm_t;
+    std::vector<AsmChild> asm_c;
+    std::vector<int2> panel_t;
+    std::vector<int4> upd_t;
+    c->plan.assign((size_t)S.n_levels, CholDev::Level{});
     for (int32_t l = 0; l < S.n_levels; ++l) {
-        size_t mf = 0, ms = 0;
+        size_t ms = 0;
+        int32_t maxk3 = 0;
+        CholDev::Level& L = c->plan[(size_t)l];
+        L.asm_off = (int32_t)asm_t.size();
         for (int32_t q = S.level_ptr[(size_t)l]; q < S.level_ptr[(size_t)l + 1]; ++q) {
-            const SnDev& d = sns[(size_t)S.level_list[(size_t)q]];
-            mf = std::max(mf, (size_t)(3 * (d.k + d.r)) * kNB * sizeof(double));
-            ms = std::max(ms, (size_t)(kSB * kSB + 3 * (d.k + d.r)) * sizeof(double));
+            const int32_t s = S.level_list[(size_t)q];
+            const SnDev& d = sns[(size_t)s];
+            const int32_t m3 = 3 * (d.k + d.r);
+            ms = std::max(ms, (size_t)(kSB * kSB + m3) * sizeof(double));
+            maxk3 = std::max(maxk3, 3 * d.k);
+            const OEnt* ob = omap.data() + d.omap_off;
+            for (int32_t c0 = 0; c0 < m3; c0 += kCT) {
+                const int32_t c1 = std::min(c0 + kCT, m3);
+                AsmTask t{s, c0, 0, 0, (int32_t)asm_c.size(), 0};
+                // omap entries with block column in [c0 / 3, (c1 - 1) / 3]
+                t.om_b = (int32_t)d.omap_off + (int32_t)(std::lower_bound(ob, ob + d.omap_n, c0 / 3,
+                             [](const OEnt& o, int32_t v) { return o.b < v; }) - ob);
+                t.om_e = (int32_t)d.omap_off + (int32_t)(std::upper_bound(ob, ob + d.omap_n, (c1 - 1) / 3,
+                             [](int32_t v, const OEnt& o) { return v < o.b; }) - ob);
+                for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
+                    const int32_t ch = S.child_list[(size_t)ci];
+                    const SnDev& cd = sns[(size_t)ch];
+                    const int32_t* rm = S.relmap.data() + cd.rows_off;
+                    int32_t ja = 3 * cd.r, jb = 0;
+                    for (int32_t j = 0; j < 3 * cd.r; ++j) {
+                        const int32_t pj = 3 * rm[j / 3] + j % 3;
+                        if (pj >= c0 && pj < c1) { ja = std::min(ja, j); jb = j + 1; }
+                    }
+                    if (jb > ja) asm_c.push_back(AsmChild{ch, ja, jb, 0});
+                }
+                t.ch_cnt = (int32_t)asm_c.size() - t.ch_off;
+                asm_t.push_back(t);
+            }
         }
-        c->lds_factor[(size_t)l] = mf;
+        L.asm_cnt = (int32_t)asm_t.size() - L.asm_off;
+        c->n_launches += 1;
+        for (int32_t j0 = 0; j0 < maxk3; j0 += kNB) {
+            CholDev::Step st{(int32_t)panel_t.size(), 0, 1, 0, (int32_t)upd_t.size(), 0};
+            int32_t maxR = 0;
+            for (int32_t q = S.level_ptr[(size_t)l]; q < S.level_ptr[(size_t)l + 1]; ++q) {
+                const int32_t s = S.level_list[(size_t)q];
+                const SnDev& d = sns[(size_t)s];
+                const int32_t m3 = 3 * (d.k + d.r), k3 = 3 * d.k;
+                if (k3 <= j0) continue;
+                panel_t.push_back(make_int2(s, j0));
+                maxR = std::max(maxR, m3 - j0);
+                const int32_t base = j0 + std::min(kNB, k3 - j0), nt = (m3 - base + kUT - 1) / kUT;
+                for (int32_t ti = 0; ti < nt; ++ti)
+                    for (int32_t tl = 0; tl <= ti; ++tl) upd_t.push_back(make_int4(s, j0, base + kUT * ti, base + kUT * tl));
+            }
+            st.panel_cnt = (int32_t)panel_t.size() - st.panel_off;
+            st.upd_cnt = (int32_t)upd_t.size() - st.upd_off;
+            st.max_rows = maxR;
+            st.rpt = maxR <= kT ? 1 : maxR <= 2 * kT ? 2 : maxR <= 4 * kT ? 4 : 0;
+            if (st.rpt == 0) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
+            L.steps.push_back(st);
+            c->n_launches += 1 + (st.upd_cnt > 0);
+        }
         c->lds_solve[(size_t)l] = ms;
-        if (mf > 160 * 1024 || ms > 160 * 1024) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
+        if (ms > 160 * 1024) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
     }
     int rc = 0;
     rc |= dalloc_copy(&c->sns, sns);
@@ -399,6 +494,10 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     rc |= dalloc_copy(&c->level_list, S.level_list);
     rc |= dalloc_copy(&c->perm, S.perm);
     rc |= dalloc_copy(&c->pos, S.pos);
+    rc |= dalloc_copy(&c->asm_tasks, asm_t);
+    rc |= dalloc_copy(&c->asm_child, asm_c);
+    rc |= dalloc_copy(&c->panel_tasks, panel_t);
+    rc |= dalloc_copy(&c->upd_tasks, upd_t);
     rc |= hipMalloc(reinterpret_cast<void**>(&c->fronts), std::max<size_t>((size_t)S.front_off[(size_t)S.ns], 1) * 8) != hipSuccess;
     rc |= hipMalloc(reinterpret_cast<void**>(&c->acc), std::max<size_t>((size_t)acc_total, 1) * 8) != hipSuccess;
     rc |= hipMalloc(reinterpret_cast<void**>(&c->ysol), (size_t)(3 * n) * 8) != hipSuccess;
@@ -416,9 +515,17 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     const double* g = hb + 9 * c->nnzb_upper;
     if (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess) return DPG_ERR_HIP;
     for (int32_t l = 0; l < S.n_levels; ++l) {
-        const int32_t b = c->level_ptr[(size_t)l], cnt = c->level_ptr[(size_t)l + 1] - b;
-        hipLaunchKernelGGL(chol_factor_level, dim3(cnt), dim3(kT), c->lds_factor[(size_t)l], st, c->level_list + b,
-                           c->sns, c->omap, hb, c->child_list, c->relmap, c->fronts, c->status);
+        const CholDev::Level& L = c->plan[(size_t)l];
+        hipLaunchKernelGGL(chol_assemble, dim3(L.asm_cnt), dim3(kT), 0, st, c->asm_tasks + L.asm_off, c->asm_child,
+                           c->sns, c->omap, hb, c->relmap, c->fronts);
+        for (const CholDev::Step& p : L.steps) {
+            const int2* pt = c->panel_tasks + p.panel_off;
+            if (p.rpt == 1) hipLaunchKernelGGL(chol_panel<kT>, dim3(p.panel_cnt), dim3(kT), 0, st, pt, c->sns, c->fronts, c->status);
+            else if (p.rpt == 2) hipLaunchKernelGGL(chol_panel<2 * kT>, dim3(p.panel_cnt), dim3(2 * kT), 0, st, pt, c->sns, c->fronts, c->status);
+            else hipLaunchKernelGGL(chol_panel<4 * kT>, dim3(p.panel_cnt), dim3(4 * kT), 0, st, pt, c->sns, c->fronts, c->status);
+            if (p.upd_cnt > 0)
+                hipLaunchKernelGGL(chol_update, dim3(p.upd_cnt), dim3(kT), 0, st, c->upd_tasks + p.upd_off, c->sns, c->fronts);
+        }
     }
     for (int32_t l = 0; l < S.n_levels; ++l) {
         const int32_t b = c->level_ptr[(size_t)l], cnt = c->level_ptr[(size_t)l + 1] - b;
