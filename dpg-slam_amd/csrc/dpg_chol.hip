@@ -11,9 +11,9 @@
 //     panel:  one workgroup per front, one panel row per thread in registers, right-looking;
 //     update: one workgroup per 32x32 tile of every front's trailing lower triangle (SYRK),
 //             so a large front's Schur complement is spread over many CUs;
-//   forward:  L y = -g  (children's pending row updates gathered, diagonal blocks solved by one
-//             wave from LDS, L21 y passed up);
-//   backward: L^T x = y (ancestors' x gathered by row position).
+//   forward:  L y = -g, ONE launch: fronts as a DAG (children's pending row updates gathered,
+//             diagonal blocks solved by one wave from LDS, L21 y handed to the parent);
+//   backward: L^T x = y, ONE launch, top-down (ancestors' x gathered by row position).
 // fp64 throughout; the fronts of one factorization stay resident in HBM (tens of MB).
 
 #include <hip/hip_runtime.h>
@@ -43,7 +43,7 @@ struct SnDev {
     int64_t child_off;          // into child_list
     int64_t omap_off;
     int64_t acc_off;            // doubles (3r pending row updates of the forward solve)
-    int32_t omap_n, pad;
+    int32_t omap_n, parent;     // parent supernode, -1 at a root
 };
 
 struct OEnt {                   // one upper 3x3 block of H -> its front position
@@ -188,17 +188,55 @@ __global__ __launch_bounds__(kT) void chol_update(const int4* __restrict__ tasks
     }
 }
 
-__global__ __launch_bounds__(kT) void chol_forward_level(const int32_t* __restrict__ level_sn,
-                                                         const SnDev* __restrict__ sns,
-                                                         const int32_t* __restrict__ child_list,
-                                                         const int32_t* __restrict__ relmap,
-                                                         const double* __restrict__ fronts,
-                                                         const double* __restrict__ g,
-                                                         const int32_t* __restrict__ perm,
-                                                         double* __restrict__ ysol, double* __restrict__ acc) {
+// ---- triangular solves: ONE launch each, fronts as a dependency DAG ----
+// Workgroups claim fronts through an atomic ticket in topological order (forward: leaves first;
+// backward: root first), so a workgroup only ever waits on fronts already claimed by running
+// workgroups.  Hand-off (cdna_hip_programming.md Guideline 16): the payload is written with
+// agent-scope (sc1, write-through) stores, drained (s_waitcnt vmcnt(0)) and the workgroup
+// synchronised before ONE lane signals with an agent-scope atomic; the consumer polls relaxed,
+// then one agent-scope acquire, then agent-scope loads.  Every spin is bounded: on timeout the
+// status word gets 2 and the solve reports failure instead of hanging.
+using u64 = unsigned long long;
+
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store(reinterpret_cast<u64*>(p), (u64)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(double* p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load(reinterpret_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void wait_geq(int32_t* w, int32_t target, int32_t* status) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {
+            atomicExch(status, 2);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+__device__ __forceinline__ int claim(const int32_t* order, int32_t* ticket) {
+    __shared__ int s_task;
+    if (threadIdx.x == 0) s_task = order[atomicAdd(ticket, 1)];
+    __syncthreads();
+    return s_task;
+}
+
+// forward: L y = -g.  A front gathers its children's pending row updates (child order: fixed
+// summation order), solves its diagonal blocks (one wave, LDS), then hands L21 y to its parent.
+__global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict__ order, int32_t* sync,
+                                                       int32_t* status, const SnDev* __restrict__ sns,
+                                                       const int32_t* __restrict__ child_list,
+                                                       const int32_t* __restrict__ relmap,
+                                                       const double* __restrict__ fronts,
+                                                       const double* __restrict__ g,
+                                                       const int32_t* __restrict__ perm,
+                                                       double* __restrict__ ysol, double* acc) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int s = level_sn[blockIdx.x];
+    const int s = claim(order, sync);
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
@@ -210,6 +248,10 @@ __global__ __launch_bounds__(kT) void chol_forward_level(const int32_t* __restri
         y[t] = -g[3 * node + t % 3];
     }
     for (int t = tid; t < r3; t += kT) aR[t] = 0.0;
+    if (S.nchild > 0) {
+        if (tid == 0) wait_geq(sync + 1 + s, S.nchild, status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
     for (int ci = 0; ci < S.nchild; ++ci) {
         const int c = child_list[S.child_off + ci];
@@ -217,7 +259,7 @@ __global__ __launch_bounds__(kT) void chol_forward_level(const int32_t* __restri
         const int32_t* rm = relmap + C.rows_off;
         for (int t = tid; t < 3 * C.r; t += kT) {
             const int li = 3 * rm[t / 3] + t % 3;
-            const double v = acc[C.acc_off + t];
+            const double v = ld_agent(acc + C.acc_off + t);
             if (li < k3) y[li] -= v;
             else aR[li - k3] += v;
         }
@@ -250,27 +292,37 @@ __global__ __launch_bounds__(kT) void chol_forward_level(const int32_t* __restri
     for (int t = tid; t < r3; t += kT) {
         double sacc = 0.0;
         for (int j = 0; j < k3; ++j) sacc += F[j * m3 + k3 + t] * y[j];
-        acc[S.acc_off + t] = aR[t] + sacc;
+        st_agent(acc + S.acc_off + t, aR[t] + sacc);
     }
     for (int t = tid; t < k3; t += kT) ysol[3 * (int64_t)S.c0 + t] = y[t];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && S.parent >= 0)
+        __hip_atomic_fetch_add(sync + 1 + S.parent, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kT) void chol_backward_level(const int32_t* __restrict__ level_sn,
-                                                          const SnDev* __restrict__ sns,
-                                                          const int32_t* __restrict__ rows,
-                                                          const double* __restrict__ fronts,
-                                                          const double* __restrict__ ysol,
-                                                          double* __restrict__ xsol) {
+// backward: L^T x = y.  A front waits for its parent (hence every ancestor), gathers x at its row
+// positions, solves, and publishes its own x.
+__global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
+                                                        int32_t* status, const SnDev* __restrict__ sns,
+                                                        const int32_t* __restrict__ rows,
+                                                        const double* __restrict__ fronts,
+                                                        const double* __restrict__ ysol, double* xsol) {
     extern __shared__ __attribute__((aligned(16))) double sm[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int s = level_sn[blockIdx.x];
+    const int s = claim(order, sync);
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     double* D = sm;
     double* z = sm + kSB * kSB;      // k3
     double* xr = z + k3;             // r3
-    for (int t = tid; t < r3; t += kT) xr[t] = xsol[3 * (int64_t)rows[S.rows_off + t / 3] + t % 3];
+    if (S.parent >= 0) {
+        if (tid == 0) wait_geq(sync + 1 + S.parent, 1, status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rows[S.rows_off + t / 3] + t % 3);
     __syncthreads();
     for (int j = tid; j < k3; j += kT) {
         double sacc = 0.0;
@@ -303,7 +355,10 @@ __global__ __launch_bounds__(kT) void chol_backward_level(const int32_t* __restr
         }
         __syncthreads();
     }
-    for (int j = tid; j < k3; j += kT) xsol[3 * (int64_t)S.c0 + j] = z[j];
+    for (int j = tid; j < k3; j += kT) st_agent(xsol + 3 * (int64_t)S.c0 + j, z[j]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(sync + 1 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T>
@@ -335,6 +390,11 @@ struct CholDev {
     std::vector<size_t> lds_solve;   // per level
     int64_t nnzb_upper = 0;
     // factorization task lists (device) and the per-level launch plan (host)
+    int32_t* order_fwd = nullptr;      // fronts bottom-up (level order) / top-down
+    int32_t* order_bwd = nullptr;
+    int32_t* sync = nullptr;           // [ticket_f, cnt_f[ns], ticket_b, done_b[ns]], zeroed per solve
+    size_t sync_bytes = 0;
+    size_t lds_solve_max = 0;
     AsmTask* asm_tasks = nullptr;
     AsmChild* asm_child = nullptr;
     int2* panel_tasks = nullptr;
@@ -351,7 +411,8 @@ extern "C" void dpg_chol_destroy(void* h) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!c) return;
     void* ptrs[] = {c->sns, c->omap, c->child_list, c->relmap, c->rows, c->level_list, c->perm, c->pos,
-                    c->fronts, c->acc, c->ysol, c->xsol, c->status, c->asm_tasks, c->asm_child, c->panel_tasks, c->upd_tasks};
+                    c->fronts, c->acc, c->ysol, c->xsol, c->status, c->asm_tasks, c->asm_child, c->panel_tasks, c->upd_tasks,
+                    c->order_fwd, c->order_bwd, c->sync};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -412,7 +473,7 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         d.omap_off = (int64_t)omap.size();
         d.omap_n = (int32_t)per[(size_t)s].size();
         d.acc_off = acc_total;
-        d.pad = 0;
+        d.parent = S.sn_parent[(size_t)s];
         acc_total += 3 * d.r;
         omap.insert(omap.end(), per[(size_t)s].begin(), per[(size_t)s].end());
     }
@@ -495,6 +556,14 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     rc |= dalloc_copy(&c->perm, S.perm);
     rc |= dalloc_copy(&c->pos, S.pos);
     rc |= dalloc_copy(&c->asm_tasks, asm_t);
+    {
+        std::vector<int32_t> bwd(S.level_list.rbegin(), S.level_list.rend());
+        rc |= dalloc_copy(&c->order_fwd, S.level_list);
+        rc |= dalloc_copy(&c->order_bwd, bwd);
+        c->sync_bytes = ((size_t)(2 + 2 * S.ns) * sizeof(int32_t) + 15) & ~size_t(15);
+        rc |= hipMalloc(reinterpret_cast<void**>(&c->sync), c->sync_bytes) != hipSuccess;
+        for (size_t v : c->lds_solve) c->lds_solve_max = std::max(c->lds_solve_max, v);
+    }
     rc |= dalloc_copy(&c->asm_child, asm_c);
     rc |= dalloc_copy(&c->panel_tasks, panel_t);
     rc |= dalloc_copy(&c->upd_tasks, upd_t);
@@ -527,16 +596,13 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
                 hipLaunchKernelGGL(chol_update, dim3(p.upd_cnt), dim3(kT), 0, st, c->upd_tasks + p.upd_off, c->sns, c->fronts);
         }
     }
-    for (int32_t l = 0; l < S.n_levels; ++l) {
-        const int32_t b = c->level_ptr[(size_t)l], cnt = c->level_ptr[(size_t)l + 1] - b;
-        hipLaunchKernelGGL(chol_forward_level, dim3(cnt), dim3(kT), c->lds_solve[(size_t)l], st, c->level_list + b,
-                           c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc);
-    }
-    for (int32_t l = S.n_levels - 1; l >= 0; --l) {
-        const int32_t b = c->level_ptr[(size_t)l], cnt = c->level_ptr[(size_t)l + 1] - b;
-        hipLaunchKernelGGL(chol_backward_level, dim3(cnt), dim3(kT), c->lds_solve[(size_t)l], st, c->level_list + b,
-                           c->sns, c->rows, c->fronts, c->ysol, c->xsol);
-    }
+    if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
+    int32_t* sync_f = c->sync;
+    int32_t* sync_b = c->sync + 1 + S.ns;
+    hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc);
+    hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
+                       c->sns, c->rows, c->fronts, c->ysol, c->xsol);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

@@ -5,12 +5,14 @@
 // laser scans: a scan is uniform in ANGLE, not in space (near the sensor its points are a few mm
 // apart, far away tens of cm), so every cloud is indexed by the angle of its points around the
 // node origin:
-//   angle_index_kernel: per node, points sorted by atan2 (bitonic sort in LDS) + a table of the
-//     first sorted position of each of B uniform angle buckets.
-//   exactness: every point p with |p - q| <= rho satisfies |angle(p) - angle(q)| <= asin(rho/|q|)
-//     (|q| > rho), so a query scans the contiguous sorted range of the buckets covering
-//     [angle(q) -+ (asin(rho'/|q|) + margin)]; the bucket map is the same monotone float function
-//     at build and query time; queries within rho' of the origin scan everything.
+//   angle_index_kernel: per node, points sorted by pseudo-angle (the "diamond angle" in [0, 4), a
+//     monotone function of atan2 computed with one division) by a bitonic sort in LDS, plus a table
+//     of the first sorted position of each of B uniform pseudo-angle buckets.
+//   exactness: every point p with |p - q| <= rho lies within the angle asin(rho/|q|) of q
+//     (|q| > rho); the window's edges are q rotated by -+ that angle (sin = rho'/|q|, cos by sqrt:
+//     no transcendental), their pseudo-angles widened by a margin far above float error, and the
+//     bucket map is the same monotone float function at build and query time; queries within rho'
+//     of the origin scan everything.
 //   icp_ang_kernel (one workgroup per edge, all iterations resident in LDS):
 //     forward 1-NN: radius = distance to the previous iteration's match (r when unseeded), the
 //       window scan keeps the exact (distance, lowest index) argmin;
@@ -32,12 +34,25 @@ namespace {
 constexpr int kT = 256;
 constexpr int kW = kT / 64;
 constexpr int kSums = 10;
-constexpr int kB = 512;                         // angle buckets per cloud
-constexpr float kPi = 3.14159265358979323846f;
-constexpr float kBucketScale = (float)kB / (2.0f * 3.14159265358979323846f);
+constexpr int kB = 512;                         // pseudo-angle buckets per cloud
+constexpr float kBucketScale = (float)kB / 4.0f;
+constexpr float kPaMargin = 1e-5f;              // pseudo-angle margin (float error is ~5e-7)
 
-__device__ __forceinline__ int bucket_of(float th) {
-    int b = (int)floorf((th + kPi) * kBucketScale);
+// pseudo-angle in [0, 4): strictly increasing with atan2(y, x) taken in [0, 2 pi); 0 at the origin
+__device__ __forceinline__ float pseudo_angle(float x, float y) {
+    if (y >= 0.0f) {
+        if (x >= 0.0f) {
+            const float s = x + y;
+            return s > 0.0f ? y / s : 0.0f;
+        }
+        return 1.0f + (-x) / (y - x);
+    }
+    if (x < 0.0f) return 2.0f + (-y) / (-x - y);
+    return 3.0f + x / (x - y);
+}
+
+__device__ __forceinline__ int bucket_of(float pa) {
+    int b = (int)floorf(pa * kBucketScale);
     return min(max(b, 0), kB - 1);
 }
 
@@ -67,7 +82,7 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
     for (int s = tid; s < P; s += kT) {
         if (s < N) {
             const float2 p = ds_pts[off + s];
-            key[s] = ((uint64_t)orderable(atan2f(p.y, p.x)) << 32) | (uint32_t)s;
+            key[s] = ((uint64_t)orderable(pseudo_angle(p.x, p.y)) << 32) | (uint32_t)s;
         } else {
             key[s] = ~0ull;
         }
@@ -90,11 +105,11 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
         const float2 p = ds_pts[off + o];
         idx_pts[off + s] = p;
         idx_orig[off + s] = (uint16_t)o;
-        const int b = bucket_of(atan2f(p.y, p.x));
+        const int b = bucket_of(pseudo_angle(p.x, p.y));
         int bp = -1;
         if (s > 0) {
             const float2 pp = ds_pts[off + (int)(key[s - 1] & 0xffffffffu)];
-            bp = bucket_of(atan2f(pp.y, pp.x));
+            bp = bucket_of(pseudo_angle(pp.x, pp.y));
         }
         for (int bb = bp + 1; bb <= b; ++bb) bk[bb] = (uint16_t)s;   // first sorted position >= bucket
         if (s == N - 1)
@@ -104,10 +119,10 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
 
 struct Lds {
     float2* tp;       // target points sorted by angle
-    float2* sp;       // source points sorted by angle (source node frame)
-    float2* sc;       // current (moved) source points, original order
+    float2* scs;      // current (moved) source points, in the source's angle order
     uint16_t* ti;     // target sorted -> original index
     uint16_t* si;     // source sorted -> original index
+    uint16_t* spos;   // source original index -> sorted position
     uint16_t* tb;     // target bucket starts [kB+1]
     uint16_t* sb;     // source bucket starts [kB+1]
     double* wpart;    // [kW][kSums + 2]
@@ -119,10 +134,10 @@ __device__ Lds carve(unsigned char* base, int cap) {
     Lds L;
     size_t o = 0;
     L.tp = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
-    L.sp = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
-    L.sc = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
+    L.scs = reinterpret_cast<float2*>(base + o);  o = a16(o + 8 * (size_t)cap);
     L.ti = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
     L.si = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
+    L.spos = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
     L.tb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
     L.sb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
     L.wpart = reinterpret_cast<double*>(base + o);
@@ -138,24 +153,21 @@ __device__ __forceinline__ float sqd(float ax, float ay, float bx, float by) {
 // the number of ranges (1 or 2), or 0 meaning "scan everything".
 __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int r0[2], int r1[2]) {
     const float rq = sqrtf(qx * qx + qy * qy);
-    const float ratio = rad / rq;
-    if (!(ratio < 0.7f)) return 0;
-    const float half = asinf(ratio) * 1.0001f + 2e-4f;
-    const float th = atan2f(qy, qx);
-    float lo = th - half, hi = th + half;
-    if (lo < -kPi) {
-        r0[0] = bk[bucket_of(lo + 2.0f * kPi)]; r1[0] = n;
-        r0[1] = 0; r1[1] = bk[bucket_of(hi) + 1];
-        return 2;
+    const float sn = rad / rq * 1.0001f + 1e-6f;   // sine of the half-angle, widened
+    if (!(sn < 0.7f)) return 0;
+    const float cs = sqrtf(1.0f - sn * sn);
+    float lo = pseudo_angle(cs * qx + sn * qy, cs * qy - sn * qx) - kPaMargin;   // q rotated by -half
+    float hi = pseudo_angle(cs * qx - sn * qy, cs * qy + sn * qx) + kPaMargin;   // q rotated by +half
+    if (lo < 0.0f) lo += 4.0f;
+    if (hi >= 4.0f) hi -= 4.0f;
+    if (lo <= hi) {
+        r0[0] = bk[bucket_of(lo)];
+        r1[0] = bk[bucket_of(hi) + 1];
+        return 1;
     }
-    if (hi > kPi) {
-        r0[0] = bk[bucket_of(lo)]; r1[0] = n;
-        r0[1] = 0; r1[1] = bk[bucket_of(hi - 2.0f * kPi) + 1];
-        return 2;
-    }
-    r0[0] = bk[bucket_of(lo)];
-    r1[0] = bk[bucket_of(hi) + 1];
-    return 1;
+    r0[0] = bk[bucket_of(lo)]; r1[0] = n;         // the window straddles pseudo-angle 0
+    r0[1] = 0; r1[1] = bk[bucket_of(hi) + 1];
+    return 2;
 }
 
 template <int PPT>
@@ -177,9 +189,10 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
         L.tp[i] = idx_pts[E.tgt_ds_off + i];
         L.ti[i] = idx_orig[E.tgt_ds_off + i];
     }
-    for (int i = t; i < N; i += kT) {
-        L.sp[i] = idx_pts[E.src_ds_off + i];
-        L.si[i] = idx_orig[E.src_ds_off + i];
+    for (int s = t; s < N; s += kT) {
+        const uint16_t o = idx_orig[E.src_ds_off + s];
+        L.si[s] = o;
+        L.spos[o] = (uint16_t)s;
     }
     for (int b = t; b <= kB; b += kT) {
         L.tb[b] = buckets[(size_t)vt * (kB + 1) + b];
@@ -188,19 +201,22 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
     float F[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) F[q] = E.guess[q];
+    __syncthreads();
     float sx[PPT], sy[PPT];
-    int seed[PPT];
+    int seed[PPT], sp[PPT];
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
         const int i = t + kT * m;
         seed[m] = -1;
+        sp[m] = 0;
         sx[m] = 0.f;
         sy[m] = 0.f;
         if (i < N) {
             const float2 p = ds_pts[E.src_ds_off + i];
             sx[m] = (F[0] * p.x + F[1] * p.y) + F[2];
             sy[m] = (F[3] * p.x + F[4] * p.y) + F[5];
-            L.sc[i] = make_float2(sx[m], sy[m]);
+            sp[m] = L.spos[i];
+            L.scs[sp[m]] = make_float2(sx[m], sy[m]);
         }
     }
     __syncthreads();
@@ -260,13 +276,12 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
                 int r0[2], r1[2];
                 int nr = window(L.sb, N, px, py, rho, r0, r1);
                 if (nr == 0) { nr = 1; r0[0] = 0; r1[0] = N; }
+                const int me = sp[m];
                 for (int w = 0; w < nr && ok; ++w) {
                     for (int s = r0[w]; s < r1[w]; ++s) {
-                        const int kk = L.si[s];
-                        if (kk == i) continue;
-                        const float2 c = L.sc[kk];
+                        const float2 c = L.scs[s];
                         const float d = sqd(c.x, c.y, tj.x, tj.y);
-                        if (d < bd || (d == bd && kk < i)) { ok = false; break; }
+                        if (d <= bd && s != me && (d < bd || (int)L.si[s] < i)) { ok = false; break; }
                     }
                 }
             }
@@ -321,7 +336,7 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             const float x = sx[m], y = sy[m];
             sx[m] = (cf * x + nsf * y) + txf;
             sy[m] = (sf * x + cf * y) + tyf;
-            if (i < N) L.sc[i] = make_float2(sx[m], sy[m]);
+            if (i < N) L.scs[sp[m]] = make_float2(sx[m], sy[m]);
         }
         float Nf[6];
         Nf[0] = cf * F[0] + nsf * F[3];
@@ -370,7 +385,7 @@ extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) {
     size_t o = 0;
     o = al(o + 8 * (size_t)cap);
     o = al(o + 8 * (size_t)cap);
-    o = al(o + 8 * (size_t)cap);
+    o = al(o + 2 * (size_t)cap);
     o = al(o + 2 * (size_t)cap);
     o = al(o + 2 * (size_t)cap);
     o = al(o + 2 * (size_t)(kB + 1));
