@@ -19,6 +19,10 @@ const int32_t* dpg_chol_pos_dev(void* chol);
 const double* dpg_chol_x_dev(void* chol);
 const int32_t* dpg_chol_status_dev(void* chol);
 void dpg_chol_stats(void* chol, double out[6]);
+#ifdef DPG_CHOL_TIMING
+int dpg_chol_prof_dump(unsigned long long* out, int n, unsigned long long* span);
+int dpg_chol_prof_reset(void);
+#endif
 }
 
 #define CK(x)                                                                        \
@@ -129,6 +133,49 @@ int main(int argc, char** argv) {
     printf("{\"n\": %lld, \"pairs\": %lld, \"supernodes\": %.0f, \"levels\": %.0f, \"max_front\": %.0f, "
            "\"mflop\": %.1f, \"ms_per_solve\": %.4f, \"residual_rel\": %.3e, \"status\": %d}\n",
            (long long)n, (long long)P, st[0], st[1], st[2], st[3] / 1e6, ms / iters, rmax / gmax, status);
+#ifdef DPG_CHOL_TIMING
+    {
+        // phase marks of workgroup 0 of every factor launch of the last solve (10 ns ticks)
+        const int slots = 40, nl = 512, nw = 2048;
+        std::vector<unsigned long long> pr((size_t)slots * 4096, 0ull), span((size_t)nl * nw * 2);
+        if (dpg_chol_prof_reset()) return 1;
+        if (dpg_chol_solve(ch, d_hb, s)) return 1;
+        CK(hipStreamSynchronize(s));
+        if (dpg_chol_prof_dump(pr.data(), slots * 4096, span.data()) == 0) {
+            unsigned long long prev_end = 0;
+            double tot = 0.0;
+            for (int l = 0; l < nl; ++l) {
+                const unsigned long long* m = pr.data() + (size_t)l * slots;
+                if (!m[0]) break;
+                unsigned long long smin = ~0ull, smax = 0, emax = 0;
+                int nwg = 0, slow = 0;
+                double dmax = 0.0;
+                for (int b = 0; b < nw; ++b) {
+                    const unsigned long long s0 = span[((size_t)l * nw + b) * 2], e0 = span[((size_t)l * nw + b) * 2 + 1];
+                    if (!s0) break;
+                    ++nwg;
+                    smin = s0 < smin ? s0 : smin;
+                    smax = s0 > smax ? s0 : smax;
+                    emax = e0 > emax ? e0 : emax;
+                    if ((double)(e0 - s0) > dmax) { dmax = (double)(e0 - s0); slow = b; }
+                }
+                unsigned long long last = m[0];
+                printf("L%03d gap %5.2f span %6.2f wgs %4d last-start %6.2f slowest wg %4d %6.2f | wg0:", l,
+                       prev_end ? ((double)smin - (double)prev_end) / 100.0 : 0.0, (double)(emax - smin) / 100.0, nwg,
+                       (double)(smax - smin) / 100.0, slow, dmax / 100.0);
+                tot += (double)(emax - smin) / 100.0;
+                for (int k = 1; k < slots; ++k)
+                    if (m[k]) {
+                        printf(" %d:%.2f", k, (double)(m[k] - last) / 100.0);
+                        last = m[k];
+                    }
+                printf("\n");
+                prev_end = emax;
+            }
+            printf("sum of spans %.1f us\n", tot);
+        }
+    }
+#endif
     dpg_chol_destroy(ch);
     return (rmax / gmax < 1e-9 && status == 0) ? 0 : 3;
 }

@@ -16,3 +16,4 @@ cat "$OUT/chol.log"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     tools/build/chol_bench "$OUT/pairs.bin" 5 > "$OUT/chol_prof.log" 2>&1
+timeout -k 10 120 tools/build/chol_bench_t "$OUT/pairs.bin" 1 > "$OUT/chol_timing.log" 2>&1
