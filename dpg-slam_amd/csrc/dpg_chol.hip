@@ -4,17 +4,20 @@
 // level-scheduled GPU factorization: the symbolic analysis (dpg_chol_sym.cpp) and the per-level
 // task lists run once per sparsity pattern; each GN iteration then runs, per elimination-tree
 // level, task-list kernels over all fronts of the level (dense fronts are column-major in HBM):
-//   assemble: one workgroup per (front, 32-column tile): zero, scatter the original 3x3 blocks
-//             of H, extend-add the children's update matrices (in child order: deterministic,
-//             no atomics);
-//   then per 32-column panel step:
-//     panel:  one workgroup per front, one panel row per thread in registers, right-looking;
+//   assemble: one workgroup per (front, 32-column tile), built in LDS: zero, scatter the
+//             original 3x3 blocks of H, add the children's update matrices child by child
+//             (deterministic order, no atomics), store once;
+//   then per 48-column panel step:
+//     panel:  one workgroup per front, one panel row per thread in registers, right-looking
+//             by 3x3 block columns;
 //     update: one workgroup per 32x32 tile of every front's trailing lower triangle (SYRK),
 //             so a large front's Schur complement is spread over many CUs;
 //   forward:  L y = -g, ONE launch: fronts as a DAG (children's pending row updates gathered,
 //             diagonal blocks solved by one wave from LDS, L21 y handed to the parent);
 //   backward: L^T x = y, ONE launch, top-down (ancestors' x gathered by row position).
-// fp64 throughout; the fronts of one factorization stay resident in HBM (tens of MB).
+// fp64 throughout, explicit fma in the inner products (this file is held to a tolerance, not to
+// bit-exactness; the build keeps -ffp-contract=off for the ICP kernels); the fronts of one
+// factorization stay resident in HBM (tens of MB).
 
 #include <hip/hip_runtime.h>
 #include <math.h>
@@ -31,10 +34,29 @@
 namespace {
 
 constexpr int kT = 256;     // threads per front workgroup
-constexpr int kNB = 32;     // factorization panel width (scalar columns)
+constexpr int kNB = 48;     // factorization panel width (scalar columns, 16 3x3 blocks)
 constexpr int kSB = 64;     // triangular-solve diagonal block
 constexpr int kCT = 32;     // assembly column tile
 constexpr int kUT = 32;     // trailing-update tile (rows and columns)
+
+// Phase timestamps (timing builds of tools/chol_bench only): workgroup 0 of launch `pid` writes
+// wall_clock64() (100 MHz) into slot [pid][k].
+#ifdef DPG_CHOL_TIMING
+constexpr int kProfSlots = 40;
+__device__ unsigned long long g_prof[4096 * kProfSlots];
+constexpr int kProfL = 512, kProfW = 2048;
+__device__ unsigned long long g_span[kProfL * kProfW * 2];   // per launch, per workgroup: start, end
+#define PROF_MARK(pid, k)                                                                       \
+    do {                                                                                        \
+        if (blockIdx.x == 0 && threadIdx.x == 0 && (pid) < 4096) g_prof[(pid) * kProfSlots + (k)] = wall_clock64(); \
+    } while (0)
+#define PROF_BEGIN(pid) do { if (threadIdx.x == 0 && (pid) < kProfL && blockIdx.x < kProfW) g_span[((size_t)(pid) * kProfW + blockIdx.x) * 2] = wall_clock64(); } while (0)
+#define PROF_END(pid) do { if (threadIdx.x == 0 && (pid) < kProfL && blockIdx.x < kProfW) g_span[((size_t)(pid) * kProfW + blockIdx.x) * 2 + 1] = wall_clock64(); } while (0)
+#else
+#define PROF_MARK(pid, k) do { } while (0)
+#define PROF_BEGIN(pid) do { } while (0)
+#define PROF_END(pid) do { } while (0)
+#endif
 
 struct SnDev {
     int32_t c0, k, r, nchild;   // k, r in 3x3 blocks
@@ -55,14 +77,15 @@ struct OEnt {                   // one upper 3x3 block of H -> its front positio
 // ---- numeric factorization: three task-list kernels per elimination-tree level ----
 // (task lists are built once per sparsity pattern in dpg_chol_create)
 
-// assembly: one workgroup per (front, kCT-column tile) -- zero the lower part of the tile's
-// columns, scatter the original H blocks, then extend-add the children's update matrices in child
-// order (a barrier between children: every element is summed in the same order on every run).
-// The omap range and each child's column range [ja, jb) for the tile are precomputed on the host.
+// assembly: one workgroup per (front, kCT-column tile), built in LDS: zeroed, the original H
+// blocks scattered in, then each child's update-matrix entries that land in the tile's columns
+// (contiguous child columns [ja, jb), precomputed) added child by child -- within a child the
+// map is injective, so all its entries are in flight at once; an LDS barrier between children
+// fixes the summation order.  The finished tile is stored once, coalesced.
 struct AsmTask {
     int32_t s, c0;              // front, first column of the tile
     int32_t om_b, om_e;         // omap entries whose block column meets the tile
-    int32_t ch_off, ch_cnt;     // into AsmChild
+    int32_t ch_off, ch_cnt;     // into AsmChild: the children with columns in the tile
 };
 struct AsmChild { int32_t c, ja, jb, pad; };
 
@@ -70,95 +93,155 @@ __global__ __launch_bounds__(kT) void chol_assemble(const AsmTask* __restrict__ 
                                                     const AsmChild* __restrict__ tchild,
                                                     const SnDev* __restrict__ sns,
                                                     const OEnt* __restrict__ omap, const double* __restrict__ hb,
-                                                    const int32_t* __restrict__ relmap, double* __restrict__ fronts) {
+                                                    const int32_t* __restrict__ relmap, double* __restrict__ fronts,
+                                                    int pid) {
+    extern __shared__ __attribute__((aligned(16))) double T[];   // [kCT][m3], column-major
     const int tid = threadIdx.x;
+    PROF_BEGIN(pid);
+    PROF_MARK(pid, 0);
     const AsmTask tk = tasks[blockIdx.x];
     const SnDev S = sns[tk.s];
     const int m3 = 3 * (S.k + S.r);
-    const int c0 = tk.c0, c1 = min(c0 + kCT, m3);
-    double* F = fronts + S.front_off;
-    for (int j = c0; j < c1; ++j)
-        for (int i = j + tid; i < m3; i += kT) F[(int64_t)j * m3 + i] = 0.0;
+    const int c0 = tk.c0, nc = min(c0 + kCT, m3) - c0;
+    for (int e = tid; e < nc * m3; e += kT) T[e] = 0.0;
     __syncthreads();
+    PROF_MARK(pid, 1);
     for (int q = tid; q < (tk.om_e - tk.om_b) * 9; q += kT) {
         const OEnt o = omap[tk.om_b + q / 9];
         const int ii = (q % 9) / 3, jj = q % 3;
         const int row = 3 * o.a + ii, col = 3 * o.b + jj;
-        if (col < c0 || col >= c1 || row < col) continue;
+        if (col < c0 || col >= c0 + nc || row < col) continue;
         const double* B = hb + 9 * (int64_t)o.u;
-        F[(int64_t)col * m3 + row] = o.tr ? B[3 * jj + ii] : B[3 * ii + jj];
+        T[(col - c0) * m3 + row] = o.tr ? B[3 * jj + ii] : B[3 * ii + jj];
     }
+    PROF_MARK(pid, 2);
     for (int q = 0; q < tk.ch_cnt; ++q) {
         __syncthreads();
         const AsmChild ch = tchild[tk.ch_off + q];
         const SnDev C = sns[ch.c];
         const int r3c = 3 * C.r, k3c = 3 * C.k, m3c = 3 * (C.k + C.r);
         const int32_t* rm = relmap + C.rows_off;
-        const double* Fc = fronts + C.front_off;
+        const double* Fc = fronts + C.front_off + (int64_t)k3c * m3c + k3c;
         const int nj = ch.jb - ch.ja;
-        for (int e = tid; e < nj * r3c; e += kT) {   // all (column, row) pairs in flight at once
-            const int j = ch.ja + e / r3c, i = e - (e / r3c) * r3c;
+        for (int e = tid; e < nj * r3c; e += kT) {
+            const int jl = e / r3c, i = e - jl * r3c, j = ch.ja + jl;
             if (i < j) continue;
             const int pj = 3 * rm[j / 3] + j % 3, pi = 3 * rm[i / 3] + i % 3;
-            F[(int64_t)pj * m3 + pi] += Fc[(int64_t)(k3c + j) * m3c + k3c + i];
+            T[(pj - c0) * m3 + pi] += Fc[(int64_t)j * m3c + i];
         }
     }
+    __syncthreads();
+    PROF_MARK(pid, 3);
+    double* F = fronts + S.front_off + (int64_t)c0 * m3;
+    for (int e = tid; e < nc * m3; e += kT) {
+        const int jl = e / m3, row = e - jl * m3;
+        if (row >= c0 + jl) F[e] = T[e];
+    }
+    PROF_MARK(pid, 4);
+    __syncthreads();
+    PROF_END(pid);
+}
+
+// 1/sqrt(d) from the hardware estimate and two Newton steps (full fp64 precision; far shorter
+// than the IEEE sqrt + divide expansions on the factorization's critical path).
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    const double h = 0.5 * d;
+    y = y * (1.5 - h * y * y);
+    y = y * (1.5 - h * y * y);
+    return y;
 }
 
 // panel: one workgroup per front, one panel row per thread in registers (NT >= rows), right-
-// looking, two barriers per column (the pivot, then the column's first w entries, broadcast
-// through LDS).  The trailing matrix is left to chol_update.
+// looking by 3x3 BLOCK columns (the system is 3x3-blocked, so panels are too): every thread
+// factors the 3x3 diagonal block itself, solves its own row's three entries, and the panel's block
+// rows are broadcast through LDS -- two barriers per three columns.  The block loop stays rolled
+// (compact code: these launches run on cold instruction caches): each step shifts the register
+// row by three so the current block is always p[0..2], and finished entries go straight to HBM.
+// The trailing matrix is left to chol_update.
 template <int NT>
 __global__ __launch_bounds__(NT) void chol_panel(const int2* __restrict__ tasks, const SnDev* __restrict__ sns,
-                                                   double* __restrict__ fronts, int32_t* __restrict__ status) {
-    __shared__ double s_col[kNB];
-    __shared__ double s_piv;
+                                                 double* __restrict__ fronts, int32_t* __restrict__ status, int pid) {
+    __shared__ double s_d[6];          // the current diagonal block (lower: 00 10 11 20 21 22)
+    __shared__ double4 s_l[kNB];       // L(c, 3b .. 3b+2) of the panel's own rows (w unused)
     const int i = threadIdx.x;
     const int2 tk = tasks[blockIdx.x];
     const SnDev S = sns[tk.x];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k;
     const int j0 = tk.y, w = min(kNB, k3 - j0), R = m3 - j0;
     double* F = fronts + S.front_off + (int64_t)j0 * m3 + j0;
+    PROF_BEGIN(pid);
+    PROF_MARK(pid, 0);
     double p[kNB];
 #pragma unroll
     for (int c = 0; c < kNB; ++c) p[c] = (i < R && c < w && c <= i) ? F[(int64_t)c * m3 + i] : 0.0;
+    PROF_MARK(pid, 1);
+    bool bad = false;
+#pragma unroll 1
+    for (int c0 = 0; c0 < w; c0 += 3) {
+        PROF_MARK(pid, 2 + c0 / 3);
+        if (i == c0) s_d[0] = p[0];
+        if (i == c0 + 1) { s_d[1] = p[0]; s_d[2] = p[1]; }
+        if (i == c0 + 2) { s_d[3] = p[0]; s_d[4] = p[1]; s_d[5] = p[2]; }
+        __syncthreads();
+        if (c0 == 3) PROF_MARK(pid, 22);
+        double d00 = s_d[0], d10 = s_d[1], d11 = s_d[2], d20 = s_d[3], d21 = s_d[4], d22 = s_d[5];
+        if (!(d00 > 0.0)) { bad = true; d00 = 1.0; }
+        const double i00 = rsqrt_nr(d00), l00 = d00 * i00;
+        const double l10 = d10 * i00, l20 = d20 * i00;
+        double e11 = d11 - l10 * l10;
+        if (!(e11 > 0.0)) { bad = true; e11 = 1.0; }
+        const double i11 = rsqrt_nr(e11), l11 = e11 * i11;
+        const double l21 = (d21 - l20 * l10) * i11;
+        double e22 = d22 - l20 * l20 - l21 * l21;
+        if (!(e22 > 0.0)) { bad = true; e22 = 1.0; }
+        const double i22 = rsqrt_nr(e22), l22 = e22 * i22;
+        double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+        if (i == c0) { x0 = l00; }
+        else if (i == c0 + 1) { x0 = l10; x1 = l11; }
+        else if (i == c0 + 2) { x0 = l20; x1 = l21; x2 = l22; }
+        else if (i > c0 + 2 && i < R) {
+            x0 = p[0] * i00;
+            x1 = (p[1] - x0 * l10) * i11;
+            x2 = (p[2] - x0 * l20 - x1 * l21) * i22;
+        }
+        if (i >= c0 && i < R) {
+            F[(int64_t)c0 * m3 + i] = x0;
+            if (i >= c0 + 1) F[(int64_t)(c0 + 1) * m3 + i] = x1;
+            if (i >= c0 + 2) F[(int64_t)(c0 + 2) * m3 + i] = x2;
+        }
+        if (c0 == 3) PROF_MARK(pid, 23);
+        if (i > c0 + 2 && i < w) s_l[i] = make_double4(x0, x1, x2, 0.0);
+        __syncthreads();
+        if (c0 == 3) PROF_MARK(pid, 24);
+        const bool upd = i > c0 + 2 && i < R;
 #pragma unroll
-    for (int t = 0; t < kNB; ++t) {
-        if (t >= w) continue;
-        if (i == t) {
-            double d = p[t];
-            if (!(d > 0.0)) {
-                atomicExch(status, 1);
-                d = 1.0;
+        for (int c = 3; c < kNB; ++c) {
+            const int cc = c0 + c;
+            double v = p[c];
+            if (upd && cc < w && cc <= i) {
+                const double4 l = s_l[cc];
+                v = fma(-x0, l.x, v);
+                v = fma(-x1, l.y, v);
+                v = fma(-x2, l.z, v);
             }
-            s_piv = sqrt(d);
+            p[c - 3] = v;
         }
-        __syncthreads();
-        const double piv = s_piv, inv = 1.0 / piv;
-        if (i == t) p[t] = piv;
-        else if (i > t && i < R) {
-            p[t] *= inv;
-            if (i < w) s_col[i] = p[t];
-        }
-        __syncthreads();
-        if (i > t && i < R) {
-            const double lt = p[t];
-#pragma unroll
-            for (int c = t + 1; c < kNB; ++c)
-                if (c < w && c <= i) p[c] -= lt * s_col[c];
-        }
+        p[kNB - 3] = p[kNB - 2] = p[kNB - 1] = 0.0;
+        if (c0 == 3) PROF_MARK(pid, 25);
     }
-    if (i < R) {
-#pragma unroll
-        for (int c = 0; c < kNB; ++c)
-            if (c < w && c <= i) F[(int64_t)c * m3 + i] = p[c];
-    }
+    if (bad && i == 0) atomicExch(status, 1);
+    PROF_MARK(pid, 20);
+    __syncthreads();
+    PROF_END(pid);
 }
 
 // update: one workgroup per 32x32 tile (rows i0.., cols l0..) of a front's trailing lower
 // triangle: F(i, l) -= sum_c L(i, j0 + c) L(l, j0 + c) over the panel's w columns.
 __global__ __launch_bounds__(kT) void chol_update(const int4* __restrict__ tasks, const SnDev* __restrict__ sns,
-                                                  double* __restrict__ fronts) {
+                                                  double* __restrict__ fronts, int pid) {
+    PROF_BEGIN(pid);
+    PROF_MARK(pid, 0);
     __shared__ double A[kNB][33], B[kNB][33];
     const int tid = threadIdx.x;
     const int4 tk = tasks[blockIdx.x];
@@ -177,15 +260,18 @@ __global__ __launch_bounds__(kT) void chol_update(const int4* __restrict__ tasks
     for (int c = 0; c < w; ++c) {
         const double a = A[c][tx];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[q] += a * B[c][4 * ty + q];
+        for (int q = 0; q < 4; ++q) acc[q] = fma(a, B[c][4 * ty + q], acc[q]);
     }
     const int i = i0 + tx;
-    if (i >= m3) return;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int l = l0 + 4 * ty + q;
-        if (l < m3 && i >= l) F[(int64_t)l * m3 + i] -= acc[q];
+        if (i < m3 && l < m3 && i >= l) F[(int64_t)l * m3 + i] -= acc[q];
     }
+#ifdef DPG_CHOL_TIMING
+    __syncthreads();
+    PROF_END(pid);
+#endif
 }
 
 // ---- triangular solves: ONE launch each, fronts as a dependency DAG ----
@@ -241,7 +327,8 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     double* D = sm;                  // kSB x kSB diagonal block
-    double* y = sm + kSB * kSB;      // k3
+    double* rd = sm + kSB * kSB;     // kSB reciprocals of its diagonal
+    double* y = rd + kSB;            // k3
     double* aR = y + k3;             // r3
     for (int t = tid; t < k3; t += kT) {
         const int node = perm[S.c0 + t / 3];
@@ -270,28 +357,29 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
         for (int e = tid; e < bw * bw; e += kT) {
             const int i = e % bw, j = e / bw;
             D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
+            if (i == j) rd[j] = 1.0 / D[j * kSB + i];
         }
         __syncthreads();
         if (wave == 0) {
             double yl = lane < bw ? y[jb + lane] : 0.0;
             for (int j = 0; j < bw; ++j) {
-                const double yj = __shfl(yl, j, 64) / D[j * kSB + j];
+                const double yj = __shfl(yl, j, 64) * rd[j];
                 if (lane == j) yl = yj;
-                else if (lane > j && lane < bw) yl -= D[j * kSB + lane] * yj;
+                else if (lane > j && lane < bw) yl = fma(-D[j * kSB + lane], yj, yl);
             }
             if (lane < bw) y[jb + lane] = yl;
         }
         __syncthreads();
         for (int i = jb + bw + tid; i < k3; i += kT) {
             double sacc = 0.0;
-            for (int j = 0; j < bw; ++j) sacc += F[(jb + j) * m3 + i] * y[jb + j];
+            for (int j = 0; j < bw; ++j) sacc = fma(F[(jb + j) * m3 + i], y[jb + j], sacc);
             y[i] -= sacc;
         }
         __syncthreads();
     }
     for (int t = tid; t < r3; t += kT) {
         double sacc = 0.0;
-        for (int j = 0; j < k3; ++j) sacc += F[j * m3 + k3 + t] * y[j];
+        for (int j = 0; j < k3; ++j) sacc = fma(F[j * m3 + k3 + t], y[j], sacc);
         st_agent(acc + S.acc_off + t, aR[t] + sacc);
     }
     for (int t = tid; t < k3; t += kT) ysol[3 * (int64_t)S.c0 + t] = y[t];
@@ -315,7 +403,8 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     double* D = sm;
-    double* z = sm + kSB * kSB;      // k3
+    double* rd = sm + kSB * kSB;     // kSB reciprocals of the diagonal block's diagonal
+    double* z = rd + kSB;            // k3
     double* xr = z + k3;             // r3
     if (S.parent >= 0) {
         if (tid == 0) wait_geq(sync + 1 + S.parent, 1, status);
@@ -326,7 +415,7 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     __syncthreads();
     for (int j = tid; j < k3; j += kT) {
         double sacc = 0.0;
-        for (int t = 0; t < r3; ++t) sacc += F[j * m3 + k3 + t] * xr[t];
+        for (int t = 0; t < r3; ++t) sacc = fma(F[j * m3 + k3 + t], xr[t], sacc);
         z[j] = ysol[3 * (int64_t)S.c0 + j] - sacc;
     }
     __syncthreads();
@@ -336,21 +425,22 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
         for (int e = tid; e < bw * bw; e += kT) {
             const int i = e % bw, j = e / bw;
             D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
+            if (i == j) rd[j] = 1.0 / D[j * kSB + i];
         }
         __syncthreads();
         if (wave == 0) {
             double zl = lane < bw ? z[jb + lane] : 0.0;
             for (int j = bw - 1; j >= 0; --j) {
-                const double xj = __shfl(zl, j, 64) / D[j * kSB + j];
+                const double xj = __shfl(zl, j, 64) * rd[j];
                 if (lane == j) zl = xj;
-                else if (lane < j) zl -= D[lane * kSB + j] * xj;   // L(jb+j, jb+lane)
+                else if (lane < j) zl = fma(-D[lane * kSB + j], xj, zl);   // L(jb+j, jb+lane)
             }
             if (lane < bw) z[jb + lane] = zl;
         }
         __syncthreads();
         for (int j = tid; j < jb; j += kT) {
             double sacc = 0.0;
-            for (int i = 0; i < bw; ++i) sacc += F[j * m3 + jb + i] * z[jb + i];
+            for (int i = 0; i < bw; ++i) sacc = fma(F[j * m3 + jb + i], z[jb + i], sacc);
             z[j] -= sacc;
         }
         __syncthreads();
@@ -400,7 +490,7 @@ struct CholDev {
     int2* panel_tasks = nullptr;
     int4* upd_tasks = nullptr;
     struct Step { int32_t panel_off, panel_cnt, rpt /* panel rows / kT, rounded up */, max_rows, upd_off, upd_cnt; };
-    struct Level { int32_t asm_off, asm_cnt; std::vector<Step> steps; };
+    struct Level { int32_t asm_off, asm_cnt; size_t lds_asm; std::vector<Step> steps; };
     std::vector<Level> plan;
     int64_t n_launches = 0;
 };
@@ -481,6 +571,7 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     c->lds_solve.assign((size_t)S.n_levels, 0);
     std::vector<AsmTask> asm_t;
     std::vector<AsmChild> asm_c;
+    std::vector<size_t> lds_asm((size_t)S.n_levels, 0);
     std::vector<int2> panel_t;
     std::vector<int4> upd_t;
     c->plan.assign((size_t)S.n_levels, CholDev::Level{});
@@ -493,7 +584,8 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
             const int32_t s = S.level_list[(size_t)q];
             const SnDev& d = sns[(size_t)s];
             const int32_t m3 = 3 * (d.k + d.r);
-            ms = std::max(ms, (size_t)(kSB * kSB + m3) * sizeof(double));
+            ms = std::max(ms, (size_t)(kSB * kSB + kSB + m3) * sizeof(double));
+            lds_asm[(size_t)l] = std::max(lds_asm[(size_t)l], (size_t)kCT * m3 * sizeof(double));
             maxk3 = std::max(maxk3, 3 * d.k);
             const OEnt* ob = omap.data() + d.omap_off;
             for (int32_t c0 = 0; c0 < m3; c0 += kCT) {
@@ -544,7 +636,8 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
             c->n_launches += 1 + (st.upd_cnt > 0);
         }
         c->lds_solve[(size_t)l] = ms;
-        if (ms > 160 * 1024) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
+        L.lds_asm = lds_asm[(size_t)l];
+        if (ms > 160 * 1024 || L.lds_asm > 160 * 1024) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
     }
     int rc = 0;
     rc |= dalloc_copy(&c->sns, sns);
@@ -583,17 +676,18 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     const dpg_chol_sym& S = c->sym;
     const double* g = hb + 9 * c->nnzb_upper;
     if (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess) return DPG_ERR_HIP;
+    int pid = 0;
     for (int32_t l = 0; l < S.n_levels; ++l) {
         const CholDev::Level& L = c->plan[(size_t)l];
-        hipLaunchKernelGGL(chol_assemble, dim3(L.asm_cnt), dim3(kT), 0, st, c->asm_tasks + L.asm_off, c->asm_child,
-                           c->sns, c->omap, hb, c->relmap, c->fronts);
+        hipLaunchKernelGGL(chol_assemble, dim3(L.asm_cnt), dim3(kT), L.lds_asm, st, c->asm_tasks + L.asm_off,
+                           c->asm_child, c->sns, c->omap, hb, c->relmap, c->fronts, pid++);
         for (const CholDev::Step& p : L.steps) {
             const int2* pt = c->panel_tasks + p.panel_off;
-            if (p.rpt == 1) hipLaunchKernelGGL(chol_panel<kT>, dim3(p.panel_cnt), dim3(kT), 0, st, pt, c->sns, c->fronts, c->status);
-            else if (p.rpt == 2) hipLaunchKernelGGL(chol_panel<2 * kT>, dim3(p.panel_cnt), dim3(2 * kT), 0, st, pt, c->sns, c->fronts, c->status);
-            else hipLaunchKernelGGL(chol_panel<4 * kT>, dim3(p.panel_cnt), dim3(4 * kT), 0, st, pt, c->sns, c->fronts, c->status);
+            if (p.rpt == 1) hipLaunchKernelGGL(chol_panel<kT>, dim3(p.panel_cnt), dim3(kT), 0, st, pt, c->sns, c->fronts, c->status, pid++);
+            else if (p.rpt == 2) hipLaunchKernelGGL(chol_panel<2 * kT>, dim3(p.panel_cnt), dim3(2 * kT), 0, st, pt, c->sns, c->fronts, c->status, pid++);
+            else hipLaunchKernelGGL(chol_panel<4 * kT>, dim3(p.panel_cnt), dim3(4 * kT), 0, st, pt, c->sns, c->fronts, c->status, pid++);
             if (p.upd_cnt > 0)
-                hipLaunchKernelGGL(chol_update, dim3(p.upd_cnt), dim3(kT), 0, st, c->upd_tasks + p.upd_off, c->sns, c->fronts);
+                hipLaunchKernelGGL(chol_update, dim3(p.upd_cnt), dim3(kT), 0, st, c->upd_tasks + p.upd_off, c->sns, c->fronts, pid++);
         }
     }
     if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
@@ -618,3 +712,16 @@ extern "C" void dpg_chol_stats(void* h, double out[6]) {
     out[4] = (double)S.front_off[(size_t)S.ns] * 8.0;
     out[5] = (double)S.n;
 }
+
+#ifdef DPG_CHOL_TIMING
+extern "C" int dpg_chol_prof_dump(unsigned long long* out, int n, unsigned long long* span) {
+    if (hipMemcpyFromSymbol(span, HIP_SYMBOL(g_span), sizeof(unsigned long long) * kProfL * kProfW * 2) != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int dpg_chol_prof_reset(void) {
+    std::vector<unsigned long long> sp((size_t)kProfL * kProfW * 2, 0ull);
+    std::vector<unsigned long long> z((size_t)4096 * kProfSlots, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z.data(), z.size() * 8) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_span), sp.data(), sp.size() * 8) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -5,14 +5,14 @@
 // laser scans: a scan is uniform in ANGLE, not in space (near the sensor its points are a few mm
 // apart, far away tens of cm), so every cloud is indexed by the angle of its points around the
 // node origin:
-//   angle_index_kernel: per node, points sorted by pseudo-angle (the "diamond angle" in [0, 4), a
-//     monotone function of atan2 computed with one division) by a bitonic sort in LDS, plus a table
-//     of the first sorted position of each of B uniform pseudo-angle buckets.
-//   exactness: every point p with |p - q| <= rho lies within the angle asin(rho/|q|) of q
-//     (|q| > rho); the window's edges are q rotated by -+ that angle (sin = rho'/|q|, cos by sqrt:
-//     no transcendental), their pseudo-angles widened by a margin far above float error, and the
-//     bucket map is the same monotone float function at build and query time; queries within rho'
-//     of the origin scan everything.
+//   angle_index_kernel: per node, points sorted by pseudo-angle (an octant polynomial of
+//     atan2 in [0, 2 pi): one reciprocal, slope within [0.98, 1.06] of the true angle's) by a
+//     bitonic sort in LDS, plus a table of the first sorted position of each of B uniform buckets.
+//   exactness: every point p with |p - q| <= rho lies within the angle asin(s) <= s / sqrt(1 - s^2)
+//     of q (s = rho/|q| < 1), so its pseudo-angle lies within 1.07 s / sqrt(1 - s^2) (+ a margin
+//     far above float error) of q's; the bucket map is the same float function at build and query
+//     time; queries with s >= 0.7 scan everything.  tests/test_window_bound.py checks the bound
+//     numerically in float32 arithmetic.
 //   icp_ang_kernel (one workgroup per edge, all iterations resident in LDS):
 //     forward 1-NN: radius = distance to the previous iteration's match (r when unseeded), the
 //       window scan keeps the exact (distance, lowest index) argmin;
@@ -35,20 +35,24 @@ constexpr int kT = 256;
 constexpr int kW = kT / 64;
 constexpr int kSums = 10;
 constexpr int kB = 512;                         // pseudo-angle buckets per cloud
-constexpr float kBucketScale = (float)kB / 4.0f;
-constexpr float kPaMargin = 1e-5f;              // pseudo-angle margin (float error is ~5e-7)
+constexpr float kTwoPi = 6.28318530717958647692f;
+constexpr float kBucketScale = (float)kB / kTwoPi;
+constexpr float kPaSlope = 1.07f;               // bound on d(pseudo-angle)/d(angle) (max 1.0584)
+constexpr float kPaMargin = 2e-5f;              // absolute pseudo-angle margin (float error ~1e-6)
 
-// pseudo-angle in [0, 4): strictly increasing with atan2(y, x) taken in [0, 2 pi); 0 at the origin
+// pseudo-angle in [0, 2 pi): atan2 approximated per octant by f(t) = t (pi/4 + 0.273 (1 - t)),
+// t = min(|x|,|y|) / max(|x|,|y|) (max error 1.5e-3 rad, slope ratio to atan in [0.98, 1.0584]);
+// 0 at the origin.
 __device__ __forceinline__ float pseudo_angle(float x, float y) {
-    if (y >= 0.0f) {
-        if (x >= 0.0f) {
-            const float s = x + y;
-            return s > 0.0f ? y / s : 0.0f;
-        }
-        return 1.0f + (-x) / (y - x);
-    }
-    if (x < 0.0f) return 2.0f + (-y) / (-x - y);
-    return 3.0f + x / (x - y);
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    if (!(mx > 0.0f)) return 0.0f;
+    const float t = mn * __builtin_amdgcn_rcpf(mx);
+    const float f = t * (1.0584f - 0.273f * t);
+    float phi = ay > ax ? 1.5707963f - f : f;
+    if (x < 0.0f) phi = 3.14159265f - phi;
+    if (y < 0.0f) phi = kTwoPi - phi;
+    return phi;
 }
 
 __device__ __forceinline__ int bucket_of(float pa) {
@@ -152,14 +156,13 @@ __device__ __forceinline__ float sqd(float ax, float ay, float bx, float by) {
 // sorted-position ranges of the points that can lie within `rad` of q (angle window); returns
 // the number of ranges (1 or 2), or 0 meaning "scan everything".
 __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int r0[2], int r1[2]) {
-    const float rq = sqrtf(qx * qx + qy * qy);
-    const float sn = rad / rq * 1.0001f + 1e-6f;   // sine of the half-angle, widened
+    const float sn = rad * __builtin_amdgcn_rsqf(qx * qx + qy * qy) * 1.0001f + 1e-6f;   // sin of the half-angle
     if (!(sn < 0.7f)) return 0;
-    const float cs = sqrtf(1.0f - sn * sn);
-    float lo = pseudo_angle(cs * qx + sn * qy, cs * qy - sn * qx) - kPaMargin;   // q rotated by -half
-    float hi = pseudo_angle(cs * qx - sn * qy, cs * qy + sn * qx) + kPaMargin;   // q rotated by +half
-    if (lo < 0.0f) lo += 4.0f;
-    if (hi >= 4.0f) hi -= 4.0f;
+    const float half = kPaSlope * sn * __builtin_amdgcn_rsqf(1.0f - sn * sn) * 1.0001f + kPaMargin;
+    const float pq = pseudo_angle(qx, qy);
+    float lo = pq - half, hi = pq + half;
+    if (lo < 0.0f) lo += kTwoPi;
+    if (hi >= kTwoPi) hi -= kTwoPi;
     if (lo <= hi) {
         r0[0] = bk[bucket_of(lo)];
         r1[0] = bk[bucket_of(hi) + 1];

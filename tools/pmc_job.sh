@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU box job: PMC counters for one bench step (each counter group in its own rocprofv3 pass,
+# kernel trace only beside --pmc).  usage: bash tools/pmc_job.sh TAG
+set -u
+TAG=${1:-pmc}
+ROOT=${GRAFT_REPO_ROOT:-$PWD}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export PYTHONPATH=$ROOT:$ROOT/dpg-slam_amd
+export TMPDIR=/tmp
+timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+run() {   # name, counters...
+    local name=$1; shift
+    timeout -k 10 400 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- \
+        python bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "$name exit $rc"
+    return $rc
+}
+run fetch FETCH_SIZE && run write WRITE_SIZE && \
+run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES
