@@ -34,7 +34,7 @@ namespace {
 constexpr int kT = 256;
 constexpr int kW = kT / 64;
 constexpr int kSums = 10;
-constexpr int kB = 512;                         // pseudo-angle buckets per cloud
+constexpr int kB = 1024;                        // pseudo-angle buckets per cloud (~1 point each)
 constexpr float kTwoPi = 6.28318530717958647692f;
 constexpr float kBucketScale = (float)kB / kTwoPi;
 constexpr float kPaSlope = 1.07f;               // bound on d(pseudo-angle)/d(angle) (max 1.0584)
@@ -121,11 +121,21 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
     }
 }
 
+// A point as the search sees it (16 B, one LDS load): coordinates + key = original index << 16 |
+// sorted position.  The exact PCL/FLANN order "(float distance, lowest original index)" is then
+// the unsigned order of the 64-bit word (bits(d) << 32 | key): d >= 0, so its bits order as it does.
+struct Rec {
+    float x, y;
+    uint32_t key, pad;
+};
+
+__device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
+    return ((uint64_t)__float_as_uint(d) << 32) | key;
+}
+
 struct Lds {
-    float2* tp;       // target points sorted by angle
-    float2* scs;      // current (moved) source points, in the source's angle order
-    uint16_t* ti;     // target sorted -> original index
-    uint16_t* si;     // source sorted -> original index
+    Rec* tp;          // target points in angle order
+    Rec* scs;         // current (moved) source points in the source's angle order
     uint16_t* spos;   // source original index -> sorted position
     uint16_t* tb;     // target bucket starts [kB+1]
     uint16_t* sb;     // source bucket starts [kB+1]
@@ -137,10 +147,8 @@ __device__ __forceinline__ size_t a16(size_t x) { return (x + 15) & ~size_t(15);
 __device__ Lds carve(unsigned char* base, int cap) {
     Lds L;
     size_t o = 0;
-    L.tp = reinterpret_cast<float2*>(base + o);   o = a16(o + 8 * (size_t)cap);
-    L.scs = reinterpret_cast<float2*>(base + o);  o = a16(o + 8 * (size_t)cap);
-    L.ti = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
-    L.si = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
+    L.tp = reinterpret_cast<Rec*>(base + o);      o = a16(o + 16 * (size_t)cap);
+    L.scs = reinterpret_cast<Rec*>(base + o);     o = a16(o + 16 * (size_t)cap);
     L.spos = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
     L.tb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
     L.sb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
@@ -153,24 +161,23 @@ __device__ __forceinline__ float sqd(float ax, float ay, float bx, float by) {
     return dx * dx + dy * dy;
 }
 
-// sorted-position ranges of the points that can lie within `rad` of q (angle window); returns
-// the number of ranges (1 or 2), or 0 meaning "scan everything".
-__device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int r0[2], int r1[2]) {
+// The sorted positions of the points that can lie within `rad` of q (angle window), as ONE
+// wrapped range: positions start, start+1, ... (mod n), `count` of them (the whole cloud when
+// the window would span too wide an angle).
+__device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int& start) {
     const float sn = rad * __builtin_amdgcn_rsqf(qx * qx + qy * qy) * 1.0001f + 1e-6f;   // sin of the half-angle
-    if (!(sn < 0.7f)) return 0;
+    if (!(sn < 0.7f)) {
+        start = 0;
+        return n;
+    }
     const float half = kPaSlope * sn * __builtin_amdgcn_rsqf(1.0f - sn * sn) * 1.0001f + kPaMargin;
     const float pq = pseudo_angle(qx, qy);
     float lo = pq - half, hi = pq + half;
     if (lo < 0.0f) lo += kTwoPi;
     if (hi >= kTwoPi) hi -= kTwoPi;
-    if (lo <= hi) {
-        r0[0] = bk[bucket_of(lo)];
-        r1[0] = bk[bucket_of(hi) + 1];
-        return 1;
-    }
-    r0[0] = bk[bucket_of(lo)]; r1[0] = n;         // the window straddles pseudo-angle 0
-    r0[1] = 0; r1[1] = bk[bucket_of(hi) + 1];
-    return 2;
+    start = bk[bucket_of(lo)];
+    const int end = bk[bucket_of(hi) + 1];
+    return lo <= hi ? end - start : (n - start) + end;   // else: straddles pseudo-angle 0
 }
 
 template <int PPT>
@@ -189,12 +196,12 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
     const int vt = E.tgt_node, vs = E.src_node;
     Lds L = carve(smem, kp.lds_tgt);
     for (int i = t; i < M; i += kT) {
-        L.tp[i] = idx_pts[E.tgt_ds_off + i];
-        L.ti[i] = idx_orig[E.tgt_ds_off + i];
+        const float2 p = idx_pts[E.tgt_ds_off + i];
+        L.tp[i] = Rec{p.x, p.y, ((uint32_t)idx_orig[E.tgt_ds_off + i] << 16) | (uint32_t)i, 0u};
     }
     for (int s = t; s < N; s += kT) {
         const uint16_t o = idx_orig[E.src_ds_off + s];
-        L.si[s] = o;
+        L.scs[s].key = ((uint32_t)o << 16) | (uint32_t)s;
         L.spos[o] = (uint16_t)s;
     }
     for (int b = t; b <= kB; b += kT) {
@@ -219,7 +226,8 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             sx[m] = (F[0] * p.x + F[1] * p.y) + F[2];
             sy[m] = (F[3] * p.x + F[4] * p.y) + F[5];
             sp[m] = L.spos[i];
-            L.scs[sp[m]] = make_float2(sx[m], sy[m]);
+            L.scs[sp[m]].x = sx[m];
+            L.scs[sp[m]].y = sy[m];
         }
     }
     __syncthreads();
@@ -238,59 +246,71 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
         for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
+            // every lane runs every step (dead lanes predicated off): the candidate loops below
+            // are wave-uniform (exit on __any), with straight-line predicated bodies
             const int i = t + kT * m;
-            if (i >= N) continue;
+            const bool live = i < N;
             const float qx = sx[m], qy = sy[m];
             // ---- forward 1-NN (target index), seeded radius ----
-            float bd = r2f;
-            int bi = 0x7fffffff, bp = -1;
+            uint64_t best = dkey(r2f, 0xffffffffu);   // "none": every candidate with d <= r beats it
             float rad = rmax;
-            if (seed[m] >= 0) {
-                const float2 s0 = L.tp[seed[m]];
-                const float d = sqd(qx, qy, s0.x, s0.y);
+            if (live && seed[m] >= 0) {
+                const Rec r = L.tp[seed[m]];
+                const float d = sqd(qx, qy, r.x, r.y);
                 if (d <= r2f) {
-                    bd = d; bi = L.ti[seed[m]]; bp = seed[m];
+                    best = dkey(d, r.key);
                     rad = sqrtf(d) * 1.0001f + 1e-6f;
                 }
             }
             {
-                int r0[2], r1[2];
-                int nr = window(L.tb, M, qx, qy, rad, r0, r1);
-                if (nr == 0) { nr = 1; r0[0] = 0; r1[0] = M; }
-                for (int w = 0; w < nr; ++w) {
-                    for (int s = r0[w]; s < r1[w]; ++s) {
-                        const float2 tq = L.tp[s];
-                        const float d = sqd(qx, qy, tq.x, tq.y);
-                        if (d <= bd) {
-                            const int j = L.ti[s];
-                            if (d < bd || j < bi) { bd = d; bi = j; bp = s; }
-                        }
+                int s = 0;
+                const int fc = live ? window(L.tb, M, qx, qy, rad, s) : 0;
+                s = s >= M ? s - M : s;
+                for (int c = 0; __any(c < fc); c += 2) {   // exact (d, original index) argmin
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const Rec r = L.tp[s];
+                        const uint64_t kd = dkey(sqd(qx, qy, r.x, r.y), r.key);
+                        best = (c + u < fc && kd < best) ? kd : best;
+                        s = s + 1 == M ? 0 : s + 1;
                     }
                 }
             }
-            seed[m] = bp;
-            bool ok = bp >= 0;
+            const uint32_t bkey = (uint32_t)best;
+            const float bd = __uint_as_float((uint32_t)(best >> 32));
+            const int bp = bkey == 0xffffffffu ? -1 : (int)(bkey & 0xffffu);
+            const int bi = (int)(bkey >> 16);
+            seed[m] = live ? bp : seed[m];
+            bool ok = live && bp >= 0;
             // ---- reciprocal test in the static source index ----
-            if (ok && kp.reciprocal) {
-                const float2 tj = L.tp[bp];
-                const double ux = (double)tj.x - (double)F[2], uy = (double)tj.y - (double)F[5];
-                const float px = (float)(i00 * ux + i01 * uy), py = (float)(i10 * ux + i11 * uy);
-                const float rho = sqrtf(bd) * 1.0001f + drift;
-                int r0[2], r1[2];
-                int nr = window(L.sb, N, px, py, rho, r0, r1);
-                if (nr == 0) { nr = 1; r0[0] = 0; r1[0] = N; }
-                const int me = sp[m];
-                for (int w = 0; w < nr && ok; ++w) {
-                    for (int s = r0[w]; s < r1[w]; ++s) {
-                        const float2 c = L.scs[s];
-                        const float d = sqd(c.x, c.y, tj.x, tj.y);
-                        if (d <= bd && s != me && (d < bd || (int)L.si[s] < i)) { ok = false; break; }
+            if (kp.reciprocal) {
+                float2 tj = make_float2(0.f, 0.f);
+                int s = 0, rc = 0;
+                if (ok) {
+                    const Rec r = L.tp[bp];
+                    tj = make_float2(r.x, r.y);
+                    const double ux = (double)tj.x - (double)F[2], uy = (double)tj.y - (double)F[5];
+                    const float px = (float)(i00 * ux + i01 * uy), py = (float)(i10 * ux + i11 * uy);
+                    rc = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
+                    s = s >= N ? s - N : s;
+                }
+                // i's own word: any other current source with a smaller (d, original index) word
+                // is closer to t_j (or tied with a lower index) and breaks reciprocity
+                const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)sp[m]);
+                for (int c = 0; __any(ok & (c < rc)); c += 2) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const Rec r = L.scs[s];
+                        const uint64_t kd = dkey(sqd(r.x, r.y, tj.x, tj.y), r.key);
+                        ok = ok & !((c + u < rc) & (kd < mine));
+                        s = s + 1 == N ? 0 : s + 1;
                     }
                 }
             }
-            if (trace && k < kp.trace_iters) trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
+            if (live && trace && k < kp.trace_iters)
+                trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
             if (ok) {
-                const float2 tq = L.tp[bp];
+                const Rec tq = L.tp[bp];
                 const double px = qx, py = qy, tx = tq.x, ty = tq.y;
                 acc[0] = acc[0] + 1.0;
                 acc[1] = acc[1] + (double)bd;
@@ -339,7 +359,10 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             const float x = sx[m], y = sy[m];
             sx[m] = (cf * x + nsf * y) + txf;
             sy[m] = (sf * x + cf * y) + tyf;
-            if (i < N) L.scs[sp[m]] = make_float2(sx[m], sy[m]);
+            if (i < N) {
+                L.scs[sp[m]].x = sx[m];
+                L.scs[sp[m]].y = sy[m];
+            }
         }
         float Nf[6];
         Nf[0] = cf * F[0] + nsf * F[3];
@@ -386,10 +409,8 @@ extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) {
     auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
     size_t o = 0;
-    o = al(o + 8 * (size_t)cap);
-    o = al(o + 8 * (size_t)cap);
-    o = al(o + 2 * (size_t)cap);
-    o = al(o + 2 * (size_t)cap);
+    o = al(o + 16 * (size_t)cap);
+    o = al(o + 16 * (size_t)cap);
     o = al(o + 2 * (size_t)cap);
     o = al(o + 2 * (size_t)(kB + 1));
     o = al(o + 2 * (size_t)(kB + 1));
