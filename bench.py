@@ -32,6 +32,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the last committed rocprofv3 PMC pass
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py: (2 x FETCH_SIZE + WRITE_SIZE) KiB,
+    the gfx950 correction of MI355X_MICROARCH.md "HBM").  None when no pass covers this kernel."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    for k, v in d.get("traffic_bytes_per_launch", {}).items():
+        if k.split("<")[0] == kernel:
+            return float(v), d.get("source")
+    return None, None
+
+
 def cpu_baseline(w, params, sample_edges: int, threads: int = 1) -> dict:
     """Oracle (CPU restatement, grid NN) timed on this host: ICP on a bounded sample of the same
     workload + the full-graph GN (block-sparse Cholesky)."""
@@ -149,6 +163,7 @@ def main():
                "sample": f"oracle (C restatement, grid NN, 1 thread) ICP on {cb['n']} random edges of "
                          f"{args.config} ({cb['icp_s']:.1f} s, mean {cb['iters_mean']:.1f} ICP iterations)"}
 
+    traffic, traffic_src = pmc_traffic(KERNEL_NAME[args.icp_variant])
     if rank == 0:
         line = {
             "metric": "ICP edges/sec + ms/GN-iter on 5k-node/20k-edge synthetic graph, 1->8 GPU",
@@ -175,7 +190,7 @@ def main():
             "icp_edges_per_s_kernel": w.E / world / (stats["icp_kernel_ms"] * 1e-3) * world,
             "icp_iters_mean": stats["icp_iters_mean"],
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": KERNEL_NAME[args.icp_variant] + " (correspondence search + fit, fused)",
                          "bytes_per_launch": algo_bytes},
             "cpu_baseline": cpu,

@@ -1,0 +1,44 @@
+// chol_analyze.cpp -- host-only: symbolic analysis statistics of a pose-graph pattern (per level:
+// fronts, largest front, flops; the elimination tree's critical path in flops).
+// usage: chol_analyze PAIRS.bin [max_cols relax]
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <vector>
+#include "../dpg-slam_amd/csrc/dpg_chol.h"
+
+int main(int argc, char** argv) {
+    FILE* f = fopen(argv[1], "rb");
+    int64_t n = 0, P = 0;
+    if (!f || fread(&n, 8, 1, f) != 1 || fread(&P, 8, 1, f) != 1) return 2;
+    std::vector<int32_t> lo((size_t)P), hi((size_t)P);
+    if (fread(lo.data(), 4, (size_t)P, f) != (size_t)P || fread(hi.data(), 4, (size_t)P, f) != (size_t)P) return 2;
+    dpg_chol_opts o{argc > 2 ? atoi(argv[2]) : 64, argc > 3 ? atof(argv[3]) : 0.3};
+    dpg_chol_sym S;
+    if (dpg_chol_symbolic(n, lo.data(), hi.data(), P, &o, &S)) return 3;
+    std::vector<double> fl((size_t)S.ns), cp((size_t)S.ns, 0.0);
+    int64_t nnzL = 0;
+    for (int s = 0; s < S.ns; ++s) {
+        const double k = 3.0 * (S.sn_c0[s + 1] - S.sn_c0[s]), r = 3.0 * (S.sn_rows_ptr[s + 1] - S.sn_rows_ptr[s]);
+        fl[s] = k * k * k / 3 + k * k * r + k * r * r;
+        nnzL += (int64_t)(k * (k + 1) / 2 + k * r);
+    }
+    double crit = 0;
+    for (int s = 0; s < S.ns; ++s) {   // children precede parents
+        cp[s] += fl[s];
+        if (S.sn_parent[s] >= 0) cp[S.sn_parent[s]] = std::max(cp[S.sn_parent[s]], cp[s]);
+        else crit = std::max(crit, cp[s]);
+    }
+    printf("n=%lld ns=%d levels=%d max_front=%d flops=%.3g nnzL=%lld fronts=%.1f MB crit_path_flops=%.3g\n",
+           (long long)n, S.ns, S.n_levels, S.max_front, S.flops, (long long)nnzL, S.front_off[S.ns] * 8e-6, crit);
+    for (int l = 0; l < S.n_levels; ++l) {
+        int cnt = 0, mk = 0, mm = 0; double lf = 0, mf = 0;
+        for (int q = S.level_ptr[l]; q < S.level_ptr[l + 1]; ++q) {
+            int s = S.level_list[q]; ++cnt;
+            int k = S.sn_c0[s + 1] - S.sn_c0[s], r = (int)(S.sn_rows_ptr[s + 1] - S.sn_rows_ptr[s]);
+            mk = std::max(mk, 3 * k); mm = std::max(mm, 3 * (k + r)); lf += fl[s]; mf = std::max(mf, fl[s]);
+        }
+        printf("L%2d fronts=%5d max_k3=%4d max_m3=%4d flops=%.3g max_front_flops=%.3g\n", l, cnt, mk, mm, lf, mf);
+    }
+    return 0;
+}
