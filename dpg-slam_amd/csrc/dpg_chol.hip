@@ -52,7 +52,19 @@ __device__ unsigned long long g_span[kProfL * kProfW * 2];   // per launch, per 
     } while (0)
 #define PROF_BEGIN(pid) do { if (threadIdx.x == 0 && (pid) < kProfL && blockIdx.x < kProfW) g_span[((size_t)(pid) * kProfW + blockIdx.x) * 2] = wall_clock64(); } while (0)
 #define PROF_END(pid) do { if (threadIdx.x == 0 && (pid) < kProfL && blockIdx.x < kProfW) g_span[((size_t)(pid) * kProfW + blockIdx.x) * 2 + 1] = wall_clock64(); } while (0)
+// per-front phase stamps of the fused kernel: [front][0 claim, 1 children ready, 2 assembled,
+// 3 factored, 4 done]
+__device__ unsigned long long g_front[16384 * 8];
+#define FT_MARK(s, k) do { if (threadIdx.x == 0 && (s) < 16384) g_front[(s) * 8 + (k)] = wall_clock64(); } while (0)
+// per-panel stamps of large fronts: [front][panel][0 wake, 1 loaded, 2 tile updated, 3 factored, 4 published]
+__device__ unsigned long long g_panel[16384 * 16 * 8];
+__device__ unsigned long long g_steps[16384 * 16 * 8];
+#define ST_MARK(s, p, k) do { if (threadIdx.x == 0 && (s) < 16384 && (p) < 16 && (k) < 8) g_steps[((s) * 16 + (p)) * 8 + (k)] = wall_clock64(); } while (0)
+#define PN_MARK(s, p, k) do { if (threadIdx.x == 0 && (s) < 16384 && (p) < 16) g_panel[((s) * 16 + (p)) * 8 + (k)] = wall_clock64(); } while (0)
 #else
+#define FT_MARK(s, k) do { } while (0)
+#define PN_MARK(s, p, k) do { } while (0)
+#define ST_MARK(s, p, k) do { } while (0)
 #define PROF_MARK(pid, k) do { } while (0)
 #define PROF_BEGIN(pid) do { } while (0)
 #define PROF_END(pid) do { } while (0)
@@ -66,6 +78,8 @@ struct SnDev {
     int64_t omap_off;
     int64_t acc_off;            // doubles (3r pending row updates of the forward solve)
     int32_t omap_n, parent;     // parent supernode, -1 at a root
+    int32_t G, need;            // fused factorization: team size, sum of the children's team sizes
+    int32_t ftask, pad;         // large fronts: first tile task
 };
 
 struct OEnt {                   // one upper 3x3 block of H -> its front position
@@ -303,11 +317,31 @@ __device__ __forceinline__ void wait_geq(int32_t* w, int32_t target, int32_t* st
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 }
+// Poll without the agent acquire: every handed-off byte the waiting workgroup reads is stored sc1
+// by its producer and loaded sc1 (ld_agent) here, so the L1 is never consulted for it (Guideline
+// 16, the sc1-load form); the wavefront fence only keeps the compiler from hoisting those loads.
+__device__ __forceinline__ void wait_geq_sc1(int32_t* w, int32_t target, int32_t* status) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 25)) {
+            atomicExch(status, 2);
+            break;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ int claim(const int32_t* order, int32_t* ticket) {
     __shared__ int s_task;
     if (threadIdx.x == 0) s_task = order[atomicAdd(ticket, 1)];
     __syncthreads();
     return s_task;
+}
+
+__device__ __forceinline__ int claim_lds(const int32_t* order, int32_t* ticket, int* slot) {
+    if (threadIdx.x == 0) *slot = order[atomicAdd(ticket, 1)];
+    __syncthreads();
+    return *slot;
 }
 
 // forward: L y = -g.  A front gathers its children's pending row updates (child order: fixed
@@ -451,6 +485,630 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     if (tid == 0) __hip_atomic_store(sync + 1 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- fused factorization + forward solve: ONE launch, fronts as a DAG ----
+// One 512-thread workgroup per front, claimed in topological order (as the solves above).  A
+// front waits for its children, then
+//   assembles itself column tile by column tile in LDS (H blocks + children's update matrices,
+//     child by child: fixed summation order),
+//   factors its k3 pivot columns right-looking by kFNB-column panels: the panel is staged in LDS,
+//     wave 0 factors its top w x w block with the rows in registers (rsq + Newton, 3x3-block steps,
+//     wave-synchronous, no workgroup barrier), every other row solves against it independently
+//     (one row per thread, L_top broadcast from LDS), then the whole workgroup applies the rank-w
+//     update to the trailing lower triangle in 64x64 tiles (4x4 register tile per thread),
+//   runs its part of the forward solve L y = -g while its L is hot (children's pending row updates
+//     gathered in child order, diagonal blocks by one wave, L21 y handed to the parent),
+//   and signals its parent.
+// Hand-off (Guideline 16, R1): everything another workgroup reads -- the update matrix (columns
+// >= k3) and the pending row updates -- is stored write-through (sc1, agent-scope relaxed stores)
+// and read back with sc1 loads; every storing wave drains, the workgroup synchronises, ONE lane
+// adds to the parent's counter; the consumer polls relaxed, then one agent-scope acquire.
+constexpr int kFT = 512;    // threads per front workgroup
+constexpr int kFNB = 24;    // panel width (scalar columns = 8 3x3 blocks)
+constexpr int kSmall = 96;  // fronts up to this many rows are assembled + factored entirely in LDS
+constexpr int kMaxCh = 8;   // ... if they have at most this many children
+constexpr int kPF = (kSmall * (kSmall + 1) / 2 + kFT - 1) / kFT;   // per-thread prefetch slots per child
+constexpr int kPFL = 4;      // large fronts: entries in flight per thread in the extend-add / publish rounds
+constexpr int kGmax = 32;    // largest team (workgroups per front)
+
+struct ChMeta { int64_t front_off, acc_off, rows_off; int32_t k, r; };
+
+
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS carve of the factorization phase (doubles): panel [kFNB][Rp] with row offset `off` so that
+// trailing rows start 32-B aligned, L_top column-major [kFNB][kFNB], 1/diag, step scratch.
+__host__ __device__ inline int fused_rp(int R, int off) { return (R + off + 3) & ~3; }
+__host__ __device__ inline size_t fused_lds_doubles(int m3, int k3) {
+    const size_t large = ((m3 + 1) & ~1) + std::max((size_t)kFNB * m3,
+                                                     (size_t)kFNB * fused_rp(m3, 3) + kFNB * kFNB + kFNB + 4 * kFNB + 16);
+    (void)k3;
+    const size_t small = m3 <= kSmall ? (size_t)m3 * m3 + m3 + (kMaxCh * sizeof(ChMeta) + kMaxCh * (kSmall / 3) * 4 + 7) / 8 : 0;
+    return 2 + std::max(small, large);
+}
+
+// packed lower triangle of an n x n matrix, column-major: entry e -> (row i, column j), i >= j
+__device__ __forceinline__ void tri_ij(int e, int n, int& i, int& j) {
+    const float b = 2.0f * (float)n + 1.0f;
+    int jj = (int)((b - sqrtf(b * b - 8.0f * (float)e)) * 0.5f);
+    jj = max(0, min(jj, n - 1));
+    while (jj > 0 && jj * n - jj * (jj - 1) / 2 > e) --jj;
+    while (jj + 1 < n && (jj + 1) * n - (jj + 1) * jj / 2 <= e) ++jj;
+    j = jj;
+    i = jj + e - (jj * n - jj * (jj - 1) / 2);
+}
+
+// A front of at most kSmall rows, entirely in LDS: H blocks and the right-hand side are scattered
+// while the children are still running; after the wait the children's update matrices and pending
+// row updates arrive through ONE pipelined round of sc1 loads (child c + 1 in flight while child c
+// is added; child order fixes the summation order); the factorization runs by 3x3 block columns
+// with the right-hand side as an extra column (so the forward solve is folded in); the finished
+// L columns, y, the update matrix (sc1) and the pending row updates (sc1) go out once.
+__device__ __forceinline__ void small_front(int s, const SnDev& S, int32_t* sync, int32_t* status, const SnDev* __restrict__ sns,
+                            const OEnt* __restrict__ omap, const int32_t* __restrict__ relmap,
+                            const int32_t* __restrict__ child_list, const double* __restrict__ hb,
+                            const double* __restrict__ g, const int32_t* __restrict__ perm, double* fronts,
+                            double* __restrict__ ysol, double* acc, double* sm) {
+    const int tid = threadIdx.x;
+    const int k3 = 3 * S.k, r3 = 3 * S.r, m3 = k3 + r3;
+    double* F = fronts + S.front_off;
+    double* A = sm;                                           // [m3][m3] column-major
+    double* bv = A + m3 * m3;                                 // [m3] right-hand side column
+    ChMeta* chm = reinterpret_cast<ChMeta*>(bv + m3);   // m3 (m3 + 1) doubles: 16-B aligned
+    int32_t* crm = reinterpret_cast<int32_t*>(chm + kMaxCh);  // [kMaxCh][kSmall / 3] child relmaps
+    const int nch = S.nchild;
+    // ---- before the wait: everything that does not come from the children
+    for (int e = tid; e < m3 * m3; e += kFT) A[e] = 0.0;
+    for (int t = tid; t < m3; t += kFT) bv[t] = t < k3 ? -g[3 * perm[S.c0 + t / 3] + t % 3] : 0.0;
+    if (tid < nch) {
+        const SnDev C = sns[child_list[S.child_off + tid]];
+        chm[tid] = ChMeta{C.front_off, C.acc_off, C.rows_off, C.k, C.r};
+        for (int q = 0; q < C.r; ++q) crm[tid * (kSmall / 3) + q] = relmap[C.rows_off + q];
+    }
+    __syncthreads();
+    for (int q = tid; q < S.omap_n * 9; q += kFT) {
+        const OEnt o = omap[S.omap_off + q / 9];
+        const int ii = (q % 9) / 3, jj = q % 3;
+        const int row = 3 * o.a + ii, col = 3 * o.b + jj;
+        if (row < col) continue;
+        const double* B = hb + 9 * (int64_t)o.u;
+        A[col * m3 + row] = o.tr ? B[3 * jj + ii] : B[3 * ii + jj];
+    }
+    if (nch > 0) {
+        if (tid == 0) wait_geq_sc1(sync + s, S.need, status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    FT_MARK(s, 1);
+    // ---- children: update matrices (packed lower triangles) + pending row updates
+    auto load_child = [&](int ci, double (&v)[kPF], double& va) {
+        const ChMeta C = chm[ci];
+        const int n = 3 * C.r, tri = n * (n + 1) / 2, m3c = 3 * (C.k + C.r), k3c = 3 * C.k;
+        double* Fc = fronts + C.front_off + (int64_t)k3c * m3c + k3c;
+#pragma unroll
+        for (int q = 0; q < kPF; ++q) {
+            const int e = tid + kFT * q;
+            v[q] = 0.0;
+            if (e < tri) {
+                int i, j;
+                tri_ij(e, n, i, j);
+                v[q] = ld_agent(Fc + (int64_t)j * m3c + i);
+            }
+        }
+        va = tid < n ? ld_agent(acc + C.acc_off + tid) : 0.0;
+    };
+    auto add_child = [&](int ci, const double (&v)[kPF], double va) {
+        const ChMeta C = chm[ci];
+        const int n = 3 * C.r, tri = n * (n + 1) / 2;
+        const int32_t* rm = crm + ci * (kSmall / 3);
+#pragma unroll
+        for (int q = 0; q < kPF; ++q) {
+            const int e = tid + kFT * q;
+            if (e < tri) {
+                int i, j;
+                tri_ij(e, n, i, j);
+                const int pj = 3 * rm[j / 3] + j % 3, pi = 3 * rm[i / 3] + i % 3;
+                A[pj * m3 + pi] += v[q];
+            }
+        }
+        if (tid < n) bv[3 * rm[tid / 3] + tid % 3] -= va;
+    };
+    if (nch > 0) {
+        double va_[kPF], vb_[kPF], aa = 0.0, ab = 0.0;
+        load_child(0, va_, aa);
+        for (int ci = 0; ci < nch; ci += 2) {
+            if (ci + 1 < nch) load_child(ci + 1, vb_, ab);
+            add_child(ci, va_, aa);
+            __syncthreads();
+            if (ci + 1 < nch) {
+                if (ci + 2 < nch) load_child(ci + 2, va_, aa);
+                add_child(ci + 1, vb_, ab);
+                __syncthreads();
+            }
+        }
+    }
+    FT_MARK(s, 2);
+    // ---- factorization by 3x3 block columns, right-hand side as column m3
+    bool bad = false;
+    for (int c0 = 0; c0 < k3; c0 += 3) {
+        const double* C0 = A + c0 * m3;
+        const double* C1 = C0 + m3;
+        const double* C2 = C1 + m3;
+        double d00 = C0[c0], d10 = C0[c0 + 1], d20 = C0[c0 + 2], d11 = C1[c0 + 1], d21 = C1[c0 + 2], d22 = C2[c0 + 2];
+        if (!(d00 > 0.0)) { bad = true; d00 = 1.0; }
+        const double i00 = rsqrt_nr(d00), l00 = d00 * i00;
+        const double l10 = d10 * i00, l20 = d20 * i00;
+        double e11 = d11 - l10 * l10;
+        if (!(e11 > 0.0)) { bad = true; e11 = 1.0; }
+        const double i11 = rsqrt_nr(e11), l11 = e11 * i11;
+        const double l21 = (d21 - l20 * l10) * i11;
+        double e22 = d22 - l20 * l20 - l21 * l21;
+        if (!(e22 > 0.0)) { bad = true; e22 = 1.0; }
+        const double i22 = rsqrt_nr(e22), l22 = e22 * i22;
+        const double y0 = bv[c0] * i00;
+        const double y1 = (bv[c0 + 1] - l10 * y0) * i11;
+        const double y2 = (bv[c0 + 2] - l20 * y0 - l21 * y1) * i22;
+        for (int i = c0 + 3 + tid; i < m3; i += kFT) {
+            const double x0 = C0[i] * i00;
+            const double x1 = (C1[i] - x0 * l10) * i11;
+            const double x2 = (C2[i] - x0 * l20 - x1 * l21) * i22;
+            A[c0 * m3 + i] = x0;
+            A[(c0 + 1) * m3 + i] = x1;
+            A[(c0 + 2) * m3 + i] = x2;
+            bv[i] -= x0 * y0 + x1 * y1 + x2 * y2;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            A[c0 * m3 + c0] = l00; A[c0 * m3 + c0 + 1] = l10; A[c0 * m3 + c0 + 2] = l20;
+            A[(c0 + 1) * m3 + c0 + 1] = l11; A[(c0 + 1) * m3 + c0 + 2] = l21; A[(c0 + 2) * m3 + c0 + 2] = l22;
+            bv[c0] = y0; bv[c0 + 1] = y1; bv[c0 + 2] = y2;
+        }
+        const int b0 = c0 + 3, nr = m3 - b0;
+        for (int e = tid; e < nr * nr; e += kFT) {
+            const int l = b0 + e / nr, i = b0 + e % nr;
+            if (i < l) continue;
+            double v = A[l * m3 + i];
+            v = fma(-C0[i], C0[l], v);
+            v = fma(-C1[i], C1[l], v);
+            v = fma(-C2[i], C2[l], v);
+            A[l * m3 + i] = v;
+        }
+        __syncthreads();
+    }
+    if (bad && tid == 0) atomicExch(status, 1);
+    FT_MARK(s, 3);
+    // ---- out: L columns + y (read by the backward solve, next launch), update matrix + pending (sc1)
+    for (int e = tid; e < k3 * m3; e += kFT) {
+        const int j = e / m3, i = e - j * m3;
+        if (i >= j) F[(int64_t)j * m3 + i] = A[e];
+    }
+    for (int t = tid; t < k3; t += kFT) ysol[3 * (int64_t)S.c0 + t] = bv[t];
+    if (S.parent >= 0) {
+        for (int e = tid; e < r3 * r3; e += kFT) {
+            const int j = k3 + e / r3, i = k3 + e % r3;
+            if (i >= j) st_agent(F + (int64_t)j * m3 + i, A[j * m3 + i]);
+        }
+        for (int t = tid; t < r3; t += kFT) st_agent(acc + S.acc_off + t, -bv[k3 + t]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    FT_MARK(s, 4);
+    if (tid == 0 && S.parent >= 0)
+        __hip_atomic_fetch_add(sync + S.parent, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A front of more than kSmall rows is factored by a TEAM of G workgroups (G consecutive tickets).
+// Its columns are cut into tiles of kFNB: pivot tiles [kFNB t, min(kFNB t + kFNB, k3)), then update
+// tiles from k3; tile t belongs to member t mod G, and only its owner ever writes it (plain stores).
+// Per pivot panel p the owner -- who has already applied panels 0..p-1 to its tile -- factors it
+// (POTRF of the top block by one wave, TRSM of the rows below, one row per thread), publishes it
+// write-through (sc1) and raises the front's panel flag; every member with tiles right of p loads
+// the panel (sc1) into LDS and applies the rank-w update to its own tiles (4x4 register tiles).
+// Member 0 also carries the right-hand side (forward solve folded in, as in small_front).  The
+// children's update matrices are added into the owners' columns in child order; at the end every
+// member republishes its update tiles write-through and adds 1 to the parent's counter (which
+// waits for the sum of its children's team sizes).
+struct Tiles {
+    int k3, m3, np, nt;
+    __device__ int c0(int t) const { return t < np ? kFNB * t : k3 + kFNB * (t - np); }
+    __device__ int c1(int t) const { return t < np ? min(kFNB * t + kFNB, k3) : min(k3 + kFNB * (t - np + 1), m3); }
+};
+
+// per (large front, tile): the H blocks and the children's column ranges that land in the tile
+struct FTask { int32_t om_b, om_e, ch_off, ch_cnt; };
+struct FChild { int32_t ja, jb, k, r; int64_t front_off, rows_off; };
+
+// Panel q of a large front: factored by its owner from its own (assembled, updated) columns,
+// published write-through, flag raised.  Leaves the panel in LDS.
+__device__ void factor_publish(int q, int s, const Tiles& T, double* F, int32_t* pflag, double* pbase, bool& bad) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k3 = T.k3, m3 = T.m3;
+    const int j0 = kFNB * q, w = min(kFNB, k3 - j0), R = m3 - j0;
+    const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+    double* P = pbase;
+    double* Lt = P + (size_t)kFNB * Rp;
+    double* rdg = Lt + kFNB * kFNB;
+    double* xs = rdg + kFNB;
+    double* sd = xs + 4 * kFNB;
+    for (int e = tid; e < w * R; e += kFT) {
+        const int c = e / R, i = e - c * R;
+        P[c * Rp + off + i] = i >= c ? F[(uint32_t)((j0 + c) * m3 + j0 + i)] : 0.0;
+    }
+    for (int e = tid; e < kFNB * kFNB; e += kFT) Lt[e] = 0.0;
+    __syncthreads();
+    PN_MARK(s, q, 5);
+    if (wave == 0) {   // POTRF of the top w x w block: lane i owns row i, pr[c] = row i, column c0 + c
+        const int i = lane;
+        double pr[kFNB];
+#pragma unroll
+        for (int c = 0; c < kFNB; ++c) pr[c] = (i < w && c < w && c <= i) ? P[c * Rp + off + i] : 0.0;
+#pragma unroll 1
+        for (int c0 = 0; c0 < w; c0 += 3) {
+            ST_MARK(s, q, c0 / 3);
+            // the step's 3x3 diagonal block and, below, the other rows' x: straight from the owning
+            // lanes' registers (v_readlane, uniform lane index) -- no LDS round trips in the chain
+            double d00 = rdlane(pr[0], c0), d10 = rdlane(pr[0], c0 + 1), d11 = rdlane(pr[1], c0 + 1);
+            double d20 = rdlane(pr[0], c0 + 2), d21 = rdlane(pr[1], c0 + 2), d22 = rdlane(pr[2], c0 + 2);
+            if (!(d00 > 0.0)) { bad = true; d00 = 1.0; }
+            const double i00 = rsqrt_nr(d00), l00 = d00 * i00;
+            const double l10 = d10 * i00, l20 = d20 * i00;
+            double e11 = d11 - l10 * l10;
+            if (!(e11 > 0.0)) { bad = true; e11 = 1.0; }
+            const double i11 = rsqrt_nr(e11), l11 = e11 * i11;
+            const double l21 = (d21 - l20 * l10) * i11;
+            double e22 = d22 - l20 * l20 - l21 * l21;
+            if (!(e22 > 0.0)) { bad = true; e22 = 1.0; }
+            const double i22 = rsqrt_nr(e22), l22 = e22 * i22;
+            double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+            if (i == c0) { x0 = l00; }
+            else if (i == c0 + 1) { x0 = l10; x1 = l11; }
+            else if (i == c0 + 2) { x0 = l20; x1 = l21; x2 = l22; }
+            else if (i > c0 + 2 && i < w) {
+                x0 = pr[0] * i00;
+                x1 = (pr[1] - x0 * l10) * i11;
+                x2 = (pr[2] - x0 * l20 - x1 * l21) * i22;
+            }
+            if (i >= c0 && i < w) {
+                Lt[c0 * kFNB + i] = x0;
+                if (i >= c0 + 1) Lt[(c0 + 1) * kFNB + i] = x1;
+                if (i >= c0 + 2) Lt[(c0 + 2) * kFNB + i] = x2;
+            }
+            if (i == c0) { rdg[c0] = i00; rdg[c0 + 1] = i11; rdg[c0 + 2] = i22; }
+            const bool upd = i > c0 + 2 && i < w;
+#pragma unroll
+            for (int c = 3; c < kFNB; ++c) {
+                const int cc = min(c0 + c, kFNB - 1);
+                const double y0 = rdlane(x0, cc), y1 = rdlane(x1, cc), y2 = rdlane(x2, cc);
+                const double v = fma(-x2, y2, fma(-x1, y1, fma(-x0, y0, pr[c])));
+                pr[c - 3] = (upd && c0 + c < w && c0 + c <= i) ? v : pr[c];
+            }
+            pr[kFNB - 3] = pr[kFNB - 2] = pr[kFNB - 1] = 0.0;
+        }
+    }
+    __syncthreads();
+    PN_MARK(s, q, 6);
+    for (int i = w + tid; i < R; i += kFT) {   // rows below: a L_top^T = row, one row per thread
+        double a[kFNB];
+#pragma unroll
+        for (int c = 0; c < kFNB; ++c) a[c] = c < w ? P[c * Rp + off + i] : 0.0;
+#pragma unroll
+        for (int c = 0; c < kFNB; ++c) {
+            if (c < w) {
+                const double x = a[c] * rdg[c];
+                a[c] = x;
+#pragma unroll
+                for (int cc = c + 1; cc < kFNB; ++cc) a[cc] = fma(-x, Lt[c * kFNB + cc], a[cc]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kFNB; ++c)
+            if (c < w) P[c * Rp + off + i] = a[c];
+    }
+    __syncthreads();
+    PN_MARK(s, q, 7);
+    for (int e = tid; e < w * w; e += kFT) {
+        const int c = e / w, r = e - c * w;
+        if (r >= c) P[c * Rp + off + r] = Lt[c * kFNB + r];
+    }
+    __syncthreads();
+    PN_MARK(s, q, 3);
+    for (int e = tid; e < w * R; e += kFT) {   // publish the panel write-through
+        const int c = e / R, i = e - c * R;
+        if (i >= c) st_agent(F + (uint32_t)((j0 + c) * m3 + j0 + i), P[c * Rp + off + i]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(pflag + s, q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    PN_MARK(s, q, 4);
+}
+
+// panel p (published) -> LDS, sc1 loads, kFT * 16 entries in flight
+__device__ void load_panel(int p, const Tiles& T, double* F, double* P) {
+    const int tid = threadIdx.x;
+    const int j0 = kFNB * p, w = min(kFNB, T.k3 - j0), R = T.m3 - j0;
+    const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+    constexpr int kB = 16;
+    for (int e0 = 0; e0 < w * R; e0 += kFT * kB) {
+        double v[kB];
+#pragma unroll
+        for (int q = 0; q < kB; ++q) {
+            const int e = e0 + tid + kFT * q;
+            const int c = e / R, i = e - c * R;
+            v[q] = (e < w * R && i >= c) ? ld_agent(F + (uint32_t)((j0 + c) * T.m3 + j0 + i)) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kB; ++q) {
+            const int e = e0 + tid + kFT * q;
+            const int c = e / R, i = e - c * R;
+            if (e < w * R) P[c * Rp + off + i] = v[q];
+        }
+    }
+}
+
+// rank-w update of tile t with panel p (in LDS), 4x4 register tiles, plain RMW of the owner's columns
+__device__ void update_tile(int t, int p, const Tiles& T, double* F, const double* P) {
+    const int tid = threadIdx.x;
+    const int m3 = T.m3, j0 = kFNB * p, w = min(kFNB, T.k3 - j0), R = m3 - j0;
+    const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+    const int l0 = T.c0(t) - j0, l1 = T.c1(t) - j0;   // the tile's columns, panel frame
+    const int g0 = ((l0 + off) & ~3) - off;            // 4-aligned group start (<= l0)
+    const int ncg = (l1 - g0 + 3) >> 2, nrg = (R - g0 + 3) >> 2;
+    for (int q = tid; q < nrg * ncg; q += kFT) {
+        const int ib = g0 + 4 * (q % nrg), lb = g0 + 4 * (q / nrg);
+        if (ib + 3 < lb) continue;
+        double ac[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) ac[a][b] = 0.0;
+#pragma unroll 1
+        for (int c = 0; c < w; ++c) {
+            {
+                const double2* pc = reinterpret_cast<const double2*>(P + c * Rp);
+                const double2 i01 = pc[(off + ib) >> 1], i23 = pc[((off + ib) >> 1) + 1];
+                const double2 l01 = pc[(off + lb) >> 1], l23 = pc[((off + lb) >> 1) + 1];
+                const double vi[4] = {i01.x, i01.y, i23.x, i23.y};
+                const double vl[4] = {l01.x, l01.y, l23.x, l23.y};
+#pragma unroll
+                for (int a = 0; a < 4; ++a)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) ac[a][b] = fma(vi[a], vl[b], ac[a][b]);
+            }
+        }
+        // the tile's current values (clamped addresses: all 16 loads issue before any store)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t o = (uint32_t)((j0 + min(max(lb + b, l0), l1 - 1)) * m3 + j0);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) ac[a][b] = F[o + (uint32_t)min(ib + a, R - 1)] - ac[a][b];
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int l = lb + b;
+            const uint32_t o = (uint32_t)((j0 + l) * m3 + j0);
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const int i = ib + a;
+                if (l >= l0 && l < l1 && i < R && i >= l) F[o + (uint32_t)i] = ac[a][b];
+            }
+        }
+    }
+}
+
+// A front of more than kSmall rows is factored by a TEAM of G workgroups (G consecutive tickets).
+// Its columns are cut into tiles of kFNB: pivot tiles [kFNB t, min(kFNB t + kFNB, k3)), then update
+// tiles from k3; tile t belongs to member t mod G, which alone assembles and writes it (plain).
+//   assembly, per own tile, in LDS: H's blocks, then the children's update-matrix columns that land
+//     in the tile (host-precomputed ranges), child by child, kFT * kPFL sc1 loads in flight;
+//   panels with lookahead: in iteration p every member holding tiles right of p loads panel p
+//     (published write-through by its owner), the owner of panel p + 1 first applies it to tile p + 1,
+//     factors and publishes panel p + 1 (so the panel chain never waits on other tiles), then every
+//     member applies panel p to its remaining tiles;
+//   member 0 carries the right-hand side (forward solve folded in, as in small_front);
+//   at the end every member republishes its update tiles write-through and adds 1 to the parent's
+//   counter (which waits for the sum of its children's team sizes).
+__device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int32_t* sync, int32_t* pflag, int32_t* status,
+                            const SnDev* __restrict__ sns, const OEnt* __restrict__ omap,
+                            const int32_t* __restrict__ relmap, const int32_t* __restrict__ child_list,
+                            const FTask* __restrict__ ftasks, const FChild* __restrict__ fchild,
+                            const double* __restrict__ hb, const double* __restrict__ g,
+                            const int32_t* __restrict__ perm, double* fronts, double* __restrict__ ysol,
+                            double* acc, double* sm) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int k3 = 3 * S.k, r3 = 3 * S.r, m3 = k3 + r3, G = S.G;
+    double* F = fronts + S.front_off;
+    Tiles T{k3, m3, (k3 + kFNB - 1) / kFNB, 0};
+    T.nt = T.np + (r3 + kFNB - 1) / kFNB;
+    const bool has_b = mem == 0;
+    const int last_own = mem + G * ((T.nt - 1 - mem) / G);
+    double* bv = sm;                               // [m3] right-hand side (member 0)
+    double* pbase = bv + ((m3 + 1) & ~1);          // tile under assembly / panel scratch
+    if (has_b)
+        for (int t = tid; t < m3; t += kFT) bv[t] = t < k3 ? -g[3 * perm[S.c0 + t / 3] + t % 3] : 0.0;
+    // ---- assembly of the own tiles in LDS (the first one's H blocks before the wait)
+    bool waited = S.need == 0;
+    for (int t = mem; t < T.nt; t += G) {
+        const FTask tk = ftasks[S.ftask + t];
+        const int cs = T.c0(t), nc = T.c1(t) - cs;
+        double* Tl = pbase;                        // [nc][m3] column-major
+        for (int e = tid; e < nc * m3; e += kFT) Tl[e] = 0.0;
+        __syncthreads();
+        for (int q = tid; q < (tk.om_e - tk.om_b) * 9; q += kFT) {
+            const OEnt o = omap[tk.om_b + q / 9];
+            const int ii = (q % 9) / 3, jj = q % 3;
+            const int row = 3 * o.a + ii, col = 3 * o.b + jj;
+            if (col < cs || col >= cs + nc || row < col) continue;
+            const double* B = hb + 9 * (int64_t)o.u;
+            Tl[(col - cs) * m3 + row] = o.tr ? B[3 * jj + ii] : B[3 * ii + jj];
+        }
+        if (!waited) {
+            if (tid == 0) wait_geq_sc1(sync + s, S.need, status);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            waited = true;
+            FT_MARK(s, 1);
+        }
+        for (int cq = 0; cq < tk.ch_cnt; ++cq) {
+            __syncthreads();
+            const FChild C = fchild[tk.ch_off + cq];
+            const int n = 3 * C.r, m3c = 3 * (C.k + C.r), k3c = 3 * C.k, nj = C.jb - C.ja;
+            double* Fc = fronts + C.front_off + (int64_t)k3c * m3c + k3c;
+            const int32_t* rm = relmap + C.rows_off;
+            for (int e0 = 0; e0 < nj * n; e0 += kFT * kPFL) {
+                double v[kPFL];
+                int dst[kPFL];
+#pragma unroll
+                for (int q = 0; q < kPFL; ++q) {
+                    const int e = e0 + tid + kFT * q;
+                    const int j = C.ja + e / n, i = e % n;
+                    dst[q] = -1;
+                    v[q] = 0.0;
+                    if (e < nj * n && i >= j) {
+                        v[q] = ld_agent(Fc + (int64_t)j * m3c + i);
+                        dst[q] = (3 * rm[j / 3] + j % 3 - cs) * m3 + 3 * rm[i / 3] + i % 3;
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < kPFL; ++q)
+                    if (dst[q] >= 0) Tl[dst[q]] += v[q];
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < nc * m3; e += kFT) {
+            const int col = cs + e / m3, row = e % m3;
+            if (row >= col) F[(uint32_t)(col * m3 + row)] = Tl[e];
+        }
+        __syncthreads();
+    }
+    if (!waited) {   // (no own tile: cannot happen, G <= tiles)
+        if (tid == 0) wait_geq_sc1(sync + s, S.need, status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (has_b) {   // the children's pending row updates, child order
+        for (int ci = 0; ci < S.nchild; ++ci) {
+            const SnDev C = sns[child_list[S.child_off + ci]];
+            const int32_t* rm = relmap + C.rows_off;
+            for (int t = tid; t < 3 * C.r; t += kFT) bv[3 * rm[t / 3] + t % 3] -= ld_agent(acc + C.acc_off + t);
+            __syncthreads();
+        }
+    }
+    FT_MARK(s, 2);
+
+    // ---- pivot panels, with lookahead
+    bool bad = false;
+    if (mem == 0) factor_publish(0, s, T, F, pflag, pbase, bad);   // tile 0 belongs to member 0
+    for (int p = 0; p < T.np; ++p) {
+        if (!has_b && last_own <= p) break;   // no tile of this member right of panel p
+        const int j0 = kFNB * p, w = min(kFNB, k3 - j0), R = m3 - j0;
+        const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+        double* P = pbase;
+        if (p % G != mem) {
+            if (tid == 0) wait_geq_sc1(pflag + s, p + 1, status);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+        if (p + 1 < T.np && (p + 1) % G == mem) PN_MARK(s, p + 1, 0);
+        load_panel(p, T, F, P);
+        __syncthreads();
+        if (has_b) {   // y of the panel's rows, then the rows below
+            if (wave == 0) {
+                double bl = lane < w ? bv[j0 + lane] : 0.0;
+                for (int c = 0; c < w; ++c) {
+                    const double yc = __shfl(bl, c, 64) / P[c * Rp + off + c];
+                    if (lane == c) bl = yc;
+                    else if (lane > c && lane < w) bl = fma(-P[c * Rp + off + lane], yc, bl);
+                }
+                if (lane < w) bv[j0 + lane] = bl;
+            }
+            __syncthreads();
+            for (int i = w + tid; i < R; i += kFT) {
+                double sacc = 0.0;
+                for (int c = 0; c < w; ++c) sacc = fma(P[c * Rp + off + i], bv[j0 + c], sacc);
+                bv[j0 + i] -= sacc;
+            }
+        }
+        const bool ahead = p + 1 < T.np && (p + 1) % G == mem;
+        if (ahead) {   // lookahead: panel p+1 first
+            PN_MARK(s, p + 1, 1);
+            update_tile(p + 1, p, T, F, P);
+            __syncthreads();
+            PN_MARK(s, p + 1, 2);
+            factor_publish(p + 1, s, T, F, pflag, pbase, bad);
+            __syncthreads();
+            load_panel(p, T, F, P);
+            __syncthreads();
+        }
+        for (int t = mem; t < T.nt; t += G)
+            if (t > p && !(ahead && t == p + 1)) update_tile(t, p, T, F, P);
+        __syncthreads();
+    }
+    if (bad && lane == 0) atomicExch(status, 1);
+    // ---- out: own update tiles write-through for the parent; member 0: y and the pending updates
+    if (S.parent >= 0) {
+        for (int t = mem; t < T.nt; t += G) {
+            if (t < T.np) continue;
+            const int cs = T.c0(t), n = (T.c1(t) - cs) * m3;
+            for (int e0 = 0; e0 < n; e0 += kFT * kPFL) {
+                double v[kPFL];
+                int a[kPFL];
+#pragma unroll
+                for (int q = 0; q < kPFL; ++q) {
+                    const int e = e0 + tid + kFT * q;
+                    const int col = cs + e / m3, row = e % m3;
+                    a[q] = (e < n && row >= col) ? col * m3 + row : -1;
+                    v[q] = a[q] >= 0 ? F[(uint32_t)a[q]] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < kPFL; ++q)
+                    if (a[q] >= 0) st_agent(F + (uint32_t)a[q], v[q]);
+            }
+        }
+    }
+    if (has_b) {
+        for (int t = tid; t < k3; t += kFT) ysol[3 * (int64_t)S.c0 + t] = bv[t];
+        if (S.parent >= 0)
+            for (int t = tid; t < r3; t += kFT) st_agent(acc + S.acc_off + t, -bv[k3 + t]);
+    }
+    FT_MARK(s, 3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (mem == 0) FT_MARK(s, 4);
+    if (tid == 0 && S.parent >= 0)
+        __hip_atomic_fetch_add(sync + S.parent, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restrict__ order, int32_t* sync,
+                                                       int32_t* status, const SnDev* __restrict__ sns,
+                                                       const OEnt* __restrict__ omap,
+                                                       const int32_t* __restrict__ relmap,
+                                                       const int32_t* __restrict__ child_list,
+                                                       const FTask* __restrict__ ftasks,
+                                                       const FChild* __restrict__ fchild,
+                                                       const double* __restrict__ hb, const double* __restrict__ g,
+                                                       const int32_t* __restrict__ perm, double* fronts,
+                                                       double* __restrict__ ysol, double* acc, int ns) {
+    extern __shared__ __attribute__((aligned(16))) double smem_f[];
+    double* sm = smem_f + 2;   // smem_f[0]: the claimed ticket (no static LDS: keeps the base 16-B aligned)
+    const int code = claim_lds(order, sync, reinterpret_cast<int*>(smem_f));
+    const int s = code >> 6, mem = code & 63;
+    const SnDev S = sns[s];
+    if (mem == 0) FT_MARK(s, 0);
+    if (S.G == 1 && 3 * (S.k + S.r) <= kSmall && S.nchild <= kMaxCh)
+        small_front(s, S, sync + 1, status, sns, omap, relmap, child_list, hb, g, perm, fronts, ysol, acc, sm);
+    else
+        large_front(s, mem, S, sync + 1, sync + 1 + ns, status, sns, omap, relmap, child_list, ftasks, fchild, hb, g,
+                    perm, fronts, ysol, acc, sm);
+}
+
 template <typename T>
 int dalloc_copy(T** d, const std::vector<T>& h) {
     const size_t n = std::max<size_t>(h.size(), 1);
@@ -481,6 +1139,10 @@ struct CholDev {
     int64_t nnzb_upper = 0;
     // factorization task lists (device) and the per-level launch plan (host)
     int32_t* order_fwd = nullptr;      // fronts bottom-up (level order) / top-down
+    int32_t* order_fac = nullptr;      // fused factorization tickets (front * 64 + member)
+    FTask* ftasks = nullptr;           // large fronts: per-tile assembly lists
+    FChild* fchild = nullptr;
+    int64_t n_tickets = 0;
     int32_t* order_bwd = nullptr;
     int32_t* sync = nullptr;           // [ticket_f, cnt_f[ns], ticket_b, done_b[ns]], zeroed per solve
     size_t sync_bytes = 0;
@@ -493,6 +1155,9 @@ struct CholDev {
     struct Level { int32_t asm_off, asm_cnt; size_t lds_asm; std::vector<Step> steps; };
     std::vector<Level> plan;
     int64_t n_launches = 0;
+    // fused DAG factorization + forward solve (used when every front fits its LDS budget)
+    bool fused = false;
+    size_t lds_fused = 0;
 };
 
 }  // namespace
@@ -502,7 +1167,7 @@ extern "C" void dpg_chol_destroy(void* h) {
     if (!c) return;
     void* ptrs[] = {c->sns, c->omap, c->child_list, c->relmap, c->rows, c->level_list, c->perm, c->pos,
                     c->fronts, c->acc, c->ysol, c->xsol, c->status, c->asm_tasks, c->asm_child, c->panel_tasks, c->upd_tasks,
-                    c->order_fwd, c->order_bwd, c->sync};
+                    c->order_fwd, c->order_bwd, c->sync, c->order_fac, c->ftasks, c->fchild};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     delete c;
@@ -564,10 +1229,91 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         d.omap_n = (int32_t)per[(size_t)s].size();
         d.acc_off = acc_total;
         d.parent = S.sn_parent[(size_t)s];
+        const int32_t m3 = 3 * (d.k + d.r);
+        d.G = (m3 <= kSmall && d.nchild <= kMaxCh)
+                  ? 1
+                  : std::min(kGmax, (3 * d.k + kFNB - 1) / kFNB + (3 * d.r + kFNB - 1) / kFNB);
+        d.need = 0;
         acc_total += 3 * d.r;
         omap.insert(omap.end(), per[(size_t)s].begin(), per[(size_t)s].end());
     }
+    for (int32_t s = 0; s < S.ns; ++s)
+        if (sns[(size_t)s].parent >= 0) sns[(size_t)sns[(size_t)s].parent].need += sns[(size_t)s].G;
+    // large fronts: per tile, the H blocks (omap range) and the children's column ranges
+    std::vector<FTask> ftasks;
+    std::vector<FChild> fchild;
+    for (int32_t s = 0; s < S.ns; ++s) {
+        SnDev& d = sns[(size_t)s];
+        d.ftask = (int32_t)ftasks.size();
+        const int32_t k3 = 3 * d.k, m3 = 3 * (d.k + d.r);
+        if (d.G == 1 && m3 <= kSmall && d.nchild <= kMaxCh) continue;
+        const OEnt* ob = omap.data() + d.omap_off;
+        std::vector<int32_t> cuts;
+        for (int32_t c = 0; c < k3; c += kFNB) cuts.push_back(c);
+        for (int32_t c = k3; c < m3; c += kFNB) cuts.push_back(c);
+        cuts.push_back(m3);
+        for (size_t t = 0; t + 1 < cuts.size(); ++t) {
+            const int32_t c0 = cuts[t], c1 = cuts[t + 1];
+            FTask ft{0, 0, (int32_t)fchild.size(), 0};
+            ft.om_b = (int32_t)d.omap_off + (int32_t)(std::lower_bound(ob, ob + d.omap_n, c0 / 3,
+                          [](const OEnt& o, int32_t v) { return o.b < v; }) - ob);
+            ft.om_e = (int32_t)d.omap_off + (int32_t)(std::upper_bound(ob, ob + d.omap_n, (c1 - 1) / 3,
+                          [](int32_t v, const OEnt& o) { return v < o.b; }) - ob);
+            for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
+                const int32_t ch = S.child_list[(size_t)ci];
+                const SnDev& cd = sns[(size_t)ch];
+                const int32_t* rm = S.relmap.data() + cd.rows_off;
+                int32_t ja = 3 * cd.r, jb = 0;
+                for (int32_t j = 0; j < 3 * cd.r; ++j) {
+                    const int32_t pj = 3 * rm[j / 3] + j % 3;
+                    if (pj >= c0 && pj < c1) { ja = std::min(ja, j); jb = j + 1; }
+                }
+                if (jb > ja) fchild.push_back(FChild{ja, jb, cd.k, cd.r, cd.front_off, cd.rows_off});
+            }
+            ft.ch_cnt = (int32_t)fchild.size() - ft.ch_off;
+            ftasks.push_back(ft);
+        }
+    }
+    std::vector<int32_t> order_fac;   // fused tickets: front * 64 + team member, children first
+    for (int32_t s : S.level_list)
+        for (int32_t m = 0; m < sns[(size_t)s].G; ++m) order_fac.push_back(s * 64 + m);
+    c->n_tickets = (int64_t)order_fac.size();
     c->level_ptr = S.level_ptr;
+    // assembly tiles of front s, `ct` columns each: the omap range and the children (with their
+    // contiguous column range) that land in the tile
+    auto build_tiles = [&](int32_t s, int32_t ct, std::vector<AsmTask>& tl, std::vector<AsmChild>& cl) {
+        const SnDev& d = sns[(size_t)s];
+        const int32_t m3 = 3 * (d.k + d.r);
+        const OEnt* ob = omap.data() + d.omap_off;
+        for (int32_t c0 = 0; c0 < m3; c0 += ct) {
+            const int32_t c1 = std::min(c0 + ct, m3);
+            AsmTask t{s, c0, 0, 0, (int32_t)cl.size(), 0};
+            // omap entries with block column in [c0 / 3, (c1 - 1) / 3]
+            t.om_b = (int32_t)d.omap_off + (int32_t)(std::lower_bound(ob, ob + d.omap_n, c0 / 3,
+                         [](const OEnt& o, int32_t v) { return o.b < v; }) - ob);
+            t.om_e = (int32_t)d.omap_off + (int32_t)(std::upper_bound(ob, ob + d.omap_n, (c1 - 1) / 3,
+                         [](int32_t v, const OEnt& o) { return v < o.b; }) - ob);
+            for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
+                const int32_t ch = S.child_list[(size_t)ci];
+                const SnDev& cd = sns[(size_t)ch];
+                const int32_t* rm = S.relmap.data() + cd.rows_off;
+                int32_t ja = 3 * cd.r, jb = 0;
+                for (int32_t j = 0; j < 3 * cd.r; ++j) {
+                    const int32_t pj = 3 * rm[j / 3] + j % 3;
+                    if (pj >= c0 && pj < c1) { ja = std::min(ja, j); jb = j + 1; }
+                }
+                if (jb > ja) cl.push_back(AsmChild{ch, ja, jb, 0});
+            }
+            t.ch_cnt = (int32_t)cl.size() - t.ch_off;
+            tl.push_back(t);
+        }
+    };
+    // fused path: LDS budget of the largest front
+    for (int32_t s = 0; s < S.ns; ++s) {
+        const SnDev& d = sns[(size_t)s];
+        c->lds_fused = std::max(c->lds_fused, 8 * fused_lds_doubles(3 * (d.k + d.r), 3 * d.k));
+    }
+    c->fused = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_LEVELS") == nullptr;
     c->lds_solve.assign((size_t)S.n_levels, 0);
     std::vector<AsmTask> asm_t;
     std::vector<AsmChild> asm_c;
@@ -587,29 +1333,7 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
             ms = std::max(ms, (size_t)(kSB * kSB + kSB + m3) * sizeof(double));
             lds_asm[(size_t)l] = std::max(lds_asm[(size_t)l], (size_t)kCT * m3 * sizeof(double));
             maxk3 = std::max(maxk3, 3 * d.k);
-            const OEnt* ob = omap.data() + d.omap_off;
-            for (int32_t c0 = 0; c0 < m3; c0 += kCT) {
-                const int32_t c1 = std::min(c0 + kCT, m3);
-                AsmTask t{s, c0, 0, 0, (int32_t)asm_c.size(), 0};
-                // omap entries with block column in [c0 / 3, (c1 - 1) / 3]
-                t.om_b = (int32_t)d.omap_off + (int32_t)(std::lower_bound(ob, ob + d.omap_n, c0 / 3,
-                             [](const OEnt& o, int32_t v) { return o.b < v; }) - ob);
-                t.om_e = (int32_t)d.omap_off + (int32_t)(std::upper_bound(ob, ob + d.omap_n, (c1 - 1) / 3,
-                             [](int32_t v, const OEnt& o) { return v < o.b; }) - ob);
-                for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
-                    const int32_t ch = S.child_list[(size_t)ci];
-                    const SnDev& cd = sns[(size_t)ch];
-                    const int32_t* rm = S.relmap.data() + cd.rows_off;
-                    int32_t ja = 3 * cd.r, jb = 0;
-                    for (int32_t j = 0; j < 3 * cd.r; ++j) {
-                        const int32_t pj = 3 * rm[j / 3] + j % 3;
-                        if (pj >= c0 && pj < c1) { ja = std::min(ja, j); jb = j + 1; }
-                    }
-                    if (jb > ja) asm_c.push_back(AsmChild{ch, ja, jb, 0});
-                }
-                t.ch_cnt = (int32_t)asm_c.size() - t.ch_off;
-                asm_t.push_back(t);
-            }
+            build_tiles(s, kCT, asm_t, asm_c);
         }
         L.asm_cnt = (int32_t)asm_t.size() - L.asm_off;
         c->n_launches += 1;
@@ -652,8 +1376,12 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     {
         std::vector<int32_t> bwd(S.level_list.rbegin(), S.level_list.rend());
         rc |= dalloc_copy(&c->order_fwd, S.level_list);
+        rc |= dalloc_copy(&c->order_fac, order_fac);
+        rc |= dalloc_copy(&c->ftasks, ftasks);
+        rc |= dalloc_copy(&c->fchild, fchild);
         rc |= dalloc_copy(&c->order_bwd, bwd);
-        c->sync_bytes = ((size_t)(2 + 2 * S.ns) * sizeof(int32_t) + 15) & ~size_t(15);
+        // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns]]
+        c->sync_bytes = ((size_t)(3 + 3 * S.ns) * sizeof(int32_t) + 15) & ~size_t(15);
         rc |= hipMalloc(reinterpret_cast<void**>(&c->sync), c->sync_bytes) != hipSuccess;
         for (size_t v : c->lds_solve) c->lds_solve_max = std::max(c->lds_solve_max, v);
     }
@@ -676,6 +1404,16 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     const dpg_chol_sym& S = c->sym;
     const double* g = hb + 9 * c->nnzb_upper;
     if (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess) return DPG_ERR_HIP;
+    if (c->fused) {
+        if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
+        hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
+                           c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
+                           c->perm, c->fronts,
+                           c->ysol, c->acc, S.ns);
+        hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
+                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol);
+        return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+    }
     int pid = 0;
     for (int32_t l = 0; l < S.n_levels; ++l) {
         const CholDev::Level& L = c->plan[(size_t)l];
@@ -717,6 +1455,23 @@ extern "C" void dpg_chol_stats(void* h, double out[6]) {
 extern "C" int dpg_chol_prof_dump(unsigned long long* out, int n, unsigned long long* span) {
     if (hipMemcpyFromSymbol(span, HIP_SYMBOL(g_span), sizeof(unsigned long long) * kProfL * kProfW * 2) != hipSuccess) return -1;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * (size_t)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int dpg_chol_steps_dump(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_steps), sizeof(unsigned long long) * 16 * 8 * (size_t)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int dpg_chol_panel_dump(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_panel), sizeof(unsigned long long) * 16 * 8 * (size_t)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int dpg_chol_front_dump(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_front), sizeof(unsigned long long) * 8 * (size_t)n) == hipSuccess ? 0 : -1;
+}
+extern "C" void dpg_chol_tree(void* h, int32_t* parent, int32_t* m3, int32_t* k3) {
+    const dpg_chol_sym& S = reinterpret_cast<CholDev*>(h)->sym;
+    for (int32_t s = 0; s < S.ns; ++s) {
+        parent[s] = S.sn_parent[(size_t)s];
+        k3[s] = 3 * (S.sn_c0[(size_t)s + 1] - S.sn_c0[(size_t)s]);
+        m3[s] = k3[s] + 3 * (int32_t)(S.sn_rows_ptr[(size_t)s + 1] - S.sn_rows_ptr[(size_t)s]);
+    }
 }
 extern "C" int dpg_chol_prof_reset(void) {
     std::vector<unsigned long long> sp((size_t)kProfL * kProfW * 2, 0ull);

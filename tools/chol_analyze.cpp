@@ -31,6 +31,28 @@ int main(int argc, char** argv) {
     }
     printf("n=%lld ns=%d levels=%d max_front=%d flops=%.3g nnzL=%lld fronts=%.1f MB crit_path_flops=%.3g\n",
            (long long)n, S.ns, S.n_levels, S.max_front, S.flops, (long long)nnzL, S.front_off[S.ns] * 8e-6, crit);
+    {
+        const int edges[] = {24, 48, 64, 96, 128, 160, 192, 256, 320, 100000};
+        int cnt[10] = {0};
+        double fl_b[10] = {0};
+        for (int s = 0; s < S.ns; ++s) {
+            const int m3 = 3 * (S.sn_c0[s + 1] - S.sn_c0[s] + (int)(S.sn_rows_ptr[s + 1] - S.sn_rows_ptr[s]));
+            int b = 0;
+            while (m3 > edges[b]) ++b;
+            ++cnt[b]; fl_b[b] += fl[s];
+        }
+        int nch_hist[6] = {0};
+        for (int s = 0; s < S.ns; ++s) {
+            const int m3 = 3 * (S.sn_c0[s + 1] - S.sn_c0[s] + (int)(S.sn_rows_ptr[s + 1] - S.sn_rows_ptr[s]));
+            if (m3 > 96) continue;
+            const int64_t nc = S.child_ptr[s + 1] - S.child_ptr[s];
+            nch_hist[nc == 0 ? 0 : nc <= 2 ? 1 : nc <= 4 ? 2 : nc <= 8 ? 3 : nc <= 16 ? 4 : 5]++;
+        }
+        printf("small-front children: 0:%d <=2:%d <=4:%d <=8:%d <=16:%d >16:%d\n", nch_hist[0], nch_hist[1], nch_hist[2], nch_hist[3], nch_hist[4], nch_hist[5]);
+        printf("m3 histogram:");
+        for (int b = 0; b < 10; ++b) printf(" <=%d:%d(%.2g)", edges[b], cnt[b], fl_b[b]);
+        printf("\n");
+    }
     for (int l = 0; l < S.n_levels; ++l) {
         int cnt = 0, mk = 0, mm = 0; double lf = 0, mf = 0;
         for (int q = S.level_ptr[l]; q < S.level_ptr[l + 1]; ++q) {

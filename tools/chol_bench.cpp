@@ -22,6 +22,10 @@ void dpg_chol_stats(void* chol, double out[6]);
 #ifdef DPG_CHOL_TIMING
 int dpg_chol_prof_dump(unsigned long long* out, int n, unsigned long long* span);
 int dpg_chol_prof_reset(void);
+int dpg_chol_front_dump(unsigned long long* out, int n);
+int dpg_chol_panel_dump(unsigned long long* out, int n);
+int dpg_chol_steps_dump(unsigned long long* out, int n);
+void dpg_chol_tree(void* h, int32_t* parent, int32_t* m3, int32_t* k3);
 #endif
 }
 
@@ -134,6 +138,70 @@ int main(int argc, char** argv) {
            "\"mflop\": %.1f, \"ms_per_solve\": %.4f, \"residual_rel\": %.3e, \"status\": %d}\n",
            (long long)n, (long long)P, st[0], st[1], st[2], st[3] / 1e6, ms / iters, rmax / gmax, status);
 #ifdef DPG_CHOL_TIMING
+    {
+        // fused path: per-front stamps of the last solve -> the critical path through the tree
+        const int ns = (int)st[0];
+        std::vector<unsigned long long> fm((size_t)ns * 8, 0ull);
+        if (dpg_chol_prof_reset()) return 1;
+        if (dpg_chol_solve(ch, d_hb, s)) return 1;
+        CK(hipStreamSynchronize(s));
+        std::vector<int32_t> par((size_t)ns), m3v((size_t)ns), k3v((size_t)ns);
+        dpg_chol_tree(ch, par.data(), m3v.data(), k3v.data());
+        if (dpg_chol_front_dump(fm.data(), ns) == 0 && fm[4] != 0) {
+            unsigned long long t0 = ~0ull, t1 = 0;
+            int root = -1;
+            for (int q = 0; q < ns; ++q) {
+                t0 = std::min(t0, fm[(size_t)q * 8]);
+                if (fm[(size_t)q * 8 + 4] > t1) { t1 = fm[(size_t)q * 8 + 4]; root = q; }
+            }
+            printf("fused factor span %.1f us (last front %d)\n", (t1 - t0) / 100.0, root);
+            double sw = 0, sa = 0, sf = 0, so = 0, sl = 0;
+            int depth = 0;
+            for (int q = root; q >= 0;) {
+                const unsigned long long* m = fm.data() + (size_t)q * 8;
+                int last = -1;
+                for (int c = 0; c < ns; ++c)
+                    if (par[(size_t)c] == q && (last < 0 || fm[(size_t)c * 8 + 4] > fm[(size_t)last * 8 + 4])) last = c;
+                const double lat = last >= 0 ? ((double)m[1] - (double)fm[(size_t)last * 8 + 4]) / 100.0 : 0.0;
+                printf("  front %5d m3 %3d k3 %3d | claim %8.2f wait %7.2f (signal->ready %5.2f) asm %6.2f factor %7.2f out %6.2f\n", q,
+                       m3v[(size_t)q], k3v[(size_t)q], (m[0] - t0) / 100.0, ((double)m[1] - (double)m[0]) / 100.0, lat,
+                       (m[2] - m[1]) / 100.0, (m[3] - m[2]) / 100.0, (m[4] - m[3]) / 100.0);
+                sw += lat; sa += (m[2] - m[1]) / 100.0; sf += (m[3] - m[2]) / 100.0; so += (m[4] - m[3]) / 100.0;
+                sl += 0; ++depth;
+                q = last;
+            }
+            std::vector<unsigned long long> pm((size_t)ns * 16 * 8, 0ull);
+            if (dpg_chol_panel_dump(pm.data(), ns) == 0) {
+                for (int q : {ns - 1, ns - 2, ns - 9}) {
+                    if (q < 0) continue;
+                    printf("  panels of front %d (k3 %d):", q, k3v[(size_t)q]);
+                    for (int pp = 0; pp < 16; ++pp) {
+                        const unsigned long long* m = pm.data() + ((size_t)q * 16 + pp) * 8;
+                        if (!m[4]) continue;
+                        printf(" [p%d pub %.1f", pp, ((double)m[4] - (double)t0) / 100.0);
+                        if (m[0]) printf(" wake->ld %.1f upd %.1f fac %.1f (ld %.1f potrf %.1f trsm %.1f) pub %.1f", ((double)m[1] - (double)m[0]) / 100.0,
+                                         ((double)m[2] - (double)m[1]) / 100.0, ((double)m[3] - (double)m[2]) / 100.0,
+                                         ((double)m[5] - (double)m[2]) / 100.0, ((double)m[6] - (double)m[5]) / 100.0,
+                                         ((double)m[7] - (double)m[6]) / 100.0, ((double)m[4] - (double)m[3]) / 100.0);
+                        printf("]");
+                    }
+                    printf("\n");
+                }
+            }
+            std::vector<unsigned long long> sm2((size_t)ns * 16 * 8, 0ull);
+            if (dpg_chol_steps_dump(sm2.data(), ns) == 0) {
+                const int q = ns - 2;
+                for (int pp = 1; pp < 3; ++pp) {
+                    const unsigned long long* m = sm2.data() + ((size_t)q * 16 + pp) * 8;
+                    const unsigned long long* pn = pm.data() + ((size_t)q * 16 + pp) * 8;
+                    printf("  front %d panel %d potrf steps (us from potrf start):", q, pp);
+                    for (int k = 0; k < 8; ++k) printf(" %.2f", ((double)m[k] - (double)pn[5]) / 100.0);
+                    printf(" end %.2f\n", ((double)pn[6] - (double)pn[5]) / 100.0);
+                }
+            }
+            printf("critical path: %d fronts, hand-off %.1f + assembly %.1f + factor %.1f + out %.1f us\n", depth, sw, sa, sf, so);
+        }
+    }
     {
         // phase marks of workgroup 0 of every factor launch of the last solve (10 ns ticks)
         const int slots = 40, nl = 512, nw = 2048;
