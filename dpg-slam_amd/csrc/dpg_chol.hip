@@ -161,9 +161,37 @@ __global__ __launch_bounds__(kT) void chol_assemble(const AsmTask* __restrict__ 
 __device__ __forceinline__ double rsqrt_nr(double d) {
     double y = __builtin_amdgcn_rsq(d);
     const double h = 0.5 * d;
-    y = y * (1.5 - h * y * y);
-    y = y * (1.5 - h * y * y);
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
     return y;
+}
+
+// Cholesky factor of a 3x3 SPD block and the inverse of that factor, from the block's leading
+// minors (d00, M2, det): the three reciprocal square roots are independent, so the dependent chain
+// is about a third of the column-by-column one (a wave64 fp64 op is ~32 cycles of latency).
+struct Chol3 { double l00, l10, l11, l20, l21, l22, m00, m10, m11, m20, m21, m22; };
+__device__ __forceinline__ Chol3 chol3(double d00, double d10, double d11, double d20, double d21, double d22,
+                                       bool& bad) {
+    double M2 = fma(d00, d11, -d10 * d10);
+    const double c0 = fma(d11, d22, -d21 * d21), c1 = fma(d10, d22, -d21 * d20), c2 = fma(d10, d21, -d11 * d20);
+    double det = fma(d00, c0, fma(-d10, c1, d20 * c2));
+    if (!(d00 > 0.0 && M2 > 0.0 && det > 0.0)) { bad = true; d00 = 1.0; M2 = 1.0; det = 1.0; d10 = d20 = d21 = 0.0; }
+    const double r0 = rsqrt_nr(d00), r1 = rsqrt_nr(M2), r2 = rsqrt_nr(det);
+    Chol3 L;
+    L.l00 = d00 * r0;                  // sqrt(d00)
+    const double s2 = M2 * r1;         // sqrt(M2)
+    L.l11 = s2 * r0;                   // sqrt(M2 / d00)
+    L.l22 = (det * r2) * r1;           // sqrt(det / M2)
+    L.m00 = r0;
+    L.m11 = L.l00 * r1;                // sqrt(d00 / M2)
+    L.m22 = s2 * r2;                   // sqrt(M2 / det)
+    L.l10 = d10 * r0;
+    L.l20 = d20 * r0;
+    L.l21 = fma(-L.l20, L.l10, d21) * L.m11;
+    L.m10 = -L.l10 * (L.m00 * L.m11);
+    L.m21 = -L.l21 * (L.m11 * L.m22);
+    L.m20 = fma(L.l10, L.l21, -L.l20 * L.l11) * (L.m00 * L.m11 * L.m22);
+    return L;
 }
 
 // panel: one workgroup per front, one panel row per thread in registers (NT >= rows), right-
@@ -519,18 +547,13 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // LDS carve of the factorization phase (doubles): panel [kFNB][Rp] with row offset `off` so that
 // trailing rows start 32-B aligned, L_top column-major [kFNB][kFNB], 1/diag, step scratch.
 __host__ __device__ inline int fused_rp(int R, int off) { return (R + off + 3) & ~3; }
 __host__ __device__ inline size_t fused_lds_doubles(int m3, int k3) {
     const size_t large = ((m3 + 1) & ~1) + std::max((size_t)kFNB * m3,
-                                                     (size_t)kFNB * fused_rp(m3, 3) + kFNB * kFNB + kFNB + 4 * kFNB + 16);
+                                                     (size_t)kFNB * fused_rp(m3, 3) + kFNB * kFNB + 8 * (kFNB / 3) + 384);
     (void)k3;
     const size_t small = m3 <= kSmall ? (size_t)m3 * m3 + m3 + (kMaxCh * sizeof(ChMeta) + kMaxCh * (kSmall / 3) * 4 + 7) / 8 : 0;
     return 2 + std::max(small, large);
@@ -737,8 +760,6 @@ __device__ void factor_publish(int q, int s, const Tiles& T, double* F, int32_t*
     double* P = pbase;
     double* Lt = P + (size_t)kFNB * Rp;
     double* rdg = Lt + kFNB * kFNB;
-    double* xs = rdg + kFNB;
-    double* sd = xs + 4 * kFNB;
     for (int e = tid; e < w * R; e += kFT) {
         const int c = e / R, i = e - c * R;
         P[c * Rp + off + i] = i >= c ? F[(uint32_t)((j0 + c) * m3 + j0 + i)] : 0.0;
@@ -746,67 +767,84 @@ __device__ void factor_publish(int q, int s, const Tiles& T, double* F, int32_t*
     for (int e = tid; e < kFNB * kFNB; e += kFT) Lt[e] = 0.0;
     __syncthreads();
     PN_MARK(s, q, 5);
-    if (wave == 0) {   // POTRF of the top w x w block: lane i owns row i, pr[c] = row i, column c0 + c
+    // POTRF of the top w x w block by all 8 waves: lane = row, wave v holds columns v, v + 8, v + 16
+    // in registers.  Per 3x3 step the three owning waves post their columns to LDS (double-
+    // buffered: one barrier per step), every wave factors the 3x3 block and computes its rows' x
+    // redundantly, and updates its own columns (the other rows' x by v_readlane).
+    {
         const int i = lane;
-        double pr[kFNB];
+        double col[3];
 #pragma unroll
-        for (int c = 0; c < kFNB; ++c) pr[c] = (i < w && c < w && c <= i) ? P[c * Rp + off + i] : 0.0;
+        for (int k = 0; k < 3; ++k) {
+            const int c = wave + 8 * k;
+            col[k] = (c < w && i < w && i >= c) ? P[c * Rp + off + i] : 0.0;
+        }
+        double* cb = rdg + 8 * (kFNB / 3);   // [2][3][64]
 #pragma unroll 1
-        for (int c0 = 0; c0 < w; c0 += 3) {
-            ST_MARK(s, q, c0 / 3);
-            // the step's 3x3 diagonal block and, below, the other rows' x: straight from the owning
-            // lanes' registers (v_readlane, uniform lane index) -- no LDS round trips in the chain
-            double d00 = rdlane(pr[0], c0), d10 = rdlane(pr[0], c0 + 1), d11 = rdlane(pr[1], c0 + 1);
-            double d20 = rdlane(pr[0], c0 + 2), d21 = rdlane(pr[1], c0 + 2), d22 = rdlane(pr[2], c0 + 2);
-            if (!(d00 > 0.0)) { bad = true; d00 = 1.0; }
-            const double i00 = rsqrt_nr(d00), l00 = d00 * i00;
-            const double l10 = d10 * i00, l20 = d20 * i00;
-            double e11 = d11 - l10 * l10;
-            if (!(e11 > 0.0)) { bad = true; e11 = 1.0; }
-            const double i11 = rsqrt_nr(e11), l11 = e11 * i11;
-            const double l21 = (d21 - l20 * l10) * i11;
-            double e22 = d22 - l20 * l20 - l21 * l21;
-            if (!(e22 > 0.0)) { bad = true; e22 = 1.0; }
-            const double i22 = rsqrt_nr(e22), l22 = e22 * i22;
-            double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-            if (i == c0) { x0 = l00; }
-            else if (i == c0 + 1) { x0 = l10; x1 = l11; }
-            else if (i == c0 + 2) { x0 = l20; x1 = l21; x2 = l22; }
-            else if (i > c0 + 2 && i < w) {
-                x0 = pr[0] * i00;
-                x1 = (pr[1] - x0 * l10) * i11;
-                x2 = (pr[2] - x0 * l20 - x1 * l21) * i22;
-            }
-            if (i >= c0 && i < w) {
-                Lt[c0 * kFNB + i] = x0;
-                if (i >= c0 + 1) Lt[(c0 + 1) * kFNB + i] = x1;
-                if (i >= c0 + 2) Lt[(c0 + 2) * kFNB + i] = x2;
-            }
-            if (i == c0) { rdg[c0] = i00; rdg[c0 + 1] = i11; rdg[c0 + 2] = i22; }
-            const bool upd = i > c0 + 2 && i < w;
+        for (int c0 = 0, st = 0; c0 < w; c0 += 3, ++st) {
+            ST_MARK(s, q, st);
+            double* cbs = cb + (st & 1) * 192;
 #pragma unroll
-            for (int c = 3; c < kFNB; ++c) {
-                const int cc = min(c0 + c, kFNB - 1);
-                const double y0 = rdlane(x0, cc), y1 = rdlane(x1, cc), y2 = rdlane(x2, cc);
-                const double v = fma(-x2, y2, fma(-x1, y1, fma(-x0, y0, pr[c])));
-                pr[c - 3] = (upd && c0 + c < w && c0 + c <= i) ? v : pr[c];
+            for (int j = 0; j < 3; ++j) {
+                const int cj = c0 + j;
+                if ((cj & 7) == wave) {
+                    const int k = cj >> 3;
+                    cbs[j * 64 + i] = k == 0 ? col[0] : (k == 1 ? col[1] : col[2]);
+                }
             }
-            pr[kFNB - 3] = pr[kFNB - 2] = pr[kFNB - 1] = 0.0;
+            __syncthreads();
+            const Chol3 L = chol3(cbs[c0], cbs[c0 + 1], cbs[64 + c0 + 1], cbs[c0 + 2], cbs[64 + c0 + 2],
+                                  cbs[128 + c0 + 2], bad);
+            const double p0 = cbs[i], p1 = cbs[64 + i], p2 = cbs[128 + i];
+            double x0 = p0 * L.m00;
+            double x1 = fma(p0, L.m10, p1 * L.m11);
+            double x2 = fma(p0, L.m20, fma(p1, L.m21, p2 * L.m22));
+            if (i == c0) { x0 = L.l00; x1 = 0.0; x2 = 0.0; }
+            else if (i == c0 + 1) { x0 = L.l10; x1 = L.l11; x2 = 0.0; }
+            else if (i == c0 + 2) { x0 = L.l20; x1 = L.l21; x2 = L.l22; }
+            if (i == 0 && wave == 0) {
+                double* mi = rdg + 2 * c0;   // 8 doubles per 3x3 block
+                mi[0] = L.m00; mi[1] = L.m10; mi[2] = L.m11; mi[3] = L.m20; mi[4] = L.m21; mi[5] = L.m22;
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int c = wave + 8 * k;
+                if (c < c0 || c >= w) continue;   // wave-uniform
+                if (c < c0 + 3) {                  // the step's own columns: final L values
+                    const double xv = c == c0 ? x0 : (c == c0 + 1 ? x1 : x2);
+                    col[k] = (i >= c && i < w) ? xv : 0.0;
+                } else {
+                    const double y0 = rdlane(x0, c), y1 = rdlane(x1, c), y2 = rdlane(x2, c);
+                    const double v = fma(-x2, y2, fma(-x1, y1, fma(-x0, y0, col[k])));
+                    col[k] = (i >= c && i < w) ? v : col[k];
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int c = wave + 8 * k;
+            if (c < w && i < w) Lt[c * kFNB + i] = col[k];
         }
     }
     __syncthreads();
     PN_MARK(s, q, 6);
-    for (int i = w + tid; i < R; i += kFT) {   // rows below: a L_top^T = row, one row per thread
+    // rows below: a L_top^T = row, one row per thread, by 3x3 blocks (x_b = a_b Minv_b^T, then the
+    // later blocks of the row are updated -- all their products independent)
+    for (int i = w + tid; i < R; i += kFT) {
         double a[kFNB];
 #pragma unroll
         for (int c = 0; c < kFNB; ++c) a[c] = c < w ? P[c * Rp + off + i] : 0.0;
 #pragma unroll
-        for (int c = 0; c < kFNB; ++c) {
-            if (c < w) {
-                const double x = a[c] * rdg[c];
-                a[c] = x;
+        for (int b = 0; b < kFNB; b += 3) {
+            if (b < w) {
+                const double* mi = rdg + 2 * b;
+                const double x0 = a[b] * mi[0];
+                const double x1 = fma(a[b], mi[1], a[b + 1] * mi[2]);
+                const double x2 = fma(a[b], mi[3], fma(a[b + 1], mi[4], a[b + 2] * mi[5]));
+                a[b] = x0; a[b + 1] = x1; a[b + 2] = x2;
 #pragma unroll
-                for (int cc = c + 1; cc < kFNB; ++cc) a[cc] = fma(-x, Lt[c * kFNB + cc], a[cc]);
+                for (int cc = b + 3; cc < kFNB; ++cc)
+                    a[cc] = fma(-x2, Lt[(b + 2) * kFNB + cc], fma(-x1, Lt[(b + 1) * kFNB + cc], fma(-x0, Lt[b * kFNB + cc], a[cc])));
             }
         }
 #pragma unroll
@@ -1274,8 +1312,21 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
             ftasks.push_back(ft);
         }
     }
-    std::vector<int32_t> order_fac;   // fused tickets: front * 64 + team member, children first
-    for (int32_t s : S.level_list)
+    // fused tickets (front * 64 + team member) in critical-path order: a front's priority is its
+    // estimated time plus its parent's priority (the longest remaining path to the root), so
+    // sorting by descending priority is topological (children first) and starts the long chains
+    // before the bulk of the leaves
+    std::vector<double> prio((size_t)S.ns, 0.0);
+    for (int32_t s = S.ns - 1; s >= 0; --s) {
+        const SnDev& d = sns[(size_t)s];
+        const int32_t m3 = 3 * (d.k + d.r);
+        const double est = d.G == 1 ? 4.0 + 0.05 * m3 : 10.0 + 20.0 * ((3 * d.k + kFNB - 1) / kFNB);
+        prio[(size_t)s] = est + (d.parent >= 0 ? prio[(size_t)d.parent] : 0.0);
+    }
+    std::vector<int32_t> fo(S.level_list.begin(), S.level_list.end());
+    std::stable_sort(fo.begin(), fo.end(), [&](int32_t a, int32_t b) { return prio[(size_t)a] > prio[(size_t)b]; });
+    std::vector<int32_t> order_fac;
+    for (int32_t s : fo)
         for (int32_t m = 0; m < sns[(size_t)s].G; ++m) order_fac.push_back(s * 64 + m);
     c->n_tickets = (int64_t)order_fac.size();
     c->level_ptr = S.level_ptr;
