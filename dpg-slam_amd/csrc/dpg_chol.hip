@@ -453,14 +453,21 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
 
 // backward: L^T x = y.  A front waits for its parent (hence every ancestor), gathers x at its row
 // positions, solves, and publishes its own x.
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
 __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                         int32_t* status, const SnDev* __restrict__ sns,
                                                         const int32_t* __restrict__ rows,
                                                         const double* __restrict__ fronts,
                                                         const double* __restrict__ ysol, double* xsol) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+    extern __shared__ __attribute__((aligned(16))) double smem_b[];
+    double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int s = claim(order, sync);
+    const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_b));
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
@@ -468,42 +475,72 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     double* rd = sm + kSB * kSB;     // kSB reciprocals of the diagonal block's diagonal
     double* z = rd + kSB;            // k3
     double* xr = z + k3;             // r3
-    if (S.parent >= 0) {
-        if (tid == 0) wait_geq(sync + 1 + S.parent, 1, status);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rows[S.rows_off + t / 3] + t % 3);
-    __syncthreads();
-    for (int j = tid; j < k3; j += kT) {
-        double sacc = 0.0;
-        for (int t = 0; t < r3; ++t) sacc = fma(F[j * m3 + k3 + t], xr[t], sacc);
-        z[j] = ysol[3 * (int64_t)S.c0 + j] - sacc;
-    }
-    __syncthreads();
+    int32_t* rp = reinterpret_cast<int32_t*>(xr + r3);   // r3 / 3 row positions
+    // before the wait: y, the row positions, the last diagonal block (all from earlier launches)
+    for (int j = tid; j < k3; j += kT) z[j] = ysol[3 * (int64_t)S.c0 + j];
+    for (int t = tid; t < S.r; t += kT) rp[t] = rows[S.rows_off + t];
     const int nblk = (k3 + kSB - 1) / kSB;
-    for (int b = nblk - 1; b >= 0; --b) {
-        const int jb = b * kSB, bw = min(kSB, k3 - jb);
+    {
+        const int jb = (nblk - 1) * kSB, bw = k3 - jb;
         for (int e = tid; e < bw * bw; e += kT) {
             const int i = e % bw, j = e / bw;
-            D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
-            if (i == j) rd[j] = 1.0 / D[j * kSB + i];
+            const double v = F[(jb + j) * m3 + jb + i];
+            D[j * kSB + i] = v;
+            if (i == j) rd[j] = 1.0 / v;
         }
-        __syncthreads();
-        if (wave == 0) {
+    }
+    if (S.parent >= 0) {
+        if (tid == 0) wait_geq_sc1(sync + 1 + S.parent, 1, status);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
+    __syncthreads();
+    for (int j = tid; j < k3; j += kT) {   // z = y - L21^T x_r, four independent accumulators
+        const double* Fj = F + (int64_t)j * m3 + k3;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int t = 0;
+        for (; t + 3 < r3; t += 4) {
+            a0 = fma(Fj[t], xr[t], a0);
+            a1 = fma(Fj[t + 1], xr[t + 1], a1);
+            a2 = fma(Fj[t + 2], xr[t + 2], a2);
+            a3 = fma(Fj[t + 3], xr[t + 3], a3);
+        }
+        for (; t < r3; ++t) a0 = fma(Fj[t], xr[t], a0);
+        z[j] -= (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+    for (int b = nblk - 1; b >= 0; --b) {
+        const int jb = b * kSB, bw = min(kSB, k3 - jb);
+        if (b != nblk - 1) {
+            for (int e = tid; e < bw * bw; e += kT) {
+                const int i = e % bw, j = e / bw;
+                D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
+                if (i == j) rd[j] = 1.0 / D[j * kSB + i];
+            }
+            __syncthreads();
+        }
+        if (wave == 0) {   // lane = row; x_j broadcast by v_readlane (uniform j): ~3 dependent ops per step
             double zl = lane < bw ? z[jb + lane] : 0.0;
+            const double rl = lane < bw ? rd[lane] : 0.0;
+            const double* Dl = D + lane * kSB;
             for (int j = bw - 1; j >= 0; --j) {
-                const double xj = __shfl(zl, j, 64) * rd[j];
-                if (lane == j) zl = xj;
-                else if (lane < j) zl = fma(-D[lane * kSB + j], xj, zl);   // L(jb+j, jb+lane)
+                const double xj = rdlane(zl * rl, j);
+                zl = lane == j ? xj : (lane < j ? fma(-Dl[j], xj, zl) : zl);   // L(jb+j, jb+lane)
             }
             if (lane < bw) z[jb + lane] = zl;
         }
         __syncthreads();
         for (int j = tid; j < jb; j += kT) {
-            double sacc = 0.0;
-            for (int i = 0; i < bw; ++i) sacc = fma(F[j * m3 + jb + i], z[jb + i], sacc);
-            z[j] -= sacc;
+            const double* Fj = F + (int64_t)j * m3 + jb;
+            double a0 = 0.0, a1 = 0.0;
+            int i = 0;
+            for (; i + 1 < bw; i += 2) {
+                a0 = fma(Fj[i], z[jb + i], a0);
+                a1 = fma(Fj[i + 1], z[jb + i + 1], a1);
+            }
+            if (i < bw) a0 = fma(Fj[i], z[jb + i], a0);
+            z[j] -= a0 + a1;
         }
         __syncthreads();
     }
@@ -541,11 +578,6 @@ constexpr int kGmax = 32;    // largest team (workgroups per front)
 struct ChMeta { int64_t front_off, acc_off, rows_off; int32_t k, r; };
 
 
-__device__ __forceinline__ double rdlane(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
 
 
 // LDS carve of the factorization phase (doubles): panel [kFNB][Rp] with row offset `off` so that
@@ -1381,7 +1413,7 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
             const int32_t s = S.level_list[(size_t)q];
             const SnDev& d = sns[(size_t)s];
             const int32_t m3 = 3 * (d.k + d.r);
-            ms = std::max(ms, (size_t)(kSB * kSB + kSB + m3) * sizeof(double));
+            ms = std::max(ms, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
             lds_asm[(size_t)l] = std::max(lds_asm[(size_t)l], (size_t)kCT * m3 * sizeof(double));
             maxk3 = std::max(maxk3, 3 * d.k);
             build_tiles(s, kCT, asm_t, asm_c);
