@@ -579,6 +579,26 @@ int dpg_gn_solve_retract(dpg_ctx* c, const double* hb_dev, double* delta_inf, do
     return DPG_OK;
 }
 
+int dpg_gn_solve_retract_async(dpg_ctx* c, const double* hb_dev) {
+    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+    if (!hb_dev) hb_dev = c->gn.hb_own;
+    HIP_TRY(hipEventRecord(c->ev[4], c->stream));
+    int rc = dpg_gn_dev_solve_async(&c->gn, hb_dev, &c->gp, c->stream);
+    if (rc) return fail(rc, "solve launch failed: %s", hipGetErrorString(hipGetLastError()));
+    HIP_TRY(hipEventRecord(c->ev[5], c->stream));
+    return DPG_OK;
+}
+
+int dpg_gn_fetch(dpg_ctx* c, const double* hb_dev, double out[3]) {
+    if (!c || !c->gn_ready || !out) return fail(DPG_ERR_STATE, "graph not set up");
+    if (!hb_dev) hb_dev = c->gn.hb_own;
+    int rc = dpg_gn_dev_fetch(&c->gn, hb_dev, c->stream, out);
+    if (rc) return fail(rc, "fetch failed");
+    float s = 0.f;
+    if (hipEventElapsedTime(&s, c->ev[4], c->ev[5]) == hipSuccess) c->solve_ms = s;
+    return DPG_OK;
+}
+
 float dpg_gn_last_assemble_ms(dpg_ctx* c) { return c ? c->asm_ms : -1.f; }
 float dpg_gn_last_solve_ms(dpg_ctx* c) { return c ? c->solve_ms : -1.f; }
 
@@ -613,12 +633,16 @@ int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F
     int it = 0;
     if (!(cur <= 0.0) && P.max_iterations > 0) {
         for (;;) {
-            double e_lin = 0.0;
-            int32_t pit = 0;
-            if ((rc = dpg_gn_solve_retract(c, nullptr, &dinf, &e_lin, &pit))) return rc;
-            S.pcg_iterations += pit;
+            // solve + retract + re-linearize enqueued back to back, one synchronisation per iteration
+            double sc[3];
+            if ((rc = dpg_gn_solve_retract_async(c, nullptr)) || (rc = dpg_gn_assemble(c, nullptr)) ||
+                (rc = dpg_gn_fetch(c, nullptr, sc)))
+                return rc;
+            if (sc[2] != 0.0) return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)sc[2]);
+            S.pcg_iterations += c->gn.last_pcg_iters;
             ++it;
-            if ((rc = dpg_gn_assemble(c, nullptr)) || (rc = read_error(c, &nw))) return rc;
+            dinf = sc[0];
+            nw = sc[1];
             if (it >= P.max_iterations) break;
             if (P.use_error_criteria) {
                 if (check_conv(&P, cur, nw) || !std::isfinite(cur)) break;

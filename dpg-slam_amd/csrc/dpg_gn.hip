@@ -84,38 +84,75 @@ __device__ __forceinline__ void atwb_acc(const double* A, const double* w, const
         }
 }
 
-__global__ void assemble_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X,
-                                const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
-                                int64_t n_nodes, int64_t nnzb_upper, int64_t shard_begin, int64_t shard_end,
-                                double* __restrict__ hb, double* __restrict__ chi2_node) {
+// per-factor linearization, once per factor: the contributions every block it touches needs,
+// computed with exactly the expressions the gather below adds (so the sums are the same as a
+// per-block evaluation):  [0..8] A_i^T W A_i, [9..17] A_i^T W (the (i, j) block), [18..20] the
+// g_i term, [21..23] the g_j term, [24] chi2 term.
+constexpr int kContrib = 25;
+__global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X, int64_t fb, int64_t fe,
+                           double* __restrict__ contrib) {
+    const int64_t fi = fb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (fi >= fe) return;
+    const dpg_factor f = F[fi];
+    double e[3], Ai[9];
+    linearize(f, X, e, Ai);
+    const double* w = f.info;
+    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double C[kContrib];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) C[q] = 0.0;
+    atwb_acc(Ai, w, Ai, C);
+    atwb_acc(Ai, w, I3, C + 9);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        C[18 + r] = Ai[r] * w[0] * e[0] + Ai[3 + r] * w[1] * e[1] + Ai[6 + r] * w[2] * e[2];
+        C[21 + r] = w[r] * e[r];
+    }
+    C[24] = 0.5 * (w[0] * e[0] * e[0] + w[1] * e[1] * e[1] + w[2] * e[2] * e[2]);
+    double* o = contrib + kContrib * fi;
+#pragma unroll
+    for (int q = 0; q < kContrib; ++q) o[q] = C[q];
+}
+
+// one lane per upper 3x3 block of H: adds the contributions of the factors touching it in factor
+// order (deterministic, no float atomics)
+__global__ void gather_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ contrib,
+                              const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
+                              int64_t n_nodes, int64_t nnzb_upper, int64_t shard_begin, int64_t shard_end,
+                              double* __restrict__ hb, double* __restrict__ chi2_node) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nnzb_upper) return;
     const bool is_diag = u < n_nodes;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     double g[3] = {0, 0, 0};
     double chi2 = 0.0;
-    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     for (int32_t q = cptr[u]; q < cptr[u + 1]; ++q) {
         const int32_t code = clist[q];
         const int32_t fi = code >> 2, role = code & 3;
         if (fi < shard_begin || fi >= shard_end) continue;
-        const dpg_factor f = F[fi];
-        double e[3], Ai[9];
-        linearize(f, X, e, Ai);
-        const double* w = f.info;
+        const double* c = contrib + kContrib * (int64_t)fi;
         if (role == 0) {          // diag i
-            atwb_acc(Ai, w, Ai, H);
 #pragma unroll
-            for (int r = 0; r < 3; ++r) g[r] += Ai[r] * w[0] * e[0] + Ai[3 + r] * w[1] * e[1] + Ai[6 + r] * w[2] * e[2];
-            chi2 += 0.5 * (w[0] * e[0] * e[0] + w[1] * e[1] * e[1] + w[2] * e[2] * e[2]);
-        } else if (role == 1) {   // diag j (A_j = I)
-            atwb_acc(I3, w, I3, H);
+            for (int k = 0; k < 9; ++k) H[k] += c[k];
 #pragma unroll
-            for (int r = 0; r < 3; ++r) g[r] += w[r] * e[r];
-        } else if (role == 2) {   // H(i, j) = A_i^T W A_j, i < j
-            atwb_acc(Ai, w, I3, H);
-        } else {                  // H(j, i) = A_j^T W A_i, j < i
-            atwb_acc(I3, w, Ai, H);
+            for (int r = 0; r < 3; ++r) g[r] += c[18 + r];
+            chi2 += c[24];
+        } else if (role == 1) {   // diag j (A_j = I): W
+            const double* w = F[fi].info;
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) H[3 * r + k] += r == k ? w[r] : 0.0;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) g[r] += c[21 + r];
+        } else if (role == 2) {   // H(i, j) = A_i^T W, i < j
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[k] += c[9 + k];
+        } else {                  // H(j, i) = W A_i, j < i
+#pragma unroll
+            for (int r = 0; r < 3; ++r)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) H[3 * r + k] += c[9 + 3 * k + r];
         }
     }
     double* o = hb + 9 * u;
@@ -299,8 +336,7 @@ __global__ void pcg_update_kernel(int it, int64_t n, const double* __restrict__ 
 // X <- X * Pose2(d); partial max |d|.  d is indexed by node, or by elimination position when
 // pos != NULL (the Cholesky's solution vector).
 __global__ void retract_kernel(double* __restrict__ X, const double* __restrict__ d, int64_t n,
-                               const int32_t* __restrict__ pos, double* __restrict__ part_max) {
-    __shared__ double red[16];
+                               const int32_t* __restrict__ pos, double* __restrict__ max_out) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double m = 0.0;
     if (v < n) {
@@ -315,17 +351,19 @@ __global__ void retract_kernel(double* __restrict__ X, const double* __restrict_
         X[3 * v + 1] = ny;
         X[3 * v + 2] = atan2(ns, nc);
         m = fmax(fabs(d0), fmax(fabs(d1), fabs(d2)));
+        if (!(m == m)) m = __longlong_as_double(0x7ff0000000000000ll);   // NaN -> +inf (stops the loop)
     }
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
-    if (lane == 0) red[wave] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double mm = 0.0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) mm = fmax(mm, red[w]);
-        part_max[blockIdx.x] = mm;
-    }
+    if ((threadIdx.x & 63) == 0)
+        atomicMax(reinterpret_cast<unsigned long long*>(max_out), (unsigned long long)__double_as_longlong(m));
+}
+
+// scal3[1] = chi2 of hb, scal3[2] = solver status (the Cholesky's, or 0)
+__global__ void scalars_kernel(const double* __restrict__ chi2, const int32_t* __restrict__ status,
+                               double* __restrict__ scal3) {
+    scal3[1] = *chi2;
+    scal3[2] = status ? (double)*status : 0.0;
 }
 
 // ICP results -> BetweenFactor measurement + diagonal information (dpg_slam.cc:331-338)
@@ -366,9 +404,10 @@ extern "C" int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g) { return 9 * g->nnzb_
 extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
     void* ptrs[] = {g->factors, g->up_row, g->up_col, g->up_cptr, g->up_clist, g->node_fptr, g->node_flist,
                     g->rowptr, g->colidx, g->src_up, g->bsr, g->minv, g->poses, g->x, g->r, g->z,
-                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own};
+                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own, g->contrib, g->scal3};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (g->scal3_host) (void)hipHostFree(g->scal3_host);
     if (g->chol) dpg_chol_destroy(g->chol);
     memset(g, 0, sizeof(*g));
 }
@@ -462,6 +501,9 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     rc |= dev_alloc(&g->partials, 6 * (size_t)g->n_blocks_rows + (size_t)n);
     rc |= dev_alloc(&g->scal, 2 * (size_t)65536);
     rc |= dev_alloc(&g->hb_own, (size_t)dpg_gn_dev_hb_size(g));
+    rc |= dev_alloc(&g->contrib, 25 * (size_t)nf);
+    rc |= dev_alloc(&g->scal3, 4);
+    if (!rc && hipHostMalloc(reinterpret_cast<void**>(&g->scal3_host), 4 * sizeof(double)) != hipSuccess) rc = DPG_ERR_HIP;
     if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
     if (nf && hipMemcpy(g->factors, F, (size_t)nf * sizeof(dpg_factor), hipMemcpyHostToDevice) != hipSuccess) rc = DPG_ERR_HIP;
     rc |= up(g->up_cptr, cptr);
@@ -490,7 +532,11 @@ extern "C" int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* re
 extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     double* chi2_node = g->partials + 6 * (size_t)g->n_blocks_rows;
-    hipLaunchKernelGGL(assemble_kernel, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->factors, g->poses,
+    const int64_t nfs = g->shard_end - g->shard_begin;
+    if (nfs > 0)
+        hipLaunchKernelGGL(lin_kernel, dim3(nblk(nfs)), dim3(kRowThreads), 0, s, g->factors, g->poses, g->shard_begin,
+                           g->shard_end, g->contrib);
+    hipLaunchKernelGGL(gather_kernel, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->factors, g->contrib,
                        g->up_cptr, g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, hb,
                        chi2_node);
     hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
@@ -500,47 +546,52 @@ extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
 
 static int pcg_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, hipStream_t s);
 
-extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, void* stream,
-                                double* delta_inf, double* error, int32_t* pcg_iters) {
+extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int nb = g->n_blocks_rows;
-    const int64_t n = g->n_nodes;
-    double* part_rz_a = g->partials;
-    double* part_rz_b = g->partials + nb;
-    double* part_rr = g->partials + 2 * (size_t)nb;
-    double* part_pq = g->partials + 3 * (size_t)nb;
-    double* part_max = g->partials + 4 * (size_t)nb;
-    int it = 0;
     const double* xout = g->x;
     const int32_t* xpos = nullptr;
-    int32_t chol_status = 0;
+    g->last_pcg_iters = 0;
     if (gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol) {
         const int rc = dpg_chol_solve(g->chol, hb, stream);
         if (rc) return rc;
         xout = dpg_chol_x_dev(g->chol);
         xpos = dpg_chol_pos_dev(g->chol);
-        if (hipMemcpyAsync(&chol_status, dpg_chol_status_dev(g->chol), sizeof(int32_t), hipMemcpyDeviceToHost, s) !=
-            hipSuccess)
-            return DPG_ERR_HIP;
     } else {
-        it = pcg_solve(g, hb, gp, s);
+        const int it = pcg_solve(g, hb, gp, s);
         if (it < 0) return DPG_ERR_HIP;
+        g->last_pcg_iters = it;
     }
-    hipLaunchKernelGGL(retract_kernel, dim3(nb), dim3(kRowThreads), 0, s, g->poses, xout, n, xpos, part_max);
-    std::vector<double> pm((size_t)nb);
-    double chi2 = 0.0;
-    if (hipMemcpyAsync(pm.data(), part_max, (size_t)nb * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
-        hipMemcpyAsync(&chi2, hb + 9 * g->nnzb_upper + 3 * n, sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (hipMemsetAsync(g->scal3, 0, sizeof(double), s) != hipSuccess) return DPG_ERR_HIP;
+    hipLaunchKernelGGL(retract_kernel, dim3(g->n_blocks_rows), dim3(kRowThreads), 0, s, g->poses, xout, g->n_nodes,
+                       xpos, g->scal3);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_dev_fetch(dpg_gn_dev* g, const double* hb, void* stream, double out[3]) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool chol = g->chol != nullptr;
+    hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(1), 0, s, hb + 9 * g->nnzb_upper + 3 * g->n_nodes,
+                       chol ? dpg_chol_status_dev(g->chol) : nullptr, g->scal3);
+    if (hipMemcpyAsync(g->scal3_host, g->scal3, 3 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess)
         return DPG_ERR_HIP;
-    if (chol_status) return DPG_ERR_NUMERIC;   // H not positive definite
-    double mx = 0.0;
-    for (double v : pm) mx = std::max(mx, v);
-    if (delta_inf) *delta_inf = mx;
-    if (error) *error = chi2;
-    if (pcg_iters) *pcg_iters = it;
-    (void)part_rz_a; (void)part_rz_b; (void)part_rr; (void)part_pq;
-    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+    out[0] = g->scal3_host[0];
+    out[1] = g->scal3_host[1];
+    out[2] = g->scal3_host[2];
+    return DPG_OK;
+}
+
+extern "C" int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, void* stream,
+                                double* delta_inf, double* error, int32_t* pcg_iters) {
+    int rc = dpg_gn_dev_solve_async(g, hb, gp, stream);
+    if (rc) return rc;
+    double sc[3];
+    if ((rc = dpg_gn_dev_fetch(g, hb, stream, sc))) return rc;
+    if (gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol && sc[2] != 0.0) return DPG_ERR_NUMERIC;
+    if (delta_inf) *delta_inf = sc[0];
+    if (error) *error = sc[1];
+    if (pcg_iters) *pcg_iters = g->last_pcg_iters;
+    return DPG_OK;
 }
 
 // block-Jacobi PCG on the full BSR; returns the iteration count (< 0 on a HIP error)

@@ -92,8 +92,11 @@ typedef struct dpg_gn_dev {
     double* scal;                  /* PCG scalars */
     double* hb_own;                /* packed [H upper | b | chi2] buffer for single-GPU solves */
     void* chol;                    /* supernodal Cholesky (dpg_chol.hip), NULL if analysis failed */
+    double* contrib;               /* [n_factors][25] per-factor contributions (lin_kernel) */
+    double* scal3;                 /* [4] device scalars: max |delta|, chi2, status, pad */
+    double* scal3_host;            /* pinned mirror of scal3 */
     int32_t n_blocks_rows;         /* grid size for row kernels */
-    int32_t pad;
+    int32_t last_pcg_iters;
 } dpg_gn_dev;
 
 /* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip). */
@@ -111,6 +114,11 @@ int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n_nodes, const dpg_factor* factors, 
 void dpg_gn_dev_free(dpg_gn_dev* g);
 int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g);
 int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb_dev, void* stream);
+/* enqueue the solve + retraction (max |delta| kept on device); no host synchronisation for the
+   Cholesky solver */
+int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb_dev, const dpg_gn_params* gp, void* stream);
+/* one synchronisation: out = {max |delta| of the last retraction, chi2 of hb, solver status} */
+int dpg_gn_dev_fetch(dpg_gn_dev* g, const double* hb_dev, void* stream, double out[3]);
 int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb_dev, const dpg_gn_params* gp, void* stream,
                      double* delta_inf, double* error, int32_t* pcg_iters);
 int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* results_dev, int64_t first,

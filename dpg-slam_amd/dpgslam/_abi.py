@@ -159,6 +159,8 @@ SIGNATURES = {
     "dpg_gn_get_poses": (C.c_int, [P, F64P]),
     "dpg_gn_assemble": (C.c_int, [P, P]),
     "dpg_gn_solve_retract": (C.c_int, [P, P, F64P, F64P, I32P]),
+    "dpg_gn_solve_retract_async": (C.c_int, [P, P]),
+    "dpg_gn_fetch": (C.c_int, [P, P, F64P]),
     "dpg_gn_last_assemble_ms": (C.c_float, [P]),
     "dpg_gn_last_solve_ms": (C.c_float, [P]),
     "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,

@@ -280,5 +280,15 @@ class Context:
                                          C.byref(e), C.byref(it)), "dpg_gn_solve_retract")
         return d.value, e.value, it.value
 
+    def gn_solve_retract_async(self, hb_dev_ptr: int | None = None):
+        check(lib().dpg_gn_solve_retract_async(self.handle, C.c_void_p(hb_dev_ptr) if hb_dev_ptr else None),
+              "dpg_gn_solve_retract_async")
+
+    def gn_fetch(self, hb_dev_ptr: int | None = None):
+        out = np.zeros(3, np.float64)
+        check(lib().dpg_gn_fetch(self.handle, C.c_void_p(hb_dev_ptr) if hb_dev_ptr else None, ptr(out, C.c_double)),
+              "dpg_gn_fetch")
+        return float(out[0]), float(out[1]), int(out[2])
+
     def gn_times_ms(self):
         return float(lib().dpg_gn_last_assemble_ms(self.handle)), float(lib().dpg_gn_last_solve_ms(self.handle))

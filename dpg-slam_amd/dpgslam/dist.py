@@ -62,8 +62,10 @@ def check_convergence(rel_tol: float, abs_tol: float, cur: float, new: float) ->
 def gn_loop(backend, allreduce, params) -> dict:
     """Batch Gauss-Newton with one all-reduce per iteration (mirrors dpg_optimize_graph).
 
-    backend: assemble(hb), chi2(hb) -> float, solve_retract(hb) -> (dinf, err, pcg_it), new_hb()
-    allreduce(hb): in-place sum over ranks (identity for one rank)."""
+    backend: new_hb(), assemble(hb), chi2(hb) -> float, solve_retract(hb) (enqueue only),
+             fetch(hb) -> (max|delta| of the last retraction, chi2 of hb, solver status)
+    allreduce(hb): in-place sum over ranks (identity for one rank).
+    Per iteration: solve + retract, re-linearize, all-reduce, then ONE read of the scalars."""
     hb = backend.new_hb()
     backend.assemble(hb)
     allreduce(hb)
@@ -73,12 +75,13 @@ def gn_loop(backend, allreduce, params) -> dict:
         return stats
     it = 0
     while True:
-        dinf, _, pit = backend.solve_retract(hb)
+        backend.solve_retract(hb)
         it += 1
-        stats["pcg_iterations"] += pit
         backend.assemble(hb)
         allreduce(hb)
-        new = backend.chi2(hb)
+        dinf, new, status = backend.fetch(hb)
+        if status != 0:
+            raise RuntimeError(f"linear solve failed (status {status}): H not positive definite")
         stats.update(iterations=it, final_error=new, last_delta_inf=dinf)
         if it >= params.max_iterations:
             break
@@ -113,4 +116,7 @@ class DeviceBackend:
         return float(hb[self.chi2_index].item())
 
     def solve_retract(self, hb):
-        return self.ctx.gn_solve_retract(hb.data_ptr())
+        self.ctx.gn_solve_retract_async(hb.data_ptr())
+
+    def fetch(self, hb):
+        return self.ctx.gn_fetch(hb.data_ptr())

@@ -229,10 +229,16 @@ int dpg_gn_set_poses(dpg_ctx* ctx, const double* poses);
 int dpg_gn_get_poses(dpg_ctx* ctx, double* poses);
 /* Linearize the local shard at the current poses into hb_dev (overwritten, not accumulated). */
 int dpg_gn_assemble(dpg_ctx* ctx, double* hb_dev);
-/* Solve (sum of all shards in hb_dev) with PCG and retract.  Blocking: returns max|delta| and
- * the error 0.5*chi2 at the linearization point. */
+/* Solve (sum of all shards in hb_dev) and retract.  Blocking: returns max|delta| and the error
+ * 0.5*chi2 at the linearization point. */
 int dpg_gn_solve_retract(dpg_ctx* ctx, const double* hb_dev, double* delta_inf, double* error,
                          int32_t* pcg_iterations);
+/* The same, enqueued only (no host synchronisation with the Cholesky solver): the GN loop then
+ * re-linearizes (dpg_gn_assemble, [all-reduce]) and reads everything it decides on with ONE
+ * dpg_gn_fetch: out = {max|delta| of the last retraction, error of hb_dev, solver status
+ * (0 = ok, 1 = H not positive definite, 2 = solver timeout)}. */
+int dpg_gn_solve_retract_async(dpg_ctx* ctx, const double* hb_dev);
+int dpg_gn_fetch(dpg_ctx* ctx, const double* hb_dev, double out[3]);
 float dpg_gn_last_assemble_ms(dpg_ctx* ctx);
 float dpg_gn_last_solve_ms(dpg_ctx* ctx);
 

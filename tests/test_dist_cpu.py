@@ -66,7 +66,10 @@ class DenseBackend:
             self.X[v, 1] += s * d[v, 0] + c * d[v, 1]
             th = self.X[v, 2] + d[v, 2]
             self.X[v, 2] = np.arctan2(np.sin(th), np.cos(th))
-        return float(np.abs(d).max()), self.chi2(hb), 0
+        self.last_dinf = float(np.abs(d).max())
+
+    def fetch(self, hb):
+        return self.last_dinf, self.chi2(hb), 0
 
 
 def _worker(rank, world, port, X0, F, nb_first, out):
