@@ -29,6 +29,14 @@
 
 #include "dpg_internal.h"
 
+#ifdef DPG_ICP_STATS
+// diagnostics build only: [0] point-iterations, [1] forward candidates, [2] forward wave trips,
+// [3] reciprocal candidates, [4] reciprocal wave trips, [5] correspondences, [6] no forward match,
+// [7] full-scan forward windows
+__device__ unsigned long long g_icp_stats[8];
+#define ICP_STAT(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
+#endif
+
 namespace {
 
 constexpr int kT = 256;
@@ -129,6 +137,14 @@ struct Rec {
     uint32_t key, pad;
 };
 
+// one ds_read_b128 per record: the pad word is kept live (an empty asm), otherwise the compiler
+// narrows the load to ds_read_b96, which costs twice the LDS cycles per wave (8 vs 4)
+__device__ __forceinline__ Rec ld_rec(const Rec* p) {
+    uint4 v = *reinterpret_cast<const uint4*>(p);
+    asm volatile("" : "+v"(v.w));
+    return Rec{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
+}
+
 __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
     return ((uint64_t)__float_as_uint(d) << 32) | key;
 }
@@ -194,15 +210,26 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
     const dpg_icp_edge E = edges[e];
     const int N = E.n_src_ds, M = E.n_tgt_ds;
     const int vt = E.tgt_node, vs = E.src_node;
-    Lds L = carve(smem, kp.lds_tgt);
-    for (int i = t; i < M; i += kT) {
-        const float2 p = idx_pts[E.tgt_ds_off + i];
-        L.tp[i] = Rec{p.x, p.y, ((uint32_t)idx_orig[E.tgt_ds_off + i] << 16) | (uint32_t)i, 0u};
+    const int cap = kp.lds_tgt, mask = cap - 1;   // cap: a power of two >= every cloud
+    Lds L = carve(smem, cap);
+    // sorted clouds, padded to cap with far-away dummies: a window [start, start + count) then
+    // runs modulo cap (one AND per candidate); the dummies in the wrap gap never win
+    for (int i = t; i < cap; i += kT) {
+        if (i < M) {
+            const float2 p = idx_pts[E.tgt_ds_off + i];
+            L.tp[i] = Rec{p.x, p.y, ((uint32_t)idx_orig[E.tgt_ds_off + i] << 16) | (uint32_t)i, 0u};
+        } else {
+            L.tp[i] = Rec{1e18f, 1e18f, 0xffffffffu, 0u};
+        }
     }
-    for (int s = t; s < N; s += kT) {
-        const uint16_t o = idx_orig[E.src_ds_off + s];
-        L.scs[s].key = ((uint32_t)o << 16) | (uint32_t)s;
-        L.spos[o] = (uint16_t)s;
+    for (int s = t; s < cap; s += kT) {
+        if (s < N) {
+            const uint16_t o = idx_orig[E.src_ds_off + s];
+            L.scs[s].key = ((uint32_t)o << 16) | (uint32_t)s;
+            L.spos[o] = (uint16_t)s;
+        } else {
+            L.scs[s] = Rec{1e18f, 1e18f, 0xffffffffu, 0u};
+        }
     }
     for (int b = t; b <= kB; b += kT) {
         L.tb[b] = buckets[(size_t)vt * (kB + 1) + b];
@@ -264,15 +291,24 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             }
             {
                 int s = 0;
-                const int fc = live ? window(L.tb, M, qx, qy, rad, s) : 0;
+                int fc = live ? window(L.tb, M, qx, qy, rad, s) : 0;
                 s = s >= M ? s - M : s;
+                if (s + fc > M) fc += cap - M;   // wraps: step over the padding gap
+#ifdef DPG_ICP_STATS
+                {
+                    int trips = 0;
+                    for (int c = 0; __any(c < fc); c += 2) ++trips;
+                    if (live) { ICP_STAT(0, 1); ICP_STAT(1, fc); if (fc >= M) ICP_STAT(7, 1); }
+                    if (lane == 0) ICP_STAT(2, trips);
+                }
+#endif
                 for (int c = 0; __any(c < fc); c += 2) {   // exact (d, original index) argmin
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
-                        const Rec r = L.tp[s];
+                        const Rec r = ld_rec(L.tp + s);
                         const uint64_t kd = dkey(sqd(qx, qy, r.x, r.y), r.key);
                         best = (c + u < fc && kd < best) ? kd : best;
-                        s = s + 1 == M ? 0 : s + 1;
+                        s = (s + 1) & mask;
                     }
                 }
             }
@@ -293,20 +329,33 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
                     const float px = (float)(i00 * ux + i01 * uy), py = (float)(i10 * ux + i11 * uy);
                     rc = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
                     s = s >= N ? s - N : s;
+                    if (s + rc > N) rc += cap - N;
                 }
                 // i's own word: any other current source with a smaller (d, original index) word
                 // is closer to t_j (or tied with a lower index) and breaks reciprocity
                 const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)sp[m]);
+#ifdef DPG_ICP_STATS
+                {
+                    int trips = 0;
+                    for (int c = 0; __any(ok & (c < rc)); c += 2) ++trips;
+                    if (ok) ICP_STAT(3, rc);
+                    if (live && !ok) ICP_STAT(6, 1);
+                    if (lane == 0) ICP_STAT(4, trips);
+                }
+#endif
                 for (int c = 0; __any(ok & (c < rc)); c += 2) {
 #pragma unroll
                     for (int u = 0; u < 2; ++u) {
-                        const Rec r = L.scs[s];
+                        const Rec r = ld_rec(L.scs + s);
                         const uint64_t kd = dkey(sqd(r.x, r.y, tj.x, tj.y), r.key);
                         ok = ok & !((c + u < rc) & (kd < mine));
-                        s = s + 1 == N ? 0 : s + 1;
+                        s = (s + 1) & mask;
                     }
                 }
             }
+#ifdef DPG_ICP_STATS
+            if (ok) ICP_STAT(5, 1);
+#endif
             if (live && trace && k < kp.trace_iters)
                 trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
             if (ok) {
@@ -406,6 +455,17 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
 
 extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 
+#ifdef DPG_ICP_STATS
+extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_icp_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
 extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) {
     auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
     size_t o = 0;
@@ -435,7 +495,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
                                   const uint16_t* buckets_dev, const dpg_icp_edge* edges_dev, int64_t n_edges, const dpg_icp_kparams* kp,
                                   int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* stream) {
     if (n_edges <= 0) return DPG_OK;
-    if (max_points > kp->lds_tgt || kp->lds_tgt > 4096) return DPG_ERR_SIZE;
+    if (max_points > kp->lds_tgt || kp->lds_tgt > 4096 || (kp->lds_tgt & (kp->lds_tgt - 1))) return DPG_ERR_SIZE;
     const size_t lds = dpg_icp_ang_lds_bytes(kp->lds_tgt);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)n_edges), block(kT);

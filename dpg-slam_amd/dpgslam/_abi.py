@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libdpg.so")
+LIB_PATH = os.environ.get("DPGSLAM_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "libdpg.so")
 
 DPG_OK = 0
 DPG_FACTOR_PRIOR = 0

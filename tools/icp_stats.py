@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""ICP candidate statistics on config4 (diagnostics build lib/libdpg_stats.so, GPU):
+   DPGSLAM_LIB=dpg-slam_amd/lib/libdpg_stats.so python tools/icp_stats.py"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dpg-slam_amd"))
+from dpgslam import _abi, api, synth  # noqa: E402
+
+w = synth.generate(sys.argv[1] if len(sys.argv) > 1 else "config4")
+p = _abi.default_icp_params()
+L = _abi.lib()
+L.dpg_icp_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+st = (C.c_ulonglong * 8)()
+with api.Context(0) as ctx:
+    ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
+    ctx.icp_prepare(w.edges, w.est, p)
+    L.dpg_icp_stats(st, 1)
+    ctx.icp_run(compute_cov=False)
+    ctx.synchronize()
+    L.dpg_icp_stats(st, 0)
+    res, _ = ctx.icp_fetch(with_hessian=False)
+it = res["iterations"]
+s = list(st)
+print(f"edges {len(it)}  iterations mean {it.mean():.2f} p50 {np.median(it):.0f} p99 {np.percentile(it, 99):.0f} max {it.max()}"
+      f"  sum {it.sum()}")
+print(f"point-iterations {s[0]}  correspondences {s[5]} ({s[5] / s[0]:.2%})  no fwd match {s[6]} ({s[6] / s[0]:.2%})"
+      f"  full-scan windows {s[7]}")
+print(f"forward: candidates/point {s[1] / s[0]:.1f}  wave trips/point-slot {2 * s[2] * 64 / s[0]:.1f} (2 cand/trip)")
+print(f"reciprocal: candidates/matched {s[3] / max(1, s[5]):.1f}  wave trips/point-slot {2 * s[4] * 64 / s[0]:.1f}")
