@@ -42,6 +42,12 @@ def workload():
 def ctx():
     """A GPU context; on a GPU box a missing/broken library must FAIL, not skip."""
     from dpgslam import api
+    try:   # torch's HIP runtime first (as bench.py does): tests hand torch device buffers to libdpg
+        import torch
+        if torch.cuda.device_count() > 0:
+            torch.cuda.init()
+    except ImportError:
+        pass
     c = api.Context(0)
     yield c
     c.close()

@@ -1,0 +1,78 @@
+"""GPU tests of the pose-graph solver itself: the one-launch DAG Cholesky against
+the level-scheduled one, a known-answer mesh graph whose elimination tree has large fronts (the
+multi-workgroup team path), and the asynchronous GN loop against dpg_optimize_graph."""
+import os
+
+import numpy as np
+import pytest
+
+from graphs import consistent_mesh_graph, pose_diff
+
+pytestmark = pytest.mark.gpu
+
+
+def _optimize(ctx, X0, F, levels=False, **kw):
+    from dpgslam import _abi
+    gp = _abi.default_gn_params()
+    for k, v in kw.items():
+        setattr(gp, k, v)
+    if levels:
+        os.environ["DPG_CHOL_LEVELS"] = "1"   # read when the Cholesky is set up (dpg_chol_create)
+    try:
+        return ctx.optimize_graph(X0, F, gp)
+    finally:
+        os.environ.pop("DPG_CHOL_LEVELS", None)
+
+
+def test_mesh_graph_known_answer(ctx):
+    """Exactly consistent measurements: GN reaches the true poses; the fused DAG factorization and
+    the level-scheduled one agree."""
+    X0, F, X = consistent_mesh_graph(V=3000, k=6, seed=11)
+    Xf, sf = _optimize(ctx, X0, F)
+    assert np.abs(pose_diff(Xf, X)).max() < 1e-8, np.abs(pose_diff(Xf, X)).max()
+    Xl, sl = _optimize(ctx, X0, F, levels=True)
+    assert np.abs(pose_diff(Xl, X)).max() < 1e-8
+    assert sf.iterations == sl.iterations
+    assert np.abs(pose_diff(Xf, Xl)).max() < 1e-10
+
+
+@pytest.mark.parametrize("name", ["config3", "config4"])
+def test_fused_and_level_cholesky_agree(ctx, workload, name):
+    from oracle import oracle as O
+    from dpgslam import _abi
+    w = workload(name)
+    p = _abi.default_icp_params()
+    ctx.upload_scans(w.pts, w.offsets, 5)
+    res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
+    F = w.factors_with_icp(res, p)
+    X0 = w.est.astype(np.float64)
+    Xf, sf = _optimize(ctx, X0, F)
+    Xl, sl = _optimize(ctx, X0, F, levels=True)
+    assert sf.iterations == sl.iterations
+    assert np.abs(pose_diff(Xf, Xl)).max() < 1e-9
+    if name == "config3":
+        Xo, _ = O.optimize_graph(X0, F)
+        assert np.abs(pose_diff(Xf, Xo)).max() < 1e-6
+
+
+def test_async_gn_loop_matches_optimize_graph(ctx, workload):
+    """dpgslam.dist.gn_loop on the device backend (enqueue-only solve/retract, one fetch per
+    iteration) performs exactly dpg_optimize_graph's operations: identical poses and iterations."""
+    import torch
+    from dpgslam import _abi
+    from dpgslam import dist as D
+    w = workload("config3")
+    p = _abi.default_icp_params()
+    ctx.upload_scans(w.pts, w.offsets, 5)
+    res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
+    F = w.factors_with_icp(res, p)
+    X0 = w.est.astype(np.float64)
+    Xc, sc = ctx.optimize_graph(X0, F)
+    dev = torch.device("cuda", 0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    n = ctx.gn_setup(w.V, F)
+    ctx.gn_set_poses(X0)
+    st = D.gn_loop(D.DeviceBackend(ctx, n, n - 2, dev), lambda hb: None, _abi.default_gn_params())
+    Xa = ctx.gn_get_poses(w.V)
+    assert st["iterations"] == sc.iterations
+    np.testing.assert_array_equal(Xa, Xc)
