@@ -68,6 +68,9 @@ def main():
     ap.add_argument("--config", default="config4")
     ap.add_argument("--cpu-sample", type=int, default=1500, help="edges in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
+                         "the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--icp-variant", default="angular", choices=["angular", "kdtree", "grid"],
                     help="nearest-neighbour machinery of the ICP kernel (results are identical)")
     args = ap.parse_args()
@@ -83,10 +86,14 @@ def main():
     from dpgslam import _abi, api, synth
     from dpgslam import dist as D
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gpu = local_rank % max(1, torch.cuda.device_count())   # == local_rank on a full node
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
 
     t0 = time.time()
     w = synth.generate(args.config)
@@ -94,7 +101,7 @@ def main():
     params = _abi.default_icp_params()
     gp = _abi.default_gn_params()
 
-    ctx = api.Context(local_rank)
+    ctx = api.Context(gpu)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     ctx.set_icp_variant(args.icp_variant)
     ctx.upload_scans(w.pts, w.offsets, params.downsample_icp_points_ratio)
