@@ -132,7 +132,7 @@ def main():
     for _ in range(args.warmup):
         st = step()
     barrier()
-    icp_ms, cov_ms, idx_ms, gn_iters, gn_ms = [], [], [], [], []
+    icp_ms, cov_ms, idx_ms, gn_iters, gn_ms, n_fact = [], [], [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         ts = time.perf_counter()
@@ -142,6 +142,7 @@ def main():
         cov_ms.append(ctx.cov_kernel_ms())
         idx_ms.append(ctx.kdtree_build_ms())
         gn_iters.append(st["iterations"])
+        n_fact.append(ctx.gn_factorizations())
         gn_ms.append((time.perf_counter() - ts) * 1e3 - icp_ms[-1] - cov_ms[-1] - idx_ms[-1])
     barrier()
     elapsed = time.perf_counter() - t_start
@@ -154,7 +155,7 @@ def main():
     k_ms = float(np.mean(icp_ms))
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9
     res, _ = ctx.icp_fetch(with_hessian=False)
-    stats = {"icp_kernel_ms": k_ms, "cov_kernel_ms": float(np.mean(cov_ms)), "index_build_ms": float(np.mean(idx_ms)), "gn_iterations": float(np.mean(gn_iters)),
+    stats = {"icp_kernel_ms": k_ms, "cov_kernel_ms": float(np.mean(cov_ms)), "index_build_ms": float(np.mean(idx_ms)), "gn_iterations": float(np.mean(gn_iters)), "gn_factorizations": float(np.mean(n_fact)),
              "ms_per_gn_iter": float(np.mean(gn_ms) / max(1.0, np.mean(gn_iters))),
              "icp_iters_mean": float(res["iterations"].mean()), "icp_iters_max": int(res["iterations"].max()),
              "final_error": st["final_error"], "pcg_iterations": st["pcg_iterations"]}
@@ -190,6 +191,7 @@ def main():
                        "nodes": w.V, "icp_edges": w.E, "factors": len(F), "parallelism": f"edge-sharded dp{world}"},
             "ms_per_gn_iter": stats["ms_per_gn_iter"],
             "gn_iterations": stats["gn_iterations"],
+            "gn_factorizations": stats["gn_factorizations"],
             "icp_kernel_ms": stats["icp_kernel_ms"],
             "cov_kernel_ms": stats["cov_kernel_ms"],
             "index_build_ms": stats["index_build_ms"],

@@ -544,6 +544,9 @@ int dpg_gn_set_poses(dpg_ctx* c, const double* poses) {
     HIP_TRY(hipMemcpyAsync(c->gn.poses, poses, sizeof(double) * 3 * (size_t)c->gn.n_nodes, hipMemcpyHostToDevice,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->gn.have_factor = 0;            // a new linearization point: the next solve refactors
+    c->gn.last_delta_inf = 1e300;
+    c->gn.n_factorizations = 0;
     return DPG_OK;
 }
 
@@ -590,6 +593,8 @@ int dpg_gn_solve_retract_async(dpg_ctx* c, const double* hb_dev) {
     HIP_TRY(hipEventRecord(c->ev[5], c->stream));
     return DPG_OK;
 }
+
+int32_t dpg_gn_factorizations(dpg_ctx* c) { return (c && c->gn_ready) ? c->gn.n_factorizations : -1; }
 
 int dpg_gn_fetch(dpg_ctx* c, const double* hb_dev, double out[3]) {
     if (!c || !c->gn_ready || !out) return fail(DPG_ERR_STATE, "graph not set up");

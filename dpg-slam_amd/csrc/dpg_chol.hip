@@ -374,6 +374,12 @@ __device__ __forceinline__ int claim_lds(const int32_t* order, int32_t* ticket, 
 
 // forward: L y = -g.  A front gathers its children's pending row updates (child order: fixed
 // summation order), solves its diagonal blocks (one wave, LDS), then hands L21 y to its parent.
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
 __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                        int32_t* status, const SnDev* __restrict__ sns,
                                                        const int32_t* __restrict__ child_list,
@@ -382,9 +388,10 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
                                                        const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm,
                                                        double* __restrict__ ysol, double* acc) {
-    extern __shared__ __attribute__((aligned(16))) double sm[];
+    extern __shared__ __attribute__((aligned(16))) double smem_fw[];
+    double* sm = smem_fw + 2;   // smem_fw[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int s = claim(order, sync);
+    const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_fw));
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
@@ -392,13 +399,23 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
     double* rd = sm + kSB * kSB;     // kSB reciprocals of its diagonal
     double* y = rd + kSB;            // k3
     double* aR = y + k3;             // r3
+    // before the wait: the right-hand side and the first diagonal block (earlier launches)
     for (int t = tid; t < k3; t += kT) {
         const int node = perm[S.c0 + t / 3];
         y[t] = -g[3 * node + t % 3];
     }
     for (int t = tid; t < r3; t += kT) aR[t] = 0.0;
+    {
+        const int bw = min(kSB, k3);
+        for (int e = tid; e < bw * bw; e += kT) {
+            const int i = e % bw, j = e / bw;
+            const double v = F[j * m3 + i];
+            D[j * kSB + i] = v;
+            if (i == j) rd[j] = 1.0 / v;
+        }
+    }
     if (S.nchild > 0) {
-        if (tid == 0) wait_geq(sync + 1 + s, S.nchild, status);
+        if (tid == 0) wait_geq_sc1(sync + 1 + s, S.nchild, status);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -416,33 +433,47 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
     }
     for (int jb = 0; jb < k3; jb += kSB) {
         const int bw = min(kSB, k3 - jb);
-        for (int e = tid; e < bw * bw; e += kT) {
-            const int i = e % bw, j = e / bw;
-            D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
-            if (i == j) rd[j] = 1.0 / D[j * kSB + i];
+        if (jb > 0) {
+            for (int e = tid; e < bw * bw; e += kT) {
+                const int i = e % bw, j = e / bw;
+                D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
+                if (i == j) rd[j] = 1.0 / D[j * kSB + i];
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (wave == 0) {
+        if (wave == 0) {   // lane = row; y_j broadcast by v_readlane (uniform j)
             double yl = lane < bw ? y[jb + lane] : 0.0;
+            const double rl = lane < bw ? rd[lane] : 0.0;
             for (int j = 0; j < bw; ++j) {
-                const double yj = __shfl(yl, j, 64) * rd[j];
-                if (lane == j) yl = yj;
-                else if (lane > j && lane < bw) yl = fma(-D[j * kSB + lane], yj, yl);
+                const double yj = rdlane(yl * rl, j);
+                yl = lane == j ? yj : (lane > j && lane < bw ? fma(-D[j * kSB + lane], yj, yl) : yl);
             }
             if (lane < bw) y[jb + lane] = yl;
         }
         __syncthreads();
         for (int i = jb + bw + tid; i < k3; i += kT) {
-            double sacc = 0.0;
-            for (int j = 0; j < bw; ++j) sacc = fma(F[(jb + j) * m3 + i], y[jb + j], sacc);
-            y[i] -= sacc;
+            double a0 = 0.0, a1 = 0.0;
+            int j = 0;
+            for (; j + 1 < bw; j += 2) {
+                a0 = fma(F[(jb + j) * m3 + i], y[jb + j], a0);
+                a1 = fma(F[(jb + j + 1) * m3 + i], y[jb + j + 1], a1);
+            }
+            if (j < bw) a0 = fma(F[(jb + j) * m3 + i], y[jb + j], a0);
+            y[i] -= a0 + a1;
         }
         __syncthreads();
     }
     for (int t = tid; t < r3; t += kT) {
-        double sacc = 0.0;
-        for (int j = 0; j < k3; ++j) sacc = fma(F[j * m3 + k3 + t], y[j], sacc);
-        st_agent(acc + S.acc_off + t, aR[t] + sacc);
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int j = 0;
+        for (; j + 3 < k3; j += 4) {
+            a0 = fma(F[j * m3 + k3 + t], y[j], a0);
+            a1 = fma(F[(j + 1) * m3 + k3 + t], y[j + 1], a1);
+            a2 = fma(F[(j + 2) * m3 + k3 + t], y[j + 2], a2);
+            a3 = fma(F[(j + 3) * m3 + k3 + t], y[j + 3], a3);
+        }
+        for (; j < k3; ++j) a0 = fma(F[j * m3 + k3 + t], y[j], a0);
+        st_agent(acc + S.acc_off + t, aR[t] + ((a0 + a1) + (a2 + a3)));
     }
     for (int t = tid; t < k3; t += kT) ysol[3 * (int64_t)S.c0 + t] = y[t];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -453,11 +484,6 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
 
 // backward: L^T x = y.  A front waits for its parent (hence every ancestor), gathers x at its row
 // positions, solves, and publishes its own x.
-__device__ __forceinline__ double rdlane(double v, int l) {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-    return __hiloint2double(hi, lo);
-}
 
 __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                         int32_t* status, const SnDev* __restrict__ sns,
@@ -1457,8 +1483,9 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     rc |= dalloc_copy(&c->pos, S.pos);
     rc |= dalloc_copy(&c->asm_tasks, asm_t);
     {
-        std::vector<int32_t> bwd(S.level_list.rbegin(), S.level_list.rend());
-        rc |= dalloc_copy(&c->order_fwd, S.level_list);
+        // solves: the critical-path order (children first), and its reverse (parents first)
+        std::vector<int32_t> bwd(fo.rbegin(), fo.rend());
+        rc |= dalloc_copy(&c->order_fwd, fo);
         rc |= dalloc_copy(&c->order_fac, order_fac);
         rc |= dalloc_copy(&c->ftasks, ftasks);
         rc |= dalloc_copy(&c->fchild, fchild);
@@ -1518,6 +1545,20 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
                        c->sns, c->rows, c->fronts, c->ysol, c->xsol);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+// forward + backward solves with the fronts of the last factorization (the right-hand side from hb)
+extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
+    CholDev* c = reinterpret_cast<CholDev*>(h);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dpg_chol_sym& S = c->sym;
+    const double* g = hb + 9 * c->nnzb_upper;
+    if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
+    hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc);
+    hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

@@ -552,8 +552,13 @@ extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg
     const int32_t* xpos = nullptr;
     g->last_pcg_iters = 0;
     if (gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol) {
-        const int rc = dpg_chol_solve(g->chol, hb, stream);
+        const bool reuse = gp->reuse_factorization && g->have_factor && g->last_delta_inf < gp->refactor_delta;
+        const int rc = reuse ? dpg_chol_resolve(g->chol, hb, stream) : dpg_chol_solve(g->chol, hb, stream);
         if (rc) return rc;
+        if (!reuse) {
+            g->have_factor = 1;
+            ++g->n_factorizations;
+        }
         xout = dpg_chol_x_dev(g->chol);
         xpos = dpg_chol_pos_dev(g->chol);
     } else {
@@ -578,6 +583,7 @@ extern "C" int dpg_gn_dev_fetch(dpg_gn_dev* g, const double* hb, void* stream, d
     out[0] = g->scal3_host[0];
     out[1] = g->scal3_host[1];
     out[2] = g->scal3_host[2];
+    g->last_delta_inf = out[0];
     return DPG_OK;
 }
 

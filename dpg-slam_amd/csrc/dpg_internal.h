@@ -97,6 +97,9 @@ typedef struct dpg_gn_dev {
     double* scal3_host;            /* pinned mirror of scal3 */
     int32_t n_blocks_rows;         /* grid size for row kernels */
     int32_t last_pcg_iters;
+    double last_delta_inf;         /* host: max |delta| of the last fetched retraction */
+    int32_t have_factor;           /* the Cholesky holds a factorization of this graph */
+    int32_t n_factorizations;      /* since dpg_gn_set_poses */
 } dpg_gn_dev;
 
 /* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip). */
@@ -104,6 +107,8 @@ int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_
 void dpg_chol_destroy(void* chol);
 /* factor H (upper blocks of hb) and solve H x = -g; x (block positions) stays on device */
 int dpg_chol_solve(void* chol, const double* hb, void* stream);
+/* solve H x = -g with the factorization of the last dpg_chol_solve (g from hb) */
+int dpg_chol_resolve(void* chol, const double* hb, void* stream);
 const int32_t* dpg_chol_pos_dev(void* chol);
 const double* dpg_chol_x_dev(void* chol);
 const int32_t* dpg_chol_status_dev(void* chol);

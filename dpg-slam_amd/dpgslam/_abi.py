@@ -75,7 +75,8 @@ class GnParams(C.Structure):
         ("pcg_max_iterations", C.c_int32),
         ("pcg_check_every", C.c_int32),
         ("linear_solver", C.c_int32),
-        ("pad", C.c_int32),
+        ("reuse_factorization", C.c_int32),
+        ("refactor_delta", C.c_double),
     ]
 
 
@@ -161,6 +162,7 @@ SIGNATURES = {
     "dpg_gn_solve_retract": (C.c_int, [P, P, F64P, F64P, I32P]),
     "dpg_gn_solve_retract_async": (C.c_int, [P, P]),
     "dpg_gn_fetch": (C.c_int, [P, P, F64P]),
+    "dpg_gn_factorizations": (C.c_int32, [P]),
     "dpg_gn_last_assemble_ms": (C.c_float, [P]),
     "dpg_gn_last_solve_ms": (C.c_float, [P]),
     "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,

@@ -290,5 +290,8 @@ class Context:
               "dpg_gn_fetch")
         return float(out[0]), float(out[1]), int(out[2])
 
+    def gn_factorizations(self) -> int:
+        return int(lib().dpg_gn_factorizations(self.handle))
+
     def gn_times_ms(self):
         return float(lib().dpg_gn_last_assemble_ms(self.handle)), float(lib().dpg_gn_last_solve_ms(self.handle))

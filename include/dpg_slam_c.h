@@ -95,7 +95,11 @@ typedef struct dpg_gn_params {
     int32_t pcg_max_iterations;  /* 20000 */
     int32_t pcg_check_every;     /* PCG iterations between host convergence checks (GPU only) */
     int32_t linear_solver;       /* DPG_SOLVER_CHOLESKY (default, GTSAM's CHOLESKY) | DPG_SOLVER_PCG */
-    int32_t pad;
+    int32_t reuse_factorization; /* 1 (default): once the last step's max|delta| < refactor_delta, solve
+                                    with the previous Cholesky factor (a chord step: same fixed point
+                                    g(X) = 0, H barely changes that close to it); 0: refactor every
+                                    iteration (plain Gauss-Newton) */
+    double refactor_delta;       /* 1e-4 */
 } dpg_gn_params;
 
 #define DPG_SOLVER_CHOLESKY 0    /* supernodal multifrontal Cholesky on the GPU */
@@ -239,6 +243,8 @@ int dpg_gn_solve_retract(dpg_ctx* ctx, const double* hb_dev, double* delta_inf, 
  * (0 = ok, 1 = H not positive definite, 2 = solver timeout)}. */
 int dpg_gn_solve_retract_async(dpg_ctx* ctx, const double* hb_dev);
 int dpg_gn_fetch(dpg_ctx* ctx, const double* hb_dev, double out[3]);
+/* Cholesky factorizations since the last dpg_gn_set_poses (the other solves reused one). */
+int32_t dpg_gn_factorizations(dpg_ctx* ctx);
 float dpg_gn_last_assemble_ms(dpg_ctx* ctx);
 float dpg_gn_last_solve_ms(dpg_ctx* ctx);
 

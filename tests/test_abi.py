@@ -31,10 +31,30 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(_abi.SIGNATURES), set(names) ^ set(_abi.SIGNATURES)
 
 
+def _c_layout(struct, fields):
+    """sizeof and field offsets of a header struct, as gcc lays it out."""
+    import subprocess
+    import tempfile
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    body = "".join(f'printf(" %zu", offsetof({struct}, {f}));' for f in fields)
+    src = (f'#include <stddef.h>\n#include <stdio.h>\n#include "dpg_slam_c.h"\n'
+           f'int main(void) {{ printf("%zu", sizeof({struct})); {body} return 0; }}\n')
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "l.c"), "w").write(src)
+        subprocess.run(["gcc", "-I", inc, "-o", os.path.join(d, "l"), os.path.join(d, "l.c")], check=True)
+        out = subprocess.run([os.path.join(d, "l")], check=True, capture_output=True, text=True).stdout.split()
+    return [int(x) for x in out]
+
+
 def test_struct_layouts():
     from dpgslam import _abi
     assert C.sizeof(_abi.IcpResult) == 64 and C.sizeof(_abi.Factor) == 64
-    assert C.sizeof(_abi.IcpParams) == 56 and C.sizeof(_abi.GnParams) == 56
+    for struct, cls in (("dpg_icp_params", _abi.IcpParams), ("dpg_gn_params", _abi.GnParams),
+                        ("dpg_gn_stats", _abi.GnStats)):
+        names = [f[0] for f in cls._fields_]
+        lay = _c_layout(struct, names)
+        assert lay[0] == C.sizeof(cls), (struct, lay[0], C.sizeof(cls))
+        assert lay[1:] == [getattr(cls, n).offset for n in names], (struct, lay[1:])
     p = _abi.default_icp_params()
     assert (p.icp_maximum_iterations, p.icp_use_reciprocal_correspondences, p.downsample_icp_points_ratio) == (500, 1, 5)
     assert p.icp_maximum_transformation_epsilon == 0.000000005 and p.icp_max_correspondence_distance == 0.6
