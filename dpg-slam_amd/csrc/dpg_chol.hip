@@ -609,9 +609,10 @@ struct ChMeta { int64_t front_off, acc_off, rows_off; int32_t k, r; };
 // LDS carve of the factorization phase (doubles): panel [kFNB][Rp] with row offset `off` so that
 // trailing rows start 32-B aligned, L_top column-major [kFNB][kFNB], 1/diag, step scratch.
 __host__ __device__ inline int fused_rp(int R, int off) { return (R + off + 3) & ~3; }
-__host__ __device__ inline size_t fused_lds_doubles(int m3, int k3) {
-    const size_t large = ((m3 + 1) & ~1) + std::max((size_t)kFNB * m3,
-                                                     (size_t)kFNB * fused_rp(m3, 3) + kFNB * kFNB + 8 * (kFNB / 3) + 384);
+constexpr int kFScr = kFNB * kFNB + 8 * (kFNB / 3) + 384;   // L_top, 3x3 inverses, POTRF exchange
+__host__ __device__ inline size_t fused_lds_doubles(int m3, int k3, bool db) {
+    // right-hand side | scratch | one or two panel buffers (the first also holds the assembly tile)
+    const size_t large = ((m3 + 1) & ~1) + kFScr + (db ? 2 : 1) * (size_t)kFNB * fused_rp(m3, 3);
     (void)k3;
     const size_t small = m3 <= kSmall ? (size_t)m3 * m3 + m3 + (kMaxCh * sizeof(ChMeta) + kMaxCh * (kSmall / 3) * 4 + 7) / 8 : 0;
     return 2 + std::max(small, large);
@@ -808,22 +809,17 @@ struct Tiles {
 struct FTask { int32_t om_b, om_e, ch_off, ch_cnt; };
 struct FChild { int32_t ja, jb, k, r; int64_t front_off, rows_off; };
 
-// Panel q of a large front: factored by its owner from its own (assembled, updated) columns,
-// published write-through, flag raised.  Leaves the panel in LDS.
-__device__ void factor_publish(int q, int s, const Tiles& T, double* F, int32_t* pflag, double* pbase, bool& bad) {
+// Panel q of a large front, in LDS (P, the panel frame: column c of the tile at P[c * Rp + off + i],
+// rows i >= c valid, zeros above): POTRF of the top w x w block, TRSM of the rows below, L_top
+// copied back.  `scr` holds L_top, the 3x3 inverses and the POTRF column exchange.
+__device__ void factor_lds(int q, int s, const Tiles& T, double* P, double* scr, bool& bad) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int k3 = T.k3, m3 = T.m3;
     const int j0 = kFNB * q, w = min(kFNB, k3 - j0), R = m3 - j0;
     const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
-    double* P = pbase;
-    double* Lt = P + (size_t)kFNB * Rp;
+    double* Lt = scr;
     double* rdg = Lt + kFNB * kFNB;
-    for (int e = tid; e < w * R; e += kFT) {
-        const int c = e / R, i = e - c * R;
-        P[c * Rp + off + i] = i >= c ? F[(uint32_t)((j0 + c) * m3 + j0 + i)] : 0.0;
-    }
     for (int e = tid; e < kFNB * kFNB; e += kFT) Lt[e] = 0.0;
-    __syncthreads();
     PN_MARK(s, q, 5);
     // POTRF of the top w x w block by all 8 waves: lane = row, wave v holds columns v, v + 8, v + 16
     // in registers.  Per 3x3 step the three owning waves post their columns to LDS (double-
@@ -917,9 +913,16 @@ __device__ void factor_publish(int q, int s, const Tiles& T, double* F, int32_t*
     }
     __syncthreads();
     PN_MARK(s, q, 3);
-    for (int e = tid; e < w * R; e += kFT) {   // publish the panel write-through
+}
+
+// the factored panel q (LDS) -> its front columns, write-through, then the panel flag
+__device__ void publish_panel(int q, int s, const Tiles& T, double* F, const double* P, int32_t* pflag) {
+    const int tid = threadIdx.x;
+    const int j0 = kFNB * q, w = min(kFNB, T.k3 - j0), R = T.m3 - j0;
+    const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+    for (int e = tid; e < w * R; e += kFT) {
         const int c = e / R, i = e - c * R;
-        if (i >= c) st_agent(F + (uint32_t)((j0 + c) * m3 + j0 + i), P[c * Rp + off + i]);
+        if (i >= c) st_agent(F + (uint32_t)((j0 + c) * T.m3 + j0 + i), P[c * Rp + off + i]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -927,7 +930,9 @@ __device__ void factor_publish(int q, int s, const Tiles& T, double* F, int32_t*
     PN_MARK(s, q, 4);
 }
 
-// panel p (published) -> LDS, sc1 loads, kFT * 16 entries in flight
+// the pivot columns of tile p (= panel p's columns) -> LDS in the panel frame, zeros above the
+// diagonal; SC1: the columns were handed off by another workgroup (sc1 loads), else plain
+template <bool SC1>
 __device__ void load_panel(int p, const Tiles& T, double* F, double* P) {
     const int tid = threadIdx.x;
     const int j0 = kFNB * p, w = min(kFNB, T.k3 - j0), R = T.m3 - j0;
@@ -939,7 +944,8 @@ __device__ void load_panel(int p, const Tiles& T, double* F, double* P) {
         for (int q = 0; q < kB; ++q) {
             const int e = e0 + tid + kFT * q;
             const int c = e / R, i = e - c * R;
-            v[q] = (e < w * R && i >= c) ? ld_agent(F + (uint32_t)((j0 + c) * T.m3 + j0 + i)) : 0.0;
+            double* a = F + (uint32_t)((j0 + c) * T.m3 + j0 + i);
+            v[q] = (e < w * R && i >= c) ? (SC1 ? ld_agent(a) : *a) : 0.0;
         }
 #pragma unroll
         for (int q = 0; q < kB; ++q) {
@@ -950,7 +956,10 @@ __device__ void load_panel(int p, const Tiles& T, double* F, double* P) {
     }
 }
 
-// rank-w update of tile t with panel p (in LDS), 4x4 register tiles, plain RMW of the owner's columns
+// rank-w update of tile t with panel p (in LDS), 4x4 register tiles, RMW of the owner's columns
+// (WT: the results are stored write-through, the tile is handed off next; SC1: the tile was handed
+// off to this workgroup, read it sc1)
+template <bool WT, bool SC1 = false>
 __device__ void update_tile(int t, int p, const Tiles& T, double* F, const double* P) {
     const int tid = threadIdx.x;
     const int m3 = T.m3, j0 = kFNB * p, w = min(kFNB, T.k3 - j0), R = m3 - j0;
@@ -968,24 +977,25 @@ __device__ void update_tile(int t, int p, const Tiles& T, double* F, const doubl
             for (int b = 0; b < 4; ++b) ac[a][b] = 0.0;
 #pragma unroll 1
         for (int c = 0; c < w; ++c) {
-            {
-                const double2* pc = reinterpret_cast<const double2*>(P + c * Rp);
-                const double2 i01 = pc[(off + ib) >> 1], i23 = pc[((off + ib) >> 1) + 1];
-                const double2 l01 = pc[(off + lb) >> 1], l23 = pc[((off + lb) >> 1) + 1];
-                const double vi[4] = {i01.x, i01.y, i23.x, i23.y};
-                const double vl[4] = {l01.x, l01.y, l23.x, l23.y};
+            const double2* pc = reinterpret_cast<const double2*>(P + c * Rp);
+            const double2 i01 = pc[(off + ib) >> 1], i23 = pc[((off + ib) >> 1) + 1];
+            const double2 l01 = pc[(off + lb) >> 1], l23 = pc[((off + lb) >> 1) + 1];
+            const double vi[4] = {i01.x, i01.y, i23.x, i23.y};
+            const double vl[4] = {l01.x, l01.y, l23.x, l23.y};
 #pragma unroll
-                for (int a = 0; a < 4; ++a)
+            for (int a = 0; a < 4; ++a)
 #pragma unroll
-                    for (int b = 0; b < 4; ++b) ac[a][b] = fma(vi[a], vl[b], ac[a][b]);
-            }
+                for (int b = 0; b < 4; ++b) ac[a][b] = fma(vi[a], vl[b], ac[a][b]);
         }
         // the tile's current values (clamped addresses: all 16 loads issue before any store)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint32_t o = (uint32_t)((j0 + min(max(lb + b, l0), l1 - 1)) * m3 + j0);
 #pragma unroll
-            for (int a = 0; a < 4; ++a) ac[a][b] = F[o + (uint32_t)min(ib + a, R - 1)] - ac[a][b];
+            for (int a = 0; a < 4; ++a) {
+                double* src = F + o + (uint32_t)min(ib + a, R - 1);
+                ac[a][b] = (SC1 ? ld_agent(src) : *src) - ac[a][b];
+            }
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
@@ -994,48 +1004,126 @@ __device__ void update_tile(int t, int p, const Tiles& T, double* F, const doubl
 #pragma unroll
             for (int a = 0; a < 4; ++a) {
                 const int i = ib + a;
-                if (l >= l0 && l < l1 && i < R && i >= l) F[o + (uint32_t)i] = ac[a][b];
+                if (l >= l0 && l < l1 && i < R && i >= l) {
+                    if (WT) st_agent(F + o + (uint32_t)i, ac[a][b]);
+                    else F[o + (uint32_t)i] = ac[a][b];
+                }
             }
         }
     }
 }
 
+// the chain's own step: pivot tile p + 1 (loaded into Pn, its panel frame) -= panel p (Pc, full
+// width) restricted to the tile; LDS to LDS, 4x4 register tiles
+__device__ void update_next_lds(int p, const Tiles& T, const double* Pc, double* Pn) {
+    const int tid = threadIdx.x;
+    const int j0 = kFNB * p, R = T.m3 - j0, Rp = fused_rp(R, 0);   // panel p is full: off 0
+    const int j1 = j0 + kFNB, w1 = min(kFNB, T.k3 - j1), R1 = R - kFNB;
+    const int off1 = (4 - (w1 & 3)) & 3, Rp1 = fused_rp(R1, off1);
+    const int ncg = (w1 + 3) >> 2, nrg = (R1 + 3) >> 2;
+    for (int q = tid; q < nrg * ncg; q += kFT) {
+        const int ib = 4 * (q % nrg), lb = 4 * (q / nrg);
+        if (ib + 3 < lb) continue;
+        double ac[4][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) ac[a][b] = 0.0;
+#pragma unroll 2
+        for (int c = 0; c < kFNB; ++c) {
+            const double2* pc = reinterpret_cast<const double2*>(Pc + c * Rp + kFNB);
+            const double2 i01 = pc[ib >> 1], i23 = pc[(ib >> 1) + 1];
+            const double2 l01 = pc[lb >> 1], l23 = pc[(lb >> 1) + 1];
+            const double vi[4] = {i01.x, i01.y, i23.x, i23.y};
+            const double vl[4] = {l01.x, l01.y, l23.x, l23.y};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) ac[a][b] = fma(vi[a], vl[b], ac[a][b]);
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int l = lb + b;
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+                const int i = ib + a;
+                if (l < w1 && i < R1 && i >= l) Pn[l * Rp1 + off1 + i] -= ac[a][b];
+            }
+        }
+    }
+}
+
+// forward solve folded in: y of panel p's rows (one wave), then the rows below (bv, LDS)
+__device__ void rhs_panel(int p, const Tiles& T, const double* P, double* bv) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int j0 = kFNB * p, w = min(kFNB, T.k3 - j0), R = T.m3 - j0;
+    const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+    if (wave == 0) {
+        double bl = lane < w ? bv[j0 + lane] : 0.0;
+        for (int c = 0; c < w; ++c) {
+            const double yc = __shfl(bl, c, 64) / P[c * Rp + off + c];
+            if (lane == c) bl = yc;
+            else if (lane > c && lane < w) bl = fma(-P[c * Rp + off + lane], yc, bl);
+        }
+        if (lane < w) bv[j0 + lane] = bl;
+    }
+    __syncthreads();
+    for (int i = w + tid; i < R; i += kFT) {
+        double sacc = 0.0;
+        for (int c = 0; c < w; ++c) sacc = fma(P[c * Rp + off + i], bv[j0 + c], sacc);
+        bv[j0 + i] -= sacc;
+    }
+    __syncthreads();
+}
+
 // A front of more than kSmall rows is factored by a TEAM of G workgroups (G consecutive tickets).
 // Its columns are cut into tiles of kFNB: pivot tiles [kFNB t, min(kFNB t + kFNB, k3)), then update
-// tiles from k3; tile t belongs to member t mod G, which alone assembles and writes it (plain).
+// tiles from k3.  Member 0 runs the panel CHAIN and owns tile 0; tile t >= 1 belongs to helper
+// 1 + (t - 1) mod (G - 1), which alone assembles it and applies the panels to it, except that the
+// last panel before a pivot tile's own (panel t - 1) is applied by member 0:
 //   assembly, per own tile, in LDS: H's blocks, then the children's update-matrix columns that land
 //     in the tile (host-precomputed ranges), child by child, kFT * kPFL sc1 loads in flight;
-//   panels with lookahead: in iteration p every member holding tiles right of p loads panel p
-//     (published write-through by its owner), the owner of panel p + 1 first applies it to tile p + 1,
-//     factors and publishes panel p + 1 (so the panel chain never waits on other tiles), then every
-//     member applies panel p to its remaining tiles;
-//   member 0 carries the right-hand side (forward solve folded in, as in small_front);
+//   chain (member 0): panel p is in LDS; it loads pivot tile p + 1 (handed off write-through by its
+//     helper once panels 0..p-1 are in: flag tready[t]), applies panel p to it LDS to LDS, factors and
+//     publishes it (write-through + panel flag) -- the chain never waits on a panel load or a flag it
+//     could not have had a step earlier; with one LDS panel buffer (db == 0, very tall fronts) the
+//     step goes through the front instead;
+//   helpers: for p = 0, 1, ..: wait for panel p, load it, first bring pivot tile p + 2 up to date and
+//     hand it off, then apply panel p to their other tiles;
+//   the owner of the last tile (a helper that loads every panel) carries the right-hand side
+//   (forward solve folded in, as in small_front);
 //   at the end every member republishes its update tiles write-through and adds 1 to the parent's
 //   counter (which waits for the sum of its children's team sizes).
-__device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int32_t* sync, int32_t* pflag, int32_t* status,
+__device__ __forceinline__ int tile_owner(int t, int G) { return t == 0 || G == 1 ? 0 : 1 + (t - 1) % (G - 1); }
+
+__device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int32_t* sync, int32_t* pflag,
+                            int32_t* tready, int32_t* status,
                             const SnDev* __restrict__ sns, const OEnt* __restrict__ omap,
                             const int32_t* __restrict__ relmap, const int32_t* __restrict__ child_list,
                             const FTask* __restrict__ ftasks, const FChild* __restrict__ fchild,
                             const double* __restrict__ hb, const double* __restrict__ g,
                             const int32_t* __restrict__ perm, double* fronts, double* __restrict__ ysol,
-                            double* acc, double* sm) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                            double* acc, double* sm, int db) {
+    const int tid = threadIdx.x;
     const int k3 = 3 * S.k, r3 = 3 * S.r, m3 = k3 + r3, G = S.G;
     double* F = fronts + S.front_off;
     Tiles T{k3, m3, (k3 + kFNB - 1) / kFNB, 0};
     T.nt = T.np + (r3 + kFNB - 1) / kFNB;
-    const bool has_b = mem == 0;
-    const int last_own = mem + G * ((T.nt - 1 - mem) / G);
+    int32_t* trdy = tready + S.ftask;
+    const bool has_b = mem == tile_owner(T.nt - 1, G);   // the right-hand side: a helper that sees every panel
+    const int t_first = mem, t_step = mem == 0 ? T.nt : G - 1;   // own tiles: t_first, += t_step
     double* bv = sm;                               // [m3] right-hand side (member 0)
-    double* pbase = bv + ((m3 + 1) & ~1);          // tile under assembly / panel scratch
+    double* scr = bv + ((m3 + 1) & ~1);            // POTRF / TRSM scratch
+    double* PA = scr + kFScr;                      // tile under assembly / panel buffers
+    double* PB = db ? PA + (size_t)kFNB * fused_rp(m3, 3) : PA;
     if (has_b)
         for (int t = tid; t < m3; t += kFT) bv[t] = t < k3 ? -g[3 * perm[S.c0 + t / 3] + t % 3] : 0.0;
     // ---- assembly of the own tiles in LDS (the first one's H blocks before the wait)
     bool waited = S.need == 0;
-    for (int t = mem; t < T.nt; t += G) {
+    for (int t = t_first; t < T.nt; t += t_step) {
         const FTask tk = ftasks[S.ftask + t];
         const int cs = T.c0(t), nc = T.c1(t) - cs;
-        double* Tl = pbase;                        // [nc][m3] column-major
+        double* Tl = PA;                           // [nc][m3] column-major
         for (int e = tid; e < nc * m3; e += kFT) Tl[e] = 0.0;
         __syncthreads();
         for (int q = tid; q < (tk.om_e - tk.om_b) * 9; q += kFT) {
@@ -1078,13 +1166,19 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
             }
         }
         __syncthreads();
+        const bool handoff = t == 1 && mem != 0;   // pivot tile 1 goes to the chain as assembled
         for (int e = tid; e < nc * m3; e += kFT) {
             const int col = cs + e / m3, row = e % m3;
-            if (row >= col) F[(uint32_t)(col * m3 + row)] = Tl[e];
+            if (row >= col) {
+                if (handoff) st_agent(F + (uint32_t)(col * m3 + row), Tl[e]);
+                else F[(uint32_t)(col * m3 + row)] = Tl[e];
+            }
         }
+        if (handoff) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (handoff && tid == 0) __hip_atomic_store(trdy + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!waited) {   // (no own tile: cannot happen, G <= tiles)
+    if (!waited) {   // a helper without tiles (G > nt cannot happen; kept for safety)
         if (tid == 0) wait_geq_sc1(sync + s, S.need, status);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -1099,58 +1193,75 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
     }
     FT_MARK(s, 2);
 
-    // ---- pivot panels, with lookahead
     bool bad = false;
-    if (mem == 0) factor_publish(0, s, T, F, pflag, pbase, bad);   // tile 0 belongs to member 0
-    for (int p = 0; p < T.np; ++p) {
-        if (!has_b && last_own <= p) break;   // no tile of this member right of panel p
-        const int j0 = kFNB * p, w = min(kFNB, k3 - j0), R = m3 - j0;
-        const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
-        double* P = pbase;
-        if (p % G != mem) {
+    if (mem == 0) {
+        // ---- the panel chain
+        double* cur = PA;
+        load_panel<false>(0, T, F, cur);   // tile 0: assembled by this workgroup
+        __syncthreads();
+        factor_lds(0, s, T, cur, scr, bad);
+        publish_panel(0, s, T, F, cur, pflag);
+        for (int p = 0; p < T.np; ++p) {
+            double* nxt = cur == PA ? PB : PA;
+            if (has_b && !db) rhs_panel(p, T, cur, bv);
+            if (p + 1 < T.np) {
+                const int t = p + 1;
+                PN_MARK(s, t, 0);
+                if (tile_owner(t, G) != 0) {
+                    if (tid == 0) wait_geq_sc1(trdy + t, 1, status);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                }
+                if (db) {
+                    load_panel<true>(t, T, F, nxt);
+                    __syncthreads();
+                    PN_MARK(s, t, 1);
+                    update_next_lds(p, T, cur, nxt);
+                } else {   // through the front: sc1 reads of the handed-off tile, then reload
+                    PN_MARK(s, t, 1);
+                    update_tile<true, true>(t, p, T, F, cur);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                    load_panel<true>(t, T, F, nxt);
+                }
+                __syncthreads();
+                PN_MARK(s, t, 2);
+                factor_lds(t, s, T, nxt, scr, bad);
+                publish_panel(t, s, T, F, nxt, pflag);
+            }
+            if (has_b && db) rhs_panel(p, T, cur, bv);
+            cur = nxt;
+        }
+    } else {
+        // ---- helpers: apply each panel to the own tiles right of it (pivot tile p + 1 excepted)
+        double* P = PA;
+        for (int p = 0; p < T.np; ++p) {
+            bool need = false;
+            for (int t = t_first; t < T.nt; t += t_step) need |= t > p && !(t == p + 1 && t < T.np);
+            if (!need && !has_b) break;
             if (tid == 0) wait_geq_sc1(pflag + s, p + 1, status);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-        }
-        if (p + 1 < T.np && (p + 1) % G == mem) PN_MARK(s, p + 1, 0);
-        load_panel(p, T, F, P);
-        __syncthreads();
-        if (has_b) {   // y of the panel's rows, then the rows below
-            if (wave == 0) {
-                double bl = lane < w ? bv[j0 + lane] : 0.0;
-                for (int c = 0; c < w; ++c) {
-                    const double yc = __shfl(bl, c, 64) / P[c * Rp + off + c];
-                    if (lane == c) bl = yc;
-                    else if (lane > c && lane < w) bl = fma(-P[c * Rp + off + lane], yc, bl);
-                }
-                if (lane < w) bv[j0 + lane] = bl;
+            load_panel<true>(p, T, F, P);
+            __syncthreads();
+            const int tc = p + 2;   // the chain's next-but-one tile first, handed off when done
+            const bool mine = tc < T.np && tile_owner(tc, G) == mem;
+            if (mine) {
+                update_tile<true>(tc, p, T, F, P);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (tid == 0) __hip_atomic_store(trdy + tc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            for (int t = t_first; t < T.nt; t += t_step)
+                if (t > p && !(t == p + 1 && t < T.np) && !(mine && t == tc)) update_tile<false>(t, p, T, F, P);
             __syncthreads();
-            for (int i = w + tid; i < R; i += kFT) {
-                double sacc = 0.0;
-                for (int c = 0; c < w; ++c) sacc = fma(P[c * Rp + off + i], bv[j0 + c], sacc);
-                bv[j0 + i] -= sacc;
-            }
+            if (has_b) rhs_panel(p, T, P, bv);
         }
-        const bool ahead = p + 1 < T.np && (p + 1) % G == mem;
-        if (ahead) {   // lookahead: panel p+1 first
-            PN_MARK(s, p + 1, 1);
-            update_tile(p + 1, p, T, F, P);
-            __syncthreads();
-            PN_MARK(s, p + 1, 2);
-            factor_publish(p + 1, s, T, F, pflag, pbase, bad);
-            __syncthreads();
-            load_panel(p, T, F, P);
-            __syncthreads();
-        }
-        for (int t = mem; t < T.nt; t += G)
-            if (t > p && !(ahead && t == p + 1)) update_tile(t, p, T, F, P);
-        __syncthreads();
     }
-    if (bad && lane == 0) atomicExch(status, 1);
+    if (bad && (tid & 63) == 0) atomicExch(status, 1);
     // ---- out: own update tiles write-through for the parent; member 0: y and the pending updates
     if (S.parent >= 0) {
-        for (int t = mem; t < T.nt; t += G) {
+        for (int t = t_first; t < T.nt; t += t_step) {
             if (t < T.np) continue;
             const int cs = T.c0(t), n = (T.c1(t) - cs) * m3;
             for (int e0 = 0; e0 < n; e0 += kFT * kPFL) {
@@ -1191,7 +1302,7 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
                                                        const FChild* __restrict__ fchild,
                                                        const double* __restrict__ hb, const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm, double* fronts,
-                                                       double* __restrict__ ysol, double* acc, int ns) {
+                                                       double* __restrict__ ysol, double* acc, int ns, int db) {
     extern __shared__ __attribute__((aligned(16))) double smem_f[];
     double* sm = smem_f + 2;   // smem_f[0]: the claimed ticket (no static LDS: keeps the base 16-B aligned)
     const int code = claim_lds(order, sync, reinterpret_cast<int*>(smem_f));
@@ -1201,8 +1312,8 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
     if (S.G == 1 && 3 * (S.k + S.r) <= kSmall && S.nchild <= kMaxCh)
         small_front(s, S, sync + 1, status, sns, omap, relmap, child_list, hb, g, perm, fronts, ysol, acc, sm);
     else
-        large_front(s, mem, S, sync + 1, sync + 1 + ns, status, sns, omap, relmap, child_list, ftasks, fchild, hb, g,
-                    perm, fronts, ysol, acc, sm);
+        large_front(s, mem, S, sync + 1, sync + 1 + ns, sync + 2 + 3 * ns, status, sns, omap, relmap, child_list,
+                    ftasks, fchild, hb, g, perm, fronts, ysol, acc, sm, db);
 }
 
 template <typename T>
@@ -1254,6 +1365,7 @@ struct CholDev {
     // fused DAG factorization + forward solve (used when every front fits its LDS budget)
     bool fused = false;
     size_t lds_fused = 0;
+    bool fused_db = true;
 };
 
 }  // namespace
@@ -1420,7 +1532,16 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     // fused path: LDS budget of the largest front
     for (int32_t s = 0; s < S.ns; ++s) {
         const SnDev& d = sns[(size_t)s];
-        c->lds_fused = std::max(c->lds_fused, 8 * fused_lds_doubles(3 * (d.k + d.r), 3 * d.k));
+        c->lds_fused = std::max(c->lds_fused, 8 * fused_lds_doubles(3 * (d.k + d.r), 3 * d.k, true));
+    }
+    // two panel buffers for the chain when every front fits, else one (the chain step goes through HBM)
+    c->fused_db = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_SINGLE_BUFFER") == nullptr;
+    if (!c->fused_db) {
+        c->lds_fused = 0;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const SnDev& d = sns[(size_t)s];
+            c->lds_fused = std::max(c->lds_fused, 8 * fused_lds_doubles(3 * (d.k + d.r), 3 * d.k, false));
+        }
     }
     c->fused = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_LEVELS") == nullptr;
     c->lds_solve.assign((size_t)S.n_levels, 0);
@@ -1490,8 +1611,9 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         rc |= dalloc_copy(&c->ftasks, ftasks);
         rc |= dalloc_copy(&c->fchild, fchild);
         rc |= dalloc_copy(&c->order_bwd, bwd);
-        // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns]]
-        c->sync_bytes = ((size_t)(3 + 3 * S.ns) * sizeof(int32_t) + 15) & ~size_t(15);
+        // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
+        //  pivot-tile hand-off flags [per large-front tile]]
+        c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
         rc |= hipMalloc(reinterpret_cast<void**>(&c->sync), c->sync_bytes) != hipSuccess;
         for (size_t v : c->lds_solve) c->lds_solve_max = std::max(c->lds_solve_max, v);
     }
@@ -1519,7 +1641,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
         hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
                            c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
                            c->perm, c->fronts,
-                           c->ysol, c->acc, S.ns);
+                           c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                            c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;

@@ -15,6 +15,8 @@ for c in 2 3 4; do
 done
 DPG_CHOL_LEVELS=1 timeout -k 10 60 tools/build/chol_bench tools/build/pairs4.bin 20 > "$OUT/levels4.log" 2>&1; rc=$?
 echo "levels config4 rc=$rc $(cat $OUT/levels4.log)"; [ $rc -eq 0 ] || exit $rc
+DPG_CHOL_SINGLE_BUFFER=1 timeout -k 10 60 tools/build/chol_bench tools/build/pairs4.bin 20 > "$OUT/single4.log" 2>&1; rc=$?
+echo "single-buffer config4 rc=$rc $(cat $OUT/single4.log)"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 60 tools/build/chol_bench_t tools/build/pairs4.bin 3 > "$OUT/timing4.log" 2>&1; rc=$?
 echo "timing rc=$rc"; grep -E "span|critical" "$OUT/timing4.log"; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp

@@ -23,12 +23,19 @@ int main(int argc, char** argv) {
         fl[s] = k * k * k / 3 + k * k * r + k * r * r;
         nnzL += (int64_t)(k * (k + 1) / 2 + k * r);
     }
-    double crit = 0;
+    double crit = 0, crit_us = 0;
+    std::vector<double> cl((size_t)S.ns, 0.0);
     for (int s = 0; s < S.ns; ++s) {   // children precede parents
         cp[s] += fl[s];
         if (S.sn_parent[s] >= 0) cp[S.sn_parent[s]] = std::max(cp[S.sn_parent[s]], cp[s]);
         else crit = std::max(crit, cp[s]);
+        // latency model of the DAG kernel: LDS small front ~3 us, team front ~8 us + 25 us per 24-col panel
+        const int k3 = 3 * (S.sn_c0[s + 1] - S.sn_c0[s]), m3 = k3 + 3 * (int)(S.sn_rows_ptr[s + 1] - S.sn_rows_ptr[s]);
+        cl[s] += m3 <= 96 ? 3.0 : 8.0 + 25.0 * ((k3 + 23) / 24);
+        if (S.sn_parent[s] >= 0) cl[S.sn_parent[s]] = std::max(cl[S.sn_parent[s]], cl[s]);
+        else crit_us = std::max(crit_us, cl[s]);
     }
+    printf("latency-model critical path %.0f us\n", crit_us);
     printf("n=%lld ns=%d levels=%d max_front=%d flops=%.3g nnzL=%lld fronts=%.1f MB crit_path_flops=%.3g\n",
            (long long)n, S.ns, S.n_levels, S.max_front, S.flops, (long long)nnzL, S.front_off[S.ns] * 8e-6, crit);
     {
