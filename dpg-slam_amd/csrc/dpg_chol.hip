@@ -61,7 +61,11 @@ __device__ unsigned long long g_panel[16384 * 16 * 8];
 __device__ unsigned long long g_steps[16384 * 16 * 8];
 #define ST_MARK(s, p, k) do { if (threadIdx.x == 0 && (s) < 16384 && (p) < 16 && (k) < 8) g_steps[((s) * 16 + (p)) * 8 + (k)] = wall_clock64(); } while (0)
 #define PN_MARK(s, p, k) do { if (threadIdx.x == 0 && (s) < 16384 && (p) < 16) g_panel[((s) * 16 + (p)) * 8 + (k)] = wall_clock64(); } while (0)
+// per-front stamps of the backward solve: [front][0 claim, 1 parent ready, 2 z updated, 3 solved, 4 done]
+__device__ unsigned long long g_bwd[16384 * 8];
+#define BW_MARK(s, k) do { if (threadIdx.x == 0 && (s) < 16384) g_bwd[(s) * 8 + (k)] = wall_clock64(); } while (0)
 #else
+#define BW_MARK(s, k) do { } while (0)
 #define FT_MARK(s, k) do { } while (0)
 #define PN_MARK(s, p, k) do { } while (0)
 #define ST_MARK(s, p, k) do { } while (0)
@@ -156,26 +160,26 @@ __global__ __launch_bounds__(kT) void chol_assemble(const AsmTask* __restrict__ 
     PROF_END(pid);
 }
 
-// 1/sqrt(d) from the hardware estimate and two Newton steps (full fp64 precision; far shorter
-// than the IEEE sqrt + divide expansions on the factorization's critical path).
+// 1/sqrt(d) from the hardware estimate (relative error ~5e-8) and ONE third-order correction:
+// with e = 1 - d y^2, 1/sqrt(d) = y (1 - e)^(-1/2) = y (1 + e/2 + 3e^2/8 + O(e^3)), the O(e^3) term
+// ~1e-22 -- full fp64 precision in 4 dependent operations (two Newton steps take 6).
 __device__ __forceinline__ double rsqrt_nr(double d) {
-    double y = __builtin_amdgcn_rsq(d);
-    const double h = 0.5 * d;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
+    const double y = __builtin_amdgcn_rsq(d);
+    const double e = fma(-(d * y), y, 1.0);
+    return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 
 // Cholesky factor of a 3x3 SPD block and the inverse of that factor, from the block's leading
 // minors (d00, M2, det): the three reciprocal square roots are independent, so the dependent chain
 // is about a third of the column-by-column one (a wave64 fp64 op is ~32 cycles of latency).
+// Branch-free: a non-positive minor only raises `bad` (the solve then reports failure).
 struct Chol3 { double l00, l10, l11, l20, l21, l22, m00, m10, m11, m20, m21, m22; };
 __device__ __forceinline__ Chol3 chol3(double d00, double d10, double d11, double d20, double d21, double d22,
                                        bool& bad) {
-    double M2 = fma(d00, d11, -d10 * d10);
+    const double M2 = fma(d00, d11, -d10 * d10);
     const double c0 = fma(d11, d22, -d21 * d21), c1 = fma(d10, d22, -d21 * d20), c2 = fma(d10, d21, -d11 * d20);
-    double det = fma(d00, c0, fma(-d10, c1, d20 * c2));
-    if (!(d00 > 0.0 && M2 > 0.0 && det > 0.0)) { bad = true; d00 = 1.0; M2 = 1.0; det = 1.0; d10 = d20 = d21 = 0.0; }
+    const double det = fma(d00, c0, fma(-d10, c1, d20 * c2));
+    bad |= !(d00 > 0.0 && M2 > 0.0 && det > 0.0);
     const double r0 = rsqrt_nr(d00), r1 = rsqrt_nr(M2), r2 = rsqrt_nr(det);
     Chol3 L;
     L.l00 = d00 * r0;                  // sqrt(d00)
@@ -495,6 +499,7 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_b));
     const SnDev S = sns[s];
+    BW_MARK(s, 0);
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     double* D = sm;
@@ -520,6 +525,7 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    BW_MARK(s, 1);
     for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
     __syncthreads();
     for (int j = tid; j < k3; j += kT) {   // z = y - L21^T x_r, four independent accumulators
@@ -536,6 +542,7 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
         z[j] -= (a0 + a1) + (a2 + a3);
     }
     __syncthreads();
+    BW_MARK(s, 2);
     for (int b = nblk - 1; b >= 0; --b) {
         const int jb = b * kSB, bw = min(kSB, k3 - jb);
         if (b != nblk - 1) {
@@ -570,10 +577,12 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
         }
         __syncthreads();
     }
+    BW_MARK(s, 3);
     for (int j = tid; j < k3; j += kT) st_agent(xsol + 3 * (int64_t)S.c0 + j, z[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_store(sync + 1 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    BW_MARK(s, 4);
 }
 
 // ---- fused factorization + forward solve: ONE launch, fronts as a DAG ----
@@ -813,7 +822,7 @@ struct FChild { int32_t ja, jb, k, r; int64_t front_off, rows_off; };
 // rows i >= c valid, zeros above): POTRF of the top w x w block, TRSM of the rows below, L_top
 // copied back.  `scr` holds L_top, the 3x3 inverses and the POTRF column exchange.
 __device__ void factor_lds(int q, int s, const Tiles& T, double* P, double* scr, bool& bad) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int k3 = T.k3, m3 = T.m3;
     const int j0 = kFNB * q, w = min(kFNB, k3 - j0), R = m3 - j0;
     const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
@@ -847,9 +856,13 @@ __device__ void factor_lds(int q, int s, const Tiles& T, double* P, double* scr,
                 }
             }
             __syncthreads();
-            const Chol3 L = chol3(cbs[c0], cbs[c0 + 1], cbs[64 + c0 + 1], cbs[c0 + 2], cbs[64 + c0 + 2],
-                                  cbs[128 + c0 + 2], bad);
-            const double p0 = cbs[i], p1 = cbs[64 + i], p2 = cbs[128 + i];
+            // every LDS read of the step issues at once (the row's values are pinned here, so the
+            // compiler cannot sink their loads behind the 3x3 factorization)
+            double p0 = cbs[i], p1 = cbs[64 + i], p2 = cbs[128 + i];
+            const double d00 = cbs[c0], d10 = cbs[c0 + 1], d11 = cbs[64 + c0 + 1];
+            const double d20 = cbs[c0 + 2], d21 = cbs[64 + c0 + 2], d22 = cbs[128 + c0 + 2];
+            asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2));
+            const Chol3 L = chol3(d00, d10, d11, d20, d21, d22, bad);
             double x0 = p0 * L.m00;
             double x1 = fma(p0, L.m10, p1 * L.m11);
             double x2 = fma(p0, L.m20, fma(p1, L.m21, p2 * L.m22));
@@ -1707,6 +1720,9 @@ extern "C" int dpg_chol_steps_dump(unsigned long long* out, int n) {
 }
 extern "C" int dpg_chol_panel_dump(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_panel), sizeof(unsigned long long) * 16 * 8 * (size_t)n) == hipSuccess ? 0 : -1;
+}
+extern "C" int dpg_chol_bwd_dump(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd), sizeof(unsigned long long) * 8 * (size_t)n) == hipSuccess ? 0 : -1;
 }
 extern "C" int dpg_chol_front_dump(unsigned long long* out, int n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_front), sizeof(unsigned long long) * 8 * (size_t)n) == hipSuccess ? 0 : -1;

@@ -23,6 +23,7 @@ void dpg_chol_stats(void* chol, double out[6]);
 int dpg_chol_prof_dump(unsigned long long* out, int n, unsigned long long* span);
 int dpg_chol_prof_reset(void);
 int dpg_chol_front_dump(unsigned long long* out, int n);
+int dpg_chol_bwd_dump(unsigned long long* out, int n);
 int dpg_chol_panel_dump(unsigned long long* out, int n);
 int dpg_chol_steps_dump(unsigned long long* out, int n);
 void dpg_chol_tree(void* h, int32_t* parent, int32_t* m3, int32_t* k3);
@@ -200,6 +201,30 @@ int main(int argc, char** argv) {
                 }
             }
             printf("critical path: %d fronts, hand-off %.1f + assembly %.1f + factor %.1f + out %.1f us\n", depth, sw, sa, sf, so);
+        }
+        std::vector<unsigned long long> bm((size_t)ns * 8, 0ull);
+        if (dpg_chol_bwd_dump(bm.data(), ns) == 0 && bm[4] != 0) {
+            // backward: the last front to finish, then its parents up to the root
+            unsigned long long t0 = ~0ull, t1 = 0;
+            int last = -1;
+            for (int q = 0; q < ns; ++q) {
+                t0 = std::min(t0, bm[(size_t)q * 8]);
+                if (bm[(size_t)q * 8 + 4] > t1) { t1 = bm[(size_t)q * 8 + 4]; last = q; }
+            }
+            printf("backward span %.1f us (last front %d)\n", (t1 - t0) / 100.0, last);
+            double sw = 0, sz = 0, sd = 0, so = 0;
+            int depth = 0;
+            for (int q = last; q >= 0; q = par[(size_t)q]) {
+                const unsigned long long* m = bm.data() + (size_t)q * 8;
+                const int pq = par[(size_t)q];
+                const double lat = pq >= 0 ? ((double)m[1] - (double)bm[(size_t)pq * 8 + 4]) / 100.0 : 0.0;
+                printf("  bwd front %5d m3 %3d k3 %3d | claim %8.2f wait %7.2f (parent->ready %5.2f) z %6.2f diag %6.2f out %6.2f\n", q,
+                       m3v[(size_t)q], k3v[(size_t)q], (m[0] - t0) / 100.0, ((double)m[1] - (double)m[0]) / 100.0, lat,
+                       (m[2] - m[1]) / 100.0, (m[3] - m[2]) / 100.0, (m[4] - m[3]) / 100.0);
+                sw += lat; sz += (m[2] - m[1]) / 100.0; sd += (m[3] - m[2]) / 100.0; so += (m[4] - m[3]) / 100.0;
+                ++depth;
+            }
+            printf("backward critical path: %d fronts, hand-off %.1f + z %.1f + diag %.1f + out %.1f us\n", depth, sw, sz, sd, so);
         }
     }
     {
