@@ -164,9 +164,7 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     }
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (c->icp_variant == DPG_ICP_ANGULAR) {
-        int32_t cap = 64;
-        while (cap < maxp) cap <<= 1;   // power of two: the windows run modulo cap
-        kp.lds_tgt = cap;
+        kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 16);   // LDS record capacity
         rc = dpg_launch_icp_ang(ds_dev, tree_pts, tree_idx, buckets, edges_dev, ne, &kp, maxp, res_dev, trace_dev,
                                 c->stream);
     } else if (c->icp_variant == DPG_ICP_KDTREE) {

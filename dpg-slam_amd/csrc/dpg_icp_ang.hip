@@ -32,15 +32,20 @@
 #ifdef DPG_ICP_STATS
 // diagnostics build only: [0] point-iterations, [1] forward candidates, [2] forward wave trips,
 // [3] reciprocal candidates, [4] reciprocal wave trips, [5] correspondences, [6] no forward match,
-// [7] full-scan forward windows
-__device__ unsigned long long g_icp_stats[8];
+// [7] full-scan forward windows; per-wave clock cycles (s_memtime) summed over waves and
+// iterations: [8] search, [9] wait at the search barrier, [10] sums + fold + wait, [11] fit +
+// update + wait, [12] waves x iterations
+__device__ unsigned long long g_icp_stats[16];
 #define ICP_STAT(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
+#define ICP_STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#else
+#define ICP_STAMP(var)
 #endif
 
 namespace {
 
-constexpr int kT = 256;
-constexpr int kW = kT / 64;
+constexpr int kT = 512;                         // ICP workgroup (8 waves)
+constexpr int kTI = 256;                        // index-build workgroup
 constexpr int kSums = 10;
 constexpr int kB = 1024;                        // pseudo-angle buckets per cloud (~1 point each)
 constexpr float kTwoPi = 6.28318530717958647692f;
@@ -74,7 +79,7 @@ __device__ __forceinline__ uint32_t orderable(float f) {
 }
 
 // one workgroup per node: points sorted by angle + bucket starts
-__global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restrict__ ds_pts,
+__global__ __launch_bounds__(kTI) void angle_index_kernel(const float2* __restrict__ ds_pts,
                                                          const int64_t* __restrict__ ds_off,
                                                          float2* __restrict__ idx_pts,
                                                          uint16_t* __restrict__ idx_orig,
@@ -85,13 +90,13 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
     const int N = (int)(ds_off[v + 1] - off);
     uint16_t* bk = buckets + (size_t)v * (kB + 1);
     if (N <= 0) {
-        for (int b = tid; b <= kB; b += kT) bk[b] = 0;
+        for (int b = tid; b <= kB; b += kTI) bk[b] = 0;
         return;
     }
     int P = 1;
     while (P < N) P <<= 1;
     uint64_t* key = reinterpret_cast<uint64_t*>(smem);   // [P]: orderable(angle) << 32 | index
-    for (int s = tid; s < P; s += kT) {
+    for (int s = tid; s < P; s += kTI) {
         if (s < N) {
             const float2 p = ds_pts[off + s];
             key[s] = ((uint64_t)orderable(pseudo_angle(p.x, p.y)) << 32) | (uint32_t)s;
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
     __syncthreads();
     for (int k = 2; k <= P; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = tid; q < P / 2; q += kT) {
+            for (int q = tid; q < P / 2; q += kTI) {
                 const int i = 2 * q - (q & (j - 1));
                 const int l = i + j;
                 const bool up = (i & k) == 0;
@@ -112,7 +117,7 @@ __global__ __launch_bounds__(kT) void angle_index_kernel(const float2* __restric
             __syncthreads();
         }
     }
-    for (int s = tid; s < N; s += kT) {
+    for (int s = tid; s < N; s += kTI) {
         const int o = (int)(key[s] & 0xffffffffu);
         const float2 p = ds_pts[off + o];
         idx_pts[off + s] = p;
@@ -149,37 +154,130 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
     return ((uint64_t)__float_as_uint(d) << 32) | key;
 }
 
+// Workgroup shape: kT = 512 threads (8 waves; 4 workgroups = 32 waves per CU at <= 64 VGPRs and
+// ~39 KB of LDS each), thread t owns the source points i = t + kT m during the search.  The fp64
+// sums keep the 256-lane fixed tree of DPG_ICP_LANES (oracle lane_tree): each point's match is
+// parked in the pad word of its LDS source record, then waves 0-3 accumulate lane l = i mod 256
+// over i = l, l + 256, ... in that order and fold as before.
+//
+// Candidate loops (R4) visit kU records per trip, wave-uniformly, with no per-candidate bounds
+// test: a lane whose own window is exhausted keeps evaluating the records that follow it.  That
+// is exact -- every record visited is a real point of the cloud, so the forward argmin over a
+// superset of the window that contains the true nearest neighbour is the same (distance, lowest
+// original index) minimum, and any extra source record that beats i at t_j is a genuine
+// reciprocity violation.  Records [n, n + kU) repeat [0, kU) mod n so that a trip never wraps
+// inside itself; the trip start advances by kU mod n.
+constexpr int kLanes = 256;   // == DPG_ICP_LANES
+constexpr int kLW = kLanes / 64;
+constexpr int kU = 4;
+constexpr uint32_t kNoMatch = 0xffffffffu;
+
+// what wave 0 hands every wave after the fit of an iteration
+struct Bcast {
+    double inv[4];   // inverse of the new 2x2 rotation block (reciprocal windows), fp64
+    double mse;
+    double prev_mse; // wave 0's convergence state
+    float F[6];      // final transform so far
+    float r[4];      // this iteration's (cos, sin, tx, ty)
+    int code;        // 0 continue, 1 converged (stop), 2 too few correspondences (stop)
+    int cnt;
+};
+
+// fp64 inverse of the 2x2 block of a 2x3 float transform (same expressions every time)
+__device__ __forceinline__ void inverse2(const float F[6], double inv[4]) {
+    const double det = (double)F[0] * (double)F[4] - (double)F[1] * (double)F[3];
+    inv[0] = (double)F[4] / det;
+    inv[1] = -(double)F[1] / det;
+    inv[2] = -(double)F[3] / det;
+    inv[3] = (double)F[0] / det;
+}
+
 struct Lds {
-    Rec* tp;          // target points in angle order
-    Rec* scs;         // current (moved) source points in the source's angle order
+    Rec* tp;          // target points in angle order, [cap + kU]
+    Rec* scs;         // current (moved) source points in the source's angle order, [cap + kU];
+                      // pad word = sorted target position of this iteration's match (kNoMatch)
     uint16_t* spos;   // source original index -> sorted position
     uint16_t* tb;     // target bucket starts [kB+1]
     uint16_t* sb;     // source bucket starts [kB+1]
-    double* wpart;    // [kW][kSums + 2]
+    double* wpart;    // [kLW][kSums + 2]
+    Bcast* bc;        // wave 0's fit, read by every wave
 };
 
-__device__ __forceinline__ size_t a16(size_t x) { return (x + 15) & ~size_t(15); }
+__host__ __device__ inline size_t ang_lds_layout(int cap, size_t* off /* [7] or null */) {
+    size_t o = 0, p[7];
+    p[0] = o; o = (o + 16 * (size_t)(cap + kU) + 15) & ~size_t(15);
+    p[1] = o; o = (o + 16 * (size_t)(cap + kU) + 15) & ~size_t(15);
+    p[2] = o; o = (o + 2 * (size_t)cap + 15) & ~size_t(15);
+    p[3] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
+    p[4] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
+    p[5] = o; o = (o + sizeof(double) * kLW * (kSums + 2) + 15) & ~size_t(15);
+    p[6] = o; o = (o + sizeof(Bcast) + 15) & ~size_t(15);
+    if (off)
+        for (int q = 0; q < 7; ++q) off[q] = p[q];
+    return o;
+}
 
 __device__ Lds carve(unsigned char* base, int cap) {
+    size_t p[7];
+    ang_lds_layout(cap, p);
     Lds L;
-    size_t o = 0;
-    L.tp = reinterpret_cast<Rec*>(base + o);      o = a16(o + 16 * (size_t)cap);
-    L.scs = reinterpret_cast<Rec*>(base + o);     o = a16(o + 16 * (size_t)cap);
-    L.spos = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)cap);
-    L.tb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
-    L.sb = reinterpret_cast<uint16_t*>(base + o); o = a16(o + 2 * (size_t)(kB + 1));
-    L.wpart = reinterpret_cast<double*>(base + o);
+    L.tp = reinterpret_cast<Rec*>(base + p[0]);
+    L.scs = reinterpret_cast<Rec*>(base + p[1]);
+    L.spos = reinterpret_cast<uint16_t*>(base + p[2]);
+    L.tb = reinterpret_cast<uint16_t*>(base + p[3]);
+    L.sb = reinterpret_cast<uint16_t*>(base + p[4]);
+    L.wpart = reinterpret_cast<double*>(base + p[5]);
+    L.bc = reinterpret_cast<Bcast*>(base + p[6]);
     return L;
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// kU consecutive records with four ds_read_b128 issued back to back and ONE wait (the compiler,
+// left alone, narrows an unused pad word to ds_read_b96 -- 8 LDS cycles instead of 4 -- or
+// serialises the loads behind per-load waits under the 64-VGPR budget)
+__device__ __forceinline__ void ld_recs(const Rec* p, uint4 (&r)[kU]) {
+    static_assert(kU == 4, "ld_recs issues four loads");
+    const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(p);   // LDS byte offset
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:16\n\t"
+        "ds_read_b128 %2, %4 offset:32\n\t"
+        "ds_read_b128 %3, %4 offset:48\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+        : "v"(a)
+        : "memory");
+}
+
+// workgroup-uniform values (the transform, the reduced sums) kept in SGPRs: frees VGPRs for the
+// candidate loops (8 waves per SIMD need <= 64)
+__device__ __forceinline__ float uni(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ double uni(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// squared distance, (ax - bx)^2 + (ay - by)^2 in float: packed subtract / multiply (v_pk_*_f32,
+// the same IEEE operations lane by lane), then one add -- bit-identical to the scalar form.
 __device__ __forceinline__ float sqd(float ax, float ay, float bx, float by) {
-    const float dx = ax - bx, dy = ay - by;
-    return dx * dx + dy * dy;
+    f2v d = (f2v){ax, ay} - (f2v){bx, by};
+    d = d * d;
+    return d.x + d.y;
+}
+
+// (s + step) mod n for s in [0, n), step = kU mod n < n: one add and an unsigned min
+__device__ __forceinline__ int advance(int s, int step, int n) {
+    const uint32_t a = (uint32_t)(s + step);
+    return (int)min(a, a - (uint32_t)n);
 }
 
 // The sorted positions of the points that can lie within `rad` of q (angle window), as ONE
-// wrapped range: positions start, start+1, ... (mod n), `count` of them (the whole cloud when
-// the window would span too wide an angle).
+// wrapped range: start in [0, n), `count` positions (the whole cloud when the window would span
+// too wide an angle).
 __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int& start) {
     const float sn = rad * __builtin_amdgcn_rsqf(qx * qx + qy * qy) * 1.0001f + 1e-6f;   // sin of the half-angle
     if (!(sn < 0.7f)) {
@@ -191,13 +289,15 @@ __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float
     float lo = pq - half, hi = pq + half;
     if (lo < 0.0f) lo += kTwoPi;
     if (hi >= kTwoPi) hi -= kTwoPi;
-    start = bk[bucket_of(lo)];
+    int s = bk[bucket_of(lo)];
     const int end = bk[bucket_of(hi) + 1];
-    return lo <= hi ? end - start : (n - start) + end;   // else: straddles pseudo-angle 0
+    const int cnt = lo <= hi ? end - s : (n - s) + end;   // else: straddles pseudo-angle 0
+    start = s >= n ? s - n : s;
+    return cnt;
 }
 
 template <int PPT>
-__global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ ds_pts,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
                                                      const float2* __restrict__ idx_pts,
                                                      const uint16_t* __restrict__ idx_orig,
                                                      const uint16_t* __restrict__ buckets,
@@ -210,26 +310,21 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
     const dpg_icp_edge E = edges[e];
     const int N = E.n_src_ds, M = E.n_tgt_ds;
     const int vt = E.tgt_node, vs = E.src_node;
-    const int cap = kp.lds_tgt, mask = cap - 1;   // cap: a power of two >= every cloud
+    const int cap = kp.lds_tgt;
+    const int stepM = M > 0 ? kU % M : 0, stepN = N > 0 ? kU % N : 0;
     Lds L = carve(smem, cap);
-    // sorted clouds, padded to cap with far-away dummies: a window [start, start + count) then
-    // runs modulo cap (one AND per candidate); the dummies in the wrap gap never win
-    for (int i = t; i < cap; i += kT) {
-        if (i < M) {
-            const float2 p = idx_pts[E.tgt_ds_off + i];
-            L.tp[i] = Rec{p.x, p.y, ((uint32_t)idx_orig[E.tgt_ds_off + i] << 16) | (uint32_t)i, 0u};
-        } else {
-            L.tp[i] = Rec{1e18f, 1e18f, 0xffffffffu, 0u};
-        }
+    // sorted target + the kU repeated records after it
+    for (int i = t; i < M + kU && M > 0; i += kT) {
+        const int p = i < M ? i : (i - M) % M;
+        const float2 q = idx_pts[E.tgt_ds_off + p];
+        L.tp[i] = Rec{q.x, q.y, ((uint32_t)idx_orig[E.tgt_ds_off + p] << 16) | (uint32_t)p, 0u};
     }
-    for (int s = t; s < cap; s += kT) {
-        if (s < N) {
-            const uint16_t o = idx_orig[E.src_ds_off + s];
-            L.scs[s].key = ((uint32_t)o << 16) | (uint32_t)s;
-            L.spos[o] = (uint16_t)s;
-        } else {
-            L.scs[s] = Rec{1e18f, 1e18f, 0xffffffffu, 0u};
-        }
+    for (int s = t; s < N + kU && N > 0; s += kT) {
+        const int p = s < N ? s : (s - N) % N;
+        const uint16_t o = idx_orig[E.src_ds_off + p];
+        L.scs[s].key = ((uint32_t)o << 16) | (uint32_t)p;
+        L.scs[s].pad = kNoMatch;
+        if (s < N) L.spos[o] = (uint16_t)s;
     }
     for (int b = t; b <= kB; b += kT) {
         L.tb[b] = buckets[(size_t)vt * (kB + 1) + b];
@@ -237,10 +332,32 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
     }
     float F[6];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) F[q] = E.guess[q];
+    for (int q = 0; q < 6; ++q) F[q] = uni(E.guess[q]);
+    if (t == 0) {   // loop state lives in LDS (SGPR budget of 8 waves per SIMD)
+        Bcast B;
+        inverse2(F, B.inv);
+        B.mse = 0.0;
+        B.prev_mse = DBL_MAX;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) B.F[q] = F[q];
+        B.r[0] = B.r[1] = B.r[2] = B.r[3] = 0.f;
+        B.code = 0;
+        B.cnt = 0;
+        *L.bc = B;
+    }
     __syncthreads();
     float sx[PPT], sy[PPT];
     int seed[PPT], sp[PPT];
+    // store the moved source point at its sorted position (and its repeat past n)
+    auto put = [&](int m) {
+        L.scs[sp[m]].x = sx[m];
+        L.scs[sp[m]].y = sy[m];
+        if (sp[m] < kU)
+            for (int r = N + sp[m]; r < N + kU; r += N) {
+                L.scs[r].x = sx[m];
+                L.scs[r].y = sy[m];
+            }
+    };
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
         const int i = t + kT * m;
@@ -253,28 +370,27 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             sx[m] = (F[0] * p.x + F[1] * p.y) + F[2];
             sy[m] = (F[3] * p.x + F[4] * p.y) + F[5];
             sp[m] = L.spos[i];
-            L.scs[sp[m]].x = sx[m];
-            L.scs[sp[m]].y = sy[m];
+            put(m);
         }
     }
     __syncthreads();
 
     const float r2f = kp.r2_f;
     const float rmax = sqrtf(r2f) * 1.0001f + 1e-5f;
-    double prev_mse = DBL_MAX, last_mse = 0.0;
-    int k = 0, converged = 0, status = DPG_ICP_OK, last_cnt = 0;
+    int k = 0, converged = 0, status = DPG_ICP_OK;
+#ifdef DPG_ICP_STATS
+    unsigned long long ph[4] = {0, 0, 0, 0}, nit = 0;
+#endif
     for (;;) {
-        const double det = (double)F[0] * (double)F[4] - (double)F[1] * (double)F[3];
-        const double i00 = (double)F[4] / det, i01 = -(double)F[1] / det;
-        const double i10 = -(double)F[3] / det, i11 = (double)F[0] / det;
+        ICP_STAMP(c0);
+        const double i00 = uni(L.bc->inv[0]), i01 = uni(L.bc->inv[1]);
+        const double i10 = uni(L.bc->inv[2]), i11 = uni(L.bc->inv[3]);
+        const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
         const float drift = 1e-4f + 5e-5f * (float)(k + 1);
-        double acc[kSums];
-#pragma unroll
-        for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
-            // every lane runs every step (dead lanes predicated off): the candidate loops below
-            // are wave-uniform (exit on __any), with straight-line predicated bodies
+            // every lane runs every trip (dead lanes included): the candidate loops are
+            // wave-uniform (exit on __any) with straight-line bodies
             const int i = t + kT * m;
             const bool live = i < N;
             const float qx = sx[m], qy = sy[m];
@@ -291,25 +407,24 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             }
             {
                 int s = 0;
-                int fc = live ? window(L.tb, M, qx, qy, rad, s) : 0;
-                s = s >= M ? s - M : s;
-                if (s + fc > M) fc += cap - M;   // wraps: step over the padding gap
+                const int fc = live ? window(L.tb, M, qx, qy, rad, s) : 0;
 #ifdef DPG_ICP_STATS
                 {
                     int trips = 0;
-                    for (int c = 0; __any(c < fc); c += 2) ++trips;
+                    for (int c = 0; __any(c < fc); c += kU) ++trips;
                     if (live) { ICP_STAT(0, 1); ICP_STAT(1, fc); if (fc >= M) ICP_STAT(7, 1); }
                     if (lane == 0) ICP_STAT(2, trips);
                 }
 #endif
-                for (int c = 0; __any(c < fc); c += 2) {   // exact (d, original index) argmin
+                for (int c = 0; __any(c < fc); c += kU) {   // exact (d, original index) argmin
+                    uint4 r[kU];
+                    ld_recs(L.tp + s, r);
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const Rec r = ld_rec(L.tp + s);
-                        const uint64_t kd = dkey(sqd(qx, qy, r.x, r.y), r.key);
-                        best = (c + u < fc && kd < best) ? kd : best;
-                        s = (s + 1) & mask;
+                    for (int u = 0; u < kU; ++u) {
+                        const uint64_t kd = dkey(sqd(qx, qy, __uint_as_float(r[u].x), __uint_as_float(r[u].y)), r[u].z);
+                        best = kd < best ? kd : best;
                     }
+                    s = advance(s, stepM, M);
                 }
             }
             const uint32_t bkey = (uint32_t)best;
@@ -325,11 +440,9 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
                 if (ok) {
                     const Rec r = L.tp[bp];
                     tj = make_float2(r.x, r.y);
-                    const double ux = (double)tj.x - (double)F[2], uy = (double)tj.y - (double)F[5];
+                    const double ux = (double)tj.x - (double)ftx, uy = (double)tj.y - (double)fty;
                     const float px = (float)(i00 * ux + i01 * uy), py = (float)(i10 * ux + i11 * uy);
                     rc = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
-                    s = s >= N ? s - N : s;
-                    if (s + rc > N) rc += cap - N;
                 }
                 // i's own word: any other current source with a smaller (d, original index) word
                 // is closer to t_j (or tied with a lower index) and breaks reciprocity
@@ -337,20 +450,23 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
 #ifdef DPG_ICP_STATS
                 {
                     int trips = 0;
-                    for (int c = 0; __any(ok & (c < rc)); c += 2) ++trips;
+                    for (int c = 0; __any(ok & (c < rc)); c += kU) ++trips;
                     if (ok) ICP_STAT(3, rc);
                     if (live && !ok) ICP_STAT(6, 1);
                     if (lane == 0) ICP_STAT(4, trips);
                 }
 #endif
-                for (int c = 0; __any(ok & (c < rc)); c += 2) {
+                for (int c = 0; __any(ok & (c < rc)); c += kU) {
+                    uint4 r[kU];
+                    ld_recs(L.scs + s, r);
+                    bool beat = false;
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) {
-                        const Rec r = ld_rec(L.scs + s);
-                        const uint64_t kd = dkey(sqd(r.x, r.y, tj.x, tj.y), r.key);
-                        ok = ok & !((c + u < rc) & (kd < mine));
-                        s = (s + 1) & mask;
+                    for (int u = 0; u < kU; ++u) {
+                        const uint64_t kd = dkey(sqd(__uint_as_float(r[u].x), __uint_as_float(r[u].y), tj.x, tj.y), r[u].z);
+                        beat = beat | (kd < mine);
                     }
+                    ok = ok & !beat;
+                    s = advance(s, stepN, N);
                 }
             }
 #ifdef DPG_ICP_STATS
@@ -358,49 +474,99 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
 #endif
             if (live && trace && k < kp.trace_iters)
                 trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
-            if (ok) {
-                const Rec tq = L.tp[bp];
-                const double px = qx, py = qy, tx = tq.x, ty = tq.y;
-                acc[0] = acc[0] + 1.0;
-                acc[1] = acc[1] + (double)bd;
-                acc[2] = acc[2] + px;
-                acc[3] = acc[3] + py;
-                acc[4] = acc[4] + tx;
-                acc[5] = acc[5] + ty;
-                acc[6] = acc[6] + px * tx;
-                acc[7] = acc[7] + px * ty;
-                acc[8] = acc[8] + py * tx;
-                acc[9] = acc[9] + py * ty;
+            if (live) L.scs[sp[m]].pad = ok ? (uint32_t)bp : kNoMatch;
+        }
+        ICP_STAMP(c1);
+        __syncthreads();
+        ICP_STAMP(c2);
+        // ---- R5 sums: the 256-lane fixed tree over the parked matches (waves 0-3) ----
+        if (t < kLanes) {
+            double acc[kSums];
+#pragma unroll
+            for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
+            for (int i = t; i < N; i += kLanes) {
+                const Rec sr = ld_rec(L.scs + L.spos[i]);
+                if (sr.pad != kNoMatch) {
+                    const Rec tq = ld_rec(L.tp + sr.pad);
+                    const float d = sqd(sr.x, sr.y, tq.x, tq.y);   // == the forward search's d
+                    const double px = sr.x, py = sr.y, tx = tq.x, ty = tq.y;
+                    acc[0] = acc[0] + 1.0;
+                    acc[1] = acc[1] + (double)d;
+                    acc[2] = acc[2] + px;
+                    acc[3] = acc[3] + py;
+                    acc[4] = acc[4] + tx;
+                    acc[5] = acc[5] + ty;
+                    acc[6] = acc[6] + px * tx;
+                    acc[7] = acc[7] + px * ty;
+                    acc[8] = acc[8] + py * tx;
+                    acc[9] = acc[9] + py * ty;
+                }
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+                for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + __shfl_down(acc[q], off, 64);
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
             }
         }
+        __syncthreads();
+        ICP_STAMP(c3);
+        // ---- R5 fit + R6 convergence, once per workgroup (wave 0), broadcast through LDS ----
+        if (wave == 0) {
+            double S[kSums];
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
+            for (int q = 0; q < kSums; ++q)
+                S[q] = uni((L.wpart[0 * (kSums + 2) + q] + L.wpart[1 * (kSums + 2) + q]) +
+                           (L.wpart[2 * (kSums + 2) + q] + L.wpart[3 * (kSums + 2) + q]));
+            Bcast B = *L.bc;
+            float F[6];
 #pragma unroll
-            for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + __shfl_down(acc[q], off, 64);
-        }
-        if (lane == 0) {
+            for (int q = 0; q < 6; ++q) F[q] = uni(B.F[q]);
+            const double prev_mse = uni(B.prev_mse);
+            B.cnt = (int)S[0];
+            if (B.cnt < kp.min_corr) {
+                B.code = 2;   // stop, "Not enough correspondences found" (transform unchanged)
+            } else {
+                const double n = S[0];
+                const double a = (S[6] + S[9]) - (S[2] * S[4] + S[3] * S[5]) / n;
+                const double b = (S[7] - S[8]) - (S[2] * S[5] - S[3] * S[4]) / n;
+                const double hh = sqrt(a * a + b * b);
+                double c = 1.0, sn = 0.0;
+                if (hh > 0.0) { c = a / hh; sn = b / hh; }
+                const double mpx = S[2] / n, mpy = S[3] / n, mqx = S[4] / n, mqy = S[5] / n;
+                const double txd = mqx - (c * mpx - sn * mpy);
+                const double tyd = mqy - (sn * mpx + c * mpy);
+                const float cf = (float)c, sf = (float)sn, txf = (float)txd, tyf = (float)tyd;
+                const float nsf = -sf;
+                B.r[0] = cf; B.r[1] = sf; B.r[2] = txf; B.r[3] = tyf;
+                float Nf[6];
+                Nf[0] = cf * F[0] + nsf * F[3];
+                Nf[1] = cf * F[1] + nsf * F[4];
+                Nf[2] = (cf * F[2] + nsf * F[5]) + txf;
+                Nf[3] = sf * F[0] + cf * F[3];
+                Nf[4] = sf * F[1] + cf * F[4];
+                Nf[5] = (sf * F[2] + cf * F[5]) + tyf;
 #pragma unroll
-            for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
+                for (int q = 0; q < 6; ++q) B.F[q] = Nf[q];
+                const double mse = S[1] / S[0];
+                B.mse = mse;
+                const float tr = ((cf + cf) + 1.0f) - 1.0f;
+                const double cos_angle = 0.5 * (double)tr;
+                const double tsq = (double)(txf * txf + tyf * tyf);
+                B.code = (k + 1 >= kp.max_iter || (cos_angle >= kp.rot_thr && tsq <= kp.eps) ||
+                          fabs(mse - prev_mse) < kp.mse_abs) ? 1 : 0;
+                B.prev_mse = mse;
+                inverse2(Nf, B.inv);
+            }
+            if (lane == 0) *L.bc = B;
         }
         __syncthreads();
-        double S[kSums];
-#pragma unroll
-        for (int q = 0; q < kSums; ++q)
-            S[q] = (L.wpart[0 * (kSums + 2) + q] + L.wpart[1 * (kSums + 2) + q]) +
-                   (L.wpart[2 * (kSums + 2) + q] + L.wpart[3 * (kSums + 2) + q]);
-        const int cnt = (int)S[0];
-        last_cnt = cnt;
-        if (cnt < kp.min_corr) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
-        const double n = S[0];
-        const double a = (S[6] + S[9]) - (S[2] * S[4] + S[3] * S[5]) / n;
-        const double b = (S[7] - S[8]) - (S[2] * S[5] - S[3] * S[4]) / n;
-        const double hh = sqrt(a * a + b * b);
-        double c = 1.0, s = 0.0;
-        if (hh > 0.0) { c = a / hh; s = b / hh; }
-        const double mpx = S[2] / n, mpy = S[3] / n, mqx = S[4] / n, mqy = S[5] / n;
-        const double txd = mqx - (c * mpx - s * mpy);
-        const double tyd = mqy - (s * mpx + c * mpy);
-        const float cf = (float)c, sf = (float)s, txf = (float)txd, tyf = (float)tyd;
+        const int code = __builtin_amdgcn_readfirstlane(L.bc->code);
+        if (code == 2) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
+        const float cf = uni(L.bc->r[0]), sf = uni(L.bc->r[1]), txf = uni(L.bc->r[2]), tyf = uni(L.bc->r[3]);
         const float nsf = -sf;
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
@@ -408,33 +574,28 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
             const float x = sx[m], y = sy[m];
             sx[m] = (cf * x + nsf * y) + txf;
             sy[m] = (sf * x + cf * y) + tyf;
-            if (i < N) {
-                L.scs[sp[m]].x = sx[m];
-                L.scs[sp[m]].y = sy[m];
-            }
+            if (i < N) put(m);
         }
-        float Nf[6];
-        Nf[0] = cf * F[0] + nsf * F[3];
-        Nf[1] = cf * F[1] + nsf * F[4];
-        Nf[2] = (cf * F[2] + nsf * F[5]) + txf;
-        Nf[3] = sf * F[0] + cf * F[3];
-        Nf[4] = sf * F[1] + cf * F[4];
-        Nf[5] = (sf * F[2] + cf * F[5]) + tyf;
-#pragma unroll
-        for (int q = 0; q < 6; ++q) F[q] = Nf[q];
         ++k;
-        const double mse = S[1] / S[0];
-        last_mse = mse;
-        __syncthreads();
-        if (k >= kp.max_iter) { converged = 1; break; }
-        const float tr = ((cf + cf) + 1.0f) - 1.0f;
-        const double cos_angle = 0.5 * (double)tr;
-        const double tsq = (double)(txf * txf + tyf * tyf);
-        if (cos_angle >= kp.rot_thr && tsq <= kp.eps) { converged = 1; break; }
-        if (fabs(mse - prev_mse) < kp.mse_abs) { converged = 1; break; }
-        prev_mse = mse;
+#ifdef DPG_ICP_STATS
+        {
+            ICP_STAMP(c4);
+            ph[0] += c1 - c0; ph[1] += c2 - c1; ph[2] += c3 - c2; ph[3] += c4 - c3; ++nit;
+        }
+#endif
+        if (code == 1) { converged = 1; break; }
+        __syncthreads();   // moved source complete before the next reciprocal tests
     }
+#ifdef DPG_ICP_STATS
+    if (lane == 0) {
+        ICP_STAT(8, ph[0]); ICP_STAT(9, ph[1]); ICP_STAT(10, ph[2]); ICP_STAT(11, ph[3]); ICP_STAT(12, nit);
+    }
+#endif
     if (t == 0) {
+        const Bcast B = *L.bc;   // on a too-few stop: the transform, MSE of the last fitted iteration
+        for (int q = 0; q < 6; ++q) F[q] = B.F[q];
+        const int last_cnt = B.cnt;
+        const double last_mse = B.mse;
         dpg_icp_result R;
 #pragma unroll
         for (int q = 0; q < 6; ++q) R.T[q] = F[q];
@@ -451,32 +612,23 @@ __global__ __launch_bounds__(kT) void icp_ang_kernel(const float2* __restrict__ 
     }
 }
 
+
 }  // namespace
 
 extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 
 #ifdef DPG_ICP_STATS
 extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        unsigned long long z[16] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_icp_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
 }
 #endif
 
-extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) {
-    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
-    size_t o = 0;
-    o = al(o + 16 * (size_t)cap);
-    o = al(o + 16 * (size_t)cap);
-    o = al(o + 2 * (size_t)cap);
-    o = al(o + 2 * (size_t)(kB + 1));
-    o = al(o + 2 * (size_t)(kB + 1));
-    o += sizeof(double) * kW * (kSums + 2);
-    return al(o);
-}
+extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) { return ang_lds_layout(cap, nullptr); }
 
 extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                                       int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
@@ -485,7 +637,7 @@ extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds
     int cap = 1;
     while (cap < max_points) cap <<= 1;
     if (cap > 4096) return DPG_ERR_SIZE;
-    hipLaunchKernelGGL(angle_index_kernel, dim3((unsigned)n_nodes), dim3(kT), 8 * (size_t)cap,
+    hipLaunchKernelGGL(angle_index_kernel, dim3((unsigned)n_nodes), dim3(kTI), 8 * (size_t)cap,
                        reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(ds_pts_dev), ds_off_dev,
                        reinterpret_cast<float2*>(idx_pts_dev), idx_orig_dev, buckets_dev);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
@@ -495,7 +647,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
                                   const uint16_t* buckets_dev, const dpg_icp_edge* edges_dev, int64_t n_edges, const dpg_icp_kparams* kp,
                                   int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* stream) {
     if (n_edges <= 0) return DPG_OK;
-    if (max_points > kp->lds_tgt || kp->lds_tgt > 4096 || (kp->lds_tgt & (kp->lds_tgt - 1))) return DPG_ERR_SIZE;
+    if (max_points > kp->lds_tgt || kp->lds_tgt > 4096) return DPG_ERR_SIZE;
     const size_t lds = dpg_icp_ang_lds_bytes(kp->lds_tgt);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const dim3 grid((unsigned)n_edges), block(kT);
@@ -509,7 +661,6 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     else if (ppt <= 2) DPG_ANG_LAUNCH(2);
     else if (ppt <= 4) DPG_ANG_LAUNCH(4);
     else if (ppt <= 8) DPG_ANG_LAUNCH(8);
-    else if (ppt <= 16) DPG_ANG_LAUNCH(16);
     else return DPG_ERR_SIZE;
 #undef DPG_ANG_LAUNCH
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;

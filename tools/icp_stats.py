@@ -15,7 +15,7 @@ w = synth.generate(sys.argv[1] if len(sys.argv) > 1 else "config4")
 p = _abi.default_icp_params()
 L = _abi.lib()
 L.dpg_icp_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-st = (C.c_ulonglong * 8)()
+st = (C.c_ulonglong * 16)()
 with api.Context(0) as ctx:
     ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
     ctx.icp_prepare(w.edges, w.est, p)
@@ -30,5 +30,12 @@ print(f"edges {len(it)}  iterations mean {it.mean():.2f} p50 {np.median(it):.0f}
       f"  sum {it.sum()}")
 print(f"point-iterations {s[0]}  correspondences {s[5]} ({s[5] / s[0]:.2%})  no fwd match {s[6]} ({s[6] / s[0]:.2%})"
       f"  full-scan windows {s[7]}")
-print(f"forward: candidates/point {s[1] / s[0]:.1f}  wave trips/point-slot {2 * s[2] * 64 / s[0]:.1f} (2 cand/trip)")
-print(f"reciprocal: candidates/matched {s[3] / max(1, s[5]):.1f}  wave trips/point-slot {2 * s[4] * 64 / s[0]:.1f}")
+KU = 4   # candidates per wave trip (dpg_icp_ang.hip kU)
+print(f"forward: candidates/point {s[1] / s[0]:.1f}  wave-level candidates/point-slot {KU * s[2] * 64 / s[0]:.1f}")
+print(f"reciprocal: candidates/matched {s[3] / max(1, s[5]):.1f}  wave-level candidates/point-slot {KU * s[4] * 64 / s[0]:.1f}")
+tot = sum(s[8:12])
+if s[12]:
+    names = ["search", "search barrier wait", "sums+fold+wait", "fit+update+wait"]
+    print(f"per wave-iteration clock (s_memtime ticks, {s[12]} wave-iterations):")
+    for n, v in zip(names, s[8:12]):
+        print(f"  {n:22s} {v / s[12]:9.0f}  ({v / tot:.1%})")
