@@ -20,8 +20,8 @@
 //     pair with d <= r^2 does an LDS 64-bit atomicMin of (bits(d) << 32 | i) on the target's
 //     key -- afterwards key[j] is the (distance, lowest index) argmin over the sources near j,
 //     i.e. the reverse 1-NN, and (i, j) is reciprocal iff key[j] == (bits(d_ij) << 32 | i);
-//   * the rigid-fit sums are fp64 in a FIXED 256-lane tree (wave shuffles, then
-//     (W0 + W1) + (W2 + W3)) that the CPU oracle replays, so transforms -- and therefore all
+//   * the rigid-fit sums are fp64 in the FIXED 512-lane tree of dpg_icp_tree.h (a 256-thread
+//     workgroup carries lanes t and t + 256) that the CPU oracle replays, so transforms -- and therefore all
 //     later correspondences -- are bit-identical to the oracle;
 //   * every lane redundantly combines the 4 wave partials and evaluates the closed-form fit and
 //     the convergence rule, so one iteration costs two workgroup barriers.
@@ -32,10 +32,11 @@
 #include <stdint.h>
 
 #include "dpg_internal.h"
+#include "dpg_icp_tree.h"
 
 namespace {
 
-constexpr int kThreads = 256;  // == DPG_ICP_LANES
+constexpr int kThreads = 256;  // DPG_ICP_LANES / 2: thread t carries tree lanes t and t + 256
 constexpr int kWaves = kThreads / 64;
 constexpr int kSums = 10;      // cnt, d, px, py, qx, qy, xx, xy, yx, yy
 
@@ -48,7 +49,7 @@ struct Lds {
     uint64_t* key1;    // [lds_tgt] odd iterations
     uint32_t* cells;   // [cells_max + 1] counts -> exclusive starts
     uint16_t* tidx;    // [lds_tgt] original target index of tp[k]
-    double* wpart;     // [kWaves][kSums + 2]
+    double* wpart;     // [2 * kWaves][kSums + 2] (tree waves)
     float* fctl;       // [16]
 };
 
@@ -62,7 +63,7 @@ __device__ Lds carve(unsigned char* base, int lds_tgt, int cells_max) {
     L.key1 = reinterpret_cast<uint64_t*>(base + o);   o = align16(o + sizeof(uint64_t) * lds_tgt);
     L.cells = reinterpret_cast<uint32_t*>(base + o);  o = align16(o + sizeof(uint32_t) * (cells_max + 1));
     L.tidx = reinterpret_cast<uint16_t*>(base + o);   o = align16(o + sizeof(uint16_t) * lds_tgt);
-    L.wpart = reinterpret_cast<double*>(base + o);    o = align16(o + sizeof(double) * kWaves * (kSums + 2));
+    L.wpart = reinterpret_cast<double*>(base + o);    o = align16(o + sizeof(double) * 2 * kWaves * (kSums + 2));
     L.fctl = reinterpret_cast<float*>(base + o);
     return L;
 }
@@ -242,10 +243,10 @@ __global__ __launch_bounds__(kThreads) void icp_edges_kernel(const float2* __res
             }
         }
         __syncthreads();
-        // ---- acceptance + fp64 lane sums (lane-ordered: m ascending) ----
-        double acc[kSums];
+        // ---- acceptance + fp64 lane sums: point i = t + 256 m goes to tree lane t + 256 (m & 1) ----
+        double acc[2][kSums];
 #pragma unroll
-        for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
+        for (int q = 0; q < kSums; ++q) acc[0][q] = acc[1][q] = 0.0;
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
             const int i = t + kThreads * m;
@@ -253,36 +254,22 @@ __global__ __launch_bounds__(kThreads) void icp_edges_kernel(const float2* __res
             if (ok && kp.reciprocal) ok = (key[bi[m]] == rev_key(bd[m], i));
             if (trace && k < kp.trace_iters && i < N)
                 trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi[m] : -1;
-            if (ok) {
-                const double px = sx[m], py = sy[m], qx = bx[m], qy = by[m];
-                acc[0] = acc[0] + 1.0;
-                acc[1] = acc[1] + (double)bd[m];
-                acc[2] = acc[2] + px;
-                acc[3] = acc[3] + py;
-                acc[4] = acc[4] + qx;
-                acc[5] = acc[5] + qy;
-                acc[6] = acc[6] + px * qx;
-                acc[7] = acc[7] + px * qy;
-                acc[8] = acc[8] + py * qx;
-                acc[9] = acc[9] + py * qy;
-            }
+            if (ok) dpg_tree::add_pair(acc[m & 1], sx[m], sy[m], bx[m], by[m], bd[m]);
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-            for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + shfl_down_d(acc[q], off);
-        }
+        dpg_tree::wave_fold(acc[0]);
+        dpg_tree::wave_fold(acc[1]);
         if (lane == 0) {
 #pragma unroll
-            for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
+            for (int q = 0; q < kSums; ++q) {
+                L.wpart[wave * (kSums + 2) + q] = acc[0][q];
+                L.wpart[(wave + kWaves) * (kSums + 2) + q] = acc[1][q];
+            }
         }
         __syncthreads();
-        // ---- every lane: combine (W0 + W1) + (W2 + W3), fit, converge (uniform control flow) ----
+        // ---- every lane: combine the eight tree waves, fit, converge (uniform control flow) ----
         double S[kSums];
 #pragma unroll
-        for (int q = 0; q < kSums; ++q)
-            S[q] = (L.wpart[0 * (kSums + 2) + q] + L.wpart[1 * (kSums + 2) + q]) +
-                   (L.wpart[2 * (kSums + 2) + q] + L.wpart[3 * (kSums + 2) + q]);
+        for (int q = 0; q < kSums; ++q) S[q] = dpg_tree::combine(L.wpart, kSums + 2, q);
         // this iteration's key buffer is free again: reset the entries this lane owns
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
@@ -403,7 +390,7 @@ extern "C" size_t dpg_icp_lds_bytes(int32_t lds_tgt, int32_t cells_max) {
     o = a16(o + sizeof(uint64_t) * lds_tgt);
     o = a16(o + sizeof(uint32_t) * (cells_max + 1));
     o = a16(o + sizeof(uint16_t) * lds_tgt);
-    o = a16(o + sizeof(double) * kWaves * (kSums + 2));
+    o = a16(o + sizeof(double) * 2 * kWaves * (kSums + 2));
     o += sizeof(float) * 16;
     return a16(o);
 }

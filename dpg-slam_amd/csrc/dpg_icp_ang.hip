@@ -19,7 +19,7 @@
 //     reciprocal test: radius query in the SOURCE index (source node frame, static) around
 //       F_k^-1 t_j with radius sqrt(d_ij) + drift_k, candidates re-checked in exact float on their
 //       CURRENT coordinates (see dpg_icp_kd.hip for the drift argument);
-//     rigid fit + convergence exactly as the other variants (fp64 256-lane fixed tree).
+//     rigid fit + convergence exactly as the other variants (fp64 512-lane fixed tree).
 // Built with -ffp-contract=off.
 
 #include <hip/hip_runtime.h>
@@ -28,15 +28,25 @@
 #include <stdint.h>
 
 #include "dpg_internal.h"
+#include "dpg_icp_tree.h"
 
-#ifdef DPG_ICP_STATS
-// diagnostics build only: [0] point-iterations, [1] forward candidates, [2] forward wave trips,
-// [3] reciprocal candidates, [4] reciprocal wave trips, [5] correspondences, [6] no forward match,
-// [7] full-scan forward windows; per-wave clock cycles (s_memtime) summed over waves and
-// iterations: [8] search, [9] wait at the search barrier, [10] sums + fold + wait, [11] fit +
-// update + wait, [12] waves x iterations
+#if defined(DPG_ICP_STATS) || defined(DPG_ICP_TIMING)
+// diagnostics builds only.  DPG_ICP_STATS (counters): [0] point-iterations, [1] forward
+// candidates, [2] forward wave trips, [3] reciprocal candidates, [4] reciprocal wave trips,
+// [5] correspondences, [6] no forward match, [7] full-scan forward windows, [13] full-scan
+// reciprocal windows, [14] sum over workgroup-iterations of the slowest wave's trips, [15] sum
+// of all waves' trips (imbalance = 8 [14] / [15]).  DPG_ICP_TIMING
+// (per-wave s_memtime cycles summed over waves and iterations, last iteration excluded):
+// [8] search, [9] sums + fold, [10] arrival + fit + publish barrier, [11] move + barrier,
+// [12] wave-iterations
+#define DPG_ICP_DIAG 1
 __device__ unsigned long long g_icp_stats[16];
-#define ICP_STAT(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
+#define ICP_STAT_ADD(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
+#endif
+#ifdef DPG_ICP_STATS
+#define ICP_STAT(k, v) ICP_STAT_ADD(k, v)
+#endif
+#ifdef DPG_ICP_TIMING
 #define ICP_STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #else
 #define ICP_STAMP(var)
@@ -46,7 +56,7 @@ namespace {
 
 constexpr int kT = 512;                         // ICP workgroup (8 waves)
 constexpr int kTI = 256;                        // index-build workgroup
-constexpr int kSums = 10;
+constexpr int kSums = dpg_tree::kSums;
 constexpr int kB = 1024;                        // pseudo-angle buckets per cloud (~1 point each)
 constexpr float kTwoPi = 6.28318530717958647692f;
 constexpr float kBucketScale = (float)kB / kTwoPi;
@@ -155,10 +165,11 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 }
 
 // Workgroup shape: kT = 512 threads (8 waves; 4 workgroups = 32 waves per CU at <= 64 VGPRs and
-// ~39 KB of LDS each), thread t owns the source points i = t + kT m during the search.  The fp64
-// sums keep the 256-lane fixed tree of DPG_ICP_LANES (oracle lane_tree): each point's match is
-// parked in the pad word of its LDS source record, then waves 0-3 accumulate lane l = i mod 256
-// over i = l, l + 256, ... in that order and fold as before.
+// ~38 KB of LDS each), thread t owns the source points i = t + kT m and is lane t of the fp64
+// reduction tree (dpg_icp_tree.h, DPG_ICP_LANES = 512): it sums its own accepted pairs right after
+// its searches, the wave folds by DPP/swizzle, and the LAST wave to arrive (LDS counter) combines
+// the eight partials, fits and decides convergence, then one barrier publishes the result.
+// Per iteration: search + sums + fold, fit by one wave, barrier, move the source, barrier.
 //
 // Candidate loops (R4) visit kU records per trip, wave-uniformly, with no per-candidate bounds
 // test: a lane whose own window is exhausted keeps evaluating the records that follow it.  That
@@ -167,12 +178,11 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 // original index) minimum, and any extra source record that beats i at t_j is a genuine
 // reciprocity violation.  Records [n, n + kU) repeat [0, kU) mod n so that a trip never wraps
 // inside itself; the trip start advances by kU mod n.
-constexpr int kLanes = 256;   // == DPG_ICP_LANES
-constexpr int kLW = kLanes / 64;
+constexpr int kWaves = kT / 64;
+static_assert(kT == dpg_tree::kLanes, "one tree lane per thread");
 constexpr int kU = 4;
-constexpr uint32_t kNoMatch = 0xffffffffu;
 
-// what wave 0 hands every wave after the fit of an iteration
+// what the fitting wave hands every wave after the fit of an iteration
 struct Bcast {
     double inv[4];   // inverse of the new 2x2 rotation block (reciprocal windows), fp64
     double mse;
@@ -194,12 +204,12 @@ __device__ __forceinline__ void inverse2(const float F[6], double inv[4]) {
 
 struct Lds {
     Rec* tp;          // target points in angle order, [cap + kU]
-    Rec* scs;         // current (moved) source points in the source's angle order, [cap + kU];
-                      // pad word = sorted target position of this iteration's match (kNoMatch)
+    Rec* scs;         // current (moved) source points in the source's angle order, [cap + kU]
     uint16_t* spos;   // source original index -> sorted position
     uint16_t* tb;     // target bucket starts [kB+1]
     uint16_t* sb;     // source bucket starts [kB+1]
-    double* wpart;    // [kLW][kSums + 2]
+    double* wpart;    // [kWaves][kSums + 2] wave partials of the tree
+    int* arrive;      // waves done with this iteration's sums
     Bcast* bc;        // wave 0's fit, read by every wave
 };
 
@@ -210,8 +220,8 @@ __host__ __device__ inline size_t ang_lds_layout(int cap, size_t* off /* [7] or 
     p[2] = o; o = (o + 2 * (size_t)cap + 15) & ~size_t(15);
     p[3] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
     p[4] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
-    p[5] = o; o = (o + sizeof(double) * kLW * (kSums + 2) + 15) & ~size_t(15);
-    p[6] = o; o = (o + sizeof(Bcast) + 15) & ~size_t(15);
+    p[5] = o; o = (o + sizeof(double) * kWaves * (kSums + 2) + 15) & ~size_t(15);
+    p[6] = o; o = (o + sizeof(Bcast) + 16 + 15) & ~size_t(15);
     if (off)
         for (int q = 0; q < 7; ++q) off[q] = p[q];
     return o;
@@ -228,6 +238,7 @@ __device__ Lds carve(unsigned char* base, int cap) {
     L.sb = reinterpret_cast<uint16_t*>(base + p[4]);
     L.wpart = reinterpret_cast<double*>(base + p[5]);
     L.bc = reinterpret_cast<Bcast*>(base + p[6]);
+    L.arrive = reinterpret_cast<int*>(base + p[6] + ((sizeof(Bcast) + 15) & ~size_t(15)));
     return L;
 }
 
@@ -311,6 +322,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     const int N = E.n_src_ds, M = E.n_tgt_ds;
     const int vt = E.tgt_node, vs = E.src_node;
     const int cap = kp.lds_tgt;
+#ifdef DPG_ICP_STATS
+    __shared__ unsigned st_wmax;
+    if (t == 0) st_wmax = 0;
+#endif
     const int stepM = M > 0 ? kU % M : 0, stepN = N > 0 ? kU % N : 0;
     Lds L = carve(smem, cap);
     // sorted target + the kU repeated records after it
@@ -323,7 +338,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
         const int p = s < N ? s : (s - N) % N;
         const uint16_t o = idx_orig[E.src_ds_off + p];
         L.scs[s].key = ((uint32_t)o << 16) | (uint32_t)p;
-        L.scs[s].pad = kNoMatch;
+        L.scs[s].pad = 0u;
         if (s < N) L.spos[o] = (uint16_t)s;
     }
     for (int b = t; b <= kB; b += kT) {
@@ -344,6 +359,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
         B.code = 0;
         B.cnt = 0;
         *L.bc = B;
+        *L.arrive = 0;
     }
     __syncthreads();
     float sx[PPT], sy[PPT];
@@ -378,7 +394,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     const float r2f = kp.r2_f;
     const float rmax = sqrtf(r2f) * 1.0001f + 1e-5f;
     int k = 0, converged = 0, status = DPG_ICP_OK;
-#ifdef DPG_ICP_STATS
+#ifdef DPG_ICP_TIMING
     unsigned long long ph[4] = {0, 0, 0, 0}, nit = 0;
 #endif
     for (;;) {
@@ -387,6 +403,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
         const double i10 = uni(L.bc->inv[2]), i11 = uni(L.bc->inv[3]);
         const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
         const float drift = 1e-4f + 5e-5f * (float)(k + 1);
+        uint32_t okm = 0;   // bit m: point t + 512 m has a (reciprocal) correspondence
+#ifdef DPG_ICP_STATS
+        unsigned wtrips = 0;
+#endif
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
             // every lane runs every trip (dead lanes included): the candidate loops are
@@ -414,6 +434,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
                     for (int c = 0; __any(c < fc); c += kU) ++trips;
                     if (live) { ICP_STAT(0, 1); ICP_STAT(1, fc); if (fc >= M) ICP_STAT(7, 1); }
                     if (lane == 0) ICP_STAT(2, trips);
+                    wtrips += trips;
                 }
 #endif
                 for (int c = 0; __any(c < fc); c += kU) {   // exact (d, original index) argmin
@@ -451,9 +472,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
                 {
                     int trips = 0;
                     for (int c = 0; __any(ok & (c < rc)); c += kU) ++trips;
-                    if (ok) ICP_STAT(3, rc);
+                    if (ok) { ICP_STAT(3, rc); if (rc >= N) ICP_STAT(13, 1); }
                     if (live && !ok) ICP_STAT(6, 1);
                     if (lane == 0) ICP_STAT(4, trips);
+                    wtrips += trips;
                 }
 #endif
                 for (int c = 0; __any(ok & (c < rc)); c += kU) {
@@ -474,53 +496,42 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 #endif
             if (live && trace && k < kp.trace_iters)
                 trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
-            if (live) L.scs[sp[m]].pad = ok ? (uint32_t)bp : kNoMatch;
+            okm |= (ok ? 1u : 0u) << m;
         }
         ICP_STAMP(c1);
-        __syncthreads();
-        ICP_STAMP(c2);
-        // ---- R5 sums: the 256-lane fixed tree over the parked matches (waves 0-3) ----
-        if (t < kLanes) {
+        // ---- R5 sums: this thread is tree lane t (points t + 512 m, m ascending) ----
+        {
             double acc[kSums];
 #pragma unroll
             for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
-            for (int i = t; i < N; i += kLanes) {
-                const Rec sr = ld_rec(L.scs + L.spos[i]);
-                if (sr.pad != kNoMatch) {
-                    const Rec tq = ld_rec(L.tp + sr.pad);
-                    const float d = sqd(sr.x, sr.y, tq.x, tq.y);   // == the forward search's d
-                    const double px = sr.x, py = sr.y, tx = tq.x, ty = tq.y;
-                    acc[0] = acc[0] + 1.0;
-                    acc[1] = acc[1] + (double)d;
-                    acc[2] = acc[2] + px;
-                    acc[3] = acc[3] + py;
-                    acc[4] = acc[4] + tx;
-                    acc[5] = acc[5] + ty;
-                    acc[6] = acc[6] + px * tx;
-                    acc[7] = acc[7] + px * ty;
-                    acc[8] = acc[8] + py * tx;
-                    acc[9] = acc[9] + py * ty;
+#pragma unroll
+            for (int m = 0; m < PPT; ++m) {
+                if ((okm >> m) & 1u) {
+                    const Rec tq = ld_rec(L.tp + seed[m]);
+                    dpg_tree::add_pair(acc, sx[m], sy[m], tq.x, tq.y, sqd(sx[m], sy[m], tq.x, tq.y));
                 }
             }
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-                for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + __shfl_down(acc[q], off, 64);
-            }
+            dpg_tree::wave_fold(acc);
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
             }
         }
-        __syncthreads();
-        ICP_STAMP(c3);
-        // ---- R5 fit + R6 convergence, once per workgroup (wave 0), broadcast through LDS ----
-        if (wave == 0) {
+        ICP_STAMP(c2);
+        // ---- the last wave to arrive combines the partials, fits (R5) and decides (R6) ----
+        int last = 0;
+#ifdef DPG_ICP_STATS
+        if (lane == 0) { atomicMax(&st_wmax, wtrips); ICP_STAT(15, wtrips); }
+#endif
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            last = atomicAdd(L.arrive, 1) == kWaves - 1;
+            if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        if (__builtin_amdgcn_readlane(last, 0)) {
             double S[kSums];
 #pragma unroll
-            for (int q = 0; q < kSums; ++q)
-                S[q] = uni((L.wpart[0 * (kSums + 2) + q] + L.wpart[1 * (kSums + 2) + q]) +
-                           (L.wpart[2 * (kSums + 2) + q] + L.wpart[3 * (kSums + 2) + q]));
+            for (int q = 0; q < kSums; ++q) S[q] = uni(dpg_tree::combine(L.wpart, kSums + 2, q));
             Bcast B = *L.bc;
             float F[6];
 #pragma unroll
@@ -561,9 +572,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
                 B.prev_mse = mse;
                 inverse2(Nf, B.inv);
             }
-            if (lane == 0) *L.bc = B;
+            if (lane == 0) {
+                *L.bc = B;
+                *L.arrive = 0;
+#ifdef DPG_ICP_STATS
+                ICP_STAT(14, st_wmax);
+                st_wmax = 0;
+#endif
+            }
         }
         __syncthreads();
+        ICP_STAMP(c3);
         const int code = __builtin_amdgcn_readfirstlane(L.bc->code);
         if (code == 2) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
         const float cf = uni(L.bc->r[0]), sf = uni(L.bc->r[1]), txf = uni(L.bc->r[2]), tyf = uni(L.bc->r[3]);
@@ -577,18 +596,19 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
             if (i < N) put(m);
         }
         ++k;
-#ifdef DPG_ICP_STATS
+        if (code == 1) { converged = 1; break; }
+        __syncthreads();   // moved source complete before the next reciprocal tests
+#ifdef DPG_ICP_TIMING
         {
             ICP_STAMP(c4);
             ph[0] += c1 - c0; ph[1] += c2 - c1; ph[2] += c3 - c2; ph[3] += c4 - c3; ++nit;
         }
 #endif
-        if (code == 1) { converged = 1; break; }
-        __syncthreads();   // moved source complete before the next reciprocal tests
     }
-#ifdef DPG_ICP_STATS
+#ifdef DPG_ICP_TIMING
     if (lane == 0) {
-        ICP_STAT(8, ph[0]); ICP_STAT(9, ph[1]); ICP_STAT(10, ph[2]); ICP_STAT(11, ph[3]); ICP_STAT(12, nit);
+        ICP_STAT_ADD(8, ph[0]); ICP_STAT_ADD(9, ph[1]); ICP_STAT_ADD(10, ph[2]); ICP_STAT_ADD(11, ph[3]);
+        ICP_STAT_ADD(12, nit);
     }
 #endif
     if (t == 0) {
@@ -617,7 +637,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 
 extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 
-#ifdef DPG_ICP_STATS
+#ifdef DPG_ICP_DIAG
 extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {

@@ -17,7 +17,7 @@
 //        to target j than the matched i" is a radius query of sqrt(d_ij) + delta_k around
 //        F_k^-1 t_j in that static tree, with every candidate re-checked in exact float on its
 //        CURRENT coordinates;
-//      rigid fit + convergence exactly as dpg_icp.hip (fp64 256-lane tree shared with the oracle).
+//      rigid fit + convergence exactly as dpg_icp.hip (fp64 512-lane tree of dpg_icp_tree.h, shared with the oracle).
 // Built with -ffp-contract=off.
 
 #include <hip/hip_runtime.h>
@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include "dpg_internal.h"
+#include "dpg_icp_tree.h"
 
 namespace {
 
@@ -133,7 +134,7 @@ struct Lds {
     float2* sc;       // current (moved) source points, original order
     uint16_t* ti;     // target tree -> original index
     uint16_t* si;     // source tree -> original index
-    double* wpart;    // [kW][kSums + 2]
+    double* wpart;    // [2 * kW][kSums + 2] (tree waves)
 };
 
 __device__ __forceinline__ size_t a16(size_t x) { return (x + 15) & ~size_t(15); }
@@ -205,9 +206,9 @@ __global__ __launch_bounds__(kT) void icp_kd_kernel(const float2* __restrict__ d
         const double i00 = (double)F[4] / det, i01 = -(double)F[1] / det;
         const double i10 = -(double)F[3] / det, i11 = (double)F[0] / det;
         const float drift = 1e-4f + 5e-5f * (float)(k + 1);
-        double acc[kSums];
+        double acc[2][kSums];   // point i = t + 256 m -> tree lane t + 256 (m & 1)
 #pragma unroll
-        for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
+        for (int q = 0; q < kSums; ++q) acc[0][q] = acc[1][q] = 0.0;
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
             const int i = t + kT * m;
@@ -282,34 +283,22 @@ __global__ __launch_bounds__(kT) void icp_kd_kernel(const float2* __restrict__ d
             if (trace && k < kp.trace_iters) trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
             if (ok) {
                 const float2 tq = L.tp[bp];
-                const double px = qx, py = qy, tx = tq.x, ty = tq.y;
-                acc[0] = acc[0] + 1.0;
-                acc[1] = acc[1] + (double)bd;
-                acc[2] = acc[2] + px;
-                acc[3] = acc[3] + py;
-                acc[4] = acc[4] + tx;
-                acc[5] = acc[5] + ty;
-                acc[6] = acc[6] + px * tx;
-                acc[7] = acc[7] + px * ty;
-                acc[8] = acc[8] + py * tx;
-                acc[9] = acc[9] + py * ty;
+                dpg_tree::add_pair(acc[m & 1], qx, qy, tq.x, tq.y, bd);
             }
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-            for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + __shfl_down(acc[q], off, 64);
-        }
+        dpg_tree::wave_fold(acc[0]);
+        dpg_tree::wave_fold(acc[1]);
         if (lane == 0) {
 #pragma unroll
-            for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
+            for (int q = 0; q < kSums; ++q) {
+                L.wpart[wave * (kSums + 2) + q] = acc[0][q];
+                L.wpart[(wave + kW) * (kSums + 2) + q] = acc[1][q];
+            }
         }
         __syncthreads();
         double S[kSums];
 #pragma unroll
-        for (int q = 0; q < kSums; ++q)
-            S[q] = (L.wpart[0 * (kSums + 2) + q] + L.wpart[1 * (kSums + 2) + q]) +
-                   (L.wpart[2 * (kSums + 2) + q] + L.wpart[3 * (kSums + 2) + q]);
+        for (int q = 0; q < kSums; ++q) S[q] = dpg_tree::combine(L.wpart, kSums + 2, q);
         const int cnt = (int)S[0];
         last_cnt = cnt;
         if (cnt < kp.min_corr) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
@@ -380,7 +369,7 @@ extern "C" size_t dpg_icp_kd_lds_bytes(int32_t cap) {
     o = al(o + 8 * (size_t)cap);
     o = al(o + 2 * (size_t)cap);
     o = al(o + 2 * (size_t)cap);
-    o += sizeof(double) * kW * (kSums + 2);
+    o += sizeof(double) * 2 * kW * (kSums + 2);
     return al(o);
 }
 

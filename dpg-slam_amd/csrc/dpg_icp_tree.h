@@ -1,0 +1,79 @@
+// dpg_icp_tree.h -- the fixed fp64 reduction tree of the ICP rigid-fit sums (R5), shared by the
+// three ICP kernels and restated by the CPU oracle (oracle/dpg_oracle.c lane_tree).
+//
+// The tree (DPG_ICP_LANES = 512 lanes = 8 waves of 64):
+//   * lane l accumulates the accepted pairs of the source points i with i mod 512 == l, in
+//     ascending i, starting from 0.0;
+//   * inside each wave, for off = 32, 16, 8, 4, 2, 1: acc[k] = acc[k] + acc[k + off] (k < off);
+//     lane 0 then holds the wave partial W_w;
+//   * S = ((W0 + W1) + (W2 + W3)) + ((W4 + W5) + (W6 + W7)).
+// Any fixed tree gives the same result on every run; this one costs the GPU one DPP/swizzle/
+// bpermute step per level and nothing in LDS.  (PCL's Umeyama sums in float in its own order,
+// which is unpinned -- SURVEY §8a R5.)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dpg_tree {
+
+constexpr int kSums = 10;       // cnt, d, px, py, qx, qy, xx, xy, yx, yy
+constexpr int kLanes = 512;     // == DPG_ICP_LANES
+constexpr int kWaves = kLanes / 64;
+
+// lane k (< off) receives lane k + off's value; other lanes' results are never used
+template <int OFF>
+__device__ __forceinline__ double down(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    int lo = (int)(uint32_t)b, hi = (int)(uint32_t)(b >> 32);
+    if constexpr (OFF == 32) {
+        lo = __shfl_down(lo, 32, 64);
+        hi = __shfl_down(hi, 32, 64);
+    } else if constexpr (OFF == 16) {   // ds_swizzle, bit mode: lane ^ 16 inside each 32-lane half
+        lo = __builtin_amdgcn_ds_swizzle(lo, 0x401F);
+        hi = __builtin_amdgcn_ds_swizzle(hi, 0x401F);
+    } else {                            // DPP row_shl:OFF (lane k reads lane k + OFF of its row)
+        lo = __builtin_amdgcn_update_dpp(0, lo, 0x100 + OFF, 0xF, 0xF, false);
+        hi = __builtin_amdgcn_update_dpp(0, hi, 0x100 + OFF, 0xF, 0xF, false);
+    }
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+// the in-wave part of the tree: lane 0 ends with W_w
+__device__ __forceinline__ void wave_fold(double (&acc)[kSums]) {
+#pragma unroll
+    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<32>(acc[q]);
+#pragma unroll
+    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<16>(acc[q]);
+#pragma unroll
+    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<8>(acc[q]);
+#pragma unroll
+    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<4>(acc[q]);
+#pragma unroll
+    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<2>(acc[q]);
+#pragma unroll
+    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<1>(acc[q]);
+}
+
+// the cross-wave part: W[w * stride + q] -> S[q]
+__device__ __forceinline__ double combine(const double* W, int stride, int q) {
+    return ((W[0 * stride + q] + W[1 * stride + q]) + (W[2 * stride + q] + W[3 * stride + q])) +
+           ((W[4 * stride + q] + W[5 * stride + q]) + (W[6 * stride + q] + W[7 * stride + q]));
+}
+
+// one accepted pair (source p moved, target q, fp32 squared distance d) into a lane's sums
+__device__ __forceinline__ void add_pair(double (&acc)[kSums], float sx, float sy, float tx, float ty, float d) {
+    const double px = sx, py = sy, qx = tx, qy = ty;
+    acc[0] = acc[0] + 1.0;
+    acc[1] = acc[1] + (double)d;
+    acc[2] = acc[2] + px;
+    acc[3] = acc[3] + py;
+    acc[4] = acc[4] + qx;
+    acc[5] = acc[5] + qy;
+    acc[6] = acc[6] + px * qx;
+    acc[7] = acc[7] + px * qy;
+    acc[8] = acc[8] + py * qx;
+    acc[9] = acc[9] + py * qy;
+}
+
+}  // namespace dpg_tree

@@ -19,7 +19,7 @@ DPG_FACTOR_PRIOR = 0
 DPG_FACTOR_BETWEEN = 1
 DPG_ICP_OK = 0
 DPG_ICP_TOO_FEW_CORR = 1
-DPG_ICP_LANES = 256
+DPG_ICP_LANES = 512
 
 
 class IcpParams(C.Structure):

@@ -33,10 +33,10 @@ extern "C" {
 #define DPG_ERR_NUMERIC (-5)
 
 /* Fixed reduction geometry of the ICP rigid fit (part of the algorithm's definition so that
- * CPU oracle and GPU agree bit for bit): lane l accumulates source points l, l+256, ... in
+ * CPU oracle and GPU agree bit for bit): lane l accumulates source points l, l+512, ... in
  * increasing order (fp64); each 64-lane wave folds acc[k] += acc[k + off], off = 32 ... 1, and
- * the four wave totals combine as (W0 + W1) + (W2 + W3). */
-#define DPG_ICP_LANES 256
+ * the eight wave totals combine as ((W0 + W1) + (W2 + W3)) + ((W4 + W5) + (W6 + W7)). */
+#define DPG_ICP_LANES 512
 
 /* ICP parameters: field names follow PoseGraphParameters (src/dpg_slam/parameters.h:105-141,
  * defaults :146,159,173,191,201,374,385,396,402) plus the PCL defaults the reference inherits

@@ -7,7 +7,7 @@
  *   R2  downsamplePointCloud               dpg_slam.cc:346-360
  *   R3  runIcp guess                       dpg_slam.cc:364-378; math_utils.cc:21-35
  *   R4  PCL determineReciprocalCorrespondences + KdTreeFLANN 1-NN (lowest-index tie rule)
- *   R5  PCL TransformationEstimationSVD/umeyama -> planar closed form, 256-lane fp64 tree
+ *   R5  PCL TransformationEstimationSVD/umeyama -> planar closed form, 512-lane fp64 tree
  *   R6  PCL ICP loop + DefaultConvergenceCriteria
  *   R7  calculate_ICP_COV                  cov_func_point_to_point.h:24-31,45-283,572-575
  *   R8  runIcp epilogue                    dpg_slam.cc:416-445
@@ -211,18 +211,20 @@ static void nn_grid(const grid_t* g, const float* pts, float qx, float qy, int32
 
 enum { S_CNT = 0, S_D, S_PX, S_PY, S_QX, S_QY, S_XX, S_XY, S_YX, S_YY, S_N };
 
-/* The 256-lane fixed reduction (DPG_ICP_LANES = 4 waves x 64 lanes): inside each 64-lane wave
- * acc[k] += acc[k + off] for off = 32, 16, ..., 1; then (W0 + W1) + (W2 + W3). */
+/* The 512-lane fixed reduction (DPG_ICP_LANES = 8 waves x 64 lanes, include/dpg_slam_c.h):
+ * inside each 64-lane wave acc[k] += acc[k + off] for off = 32, 16, ..., 1; then
+ * ((W0 + W1) + (W2 + W3)) + ((W4 + W5) + (W6 + W7)).  GPU side: csrc/dpg_icp_tree.h. */
 static void lane_tree(double acc[DPG_ICP_LANES][S_N], double out[S_N]) {
-    double W[4][S_N];
-    for (int w = 0; w < 4; ++w) {
+    double W[8][S_N];
+    for (int w = 0; w < 8; ++w) {
         double (*a)[S_N] = acc + 64 * w;
         for (int off = 32; off >= 1; off >>= 1)
             for (int k = 0; k < off; ++k)
                 for (int q = 0; q < S_N; ++q) a[k][q] = a[k][q] + a[k + off][q];
         for (int q = 0; q < S_N; ++q) W[w][q] = a[0][q];
     }
-    for (int q = 0; q < S_N; ++q) out[q] = (W[0][q] + W[1][q]) + (W[2][q] + W[3][q]);
+    for (int q = 0; q < S_N; ++q)
+        out[q] = ((W[0][q] + W[1][q]) + (W[2][q] + W[3][q])) + ((W[4][q] + W[5][q]) + (W[6][q] + W[7][q]));
 }
 
 /* Planar rigid fit from the reduced sums; returns (c, s, tx, ty) rounded to float. */
@@ -302,7 +304,7 @@ int oracle_icp_align(const float* src_in, int64_t n_src, const float* tgt, int64
             status = DPG_ICP_TOO_FEW_CORR;
             break;
         }
-        /* R5: sums over accepted pairs, 256-lane tree */
+        /* R5: sums over accepted pairs, 512-lane tree */
         memset(acc, 0, sizeof(double) * DPG_ICP_LANES * S_N);
         for (int64_t i = 0; i < n_src; ++i) {
             if (fwd[i] < 0) continue;

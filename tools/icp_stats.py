@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""ICP candidate statistics on config4 (diagnostics build lib/libdpg_stats.so, GPU):
-   DPGSLAM_LIB=dpg-slam_amd/lib/libdpg_stats.so python tools/icp_stats.py"""
+"""ICP diagnostics on config4 (GPU): candidate counters with the lib/libdpg_stats.so build,
+per-phase clock with the lib/libdpg_timing.so build:
+   DPGSLAM_LIB=dpg-slam_amd/lib/libdpg_stats.so python tools/icp_stats.py
+   DPGSLAM_LIB=dpg-slam_amd/lib/libdpg_timing.so python tools/icp_stats.py"""
 import ctypes as C
 import os
 import sys
@@ -28,14 +30,16 @@ it = res["iterations"]
 s = list(st)
 print(f"edges {len(it)}  iterations mean {it.mean():.2f} p50 {np.median(it):.0f} p99 {np.percentile(it, 99):.0f} max {it.max()}"
       f"  sum {it.sum()}")
-print(f"point-iterations {s[0]}  correspondences {s[5]} ({s[5] / s[0]:.2%})  no fwd match {s[6]} ({s[6] / s[0]:.2%})"
+if s[0]:
+  print(f"point-iterations {s[0]}  correspondences {s[5]} ({s[5] / s[0]:.2%})  no fwd match {s[6]} ({s[6] / s[0]:.2%})"
       f"  full-scan windows {s[7]}")
-KU = 4   # candidates per wave trip (dpg_icp_ang.hip kU)
-print(f"forward: candidates/point {s[1] / s[0]:.1f}  wave-level candidates/point-slot {KU * s[2] * 64 / s[0]:.1f}")
-print(f"reciprocal: candidates/matched {s[3] / max(1, s[5]):.1f}  wave-level candidates/point-slot {KU * s[4] * 64 / s[0]:.1f}")
+  KU = 4   # candidates per wave trip (dpg_icp_ang.hip kU)
+  print(f"forward: candidates/point {s[1] / s[0]:.1f}  wave-level candidates/point-slot {KU * s[2] * 64 / s[0]:.1f}")
+  print(f"full-scan reciprocal windows {s[13]}  wave imbalance (slowest wave trips x 8 / all trips) {8 * s[14] / max(1, s[15]):.2f}")
+  print(f"reciprocal: candidates/matched {s[3] / max(1, s[5]):.1f}  wave-level candidates/point-slot {KU * s[4] * 64 / s[0]:.1f}")
 tot = sum(s[8:12])
 if s[12]:
-    names = ["search", "search barrier wait", "sums+fold+wait", "fit+update+wait"]
+    names = ["search", "sums+fold", "arrive+fit+barrier", "move+barrier"]
     print(f"per wave-iteration clock (s_memtime ticks, {s[12]} wave-iterations):")
     for n, v in zip(names, s[8:12]):
         print(f"  {n:22s} {v / s[12]:9.0f}  ({v / tot:.1%})")
