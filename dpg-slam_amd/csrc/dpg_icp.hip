@@ -38,7 +38,7 @@ namespace {
 
 constexpr int kThreads = 256;  // DPG_ICP_LANES / 2: thread t carries tree lanes t and t + 256
 constexpr int kWaves = kThreads / 64;
-constexpr int kSums = 10;      // cnt, d, px, py, qx, qy, xx, xy, yx, yy
+constexpr int kSums = dpg_tree::kSums;
 
 __device__ __forceinline__ double shfl_down_d(double v, int off) { return __shfl_down(v, off, 64); }
 __device__ __forceinline__ float shfl_xor_f(float v, int off) { return __shfl_xor(v, off, 64); }
@@ -281,8 +281,8 @@ __global__ __launch_bounds__(kThreads) void icp_edges_kernel(const float2* __res
         if (cnt < kp.min_corr) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
         // R5 planar closed form (see oracle rigid_from_sums)
         const double n = S[0];
-        const double a = (S[6] + S[9]) - (S[2] * S[4] + S[3] * S[5]) / n;
-        const double b = (S[7] - S[8]) - (S[2] * S[5] - S[3] * S[4]) / n;
+        double a, b;
+        dpg_tree::fit_ab(S, a, b);
         const double hh = sqrt(a * a + b * b);
         double c = 1.0, s = 0.0;
         if (hh > 0.0) { c = a / hh; s = b / hh; }

@@ -181,6 +181,9 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 constexpr int kWaves = kT / 64;
 static_assert(kT == dpg_tree::kLanes, "one tree lane per thread");
 constexpr int kU = 4;
+// an unmatched point searches kClear beyond r once; while the distance it has moved since stays
+// below the margin found, it provably has no target within r and skips its forward search
+constexpr float kClear = 0.1f;
 
 // what the fitting wave hands every wave after the fit of an iteration
 struct Bcast {
@@ -393,14 +396,16 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
 
     const float r2f = kp.r2_f;
     const float rmax = sqrtf(r2f) * 1.0001f + 1e-5f;
+    const float rmax_hi = sqrtf(r2f) * 1.00001f + 1e-6f;   // every target beyond it has float d > r^2
+    const float rext = rmax + kClear, r2ext = rext * rext;
     int k = 0, converged = 0, status = DPG_ICP_OK;
 #ifdef DPG_ICP_TIMING
     unsigned long long ph[4] = {0, 0, 0, 0}, nit = 0;
 #endif
     for (;;) {
         ICP_STAMP(c0);
-        const double i00 = uni(L.bc->inv[0]), i01 = uni(L.bc->inv[1]);
-        const double i10 = uni(L.bc->inv[2]), i11 = uni(L.bc->inv[3]);
+        const float i00 = uni((float)L.bc->inv[0]), i01 = uni((float)L.bc->inv[1]);
+        const float i10 = uni((float)L.bc->inv[2]), i11 = uni((float)L.bc->inv[3]);
         const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
         const float drift = 1e-4f + 5e-5f * (float)(k + 1);
         uint32_t okm = 0;   // bit m: point t + 512 m has a (reciprocal) correspondence
@@ -415,10 +420,18 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
             const bool live = i < N;
             const float qx = sx[m], qy = sy[m];
             // ---- forward 1-NN (target index), seeded radius ----
+            // seed[m] >= 0: last match (its distance seeds the radius); -1: no knowledge;
+            // < -1: clearance -- provably no target within r of this point -- so no search
             uint64_t best = dkey(r2f, 0xffffffffu);   // "none": every candidate with d <= r beats it
             float rad = rmax;
-            if (live && seed[m] >= 0) {
-                const Rec r = L.tp[seed[m]];
+            const int sd = seed[m];
+            const bool search = live && sd >= -1;
+            const bool ext = search && sd == -1;   // unseeded: search r + kClear to learn a clearance
+            if (ext) {
+                rad = rext;
+                best = dkey(r2ext, 0xffffffffu);
+            } else if (search) {
+                const Rec r = L.tp[sd];
                 const float d = sqd(qx, qy, r.x, r.y);
                 if (d <= r2f) {
                     best = dkey(d, r.key);
@@ -427,7 +440,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
             }
             {
                 int s = 0;
-                const int fc = live ? window(L.tb, M, qx, qy, rad, s) : 0;
+                const int fc = search ? window(L.tb, M, qx, qy, rad, s) : 0;
 #ifdef DPG_ICP_STATS
                 {
                     int trips = 0;
@@ -450,9 +463,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
             }
             const uint32_t bkey = (uint32_t)best;
             const float bd = __uint_as_float((uint32_t)(best >> 32));
-            const int bp = bkey == 0xffffffffu ? -1 : (int)(bkey & 0xffffu);
+            const int bp = (bkey == 0xffffffffu || bd > r2f) ? -1 : (int)(bkey & 0xffffu);   // R4: d > r^2 rejected
             const int bi = (int)(bkey >> 16);
-            seed[m] = live ? bp : seed[m];
+            if (search) {
+                int nsd = bp;
+                if (bp < 0 && ext) {   // nothing within r: the nearest target is >= min(sqrt(bd), rext) away
+                    const float clr = fminf(sqrtf(bd), rext) * 0.99999f - rmax_hi;
+                    const int q = clr > 0.f ? (int)(clr * 1e4f) : 0;   // units of 1e-4 m, rounded down
+                    nsd = -1 - q;
+                }
+                seed[m] = nsd;
+            }
             bool ok = live && bp >= 0;
             // ---- reciprocal test in the static source index ----
             if (kp.reciprocal) {
@@ -461,8 +482,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
                 if (ok) {
                     const Rec r = L.tp[bp];
                     tj = make_float2(r.x, r.y);
-                    const double ux = (double)tj.x - (double)ftx, uy = (double)tj.y - (double)fty;
-                    const float px = (float)(i00 * ux + i01 * uy), py = (float)(i10 * ux + i11 * uy);
+                    // t_j in the source node frame; float error ~1e-6 m, far inside the window margin
+                    const float ux = tj.x - ftx, uy = tj.y - fty;
+                    const float px = i00 * ux + i01 * uy, py = i10 * ux + i11 * uy;
                     rc = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
                 }
                 // i's own word: any other current source with a smaller (d, original index) word
@@ -511,7 +533,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
                     dpg_tree::add_pair(acc, sx[m], sy[m], tq.x, tq.y, sqd(sx[m], sy[m], tq.x, tq.y));
                 }
             }
-            dpg_tree::wave_fold(acc);
+            dpg_tree::wave_fold<1>(acc);   // the count is an integer: ballots instead
+            int cnt = 0;
+#pragma unroll
+            for (int m = 0; m < PPT; ++m) cnt += __popcll(__ballot((okm >> m) & 1u));
+            acc[0] = (double)cnt;
             if (lane == 0) {
 #pragma unroll
                 for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
@@ -542,8 +568,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
                 B.code = 2;   // stop, "Not enough correspondences found" (transform unchanged)
             } else {
                 const double n = S[0];
-                const double a = (S[6] + S[9]) - (S[2] * S[4] + S[3] * S[5]) / n;
-                const double b = (S[7] - S[8]) - (S[2] * S[5] - S[3] * S[4]) / n;
+                double a, b;
+                dpg_tree::fit_ab(S, a, b);
                 const double hh = sqrt(a * a + b * b);
                 double c = 1.0, sn = 0.0;
                 if (hh > 0.0) { c = a / hh; sn = b / hh; }
@@ -594,6 +620,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void
             sx[m] = (cf * x + nsf * y) + txf;
             sy[m] = (sf * x + cf * y) + tyf;
             if (i < N) put(m);
+            if (seed[m] < -1) {   // the clearance shrinks by the distance the point just moved
+                const float dx = sx[m] - x, dy = sy[m] - y;
+                const float mv = sqrtf(dx * dx + dy * dy) * 1.0001f + 1e-6f;
+                const int q = (-1 - seed[m]) - (int)ceilf(mv * 1e4f);
+                seed[m] = q > 0 ? -1 - q : -1;
+            }
         }
         ++k;
         if (code == 1) { converged = 1; break; }

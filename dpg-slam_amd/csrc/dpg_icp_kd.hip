@@ -31,7 +31,7 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kW = kT / 64;
-constexpr int kSums = 10;
+constexpr int kSums = dpg_tree::kSums;
 
 __device__ __forceinline__ int level_of(int i) { return 31 - __clz(i + 1); }
 
@@ -303,8 +303,8 @@ __global__ __launch_bounds__(kT) void icp_kd_kernel(const float2* __restrict__ d
         last_cnt = cnt;
         if (cnt < kp.min_corr) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
         const double n = S[0];
-        const double a = (S[6] + S[9]) - (S[2] * S[4] + S[3] * S[5]) / n;
-        const double b = (S[7] - S[8]) - (S[2] * S[5] - S[3] * S[4]) / n;
+        double a, b;
+        dpg_tree::fit_ab(S, a, b);
         const double hh = sqrt(a * a + b * b);
         double c = 1.0, s = 0.0;
         if (hh > 0.0) { c = a / hh; s = b / hh; }

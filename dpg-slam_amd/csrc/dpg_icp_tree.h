@@ -1,7 +1,10 @@
 // dpg_icp_tree.h -- the fixed fp64 reduction tree of the ICP rigid-fit sums (R5), shared by the
 // three ICP kernels and restated by the CPU oracle (oracle/dpg_oracle.c lane_tree).
 //
-// The tree (DPG_ICP_LANES = 512 lanes = 8 waves of 64):
+// The sums: [0] count, [1] sum d, [2..3] sum p, [4..5] sum q, [6] sum (px qx + py qy), [7] sum
+// (px qy - py qx) -- p the moved source point, q its target, d the fp32 squared distance; each
+// pair's terms are exact fp64 products with one rounded add/subtract.  The count is an integer,
+// exact in any order.  The tree for sums [1..7] (DPG_ICP_LANES = 512 lanes = 8 waves of 64):
 //   * lane l accumulates the accepted pairs of the source points i with i mod 512 == l, in
 //     ascending i, starting from 0.0;
 //   * inside each wave, for off = 32, 16, 8, 4, 2, 1: acc[k] = acc[k] + acc[k + off] (k < off);
@@ -17,7 +20,7 @@
 
 namespace dpg_tree {
 
-constexpr int kSums = 10;       // cnt, d, px, py, qx, qy, xx, xy, yx, yy
+constexpr int kSums = 8;        // cnt, d, px, py, qx, qy, dot, cross
 constexpr int kLanes = 512;     // == DPG_ICP_LANES
 constexpr int kWaves = kLanes / 64;
 
@@ -39,20 +42,21 @@ __device__ __forceinline__ double down(double v) {
     return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
 }
 
-// the in-wave part of the tree: lane 0 ends with W_w
+// the in-wave part of the tree for sums [FIRST, kSums): lane 0 ends with W_w
+template <int FIRST = 0>
 __device__ __forceinline__ void wave_fold(double (&acc)[kSums]) {
 #pragma unroll
-    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<32>(acc[q]);
+    for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<32>(acc[q]);
 #pragma unroll
-    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<16>(acc[q]);
+    for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<16>(acc[q]);
 #pragma unroll
-    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<8>(acc[q]);
+    for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<8>(acc[q]);
 #pragma unroll
-    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<4>(acc[q]);
+    for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<4>(acc[q]);
 #pragma unroll
-    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<2>(acc[q]);
+    for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<2>(acc[q]);
 #pragma unroll
-    for (int q = 0; q < kSums; ++q) acc[q] = acc[q] + down<1>(acc[q]);
+    for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<1>(acc[q]);
 }
 
 // the cross-wave part: W[w * stride + q] -> S[q]
@@ -70,10 +74,15 @@ __device__ __forceinline__ void add_pair(double (&acc)[kSums], float sx, float s
     acc[3] = acc[3] + py;
     acc[4] = acc[4] + qx;
     acc[5] = acc[5] + qy;
-    acc[6] = acc[6] + px * qx;
-    acc[7] = acc[7] + px * qy;
-    acc[8] = acc[8] + py * qx;
-    acc[9] = acc[9] + py * qy;
+    acc[6] = acc[6] + (px * qx + py * qy);
+    acc[7] = acc[7] + (px * qy - py * qx);
+}
+
+// R5 closed form from the reduced sums: a = S_dot - (Sp . Sq) / n, b = S_cross - (Sp x Sq) / n
+__device__ __forceinline__ void fit_ab(const double* S, double& a, double& b) {
+    const double n = S[0];
+    a = S[6] - (S[2] * S[4] + S[3] * S[5]) / n;
+    b = S[7] - (S[2] * S[5] - S[3] * S[4]) / n;
 }
 
 }  // namespace dpg_tree

@@ -209,7 +209,8 @@ static void nn_grid(const grid_t* g, const float* pts, float qx, float qy, int32
 
 /* ------------------------------------------------------------------ R5/R6 ICP */
 
-enum { S_CNT = 0, S_D, S_PX, S_PY, S_QX, S_QY, S_XX, S_XY, S_YX, S_YY, S_N };
+/* sums (csrc/dpg_icp_tree.h): count, d, p, q, dot = px qx + py qy, cross = px qy - py qx */
+enum { S_CNT = 0, S_D, S_PX, S_PY, S_QX, S_QY, S_DOT, S_CROSS, S_N };
 
 /* The 512-lane fixed reduction (DPG_ICP_LANES = 8 waves x 64 lanes, include/dpg_slam_c.h):
  * inside each 64-lane wave acc[k] += acc[k + off] for off = 32, 16, ..., 1; then
@@ -230,8 +231,8 @@ static void lane_tree(double acc[DPG_ICP_LANES][S_N], double out[S_N]) {
 /* Planar rigid fit from the reduced sums; returns (c, s, tx, ty) rounded to float. */
 static void rigid_from_sums(const double S[S_N], float* cf, float* sf, float* txf, float* tyf) {
     double n = S[S_CNT];
-    double a = (S[S_XX] + S[S_YY]) - (S[S_PX] * S[S_QX] + S[S_PY] * S[S_QY]) / n;
-    double b = (S[S_XY] - S[S_YX]) - (S[S_PX] * S[S_QY] - S[S_PY] * S[S_QX]) / n;
+    double a = S[S_DOT] - (S[S_PX] * S[S_QX] + S[S_PY] * S[S_QY]) / n;
+    double b = S[S_CROSS] - (S[S_PX] * S[S_QY] - S[S_PY] * S[S_QX]) / n;
     double h = sqrt(a * a + b * b);
     double c = 1.0, s = 0.0;
     if (h > 0.0) { c = a / h; s = b / h; }
@@ -317,10 +318,8 @@ int oracle_icp_align(const float* src_in, int64_t n_src, const float* tgt, int64
             acc[l][S_PY] = acc[l][S_PY] + py;
             acc[l][S_QX] = acc[l][S_QX] + qx;
             acc[l][S_QY] = acc[l][S_QY] + qy;
-            acc[l][S_XX] = acc[l][S_XX] + px * qx;
-            acc[l][S_XY] = acc[l][S_XY] + px * qy;
-            acc[l][S_YX] = acc[l][S_YX] + py * qx;
-            acc[l][S_YY] = acc[l][S_YY] + py * qy;
+            acc[l][S_DOT] = acc[l][S_DOT] + (px * qx + py * qy);
+            acc[l][S_CROSS] = acc[l][S_CROSS] + (px * qy - py * qx);
         }
         double S[S_N];
         lane_tree(acc, S);
