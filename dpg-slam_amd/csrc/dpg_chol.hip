@@ -384,6 +384,73 @@ __device__ __forceinline__ double rdlane(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
+// The diagonal block at (jb, jb) of a front (bw x bw) into LDS (leading dimension kSB), padded
+// to nb = chain_len(bw): its STRICT lower triangle (zero elsewhere and past bw), and the
+// reciprocals of its diagonal (0 past bw).
+__device__ __forceinline__ int chain_len(int bw) { return bw <= 8 ? 8 : bw <= 16 ? 16 : bw <= 32 ? 32 : 64; }
+__device__ __forceinline__ void load_diag(double* D, double* rd, const double* F, int m3, int jb, int bw) {
+    const int nb = chain_len(bw);
+    for (int e = threadIdx.x; e < nb * nb; e += kT) {
+        const int i = e % nb, j = e / nb;
+        const double v = (i < bw && j < bw && i >= j) ? F[(int64_t)(jb + j) * m3 + jb + i] : 0.0;
+        D[j * kSB + i] = i > j ? v : 0.0;
+        if (i == j) rd[j] = j < bw ? 1.0 / v : 0.0;
+    }
+}
+
+// One wave solves the padded unit-scaled triangle by a readlane -> fma chain; lane = row, the
+// lane's scaled entries in registers (lanes >= N compute garbage nobody reads).
+// forward (L y = b):  yl_i -= L(i, j) / L(j, j) * yl_j, j ascending; y = yl / L_ii afterwards
+template <int N>
+__device__ __forceinline__ double fwd_chain(const double* D, const double* rd, double yl, int lane) {
+    double dr[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) dr[j] = D[j * kSB + lane] * rd[j];
+#pragma unroll
+    for (int j = 0; j < N; ++j) yl = fma(-dr[j], rdlane(yl, j), yl);
+    return yl;
+}
+// backward (L^T x = z): zl_i -= L(j, i) / L(j, j) * zl_j, j descending; x = zl / L_ii afterwards
+template <int N>
+__device__ __forceinline__ double bwd_chain(const double* D, const double* rd, double zl, int lane) {
+    double dr[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) dr[j] = D[lane * kSB + j] * rd[j];
+#pragma unroll
+    for (int j = N - 1; j >= 0; --j) zl = fma(-dr[j], rdlane(zl, j), zl);
+    return zl;
+}
+
+// 16-lane groups: sum of a partial over the group (xor butterfly: every lane gets the total)
+__device__ __forceinline__ double group16_sum(double a) {
+    a += __shfl_xor(a, 8, 16);
+    a += __shfl_xor(a, 4, 16);
+    a += __shfl_xor(a, 2, 16);
+    a += __shfl_xor(a, 1, 16);
+    return a;
+}
+
+// z[j] -= sum_t A[j * lda + t] x[t] for j < nj, t < nt (A column-major, the dot runs down a
+// column: contiguous): 16 lanes per j, so a long dot is 1/16 of the serial chain.
+__device__ __forceinline__ void sub_coldots(double* z, const double* A, int64_t lda, const double* x, int nj, int nt) {
+    const int g = threadIdx.x >> 4, gl = threadIdx.x & 15;
+    for (int j0 = 0; j0 < nj; j0 += kT / 16) {
+        const int j = j0 + g;
+        double a0 = 0.0, a1 = 0.0;
+        if (j < nj) {
+            const double* Aj = A + (int64_t)j * lda;
+            int t = gl;
+            for (; t + 16 < nt; t += 32) {
+                a0 = fma(Aj[t], x[t], a0);
+                a1 = fma(Aj[t + 16], x[t + 16], a1);
+            }
+            if (t < nt) a0 = fma(Aj[t], x[t], a0);
+        }
+        const double a = group16_sum(a0 + a1);
+        if (j < nj && gl == 0) z[j] -= a;
+    }
+}
+
 __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                        int32_t* status, const SnDev* __restrict__ sns,
                                                        const int32_t* __restrict__ child_list,
@@ -409,15 +476,7 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
         y[t] = -g[3 * node + t % 3];
     }
     for (int t = tid; t < r3; t += kT) aR[t] = 0.0;
-    {
-        const int bw = min(kSB, k3);
-        for (int e = tid; e < bw * bw; e += kT) {
-            const int i = e % bw, j = e / bw;
-            const double v = F[j * m3 + i];
-            D[j * kSB + i] = v;
-            if (i == j) rd[j] = 1.0 / v;
-        }
-    }
+    load_diag(D, rd, F, m3, 0, min(kSB, k3));
     if (S.nchild > 0) {
         if (tid == 0) wait_geq_sc1(sync + 1 + s, S.nchild, status);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -438,21 +497,16 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
     for (int jb = 0; jb < k3; jb += kSB) {
         const int bw = min(kSB, k3 - jb);
         if (jb > 0) {
-            for (int e = tid; e < bw * bw; e += kT) {
-                const int i = e % bw, j = e / bw;
-                D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
-                if (i == j) rd[j] = 1.0 / D[j * kSB + i];
-            }
+            load_diag(D, rd, F, m3, jb, bw);
             __syncthreads();
         }
         if (wave == 0) {   // lane = row; y_j broadcast by v_readlane (uniform j)
             double yl = lane < bw ? y[jb + lane] : 0.0;
             const double rl = lane < bw ? rd[lane] : 0.0;
-            for (int j = 0; j < bw; ++j) {
-                const double yj = rdlane(yl * rl, j);
-                yl = lane == j ? yj : (lane > j && lane < bw ? fma(-D[j * kSB + lane], yj, yl) : yl);
-            }
-            if (lane < bw) y[jb + lane] = yl;
+            const int nb = chain_len(bw);
+            yl = nb == 8 ? fwd_chain<8>(D, rd, yl, lane) : nb == 16 ? fwd_chain<16>(D, rd, yl, lane)
+               : nb == 32 ? fwd_chain<32>(D, rd, yl, lane) : fwd_chain<64>(D, rd, yl, lane);
+            if (lane < bw) y[jb + lane] = yl * rl;
         }
         __syncthreads();
         for (int i = jb + bw + tid; i < k3; i += kT) {
@@ -512,13 +566,8 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     for (int t = tid; t < S.r; t += kT) rp[t] = rows[S.rows_off + t];
     const int nblk = (k3 + kSB - 1) / kSB;
     {
-        const int jb = (nblk - 1) * kSB, bw = k3 - jb;
-        for (int e = tid; e < bw * bw; e += kT) {
-            const int i = e % bw, j = e / bw;
-            const double v = F[(jb + j) * m3 + jb + i];
-            D[j * kSB + i] = v;
-            if (i == j) rd[j] = 1.0 / v;
-        }
+        const int jb = (nblk - 1) * kSB;
+        load_diag(D, rd, F, m3, jb, k3 - jb);
     }
     if (S.parent >= 0) {
         if (tid == 0) wait_geq_sc1(sync + 1 + S.parent, 1, status);
@@ -528,53 +577,25 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     BW_MARK(s, 1);
     for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
     __syncthreads();
-    for (int j = tid; j < k3; j += kT) {   // z = y - L21^T x_r, four independent accumulators
-        const double* Fj = F + (int64_t)j * m3 + k3;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        int t = 0;
-        for (; t + 3 < r3; t += 4) {
-            a0 = fma(Fj[t], xr[t], a0);
-            a1 = fma(Fj[t + 1], xr[t + 1], a1);
-            a2 = fma(Fj[t + 2], xr[t + 2], a2);
-            a3 = fma(Fj[t + 3], xr[t + 3], a3);
-        }
-        for (; t < r3; ++t) a0 = fma(Fj[t], xr[t], a0);
-        z[j] -= (a0 + a1) + (a2 + a3);
-    }
+    sub_coldots(z, F + k3, m3, xr, k3, r3);   // z = y - L21^T x_r
     __syncthreads();
     BW_MARK(s, 2);
     for (int b = nblk - 1; b >= 0; --b) {
         const int jb = b * kSB, bw = min(kSB, k3 - jb);
         if (b != nblk - 1) {
-            for (int e = tid; e < bw * bw; e += kT) {
-                const int i = e % bw, j = e / bw;
-                D[j * kSB + i] = F[(jb + j) * m3 + jb + i];
-                if (i == j) rd[j] = 1.0 / D[j * kSB + i];
-            }
+            load_diag(D, rd, F, m3, jb, bw);
             __syncthreads();
         }
         if (wave == 0) {   // lane = row; x_j broadcast by v_readlane (uniform j): ~3 dependent ops per step
             double zl = lane < bw ? z[jb + lane] : 0.0;
             const double rl = lane < bw ? rd[lane] : 0.0;
-            const double* Dl = D + lane * kSB;
-            for (int j = bw - 1; j >= 0; --j) {
-                const double xj = rdlane(zl * rl, j);
-                zl = lane == j ? xj : (lane < j ? fma(-Dl[j], xj, zl) : zl);   // L(jb+j, jb+lane)
-            }
-            if (lane < bw) z[jb + lane] = zl;
+            const int nb = chain_len(bw);
+            zl = nb == 8 ? bwd_chain<8>(D, rd, zl, lane) : nb == 16 ? bwd_chain<16>(D, rd, zl, lane)
+               : nb == 32 ? bwd_chain<32>(D, rd, zl, lane) : bwd_chain<64>(D, rd, zl, lane);
+            if (lane < bw) z[jb + lane] = zl * rl;
         }
         __syncthreads();
-        for (int j = tid; j < jb; j += kT) {
-            const double* Fj = F + (int64_t)j * m3 + jb;
-            double a0 = 0.0, a1 = 0.0;
-            int i = 0;
-            for (; i + 1 < bw; i += 2) {
-                a0 = fma(Fj[i], z[jb + i], a0);
-                a1 = fma(Fj[i + 1], z[jb + i + 1], a1);
-            }
-            if (i < bw) a0 = fma(Fj[i], z[jb + i], a0);
-            z[j] -= a0 + a1;
-        }
+        sub_coldots(z, F + jb, m3, z + jb, jb, bw);
         __syncthreads();
     }
     BW_MARK(s, 3);
@@ -1638,6 +1659,7 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     rc |= hipMalloc(reinterpret_cast<void**>(&c->ysol), (size_t)(3 * n) * 8) != hipSuccess;
     rc |= hipMalloc(reinterpret_cast<void**>(&c->xsol), (size_t)(3 * n) * 8) != hipSuccess;
     rc |= hipMalloc(reinterpret_cast<void**>(&c->status), sizeof(int32_t)) != hipSuccess;
+    if (!rc) rc |= hipMemset(c->status, 0, sizeof(int32_t)) != hipSuccess;
     if (rc) { dpg_chol_destroy(c); return DPG_ERR_HIP; }
     *out = c;
     return DPG_OK;

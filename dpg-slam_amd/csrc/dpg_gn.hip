@@ -551,7 +551,8 @@ extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg
     const double* xout = g->x;
     const int32_t* xpos = nullptr;
     g->last_pcg_iters = 0;
-    if (gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol) {
+    g->last_used_chol = gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol;
+    if (g->last_used_chol) {
         const bool reuse = gp->reuse_factorization && g->have_factor && g->last_delta_inf < gp->refactor_delta;
         const int rc = reuse ? dpg_chol_resolve(g->chol, hb, stream) : dpg_chol_solve(g->chol, hb, stream);
         if (rc) return rc;
@@ -574,7 +575,7 @@ extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg
 
 extern "C" int dpg_gn_dev_fetch(dpg_gn_dev* g, const double* hb, void* stream, double out[3]) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const bool chol = g->chol != nullptr;
+    const bool chol = g->chol != nullptr && g->last_used_chol;
     hipLaunchKernelGGL(scalars_kernel, dim3(1), dim3(1), 0, s, hb + 9 * g->nnzb_upper + 3 * g->n_nodes,
                        chol ? dpg_chol_status_dev(g->chol) : nullptr, g->scal3);
     if (hipMemcpyAsync(g->scal3_host, g->scal3, 3 * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||

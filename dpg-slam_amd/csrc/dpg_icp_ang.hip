@@ -180,7 +180,13 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 // inside itself; the trip start advances by kU mod n.
 constexpr int kWaves = kT / 64;
 static_assert(kT == dpg_tree::kLanes, "one tree lane per thread");
-constexpr int kU = 4;
+#ifndef DPG_ANG_KU
+#define DPG_ANG_KU 4
+#endif
+#ifndef DPG_ANG_WPE
+#define DPG_ANG_WPE 8
+#endif
+constexpr int kU = DPG_ANG_KU;   // candidates per trip
 // an unmatched point searches kClear beyond r once; while the distance it has moved since stays
 // below the margin found, it provably has no target within r and skips its forward search
 constexpr float kClear = 0.1f;
@@ -251,17 +257,33 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // left alone, narrows an unused pad word to ds_read_b96 -- 8 LDS cycles instead of 4 -- or
 // serialises the loads behind per-load waits under the 64-VGPR budget)
 __device__ __forceinline__ void ld_recs(const Rec* p, uint4 (&r)[kU]) {
-    static_assert(kU == 4, "ld_recs issues four loads");
+    static_assert(kU == 4 || kU == 8, "ld_recs issues four or eight loads");
     const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(p);   // LDS byte offset
-    asm volatile(
-        "ds_read_b128 %0, %4\n\t"
-        "ds_read_b128 %1, %4 offset:16\n\t"
-        "ds_read_b128 %2, %4 offset:32\n\t"
-        "ds_read_b128 %3, %4 offset:48\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
-        : "v"(a)
-        : "memory");
+    if constexpr (kU == 4) {
+        asm volatile(
+            "ds_read_b128 %0, %4\n\t"
+            "ds_read_b128 %1, %4 offset:16\n\t"
+            "ds_read_b128 %2, %4 offset:32\n\t"
+            "ds_read_b128 %3, %4 offset:48\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3])
+            : "v"(a)
+            : "memory");
+    } else {
+        asm volatile(
+            "ds_read_b128 %0, %8\n\t"
+            "ds_read_b128 %1, %8 offset:16\n\t"
+            "ds_read_b128 %2, %8 offset:32\n\t"
+            "ds_read_b128 %3, %8 offset:48\n\t"
+            "ds_read_b128 %4, %8 offset:64\n\t"
+            "ds_read_b128 %5, %8 offset:80\n\t"
+            "ds_read_b128 %6, %8 offset:96\n\t"
+            "ds_read_b128 %7, %8 offset:112\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+            : "v"(a)
+            : "memory");
+    }
 }
 
 // workgroup-uniform values (the transform, the reduced sums) kept in SGPRs: frees VGPRs for the
@@ -311,7 +333,7 @@ __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float
 }
 
 template <int PPT>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(8, 8))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE, DPG_ANG_WPE))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
                                                      const float2* __restrict__ idx_pts,
                                                      const uint16_t* __restrict__ idx_orig,
                                                      const uint16_t* __restrict__ buckets,

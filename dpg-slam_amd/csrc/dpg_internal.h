@@ -97,6 +97,7 @@ typedef struct dpg_gn_dev {
     double* scal3_host;            /* pinned mirror of scal3 */
     int32_t n_blocks_rows;         /* grid size for row kernels */
     int32_t last_pcg_iters;
+    int32_t last_used_chol;        /* the last solve ran the Cholesky (its status word is meaningful) */
     double last_delta_inf;         /* host: max |delta| of the last fetched retraction */
     int32_t have_factor;           /* the Cholesky holds a factorization of this graph */
     int32_t n_factorizations;      /* since dpg_gn_set_poses */
