@@ -40,11 +40,16 @@
 // [8] search, [9] sums + fold, [10] arrival + fit + publish barrier, [11] move + barrier,
 // [12] wave-iterations
 #define DPG_ICP_DIAG 1
-__device__ unsigned long long g_icp_stats[16];
+__device__ unsigned long long g_icp_stats[40];
 #define ICP_STAT_ADD(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
 #endif
 #ifdef DPG_ICP_STATS
 #define ICP_STAT(k, v) ICP_STAT_ADD(k, v)
+// [16..27] forward / [28..39] reciprocal wave trips of a slot, summed per bin of trips per slot:
+// 0, 1, 2, 3, 4, 5-8, 9-16, 17-32, 33-64, 65-128, 129-256, >256
+__device__ __forceinline__ int trip_bin(int t) {
+    return t <= 4 ? t : t <= 8 ? 5 : t <= 16 ? 6 : t <= 32 ? 7 : t <= 64 ? 8 : t <= 128 ? 9 : t <= 256 ? 10 : 11;
+}
 #endif
 #ifdef DPG_ICP_TIMING
 #define ICP_STAMP(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
@@ -450,8 +455,20 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             const bool search = live && sd >= -1;
             const bool ext = search && sd == -1;   // unseeded: search r + kClear to learn a clearance
             if (ext) {
+                // unseeded: the target at q's own bearing (first point of q's bucket) bounds the
+                // nearest distance -- on a surface both scans see it is a few cm away
                 rad = rext;
                 best = dkey(r2ext, 0xffffffffu);
+                int p0 = L.tb[bucket_of(pseudo_angle(qx, qy))];
+                p0 = p0 >= M ? 0 : p0;
+                if (M > 0) {
+                    const Rec r = L.tp[p0];
+                    const float d = sqd(qx, qy, r.x, r.y);
+                    if (d <= r2ext) {
+                        best = dkey(d, r.key);
+                        rad = sqrtf(d) * 1.0001f + 1e-6f;
+                    }
+                }
             } else if (search) {
                 const Rec r = L.tp[sd];
                 const float d = sqd(qx, qy, r.x, r.y);
@@ -468,7 +485,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
                     int trips = 0;
                     for (int c = 0; __any(c < fc); c += kU) ++trips;
                     if (live) { ICP_STAT(0, 1); ICP_STAT(1, fc); if (fc >= M) ICP_STAT(7, 1); }
-                    if (lane == 0) ICP_STAT(2, trips);
+                    if (lane == 0) { ICP_STAT(2, trips); ICP_STAT(16 + trip_bin(trips), trips); }
                     wtrips += trips;
                 }
 #endif
@@ -518,7 +535,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
                     for (int c = 0; __any(ok & (c < rc)); c += kU) ++trips;
                     if (ok) { ICP_STAT(3, rc); if (rc >= N) ICP_STAT(13, 1); }
                     if (live && !ok) ICP_STAT(6, 1);
-                    if (lane == 0) ICP_STAT(4, trips);
+                    if (lane == 0) { ICP_STAT(4, trips); ICP_STAT(28 + trip_bin(trips), trips); }
                     wtrips += trips;
                 }
 #endif
@@ -693,9 +710,9 @@ extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 
 #ifdef DPG_ICP_DIAG
 extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 40 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[40] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_icp_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
