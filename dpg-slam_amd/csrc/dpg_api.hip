@@ -621,24 +621,17 @@ static int check_conv(const dpg_gn_params* gp, double cur, double nw) {
     return (gp->relative_error_tol != 0.0 && rel_dec <= gp->relative_error_tol) || (abs_dec <= gp->absolute_error_tol);
 }
 
-int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params* gp,
-                       dpg_gn_stats* st) {
-    const double t0 = now_ms();
-    dpg_gn_params P;
-    if (gp) P = *gp;
-    else dpg_gn_params_default(&P);
-    int rc = dpg_gn_setup(c, V, F, nf, 0, nf, &P);
-    if (rc) return rc;
-    if ((rc = dpg_gn_set_poses(c, poses))) return rc;
-    const double t1 = now_ms();
+// The Gauss-Newton loop on a set-up graph whose poses are set: solve + retract + re-linearize
+// enqueued back to back, one synchronisation per iteration.  t1: when the iterations started.
+static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0, double t1, dpg_gn_stats* st) {
     dpg_gn_stats S;
     memset(&S, 0, sizeof(S));
+    int rc;
     if ((rc = dpg_gn_assemble(c, nullptr)) || (rc = read_error(c, &S.initial_error))) return rc;
     double cur = S.initial_error, nw = cur, dinf = 0.0;
     int it = 0;
     if (!(cur <= 0.0) && P.max_iterations > 0) {
         for (;;) {
-            // solve + retract + re-linearize enqueued back to back, one synchronisation per iteration
             double sc[3];
             if ((rc = dpg_gn_solve_retract_async(c, nullptr)) || (rc = dpg_gn_assemble(c, nullptr)) ||
                 (rc = dpg_gn_fetch(c, nullptr, sc)))
@@ -664,6 +657,177 @@ int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F
     S.last_delta_inf = dinf;
     S.ms_total = t2 - t0;
     S.ms_per_iteration = it ? (t2 - t1) / it : 0.0;
+    if (st) *st = S;
+    return DPG_OK;
+}
+
+int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params* gp,
+                       dpg_gn_stats* st) {
+    const double t0 = now_ms();
+    dpg_gn_params P;
+    if (gp) P = *gp;
+    else dpg_gn_params_default(&P);
+    int rc = dpg_gn_setup(c, V, F, nf, 0, nf, &P);
+    if (rc) return rc;
+    if ((rc = dpg_gn_set_poses(c, poses))) return rc;
+    return gn_loop(c, P, poses, t0, now_ms(), st);
+}
+
+// ---- re-linearisation sweep (DpgSLAM::reoptimize) ----
+
+void dpg_reopt_params_default(dpg_reopt_params* p) {
+    if (!p) return;
+    p->max_node_dist_within_pass = 5.0f;
+    p->max_node_dist_across_passes = 2.0f;
+    p->new_pass_std_dev[0] = 0.2f;
+    p->new_pass_std_dev[1] = 0.2f;
+    p->new_pass_std_dev[2] = 0.15f;
+    for (int k = 0; k < 4; ++k) p->motion_model[k] = 0.4f;
+    p->odometry_constraints = 1;
+}
+
+// candidate pairs on the GPU (dpg_reopt.hip): count per node, host prefix sum, write
+static int64_t lc_candidates(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, float within,
+                             float across, std::vector<int32_t>& pairs) {
+    DevBuf<float> dposes;
+    DevBuf<int32_t> dpass, dcount, dpairs;
+    DevBuf<int64_t> doff;
+    if (dposes.reserve((size_t)(3 * V)) || dpass.reserve((size_t)V) || dcount.reserve((size_t)V) ||
+        doff.reserve((size_t)V))
+        return fail(DPG_ERR_HIP, "allocation failed");
+    int64_t K = -1;
+    std::vector<int32_t> cnt((size_t)V);
+    std::vector<int64_t> off((size_t)V);
+    do {
+        if (hipMemcpyAsync(dposes.p, est, sizeof(float) * 3 * V, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipMemcpyAsync(dpass.p, pass, sizeof(int32_t) * V, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            break;
+        if (dpg_launch_lc_count(dposes.p, dpass.p, V, within, across, dcount.p, c->stream)) break;
+        if (hipMemcpyAsync(cnt.data(), dcount.p, sizeof(int32_t) * V, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            break;
+        int64_t acc = 0;
+        for (int64_t i = 0; i < V; ++i) { off[(size_t)i] = acc; acc += cnt[(size_t)i]; }
+        pairs.assign((size_t)(2 * acc), 0);
+        if (acc > 0) {
+            if (dpairs.reserve((size_t)(2 * acc))) break;
+            if (hipMemcpyAsync(doff.p, off.data(), sizeof(int64_t) * V, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+                break;
+            if (dpg_launch_lc_write(dposes.p, dpass.p, V, within, across, doff.p, dpairs.p, c->stream)) break;
+            if (hipMemcpyAsync(pairs.data(), dpairs.p, sizeof(int32_t) * 2 * acc, hipMemcpyDeviceToHost, c->stream) !=
+                    hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess)
+                break;
+        }
+        K = acc;
+    } while (false);
+    dposes.release();
+    dpass.release();
+    dcount.release();
+    dpairs.release();
+    doff.release();
+    if (K < 0) return fail(DPG_ERR_HIP, "loop-closure candidate search failed: %s", hipGetErrorString(hipGetLastError()));
+    return K;
+}
+
+int64_t dpg_loop_closure_candidates(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, float within,
+                                    float across, int32_t* pairs_out, int64_t cap) {
+    if (!c || V < 0 || (V > 0 && (!pass || !est))) return fail(DPG_ERR_ARG, "bad arguments");
+    std::vector<int32_t> pairs;
+    const int64_t K = lc_candidates(c, V, pass, est, within, across, pairs);
+    if (K < 0) return K;
+    if (pairs_out && cap > 0) memcpy(pairs_out, pairs.data(), sizeof(int32_t) * 2 * (size_t)std::min(K, cap));
+    return K;
+}
+
+int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, const float* odom,
+                   const dpg_icp_params* ip, const dpg_gn_params* gp, const dpg_reopt_params* rp, double* poses_out,
+                   dpg_reopt_stats* st) {
+    if (!c || V <= 0 || !pass || !est || !odom || !poses_out) return fail(DPG_ERR_ARG, "bad arguments");
+    if (c->n_nodes != V) return fail(DPG_ERR_STATE, "scans of %lld nodes uploaded, sweep over %lld",
+                                     (long long)c->n_nodes, (long long)V);
+    dpg_icp_params I;
+    if (ip) I = *ip;
+    else dpg_icp_params_default(&I);
+    dpg_gn_params P;
+    if (gp) P = *gp;
+    else dpg_gn_params_default(&P);
+    dpg_reopt_params R;
+    if (rp) R = *rp;
+    else dpg_reopt_params_default(&R);
+    dpg_reopt_stats S;
+    memset(&S, 0, sizeof(S));
+    const double t0 = now_ms();
+    // 1. loop-closure candidates (dpg_slam.cc:91-98)
+    std::vector<int32_t> lc;
+    const int64_t K = lc_candidates(c, V, pass, est, R.max_node_dist_within_pass, R.max_node_dist_across_passes, lc);
+    if (K < 0) return (int)K;
+    const double t1 = now_ms();
+    // 2. ICP edges: successive (i-1, i), then the candidates (j, i) -- {node_1 target, node_2 source}
+    const int64_t n_succ = V - 1, E = n_succ + K;
+    std::vector<int32_t> edges((size_t)(2 * E));
+    for (int64_t i = 1; i < V; ++i) { edges[(size_t)(2 * (i - 1))] = (int32_t)(i - 1); edges[(size_t)(2 * (i - 1) + 1)] = (int32_t)i; }
+    if (K > 0) memcpy(edges.data() + 2 * n_succ, lc.data(), sizeof(int32_t) * 2 * (size_t)K);
+    // 3. factors: per node a prior (new pass) or the odometry Between (dpg_slam.cc:40-79), then one
+    //    slot per ICP edge (measurements filled on device after the batch)
+    std::vector<dpg_factor> F;
+    F.reserve((size_t)(V + E));
+    int32_t cur_pass = -1;
+    for (int64_t i = 0; i < V; ++i) {
+        if (i == 0 || pass[i] != cur_pass) {
+            dpg_factor f;
+            memset(&f, 0, sizeof(f));
+            f.kind = DPG_FACTOR_PRIOR;
+            f.i = (int32_t)i;
+            for (int k = 0; k < 3; ++k) {
+                const double sd = (double)R.new_pass_std_dev[k];
+                f.info[k] = 1.0 / (sd * sd);
+            }
+            F.push_back(f);
+            cur_pass = pass[i];
+        } else if (R.odometry_constraints) {
+            dpg_factor f;
+            const int rc = dpg_odometry_factor(odom + 3 * (i - 1), odom + 3 * i, (int32_t)(i - 1), (int32_t)i,
+                                               R.motion_model[0], R.motion_model[1], R.motion_model[2],
+                                               R.motion_model[3], &f);
+            if (rc) return fail(rc, "odometry factor %lld has no motion (zero sigma)", (long long)i);
+            F.push_back(f);
+        }
+    }
+    const int64_t first_icp = (int64_t)F.size();
+    for (int64_t e = 0; e < E; ++e) {
+        dpg_factor f;
+        memset(&f, 0, sizeof(f));
+        f.kind = DPG_FACTOR_BETWEEN;
+        f.i = edges[(size_t)(2 * e)];
+        f.j = edges[(size_t)(2 * e + 1)];
+        F.push_back(f);
+    }
+    // 4. one batched ICP of every edge from the estimated poses (runIcp, dpg_slam.cc:362-446)
+    int rc = dpg_icp_batch_prepare(c, edges.data(), E, est, &I);
+    if (!rc) rc = dpg_icp_batch_run(c, 0, 0);
+    if (rc) return rc;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(DPG_ERR_HIP, "ICP batch failed");
+    const double t2 = now_ms();
+    // 5. batch Gauss-Newton from the estimated poses (optimizeGraph, dpg_slam.cc:111-119, 316-329)
+    if ((rc = dpg_gn_setup(c, V, F.data(), (int64_t)F.size(), 0, (int64_t)F.size(), &P))) return rc;
+    if ((rc = dpg_gn_take_icp_measurements(c, first_icp, E, n_succ, &I))) return rc;
+    {
+        std::vector<dpg_icp_result> res((size_t)E);
+        if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+        for (int64_t e = n_succ; e < E; ++e)
+            S.n_loop_closures += (res[(size_t)e].converged && res[(size_t)e].status == DPG_ICP_OK) ? 1 : 0;
+    }
+    for (int64_t v = 0; v < 3 * V; ++v) poses_out[v] = (double)est[v];
+    if ((rc = dpg_gn_set_poses(c, poses_out))) return rc;
+    if ((rc = gn_loop(c, P, poses_out, t2, now_ms(), &S.gn))) return rc;
+    const double t3 = now_ms();
+    S.n_factors = (int64_t)F.size();
+    S.n_icp_edges = E;
+    S.n_candidates = K;
+    S.ms_candidates = t1 - t0;
+    S.ms_icp = t2 - t1;
+    S.ms_gn = t3 - t2;
     if (st) *st = S;
     return DPG_OK;
 }

@@ -338,17 +338,6 @@ __device__ __forceinline__ double ld_agent(double* p) {
     return __longlong_as_double(
         (long long)__hip_atomic_load(reinterpret_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
-__device__ __forceinline__ void wait_geq(int32_t* w, int32_t target, int32_t* status) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) {
-            atomicExch(status, 2);
-            break;
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
 // Poll without the agent acquire: every handed-off byte the waiting workgroup reads is stored sc1
 // by its producer and loaded sc1 (ld_agent) here, so the L1 is never consulted for it (Guideline
 // 16, the sc1-load form); the wavefront fence only keeps the compiler from hoisting those loads.
@@ -363,13 +352,6 @@ __device__ __forceinline__ void wait_geq_sc1(int32_t* w, int32_t target, int32_t
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-__device__ __forceinline__ int claim(const int32_t* order, int32_t* ticket) {
-    __shared__ int s_task;
-    if (threadIdx.x == 0) s_task = order[atomicAdd(ticket, 1)];
-    __syncthreads();
-    return s_task;
-}
-
 __device__ __forceinline__ int claim_lds(const int32_t* order, int32_t* ticket, int* slot) {
     if (threadIdx.x == 0) *slot = order[atomicAdd(ticket, 1)];
     __syncthreads();

@@ -58,6 +58,11 @@ int dpg_launch_icp_kd(const float* ds_pts_dev, const float* tree_pts_dev, const 
 size_t dpg_icp_kd_lds_bytes(int32_t cap);
 /* angular-index variant (dpg_icp_ang.hip, the default): per-node angle-sorted clouds + buckets. */
 int32_t dpg_angle_buckets(void);
+/* loop-closure candidate search of the re-linearisation sweep (dpg_reopt.hip) */
+int dpg_launch_lc_count(const float* poses_dev, const int32_t* pass_dev, int64_t V, float within, float across,
+                        int32_t* count_dev, void* stream);
+int dpg_launch_lc_write(const float* poses_dev, const int32_t* pass_dev, int64_t V, float within, float across,
+                        const int64_t* off_dev, int32_t* pairs_dev, void* stream);
 int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                            int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
                            uint16_t* buckets_dev, void* stream);

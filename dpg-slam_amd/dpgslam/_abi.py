@@ -96,6 +96,29 @@ class GnStats(C.Structure):
     ]
 
 
+class ReoptParams(C.Structure):
+    _fields_ = [
+        ("max_node_dist_within_pass", C.c_float),
+        ("max_node_dist_across_passes", C.c_float),
+        ("new_pass_std_dev", C.c_float * 3),
+        ("motion_model", C.c_float * 4),
+        ("odometry_constraints", C.c_int32),
+    ]
+
+
+class ReoptStats(C.Structure):
+    _fields_ = [
+        ("n_factors", C.c_int64),
+        ("n_icp_edges", C.c_int64),
+        ("n_candidates", C.c_int64),
+        ("n_loop_closures", C.c_int64),
+        ("ms_candidates", C.c_double),
+        ("ms_icp", C.c_double),
+        ("ms_gn", C.c_double),
+        ("gn", GnStats),
+    ]
+
+
 # numpy mirrors of the array-of-struct types (same layout as the C structs)
 RESULT_DTYPE = np.dtype(
     [("T", "<f4", (6,)), ("z", "<f4", (3,)), ("converged", "<i4"), ("iterations", "<i4"),
@@ -167,7 +190,17 @@ SIGNATURES = {
     "dpg_gn_last_solve_ms": (C.c_float, [P]),
     "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,
                                     C.c_float, F64P, F64P]),
+    "dpg_reopt_params_default": (None, [C.POINTER(ReoptParams)]),
+    "dpg_loop_closure_candidates": (C.c_int64, [P, C.c_int64, I32P, F32P, C.c_float, C.c_float, I32P, C.c_int64]),
+    "dpg_reoptimize": (C.c_int, [P, C.c_int64, I32P, F32P, F32P, C.POINTER(IcpParams), C.POINTER(GnParams),
+                                 C.POINTER(ReoptParams), F64P, C.POINTER(ReoptStats)]),
 }
+
+
+def default_reopt_params() -> ReoptParams:
+    p = ReoptParams()
+    lib().dpg_reopt_params_default(C.byref(p))
+    return p
 
 _LIB = None
 

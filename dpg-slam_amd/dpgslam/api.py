@@ -293,5 +293,37 @@ class Context:
     def gn_factorizations(self) -> int:
         return int(lib().dpg_gn_factorizations(self.handle))
 
+    def loop_closure_candidates(self, est: np.ndarray, passes: np.ndarray, within: float = 5.0,
+                                across: float = 2.0) -> np.ndarray:
+        """reoptimize's candidate pairs (j, i) on the GPU (dpg_slam.cc:91-98), reference order."""
+        e, ps = _f32(est).reshape(-1, 3), np.ascontiguousarray(passes, np.int32)
+        L = lib()
+        n = L.dpg_loop_closure_candidates(self.handle, len(e), ptr(ps, C.c_int32), ptr(e, C.c_float), within, across,
+                                          None, 0)
+        if n < 0:
+            check(int(n), "dpg_loop_closure_candidates")
+        out = np.zeros((max(n, 1), 2), np.int32)
+        n2 = L.dpg_loop_closure_candidates(self.handle, len(e), ptr(ps, C.c_int32), ptr(e, C.c_float), within, across,
+                                           ptr(out, C.c_int32), n)
+        if n2 < 0:
+            check(int(n2), "dpg_loop_closure_candidates")
+        return out[:n]
+
+    def reoptimize(self, passes: np.ndarray, est: np.ndarray, odom: np.ndarray, icp_params=None, gn_params=None,
+                   reopt_params=None):
+        """DpgSLAM::reoptimize (dpg_slam.cc:35-120) over the uploaded scans: candidate search, one
+        batched ICP of every edge, factors, batch GN.  Returns (poses [V,3] f64, ReoptStats)."""
+        e, o = _f32(est).reshape(-1, 3), _f32(odom).reshape(-1, 3)
+        ps = np.ascontiguousarray(passes, np.int32)
+        ip = icp_params or _abi.default_icp_params()
+        gp = gn_params or _abi.default_gn_params()
+        rp = reopt_params or _abi.default_reopt_params()
+        X = np.zeros((len(e), 3), np.float64)
+        st = _abi.ReoptStats()
+        check(lib().dpg_reoptimize(self.handle, len(e), ptr(ps, C.c_int32), ptr(e, C.c_float), ptr(o, C.c_float),
+                                   C.byref(ip), C.byref(gp), C.byref(rp), ptr(X, C.c_double), C.byref(st)),
+              "dpg_reoptimize")
+        return X, st
+
     def gn_times_ms(self):
         return float(lib().dpg_gn_last_assemble_ms(self.handle)), float(lib().dpg_gn_last_solve_ms(self.handle))

@@ -248,6 +248,50 @@ int32_t dpg_gn_factorizations(dpg_ctx* ctx);
 float dpg_gn_last_assemble_ms(dpg_ctx* ctx);
 float dpg_gn_last_solve_ms(dpg_ctx* ctx);
 
+/* ---- re-linearisation sweep (DpgSLAM::reoptimize, dpg_slam.cc:35-120) ---- */
+typedef struct dpg_reopt_params {
+    float max_node_dist_within_pass;    /* 5.0 (parameters.h:212) */
+    float max_node_dist_across_passes;  /* 2.0 (parameters.h:224) */
+    float new_pass_std_dev[3];          /* prior sigmas x, y, theta: 0.2, 0.2, 0.15 (parameters.h:264-274) */
+    float motion_model[4];              /* transl<-transl, transl<-rot, rot<-transl, rot<-rot: 0.4 each
+                                           (parameters.h:279-309) */
+    int32_t odometry_constraints;       /* 1 (parameters.h:364) */
+} dpg_reopt_params;
+
+typedef struct dpg_reopt_stats {
+    int64_t n_factors;          /* priors + odometry + ICP factor slots */
+    int64_t n_icp_edges;        /* successive + loop-closure candidates (all aligned) */
+    int64_t n_candidates;       /* loop-closure candidates (j, i), j < i - 1, within the distance rule */
+    int64_t n_loop_closures;    /* candidates whose alignment converged (became factors) */
+    double ms_candidates;       /* GPU candidate search incl. the copy back of the pair list */
+    double ms_icp;              /* batched ICP (angle index + kernel) */
+    double ms_gn;               /* graph setup (symbolic analysis) + Gauss-Newton */
+    dpg_gn_stats gn;
+} dpg_reopt_stats;
+
+void dpg_reopt_params_default(dpg_reopt_params* p);
+
+/* The candidate pairs of the sweep (dpg_slam.cc:91-98): for i ascending, j = 0 .. i-2 ascending,
+ * (j, i) when the float distance of the estimated positions est_poses[j] - est_poses[i] (Eigen
+ * Vector2f::norm) is <= max_node_dist_within_pass (same pass_numbers) or
+ * <= max_node_dist_across_passes.  Computed on the GPU; writes min(count, cap) pairs {j, i} and
+ * returns the count (negative: error). */
+int64_t dpg_loop_closure_candidates(dpg_ctx* ctx, int64_t n_nodes, const int32_t* pass_numbers,
+                                    const float* est_poses /*[V][3]*/, float max_dist_within_pass,
+                                    float max_dist_across_passes, int32_t* pairs_out /*[cap][2]*/, int64_t cap);
+
+/* The whole sweep on the uploaded scans (dpg_scans_upload of all V nodes):
+ *   factors per node i in order: a prior (0, 0, 0) on the first node of each pass, otherwise the
+ *   odometry Between (i-1, i) from odom_only (if odometry_constraints); the ICP edges: every
+ *   successive pair (i-1, i) (always a factor, dpg_slam.cc:85-89) and every loop-closure
+ *   candidate (j, i) (a factor when the alignment converged, dpg_slam.cc:101-104) -- one batched
+ *   ICP of all of them from the estimated poses; then batch Gauss-Newton from est_poses (the
+ *   ISAM2 update of optimizeGraph, run to convergence: SURVEY Q1/Q6).
+ * poses_out[V][3] (double) receives the optimised poses. */
+int dpg_reoptimize(dpg_ctx* ctx, int64_t n_nodes, const int32_t* pass_numbers, const float* est_poses,
+                   const float* odom_only, const dpg_icp_params* icp_params, const dpg_gn_params* gn_params,
+                   const dpg_reopt_params* params, double* poses_out, dpg_reopt_stats* stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -192,3 +192,77 @@ def gn_delta(poses, factors):
     if rc:
         raise RuntimeError(f"oracle_gn_delta failed ({rc})")
     return d.reshape(-1, 3), err.value
+
+
+def loop_closure_candidates(est, passes, within=5.0, across=2.0):
+    """reoptimize's candidate pairs (dpg_slam.cc:91-98): for i ascending, j = 0 .. i-2 ascending,
+    (j, i) when the float32 (p_j - p_i).norm() (Eigen Vector2f: sqrt(dx*dx + dy*dy), correctly
+    rounded) is <= within (same pass, parameters.h:212) or <= across (parameters.h:224)."""
+    e = _f32(est).reshape(-1, 3)
+    ps = np.asarray(passes, np.int64)
+    out = []
+    for i in range(2, len(e)):
+        d = e[:i - 1, :2] - e[i, :2]
+        dist = np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1])
+        thr = np.where(ps[:i - 1] == ps[i], np.float32(within), np.float32(across))
+        js = np.nonzero(dist <= thr)[0]
+        out.extend((int(j), i) for j in js)
+    return np.array(out, np.int32).reshape(-1, 2)
+
+
+def odometry_factor(odom_prev, odom_cur, i_prev, i_cur, motion=(0.4, 0.4, 0.4, 0.4)):
+    """The odometry Between of reoptimize (dpg_slam.cc:55-75): displacement by
+    inverseTransformPoint, sigmas from the motion model in float, Diagonal::Sigmas -> 1/sigma^2."""
+    from dpgslam import _abi
+    d = inverse_transform_point(_f32(odom_cur), _f32(odom_prev))
+    f32 = np.float32
+    norm = np.sqrt(f32(d[0]) * f32(d[0]) + f32(d[1]) * f32(d[1]))
+    m = [f32(x) for x in motion]
+    st = f32(m[0] * norm) + f32(m[1] * np.abs(f32(d[2])))
+    sr = f32(m[2] * norm) + f32(m[3] * np.abs(f32(d[2])))
+    f = np.zeros(1, _abi.FACTOR_DTYPE)
+    f["kind"], f["i"], f["j"] = _abi.DPG_FACTOR_BETWEEN, i_prev, i_cur
+    f["z"] = np.asarray(d, np.float32).astype(np.float64)
+    st, sr = float(st), float(sr)
+    f["info"] = [1.0 / (st * st), 1.0 / (st * st), 1.0 / (sr * sr)]
+    return f
+
+
+def reoptimize(pts, offsets, passes, est, odom, icp_params=None, gn_params=None, within=5.0, across=2.0,
+               prior_sigmas=(0.2, 0.2, 0.15), threads=1):
+    """DpgSLAM::reoptimize (dpg_slam.cc:35-120), restated: per node a prior on the first node of a
+    pass or the odometry Between; the successive alignment (always a factor) and every loop-closure
+    candidate (a factor when converged); batch GN from the estimated poses.  The oracle ICP aligns
+    every edge (grid NN); returns (poses, edges, results)."""
+    from dpgslam import _abi
+    e = _f32(est).reshape(-1, 3)
+    V = len(e)
+    p = icp_params or _abi.default_icp_params()
+    lc = loop_closure_candidates(e, passes, within, across)
+    succ = np.stack([np.arange(V - 1), np.arange(1, V)], 1).astype(np.int32)
+    edges = np.concatenate([succ, lc], 0).astype(np.int32)
+    res, _ = icp_batch(pts, offsets, edges, e, p, NN_GRID, threads)
+    F = []
+    cur = None
+    for i in range(V):
+        if i == 0 or passes[i] != cur:
+            f = np.zeros(1, _abi.FACTOR_DTYPE)
+            f["kind"], f["i"] = _abi.DPG_FACTOR_PRIOR, i
+            s = np.asarray(prior_sigmas, np.float32).astype(np.float64)
+            f["info"] = 1.0 / (s * s)
+            F.append(f)
+            cur = passes[i]
+        else:
+            F.append(odometry_factor(odom[i - 1], odom[i], i - 1, i))
+    info = np.array([1.0 / float(np.float32(p.laser_x_variance)), 1.0 / float(np.float32(p.laser_y_variance)),
+                     1.0 / float(np.float32(p.laser_theta_variance))])
+    for k, (a, b) in enumerate(edges):
+        keep = k < len(succ) or (res["converged"][k] != 0 and res["status"][k] == _abi.DPG_ICP_OK)
+        if keep:
+            f = np.zeros(1, _abi.FACTOR_DTYPE)
+            f["kind"], f["i"], f["j"] = _abi.DPG_FACTOR_BETWEEN, a, b
+            f["z"] = res["z"][k].astype(np.float64)
+            f["info"] = info
+            F.append(f)
+    X, st = optimize_graph(e.astype(np.float64), np.concatenate(F), gn_params)
+    return X, edges, res, st

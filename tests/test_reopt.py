@@ -1,0 +1,86 @@
+"""Re-linearisation sweep (DpgSLAM::reoptimize, dpg_slam.cc:35-120): the GPU
+loop-closure candidate search, and the whole sweep (candidates -> batched ICP -> factors -> batch
+GN) against the oracle's restatement."""
+import numpy as np
+import pytest
+
+from conftest import angle_wrap
+
+
+def _passes(V, split):
+    p = np.zeros(V, np.int32)
+    p[split:] = 1
+    return p
+
+
+def test_candidate_rule_oracle_vs_kdtree(workload):
+    """The oracle's O(V^2) candidate rule == an independent k-d tree formulation (float32 norm,
+    <= threshold by pass), on config 2 with a pass boundary."""
+    from scipy.spatial import cKDTree
+    from oracle import oracle as O
+    w = workload("config2")
+    passes = _passes(w.V, 250)
+    c = O.loop_closure_candidates(w.est, passes)
+    xy = w.est[:, :2].astype(np.float64)
+    pr = cKDTree(xy).query_pairs(5.0 * 1.001, output_type="ndarray")
+    j, i = np.minimum(pr[:, 0], pr[:, 1]), np.maximum(pr[:, 0], pr[:, 1])
+    keep = i - j >= 2
+    j, i = j[keep], i[keep]
+    d = w.est[j, :2] - w.est[i, :2]
+    dist = np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1])
+    thr = np.where(passes[j] == passes[i], np.float32(5.0), np.float32(2.0))
+    ok = dist <= thr
+    ref = np.stack([j[ok], i[ok]], 1)
+    ref = ref[np.lexsort((ref[:, 0], ref[:, 1]))]
+    np.testing.assert_array_equal(c, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("split", [5000, 2500])
+def test_gpu_candidates_match_oracle(ctx, workload, split):
+    from oracle import oracle as O
+    w = workload("config4")
+    passes = _passes(w.V, split)
+    g = ctx.loop_closure_candidates(w.est, passes)
+    o = O.loop_closure_candidates(w.est, passes)
+    assert len(o) > 0
+    np.testing.assert_array_equal(g, o)
+
+
+@pytest.mark.gpu
+def test_gpu_candidates_edge_cases(ctx):
+    from oracle import oracle as O
+    for V in (1, 2, 3):
+        est = np.zeros((V, 3), np.float32)
+        assert len(ctx.loop_closure_candidates(est, np.zeros(V, np.int32))) == len(O.loop_closure_candidates(est, np.zeros(V, np.int32)))
+    # exactly on the threshold (float): 5.0 is in, the next float above is out; across passes 2.0
+    est = np.zeros((6, 3), np.float32)
+    est[3, 0] = 5.0
+    est[4, 0] = np.nextafter(np.float32(5.0), np.float32(6.0))
+    est[5, 0] = 2.0
+    passes = np.array([0, 0, 0, 0, 0, 1], np.int32)
+    g = ctx.loop_closure_candidates(est, passes)
+    np.testing.assert_array_equal(g, O.loop_closure_candidates(est, passes))
+    assert [0, 3] in g.tolist() and [0, 4] not in g.tolist() and [0, 5] in g.tolist()
+
+
+@pytest.mark.gpu
+def test_reoptimize_matches_oracle(ctx, workload):
+    """The whole sweep on 60 nodes of config 2 split into two passes: same candidate set and
+    loop-closure decisions, poses within 1e-6 of the oracle's (GPU ICP is bit-exact, GN to
+    max|delta| < 1e-10 on both sides)."""
+    from oracle import oracle as O
+    w = workload("config2")
+    V = 60
+    pts = w.pts[:w.offsets[V]]
+    offs = w.offsets[:V + 1]
+    passes = _passes(V, 30)
+    ctx.upload_scans(pts, offs, 5)
+    X, st = ctx.reoptimize(passes, w.est[:V], w.odom[:V])
+    Xo, edges, res, so = O.reoptimize(pts, offs, passes, w.est[:V], w.odom[:V])
+    assert st.n_icp_edges == len(edges) and st.n_candidates == len(edges) - (V - 1)
+    conv = (res["converged"][V - 1:] != 0) & (res["status"][V - 1:] == 0)
+    assert st.n_loop_closures == int(conv.sum()) and st.n_loop_closures > 0
+    err = np.abs(np.concatenate([X[:, :2] - Xo[:, :2], angle_wrap(X[:, 2:] - Xo[:, 2:])], 1)).max()
+    assert err < 1e-6, err
+    assert st.gn.iterations < 100
