@@ -82,6 +82,8 @@ struct dpg_ctx {
     bool own_stream = false;
     hipEvent_t ev[8] = {};
     int32_t icp_variant = DPG_ICP_ANGULAR;
+    float map_ms = 0.f;             // last dpg_get_map kernel (HIP events map_ev)
+    hipEvent_t map_ev[2] = {};
     // scan store (batch form)
     DevBuf<float> full, ds;
     DevBuf<int64_t> ds_off_dev;
@@ -238,6 +240,7 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     c->buckets.release(); c->s_buckets.release();
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+    for (auto& e : c->map_ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     if (c == g_default_ctx) g_default_ctx = nullptr;
     delete c;
@@ -739,6 +742,52 @@ int64_t dpg_loop_closure_candidates(dpg_ctx* c, int64_t V, const int32_t* pass, 
     if (pairs_out && cap > 0) memcpy(pairs_out, pairs.data(), sizeof(int32_t) * 2 * (size_t)std::min(K, cap));
     return K;
 }
+
+int64_t dpg_get_map(dpg_ctx* c, const float* est, int32_t fraction, float* out, int64_t cap) {
+    if (!c || !est || fraction <= 0) return fail(DPG_ERR_ARG, "bad arguments");
+    const int64_t V = c->n_nodes;
+    if (V <= 0 || (int64_t)c->full_off.size() != V + 1) return fail(DPG_ERR_STATE, "no scans uploaded");
+    const int64_t P = c->full_off[(size_t)V];
+    const int64_t K = (P + fraction - 1) / fraction;
+    if (!out || cap <= 0 || K == 0) return K;
+    // Rotation2Df(angle): cosf/sinf on the host, as the reference evaluates them
+    std::vector<float> fr((size_t)(4 * V));
+    for (int64_t v = 0; v < V; ++v) {
+        fr[(size_t)(4 * v)] = est[3 * v];
+        fr[(size_t)(4 * v + 1)] = est[3 * v + 1];
+        fr[(size_t)(4 * v + 2)] = cosf(est[3 * v + 2]);
+        fr[(size_t)(4 * v + 3)] = sinf(est[3 * v + 2]);
+    }
+    DevBuf<float> dfr, dout;
+    DevBuf<int64_t> doff;
+    int64_t ret = -1;
+    do {
+        if (dfr.reserve((size_t)(4 * V)) || dout.reserve((size_t)(2 * K)) || doff.reserve((size_t)(V + 1))) break;
+        if (hipMemcpyAsync(dfr.p, fr.data(), sizeof(float) * 4 * V, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipMemcpyAsync(doff.p, c->full_off.data(), sizeof(int64_t) * (V + 1), hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess)
+            break;
+        if (!c->map_ev[0] && (hipEventCreate(&c->map_ev[0]) != hipSuccess || hipEventCreate(&c->map_ev[1]) != hipSuccess))
+            break;
+        if (hipEventRecord(c->map_ev[0], c->stream) != hipSuccess) break;
+        if (dpg_launch_map_points(c->full.p, doff.p, dfr.p, V, fraction, dout.p, c->stream)) break;
+        if (hipEventRecord(c->map_ev[1], c->stream) != hipSuccess) break;
+        if (hipMemcpyAsync(out, dout.p, sizeof(float) * 2 * std::min(K, cap), hipMemcpyDeviceToHost, c->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            break;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, c->map_ev[0], c->map_ev[1]) == hipSuccess) c->map_ms = ms;
+        ret = K;
+    } while (false);
+    dfr.release();
+    dout.release();
+    doff.release();
+    if (ret < 0) return fail(DPG_ERR_HIP, "map assembly failed: %s", hipGetErrorString(hipGetLastError()));
+    return ret;
+}
+
+float dpg_get_map_kernel_ms(dpg_ctx* c) { return c ? c->map_ms : -1.f; }
 
 int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, const float* odom,
                    const dpg_icp_params* ip, const dpg_gn_params* gp, const dpg_reopt_params* rp, double* poses_out,

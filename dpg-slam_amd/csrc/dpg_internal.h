@@ -63,6 +63,9 @@ int dpg_launch_lc_count(const float* poses_dev, const int32_t* pass_dev, int64_t
                         int32_t* count_dev, void* stream);
 int dpg_launch_lc_write(const float* poses_dev, const int32_t* pass_dev, int64_t V, float within, float across,
                         const int64_t* off_dev, int32_t* pairs_dev, void* stream);
+/* map assembly (GetMap): frames_dev[V][4] = x, y, cos, sin (dpg_reopt.hip) */
+int dpg_launch_map_points(const float* pts_dev, const int64_t* off_dev, const float* frames_dev, int64_t V,
+                          int32_t fraction, float* out_dev, void* stream);
 int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                            int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
                            uint16_t* buckets_dev, void* stream);

@@ -83,3 +83,42 @@ extern "C" int dpg_launch_lc_write(const float* poses_dev, const int32_t* pass_d
                        off_dev, pairs_dev);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
+
+// ---- map assembly (DpgSLAM::GetMap, dpg_slam.cc:555-575) ----
+// Every node's base_link cloud into the map frame with the node's estimated pose
+// (math_utils::transformPoint(p, 0, pos, angle): Rotation2Df(angle) * p + pos), keeping the points
+// whose running index over all nodes is a multiple of display_points_fraction_.  cos/sin of each
+// node's angle come from the host (float cosf/sinf, what Eigen's Rotation2Df evaluates) so the
+// device does only the multiply-adds -- bit-identical.  One workgroup per node; a streaming,
+// HBM-bound kernel (8 B read per point, 8 B written per kept point).
+namespace {
+__global__ __launch_bounds__(kRT) void map_points_kernel(const float2* __restrict__ pts,
+                                                         const int64_t* __restrict__ off,
+                                                         const float4* __restrict__ frame /* x, y, c, s */,
+                                                         int32_t fraction, float2* __restrict__ out) {
+    const int v = blockIdx.x;
+    const int64_t b = off[v], e = off[v + 1];
+    const float4 f = frame[v];
+    const float ns = -f.w;
+    int64_t g = b + threadIdx.x;
+    int64_t r = g % fraction;
+    for (; g < e; g += kRT) {
+        if (r == 0) {
+            const float2 p = pts[g];
+            out[g / fraction] = make_float2(f.x + (f.z * p.x + ns * p.y), f.y + (f.w * p.x + f.z * p.y));
+        }
+        r += kRT % fraction;
+        if (r >= fraction) r -= fraction;
+    }
+}
+}  // namespace
+
+extern "C" int dpg_launch_map_points(const float* pts_dev, const int64_t* off_dev, const float* frames_dev, int64_t V,
+                                     int32_t fraction, float* out_dev, void* stream) {
+    if (V <= 0) return DPG_OK;
+    if (fraction <= 0) return DPG_ERR_ARG;
+    hipLaunchKernelGGL(map_points_kernel, dim3((unsigned)V), dim3(kRT), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const float2*>(pts_dev), off_dev, reinterpret_cast<const float4*>(frames_dev),
+                       fraction, reinterpret_cast<float2*>(out_dev));
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}

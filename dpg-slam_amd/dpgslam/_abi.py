@@ -191,6 +191,8 @@ SIGNATURES = {
     "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,
                                     C.c_float, F64P, F64P]),
     "dpg_reopt_params_default": (None, [C.POINTER(ReoptParams)]),
+    "dpg_get_map": (C.c_int64, [P, F32P, C.c_int32, F32P, C.c_int64]),
+    "dpg_get_map_kernel_ms": (C.c_float, [P]),
     "dpg_loop_closure_candidates": (C.c_int64, [P, C.c_int64, I32P, F32P, C.c_float, C.c_float, I32P, C.c_int64]),
     "dpg_reoptimize": (C.c_int, [P, C.c_int64, I32P, F32P, F32P, C.POINTER(IcpParams), C.POINTER(GnParams),
                                  C.POINTER(ReoptParams), F64P, C.POINTER(ReoptStats)]),

@@ -309,6 +309,22 @@ class Context:
             check(int(n2), "dpg_loop_closure_candidates")
         return out[:n]
 
+    def get_map(self, est: np.ndarray, display_points_fraction: int = 10) -> np.ndarray:
+        """DpgSLAM::GetMap (dpg_slam.cc:555-575) over the uploaded clouds: map-frame points [K, 2]."""
+        e = _f32(est).reshape(-1, 3)
+        L = lib()
+        n = L.dpg_get_map(self.handle, ptr(e, C.c_float), display_points_fraction, None, 0)
+        if n < 0:
+            check(int(n), "dpg_get_map")
+        out = np.zeros((max(n, 1), 2), np.float32)
+        n2 = L.dpg_get_map(self.handle, ptr(e, C.c_float), display_points_fraction, ptr(out, C.c_float), n)
+        if n2 < 0:
+            check(int(n2), "dpg_get_map")
+        return out[:n]
+
+    def get_map_kernel_ms(self) -> float:
+        return float(lib().dpg_get_map_kernel_ms(self.handle))
+
     def reoptimize(self, passes: np.ndarray, est: np.ndarray, odom: np.ndarray, icp_params=None, gn_params=None,
                    reopt_params=None):
         """DpgSLAM::reoptimize (dpg_slam.cc:35-120) over the uploaded scans: candidate search, one

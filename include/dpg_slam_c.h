@@ -288,6 +288,14 @@ int64_t dpg_loop_closure_candidates(dpg_ctx* ctx, int64_t n_nodes, const int32_t
  *   ICP of all of them from the estimated poses; then batch Gauss-Newton from est_poses (the
  *   ISAM2 update of optimizeGraph, run to convergence: SURVEY Q1/Q6).
  * poses_out[V][3] (double) receives the optimised poses. */
+/* DpgSLAM::GetMap (dpg_slam.cc:555-575) over the uploaded full clouds: every node's base_link
+ * points in the map frame (transformPoint with the node's estimated pose), one point in
+ * display_points_fraction (10, parameters.h:22) by the running index over all nodes.  Writes
+ * min(count, cap) points and returns the count, ceil(P / fraction) (negative: error). */
+int64_t dpg_get_map(dpg_ctx* ctx, const float* est_poses /*[V][3]*/, int32_t display_points_fraction,
+                    float* map_out /*[cap][2]*/, int64_t cap);
+float dpg_get_map_kernel_ms(dpg_ctx* ctx);   /* device time of the last dpg_get_map kernel */
+
 int dpg_reoptimize(dpg_ctx* ctx, int64_t n_nodes, const int32_t* pass_numbers, const float* est_poses,
                    const float* odom_only, const dpg_icp_params* icp_params, const dpg_gn_params* gn_params,
                    const dpg_reopt_params* params, double* poses_out, dpg_reopt_stats* stats);

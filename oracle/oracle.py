@@ -266,3 +266,26 @@ def reoptimize(pts, offsets, passes, est, odom, icp_params=None, gn_params=None,
             F.append(f)
     X, st = optimize_graph(e.astype(np.float64), np.concatenate(F), gn_params)
     return X, edges, res, st
+
+
+def get_map(pts, offsets, est, fraction=10):
+    """DpgSLAM::GetMap (dpg_slam.cc:555-575): every node's base_link point in the map frame by
+    math_utils::transformPoint (Rotation2Df(angle) * p + pos, float; cos/sin as cosf/sinf), one in
+    `fraction` by the running point index over all nodes (display_points_fraction_)."""
+    p = _f32(pts).reshape(-1, 2)
+    e = _f32(est).reshape(-1, 3)
+    offs = np.asarray(offsets, np.int64)
+    keep = np.arange(0, offs[-1], fraction)
+    node = np.searchsorted(offs, keep, side="right") - 1
+    c = np.array([_cos_sin(e[v, 2]) for v in range(len(e))], np.float32)
+    x, y = p[keep, 0], p[keep, 1]
+    cc, ss = c[node, 0], c[node, 1]
+    rx = cc * x + (-ss) * y
+    ry = ss * x + cc * y
+    return np.stack([e[node, 0] + rx, e[node, 1] + ry], 1).astype(np.float32)
+
+
+def _cos_sin(th):
+    """cosf/sinf of a float angle via the oracle's C transformPoint of unit vectors."""
+    a = transform_point(np.array([1.0, 0.0, 0.0], np.float32), np.array([0.0, 0.0, th], np.float32))
+    return a[0], a[1]

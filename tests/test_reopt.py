@@ -84,3 +84,16 @@ def test_reoptimize_matches_oracle(ctx, workload):
     err = np.abs(np.concatenate([X[:, :2] - Xo[:, :2], angle_wrap(X[:, 2:] - Xo[:, 2:])], 1)).max()
     assert err < 1e-6, err
     assert st.gn.iterations < 100
+
+
+@pytest.mark.gpu
+def test_get_map_bit_exact(ctx, workload):
+    """GetMap (dpg_slam.cc:555-575) on config 2's 500 full clouds (2.5 M points): every kept point
+    bit-identical to the oracle's transformPoint, fraction 10 (parameters.h:22) and 7."""
+    from oracle import oracle as O
+    w = workload("config2")
+    ctx.upload_scans(w.pts, w.offsets, 5)
+    for frac in (10, 7):
+        g = ctx.get_map(w.est, frac)
+        o = O.get_map(w.pts, w.offsets, w.est, frac)
+        assert g.shape == o.shape and g.tobytes() == o.tobytes()
