@@ -635,7 +635,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
                 B.code = (k + 1 >= kp.max_iter || (cos_angle >= kp.rot_thr && tsq <= kp.eps) ||
                           fabs(mse - prev_mse) < kp.mse_abs) ? 1 : 0;
                 B.prev_mse = mse;
-                inverse2(Nf, B.inv);
             }
             if (lane == 0) {
                 *L.bc = B;
@@ -668,6 +667,16 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
         }
         ++k;
         if (code == 1) { converged = 1; break; }
+        if (__builtin_amdgcn_readlane(last, 0)) {   // off the publish path: the next reciprocal
+            double inv[4];                          // tests' inverse, while the others move points
+            float Fn[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) Fn[q] = uni(L.bc->F[q]);
+            inverse2(Fn, inv);
+            if (lane == 0)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) L.bc->inv[q] = inv[q];
+        }
         __syncthreads();   // moved source complete before the next reciprocal tests
 #ifdef DPG_ICP_TIMING
         {
