@@ -200,6 +200,11 @@ dpg_ctx* g_default_ctx = nullptr;
 extern "C" {
 
 const char* dpg_last_error(void) { return g_err.c_str(); }
+
+// internal (dpg_internal.h): error reporting and the context's stream for the other TUs
+int dpg_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+void* dpg_ctx_stream_of(dpg_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
+int dpg_ctx_device_of(dpg_ctx* c) { return c ? c->device : -1; }
 const char* dpg_version(void) { return "dpg-mi355x 0.1 (gfx950)"; }
 
 dpg_ctx* dpg_ctx_create(int device) {

@@ -13,6 +13,11 @@
 extern "C" {
 #endif
 
+/* error message + code for dpg_last_error; the context's stream / device (dpg_api.hip) */
+int dpg_set_error(int code, const char* msg);
+void* dpg_ctx_stream_of(dpg_ctx* c);
+int dpg_ctx_device_of(dpg_ctx* c);
+
 /* One ICP edge as the kernel sees it (64 B).  Offsets/counts are in points (float2). */
 typedef struct dpg_icp_edge {
     int32_t src_ds_off, n_src_ds;    /* downsampled node_2 cloud (ICP source) */

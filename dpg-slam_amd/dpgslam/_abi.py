@@ -134,8 +134,43 @@ F32P = C.POINTER(C.c_float)
 F64P = C.POINTER(C.c_double)
 I32P = C.POINTER(C.c_int32)
 I64P = C.POINTER(C.c_int64)
+U8P = C.POINTER(C.c_uint8)
 
 # name -> (restype, argtypes); the full exported surface of include/*.h
+
+class ChangeParams(C.Structure):
+    """dpg_change_params -- DpgParameters (parameters.h:37-87) + the laser pose (parameters.h:319-339)."""
+
+    _fields_ = [
+        ("num_sectors", C.c_int32),
+        ("current_pose_chain_len", C.c_int32),
+        ("num_bins_for_change_detection", C.c_int32),
+        ("pad", C.c_int32),
+        ("delta_change_threshold", C.c_double),
+        ("current_pose_graph_coverage_threshold", C.c_double),
+        ("occ_grid_resolution", C.c_double),
+        ("minimum_percent_active_sectors", C.c_float),
+        ("distance_threshold_for_local_submap_nodes", C.c_float),
+        ("laser", C.c_float * 3),
+        ("pad2", C.c_float),
+    ]
+
+
+class ChangeStats(C.Structure):
+    """dpg_change_stats -- counters and timings of one dpg_execute_dpg."""
+
+    _fields_ = [(n, C.c_int64) for n in (
+        "n_chain", "n_candidates", "n_submap_nodes", "n_chain_cells", "n_uncovered", "n_added", "n_removed",
+        "n_committed", "n_sectors_deactivated", "n_nodes_deactivated", "grid_cells", "n_samples")] + [
+        ("ms_total", C.c_double), ("ms_kernels", C.c_double)]
+
+    COUNTERS = ("n_chain", "n_candidates", "n_submap_nodes", "n_chain_cells", "n_uncovered", "n_added",
+                "n_removed", "n_committed", "n_sectors_deactivated", "n_nodes_deactivated")
+
+    def counters(self) -> dict:
+        return {k: int(getattr(self, k)) for k in self.COUNTERS}
+
+
 SIGNATURES = {
     "dpg_last_error": (C.c_char_p, []),
     "dpg_version": (C.c_char_p, []),
@@ -194,6 +229,13 @@ SIGNATURES = {
     "dpg_get_map": (C.c_int64, [P, F32P, C.c_int32, F32P, C.c_int64]),
     "dpg_get_map_kernel_ms": (C.c_float, [P]),
     "dpg_loop_closure_candidates": (C.c_int64, [P, C.c_int64, I32P, F32P, C.c_float, C.c_float, I32P, C.c_int64]),
+    "dpg_change_params_default": (None, [C.POINTER(ChangeParams)]),
+    "dpg_dpg_create": (P, [P, C.c_int64, I64P, F32P, F32P, C.POINTER(ChangeParams)]),
+    "dpg_dpg_destroy": (None, [P]),
+    "dpg_execute_dpg": (C.c_int, [P, C.c_int64, C.c_int64, F32P, C.POINTER(ChangeStats)]),
+    "dpg_dpg_fetch": (C.c_int, [P, U8P, U8P, U8P]),
+    "dpg_dpg_load": (C.c_int, [P, U8P, U8P, U8P]),
+    "dpg_active_dynamic_points": (C.c_int64, [P, C.c_int64, F32P, F32P, C.c_int64, I64P]),
     "dpg_reoptimize": (C.c_int, [P, C.c_int64, I32P, F32P, F32P, C.POINTER(IcpParams), C.POINTER(GnParams),
                                  C.POINTER(ReoptParams), F64P, C.POINTER(ReoptStats)]),
 }
@@ -251,6 +293,15 @@ def default_icp_params() -> IcpParams:
     p = IcpParams()
     lib().dpg_icp_params_default(C.byref(p))
     return p
+
+
+def default_change_params() -> ChangeParams:
+    p = ChangeParams()
+    lib().dpg_change_params_default(C.byref(p))
+    return p
+
+
+default_change_params_host = default_change_params
 
 
 def default_gn_params() -> GnParams:

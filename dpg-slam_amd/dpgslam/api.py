@@ -343,3 +343,77 @@ class Context:
 
     def gn_times_ms(self):
         return float(lib().dpg_gn_last_assemble_ms(self.handle)), float(lib().dpg_gn_last_solve_ms(self.handle))
+
+
+# ------------------------------------------------------------------ DPG change detection
+class DpgStore:
+    """The dynamic node state of DpgSLAM (per-beam labels and sectors, per-node sector activation and
+    activity, dpg_measurement.h / dpg_node.h), resident on the context's GPU, and executeDPG over it
+    (dpg_slam.cc:865-886).  ranges: [V, n_beams] (or concatenated with offsets); geom: [V, 3] =
+    angle_min, angle_max, range_max per scan."""
+
+    def __init__(self, ctx: Context, ranges, geom, offsets=None, params=None):
+        r = _f32(ranges)
+        if offsets is None:
+            V, nb = r.shape
+            offsets = np.arange(V + 1, dtype=np.int64) * nb
+        off = np.ascontiguousarray(offsets, np.int64)
+        self.V = len(off) - 1
+        self.B = int(off[-1])
+        g = _f32(geom).reshape(self.V, 3)
+        self.params = params or _abi.default_change_params()
+        self.ctx = ctx
+        self.handle = lib().dpg_dpg_create(ctx.handle, self.V, ptr(off, C.c_int64), ptr(r.reshape(-1), C.c_float),
+                                           ptr(g, C.c_float), C.byref(self.params))
+        if not self.handle:
+            raise _abi.DpgError("dpg_dpg_create failed: " + (lib().dpg_last_error() or b"").decode())
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().dpg_dpg_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def execute_dpg(self, n_nodes: int, current_pass_len: int, est) -> "_abi.ChangeStats":
+        e = _f32(est).reshape(-1, 3)
+        st = _abi.ChangeStats()
+        check(lib().dpg_execute_dpg(self.handle, n_nodes, current_pass_len, ptr(e, C.c_float), C.byref(st)),
+              "dpg_execute_dpg")
+        return st
+
+    def fetch(self):
+        """(labels [B] u8, sector_active [V] u8 bitmask, node_active [V] u8)."""
+        lab = np.zeros(self.B, np.uint8)
+        sec = np.zeros(self.V, np.uint8)
+        act = np.zeros(self.V, np.uint8)
+        check(lib().dpg_dpg_fetch(self.handle, ptr(lab, C.c_uint8), ptr(sec, C.c_uint8), ptr(act, C.c_uint8)),
+              "dpg_dpg_fetch")
+        return lab, sec, act
+
+    def load(self, labels=None, sector_active=None, node_active=None):
+        a = [None if x is None else np.ascontiguousarray(x, np.uint8) for x in (labels, sector_active, node_active)]
+        check(lib().dpg_dpg_load(self.handle, *[ptr(x, C.c_uint8) for x in a]), "dpg_dpg_load")
+
+    def active_dynamic_points(self, n_nodes: int, est):
+        """getActiveAndDynamicMapPoints (dpg_slam.cc:832-863): dict of the four [n, 2] point lists."""
+        e = _f32(est).reshape(-1, 3)
+        counts = np.zeros(4, np.int64)
+        n = lib().dpg_active_dynamic_points(self.handle, n_nodes, ptr(e, C.c_float), None, 0, ptr(counts, C.c_int64))
+        if n < 0:
+            check(int(n), "dpg_active_dynamic_points")
+        out = np.zeros((max(n, 1), 2), np.float32)
+        n2 = lib().dpg_active_dynamic_points(self.handle, n_nodes, ptr(e, C.c_float), ptr(out, C.c_float), n,
+                                             ptr(counts, C.c_int64))
+        if n2 < 0:
+            check(int(n2), "dpg_active_dynamic_points")
+        names = ("active_static", "active_added", "dynamic_removed", "dynamic_added")
+        res, k = {}, 0
+        for name, c in zip(names, counts):
+            res[name] = out[k:k + c].copy()
+            k += int(c)
+        return res

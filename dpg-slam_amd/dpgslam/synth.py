@@ -190,3 +190,70 @@ def generate(cfg: SynthConfig | str) -> Workload:
     base = np.concatenate(base).astype(FACTOR_DTYPE)
     return Workload(cfg=cfg, segs=segs, gt=gt, ranges=ranges, pts=pts, offsets=offs, est=est, odom=odom,
                     edges=edges, n_successive=len(succ), base_factors=base, icp_factor_first=len(base))
+
+
+# ------------------------------------------------------------------ config 5 (dynamic passes)
+@dataclass
+class DynamicWorkload:
+    """Multi-pass workload for DPG change detection (BASELINE config 5): one static world,
+    a set of movable boxes of which each pass sees its own subset (boxes added or removed between
+    passes), one trajectory per pass through the same area, exactly ray-cast scans per pass."""
+    ranges: np.ndarray      # [V, n_beams] f32
+    geom: np.ndarray        # [V, 3] f32: angle_min, angle_max, range_max
+    est: np.ndarray         # [V, 3] f32 node poses (map frame = world frame)
+    pass_of: np.ndarray     # [V] i32
+    pass_start: np.ndarray  # [P + 1] first node of each pass
+    boxes: np.ndarray       # [K, 4] x0, y0, x1, y1 of the movable boxes
+    present: np.ndarray     # [P, K] bool
+
+    @property
+    def V(self) -> int:
+        return len(self.est)
+
+
+def _box_segs(b) -> list:
+    x0, y0, x1, y1 = (float(v) for v in b)
+    return [[x0, y0, x1, y0], [x1, y0, x1, y1], [x1, y1, x0, y1], [x0, y1, x0, y0]]
+
+
+def make_dynamic(n_passes: int = 4, nodes_per_pass: int = 2500, n_beams: int = 5000, seed: int = 5,
+                 world_size: float = 40.0, range_max: float = RANGE_MAX, n_boxes: int = 24,
+                 range_noise: float = 0.01, threads: int = 0) -> DynamicWorkload:
+    L = lib()
+    segs = np.zeros((4096, 4), np.float32)
+    ns = L.dpg_synth_world(seed, world_size, ptr(segs, C.c_float), len(segs))
+    static = segs[:ns]
+    rng = np.random.default_rng(seed)
+    boxes = []
+    for _ in range(n_boxes):
+        w, h = rng.uniform(0.4, 1.2, 2)
+        x, y = rng.uniform(2.0, world_size - 2.0 - 1.2, 2)
+        boxes.append([x, y, x + w, y + h])
+    boxes = np.asarray(boxes, np.float32)
+    present = np.zeros((n_passes, n_boxes), bool)
+    present[0] = rng.random(n_boxes) < 0.5
+    for p in range(1, n_passes):   # each later pass moves about a third of the boxes in or out
+        flip = rng.random(n_boxes) < 0.33
+        present[p] = present[p - 1] ^ flip
+    all_segs = np.ascontiguousarray(np.concatenate([static, np.asarray(sum((_box_segs(b) for b in boxes), []),
+                                                                       np.float32)]), np.float32)
+    threads = threads or min(16, os.cpu_count() or 1)
+    gts, rs = [], []
+    for p in range(n_passes):
+        gt = np.zeros((nodes_per_pass, 3), np.float64)
+        _abi.check(L.dpg_synth_trajectory(seed * 131 + p, nodes_per_pass, ptr(all_segs, C.c_float), len(all_segs),
+                                          world_size, 1.0, ptr(gt, C.c_double)), "dpg_synth_trajectory")
+        bs = [s for k in range(n_boxes) if present[p, k] for s in _box_segs(boxes[k])]
+        world = np.ascontiguousarray(np.concatenate([static, np.asarray(bs, np.float32).reshape(-1, 4)]), np.float32)
+        r = np.zeros((nodes_per_pass, n_beams), np.float32)
+        _abi.check(L.dpg_synth_scans(ptr(gt, C.c_double), nodes_per_pass, ptr(world, C.c_float), len(world), n_beams,
+                                     ANGLE_MIN, ANGLE_MAX, range_max, LASER[0], LASER[1], LASER[2], range_noise,
+                                     seed * 7919 + 17 * p + 1, threads, ptr(r, C.c_float)), "dpg_synth_scans")
+        gts.append(gt)
+        rs.append(r)
+    V = n_passes * nodes_per_pass
+    geom = np.tile(np.array([ANGLE_MIN, ANGLE_MAX, range_max], np.float32), (V, 1))
+    return DynamicWorkload(ranges=np.concatenate(rs), geom=geom, est=np.concatenate(gts).astype(np.float32),
+                           pass_of=np.repeat(np.arange(n_passes, dtype=np.int32), nodes_per_pass),
+                           pass_start=np.arange(n_passes + 1, dtype=np.int64) * nodes_per_pass,
+                           boxes=boxes, present=present)

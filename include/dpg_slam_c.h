@@ -300,6 +300,74 @@ int dpg_reoptimize(dpg_ctx* ctx, int64_t n_nodes, const int32_t* pass_numbers, c
                    const float* odom_only, const dpg_icp_params* icp_params, const dpg_gn_params* gn_params,
                    const dpg_reopt_params* params, double* poses_out, dpg_reopt_stats* stats);
 
+/* ---- DPG change detection (DpgSLAM::executeDPG, dpg_slam.cc:865-886) ----
+ * The dynamic node state (DpgNode/Measurement: per-beam label and sector, per-node sector
+ * activation and active flag) lives on the device in a dpg_dpg store; executeDPG runs on it.
+ * Semantics are the reference's with its Q8 defects fixed ("DPG"): a grid point is
+ * transformed into the map frame once; unlabelled points count as STATIC; the uncovered-cell set
+ * loses every cell the candidate covers; the bin ratio is a real division; the bin score uses the
+ * pose-chain node whose grid is tested and its own scan's angle range; removed points are labelled
+ * on their own node; a deactivated sector skips one removed point (continue, not break). */
+enum { DPG_LABEL_STATIC = 0, DPG_LABEL_ADDED = 1, DPG_LABEL_REMOVED = 2, DPG_LABEL_NOT_YET_LABELED = 3,
+       DPG_LABEL_MAX_RANGE = 4 };   /* PointLabel, dpg_measurement.h:21 */
+
+typedef struct dpg_change_params {
+    int32_t num_sectors;                        /* 5 (parameters.h:44) */
+    int32_t current_pose_chain_len;             /* 5 (parameters.h:57), <= 15 */
+    int32_t num_bins_for_change_detection;      /* uninitialised in the reference (parameters.h:62); 36 */
+    int32_t pad;
+    double delta_change_threshold;              /* 0.20 (parameters.h:67) */
+    double current_pose_graph_coverage_threshold; /* 1.0 (parameters.h:72) */
+    double occ_grid_resolution;                 /* 0.05 (parameters.h:77) */
+    float minimum_percent_active_sectors;       /* 0.5 (parameters.h:82) */
+    float distance_threshold_for_local_submap_nodes; /* 5.0 (parameters.h:87) */
+    float laser[3];                             /* laser pose in base_link: 0.2, 0, 0 (parameters.h:319-339) */
+    float pad2;
+} dpg_change_params;
+
+typedef struct dpg_change_stats {
+    int64_t n_chain;            /* current pose chain length used */
+    int64_t n_candidates;       /* active past nodes within the proximity threshold */
+    int64_t n_submap_nodes;     /* candidates merged into the local submap */
+    int64_t n_chain_cells;      /* cells of the pose-chain grids (the uncovered set at the start) */
+    int64_t n_uncovered;        /* chain cells left uncovered by the submap */
+    int64_t n_added;            /* points labelled ADDED (committed nodes only) */
+    int64_t n_removed;          /* distinct points labelled REMOVED */
+    int64_t n_committed;        /* pose-chain nodes whose bin score passed */
+    int64_t n_sectors_deactivated; /* by updateNodesAndSectorStatus */
+    int64_t n_nodes_deactivated;
+    int64_t grid_cells;         /* dense window cells (W x H) */
+    int64_t n_samples;          /* ray samples marched (all rasterisation passes) */
+    double ms_total;            /* wall time of dpg_execute_dpg */
+    double ms_kernels;          /* device time, HIP events around the device work */
+} dpg_change_stats;
+
+typedef struct dpg_dpg dpg_dpg;
+
+void dpg_change_params_default(dpg_change_params* p);
+/* Node store: n_nodes scans (ranges[beam_offsets[v] .. beam_offsets[v+1]), geom[v] = angle_min,
+ * angle_max, range_max).  Labels start as MeasurementPoint's constructor sets them
+ * (dpg_measurement.h:41-46), sectors as createNode numbers them (dpg_slam.cc:499-507), every sector
+ * and node active.  NULL on error (dpg_last_error). */
+dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t n_nodes, const int64_t* beam_offsets, const float* ranges,
+                        const float* geom /*[V][3]*/, const dpg_change_params* params);
+void dpg_dpg_destroy(dpg_dpg* d);
+/* executeDPG after node n_nodes-1 was added: dpg_nodes_ = nodes [0, n_nodes), current_pass_nodes_ =
+ * the last current_pass_len of them; est_poses[n_nodes][3] the estimated node poses. */
+int dpg_execute_dpg(dpg_dpg* d, int64_t n_nodes, int64_t current_pass_len, const float* est_poses,
+                    dpg_change_stats* stats);
+/* Copy the node state back (any pointer may be NULL): labels[B], sector_active[V] (bit s = sector s
+ * active), node_active[V]. */
+int dpg_dpg_fetch(dpg_dpg* d, uint8_t* labels, uint8_t* sector_active, uint8_t* node_active);
+/* Overwrite the node state (tests, checkpoint restore); NULL leaves that part unchanged. */
+int dpg_dpg_load(dpg_dpg* d, const uint8_t* labels, const uint8_t* sector_active, const uint8_t* node_active);
+/* DpgSLAM::getActiveAndDynamicMapPoints (dpg_slam.cc:832-863) over nodes [0, n_nodes): the four
+ * point lists in node/beam order, concatenated into out[cap][2] as active_static | active_added |
+ * dynamic_removed | dynamic_added; counts[4] receives their sizes.  Returns the total (negative:
+ * error); writes nothing past cap. */
+int64_t dpg_active_dynamic_points(dpg_dpg* d, int64_t n_nodes, const float* est_poses, float* out,
+                                  int64_t cap, int64_t counts[4]);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,12 @@ def lib():
             "oracle_optimize_graph": (C.c_int, [F64P, C.c_int64, P, C.c_int64, C.POINTER(_abi.GnParams),
                                                 C.POINTER(_abi.GnStats)]),
             "oracle_gn_delta": (C.c_int, [F64P, C.c_int64, P, C.c_int64, F64P, F64P]),
+            "oracle_dpg_create": (P, [C.c_int64, I64P, F32P, F32P, C.POINTER(_abi.ChangeParams)]),
+            "oracle_dpg_destroy": (None, [P]),
+            "oracle_execute_dpg": (C.c_int, [P, C.c_int64, C.c_int64, F32P, C.POINTER(_abi.ChangeStats)]),
+            "oracle_dpg_fetch": (None, [P, _abi.U8P, _abi.U8P, _abi.U8P]),
+            "oracle_dpg_load": (None, [P, _abi.U8P, _abi.U8P, _abi.U8P]),
+            "oracle_active_dynamic_points": (C.c_int64, [P, C.c_int64, F32P, F32P, C.c_int64, I64P]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -289,3 +295,57 @@ def _cos_sin(th):
     """cosf/sinf of a float angle via the oracle's C transformPoint of unit vectors."""
     a = transform_point(np.array([1.0, 0.0, 0.0], np.float32), np.array([0.0, 0.0, th], np.float32))
     return a[0], a[1]
+
+
+class OracleDpgStore:
+    """CPU restatement of the DPG node store + executeDPG (dpg_change_oracle.cpp); same interface as
+    dpgslam.api.DpgStore."""
+
+    def __init__(self, ranges, geom, offsets=None, params=None):
+        from dpgslam import _abi
+        r = _f32(ranges)
+        if offsets is None:
+            V, nb = r.shape
+            offsets = np.arange(V + 1, dtype=np.int64) * nb
+        off = np.ascontiguousarray(offsets, np.int64)
+        self.V, self.B = len(off) - 1, int(off[-1])
+        g = _f32(geom).reshape(self.V, 3)
+        self.params = params or _abi.default_change_params_host()
+        self.handle = lib().oracle_dpg_create(self.V, _p(off, C.c_int64), _p(r.reshape(-1), C.c_float),
+                                              _p(g, C.c_float), C.byref(self.params))
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            lib().oracle_dpg_destroy(self.handle)
+            self.handle = None
+
+    def execute_dpg(self, n_nodes, current_pass_len, est):
+        from dpgslam import _abi
+        e = _f32(est).reshape(-1, 3)
+        st = _abi.ChangeStats()
+        rc = lib().oracle_execute_dpg(self.handle, n_nodes, current_pass_len, _p(e, C.c_float), C.byref(st))
+        assert rc == 0, rc
+        return st
+
+    def fetch(self):
+        lab, sec, act = np.zeros(self.B, np.uint8), np.zeros(self.V, np.uint8), np.zeros(self.V, np.uint8)
+        lib().oracle_dpg_fetch(self.handle, _p(lab, C.c_uint8), _p(sec, C.c_uint8), _p(act, C.c_uint8))
+        return lab, sec, act
+
+    def load(self, labels=None, sector_active=None, node_active=None):
+        a = [None if x is None else np.ascontiguousarray(x, np.uint8) for x in (labels, sector_active, node_active)]
+        lib().oracle_dpg_load(self.handle, *[_p(x, C.c_uint8) for x in a])
+
+    def active_dynamic_points(self, n_nodes, est):
+        e = _f32(est).reshape(-1, 3)
+        counts = np.zeros(4, np.int64)
+        n = lib().oracle_active_dynamic_points(self.handle, n_nodes, _p(e, C.c_float), None, 0, _p(counts, C.c_int64))
+        out = np.zeros((max(n, 1), 2), np.float32)
+        lib().oracle_active_dynamic_points(self.handle, n_nodes, _p(e, C.c_float), _p(out, C.c_float), n,
+                                           _p(counts, C.c_int64))
+        names = ("active_static", "active_added", "dynamic_removed", "dynamic_added")
+        res, k = {}, 0
+        for name, c in zip(names, counts):
+            res[name] = out[k:k + c].copy()
+            k += int(c)
+        return res
