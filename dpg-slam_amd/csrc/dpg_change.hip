@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "dpg_atan2f.h"
 #include "dpg_internal.h"
 
 namespace {
@@ -121,7 +122,7 @@ __device__ __forceinline__ void score_bin(const DS& d, int k, float2 q) {
     const int64_t c = d.chain[k];
     const float4 gm = d.geom[c];
     const float2 r = rel_lidar(d, c, q);
-    const float a = atan2f(r.y, r.x);
+    const float a = dpg_atan2f(r.y, r.x);   // the host libm's atan2f, bit for bit
     if (a > gm.y || a < gm.x) return;
     const float inc = (gm.y - gm.x) / (float)d.total_bins;
     const uint32_t bin = (uint16_t)((a - gm.x) / inc);
@@ -333,7 +334,7 @@ __global__ __launch_bounds__(kT) void deactivate_kernel(DS d, int64_t n_removed)
         const float2 r = rel_lidar(d, v, d.removed_xy[q]);
         const float norm = __fsqrt_rn(r.x * r.x + r.y * r.y);
         if (norm > gm.z) continue;
-        const float a = atan2f(r.y, r.x);
+        const float a = dpg_atan2f(r.y, r.x);   // the host libm's atan2f, bit for bit
         if (a > gm.y || a < gm.x) continue;
         const uint32_t s = (uint8_t)((a - gm.x) / sector_size);
         if ((int)s >= d.num_sectors || !((mask >> s) & 1u)) continue;
@@ -521,6 +522,10 @@ int upload_frames(dpg_dpg* d, int64_t V, const float* est) {
 
 }  // namespace
 
+namespace {
+int finish_call(dpg_dpg* d, int64_t V, int64_t chain_n, double t0, dpg_change_stats* st);
+}  // namespace
+
 extern "C" {
 
 void dpg_change_params_default(dpg_change_params* p) {
@@ -634,9 +639,18 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         }
     }
     st->n_candidates = (int64_t)cand.size();
-    if (chain_n == 0) { st->ms_total = now_ms() - t0; return DPG_OK; }
     int rc = upload_frames(d, V, est);
     if (rc) return rc;
+    if (d->d_ctl.reserve(1)) return dpg_set_error(DPG_ERR_HIP, "hipMalloc(ctl) failed");
+    if (chain_n == 0) {   // no pose chain: only the sector/node update of the (empty) removed set runs
+        DS ds = make_ds(d);
+        DTRY(hipEventRecord(d->ev[0], s));
+        DTRY(hipMemsetAsync(d->d_ctl.p, 0, sizeof(Ctl), s));
+        if (n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds, 0);
+        DTRY(hipGetLastError());
+        DTRY(hipEventRecord(d->ev[1], s));
+        return finish_call(d, V, 0, t0, st);
+    }
     // window: every chain ray stays within its longest range of the lidar
     std::vector<float> fr;
     node_frames(d, V, est, fr);
@@ -694,12 +708,25 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     DTRY(hipMemcpyAsync(d->h_ctl, d->d_ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, s));
     DTRY(hipStreamSynchronize(s));
     const int64_t n_removed = (int64_t)d->h_ctl->n_removed;
-    if (n_removed > 0 && n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds, n_removed);
+    // every active past node re-checks its active-sector fraction, removed points or not (dpg_node.cc:93-95)
+    if (n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds, n_removed);
     DTRY(hipGetLastError());
     DTRY(hipEventRecord(d->ev[1], s));
+    return finish_call(d, V, chain_n, t0, st);
+}
+
+}  // extern "C"
+
+namespace {
+
+// read back the counters and the node activity of one dpg_execute_dpg (one synchronisation)
+int finish_call(dpg_dpg* d, int64_t V, int64_t chain_n, double t0, dpg_change_stats* st) {
+    hipStream_t s = d->s;
     DTRY(hipMemcpyAsync(d->h_ctl, d->d_ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, s));
     std::vector<uint32_t> act((size_t)V);
     DTRY(hipMemcpyAsync(act.data(), d->d_active.p, sizeof(uint32_t) * V, hipMemcpyDeviceToHost, s));
+    std::vector<int32_t> cm((size_t)chain_n + 1, 0);
+    if (chain_n) DTRY(hipMemcpyAsync(cm.data(), d->d_commit.p, sizeof(int32_t) * (chain_n + 1), hipMemcpyDeviceToHost, s));
     DTRY(hipStreamSynchronize(s));
     for (int64_t v = 0; v < V; ++v) d->active_h[(size_t)v] = act[(size_t)v] ? 1 : 0;
     const Ctl& c = *d->h_ctl;
@@ -712,8 +739,6 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     st->n_sectors_deactivated = (int64_t)c.sect_off;
     st->n_nodes_deactivated = (int64_t)c.nodes_off;
     st->n_samples = (int64_t)c.samples;
-    std::vector<int32_t> cm((size_t)chain_n + 1);
-    DTRY(hipMemcpy(cm.data(), d->d_commit.p, sizeof(int32_t) * (chain_n + 1), hipMemcpyDeviceToHost));
     for (int64_t k = 0; k < chain_n; ++k) st->n_committed += cm[(size_t)k] != 0;
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, d->ev[0], d->ev[1]);
@@ -721,6 +746,10 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     st->ms_total = now_ms() - t0;
     return DPG_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int dpg_dpg_fetch(dpg_dpg* d, uint8_t* labels, uint8_t* sector_active, uint8_t* node_active) {
     if (!d) return dpg_set_error(DPG_ERR_ARG, "bad arguments");

@@ -211,3 +211,17 @@ def test_gpu_params_edges():
         cur = int(v - w.pass_start[pp] + 1)
         assert g.execute_dpg(v + 1, cur, w.est[:v + 1]).counters() == o.execute_dpg(v + 1, cur, w.est[:v + 1]).counters()
         _same_state(g, o)
+
+
+def test_atan2f_restatement_matches_libm(tmp_path):
+    """dpg_atan2f (the GPU's bearing function) == the host C library's atan2f on 40 M arguments and
+    the special cases; run on the host (hipcc compiles the __host__ __device__ code for the CPU)."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "atan2f_check")
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-ffp-contract=off", "-o", exe,
+                    os.path.join(root, "tools", "atan2f_check.hip")], check=True, capture_output=True)
+    out = subprocess.run([exe], capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout
+    assert "mismatches: 0 of" in out.stdout
