@@ -76,16 +76,26 @@ struct DS {                      // device view of the node store + per-call scr
     uint16_t* rmask;             // [n_cand][max_beams]
     float2* removed_xy;
     Ctl* ctl;
-    double res;
+    double res, inv_res;
     int32_t max_beams, n_chain, n_cand, bin_words, total_bins, num_sectors;
     float min_pct;
     double change_thr, cover_thr;
     Box box;
 };
 
+// round((double)v / res) exactly (convertToKeyForm, :923-929): v * (1/res) is within ~2 ulp of the
+// quotient, so unless its fraction lies within 1e-6 of one half it rounds to the same integer as
+// the correctly rounded division; only those rare near-ties pay for the fp64 division
+__device__ __forceinline__ int key_of(const DS& d, float v) {
+    const double q = (double)v * d.inv_res;
+    const double fl = floor(q), fr = q - fl;
+    if (fabs(fr - 0.5) > 1e-6) return (int)(fr < 0.5 ? fl : fl + 1.0);
+    return (int)round((double)v / d.res);
+}
+
 __device__ __forceinline__ bool cell_of(const DS& d, float x, float y, int64_t* idx) {
-    const int kx = (int)round((double)x / d.res);      // convertToKeyForm (:923-929)
-    const int ky = (int)round((double)y / d.res);
+    const int kx = key_of(d, x);
+    const int ky = key_of(d, y);
     const int ix = kx - d.box.x0, iy = ky - d.box.y0;
     if (ix < 0 || iy < 0 || ix >= d.box.w || iy >= d.box.h) return false;
     *idx = (int64_t)iy * d.box.w + ix;
@@ -130,73 +140,130 @@ __device__ __forceinline__ void score_bin(const DS& d, int k, float2 q) {
     d.inrange[k] = 1;
 }
 
+// kG lanes share a beam: every lane steps the float t chain (one add per sample, the reference's
+// exact sequence) and marks one contiguous kG-th of the samples; a block covers kT / kG adjacent beams of one
+// scan.  Near the lidar those rays cross the same cells over and over (hundreds of rays per cell
+// within a metre), so each block first inserts a cell into an LDS hash set and only the first
+// insertion issues the global atomic; the marking is a set union, so dropping repeats is exact.
+constexpr int kG = 8;
+constexpr int kH = 4096;   // LDS hash slots (16 KB)
+constexpr uint32_t kEmpty = 0xffffffffu;
+
+template <int MODE>
+__device__ __forceinline__ void mark_cell(const DS& d, uint32_t* hset, int64_t c, bool occ, int k,
+                                          uint32_t chain_mask, uint32_t fbit, uint32_t obit) {
+    const uint32_t key = ((uint32_t)c << 1) | (occ ? 1u : 0u);      // c < 2^28
+    uint32_t h = (key * 2654435761u) >> 20;                         // 12-bit multiplicative hash
+    bool fresh = true;
+    for (int probe = 0; probe < 8; ++probe, h = (h + 1) & (kH - 1)) {
+        const uint32_t old = atomicCAS(&hset[h], kEmpty, key);
+        if (old == kEmpty) break;
+        if (old == key) { fresh = false; break; }
+    }
+    if (!fresh) return;
+    // fire-and-forget atomics (no return value, so the wave does not wait on them); first[] of a
+    // cell outside the chain grids is never read
+    if (MODE == 1) atomicMin(&d.first[c], k);
+    else atomicOr(&d.grid[c], occ ? obit : fbit);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kT) void raster_kernel(DS d) {
+    __shared__ uint32_t hset[kH];
+    __shared__ unsigned long long red[2];
     const int k = blockIdx.y;
-    int64_t v;
-    if (MODE == 0) {
-        v = d.chain[k];
-    } else {
-        if (MODE == 2 && !d.acc[k]) return;
-        v = d.cand[k];
-    }
-    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int lane = threadIdx.x % kG;
+    for (int q = threadIdx.x; q < kH; q += kT) hset[q] = kEmpty;
+    if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; }
+    __syncthreads();
+    bool live = !(MODE == 2 && !d.acc[k]);
+    const int64_t v = MODE == 0 ? d.chain[k] : d.cand[k];
+    const int64_t i = (int64_t)blockIdx.x * (kT / kG) + threadIdx.x / kG;
     const int64_t b0 = d.off[v], nb = d.off[v + 1] - b0;
-    if (i >= nb) return;
     const int64_t b = b0 + i;
-    if (!included(d, v, b)) return;
+    live = live && i < nb && included(d, v, b);
     const uint32_t chain_mask = (1u << (2 * d.n_chain)) - 1u;
     const uint32_t fbit = MODE == 0 ? 1u << (2 * k) : kSubFree;
     const uint32_t obit = MODE == 0 ? 1u << (2 * k + 1) : kSubOcc;
-    const float4 f = d.frame[2 * v];
-    const float2 m = map_point(d, v, b);
-    unsigned long long oob = 0;
-    int64_t c;
-    if (d.label[b] != DPG_LABEL_MAX_RANGE) {      // occupied end point (:993-997)
-        if (cell_of(d, m.x, m.y, &c)) {
-            if (MODE == 1) {
-                if ((d.grid[c] & chain_mask) && d.first[c] > k) atomicMin(&d.first[c], k);
-            } else if (!(d.grid[c] & obit)) {
-                atomicOr(&d.grid[c], obit);
-            }
-        } else {
-            ++oob;
+    unsigned long long oob = 0, ns = 0;
+    if (live) {
+        const float4 f = d.frame[2 * v];
+        const float2 m = map_point(d, v, b);
+        int64_t c;
+        if (lane == 0 && d.label[b] != DPG_LABEL_MAX_RANGE) {      // occupied end point (:993-997)
+            if (cell_of(d, m.x, m.y, &c)) mark_cell<MODE>(d, hset, c, true, k, chain_mask, fbit, obit);
+            else ++oob;
+        }
+        // getIntermediateFreeCellsInFOV: num_bins = round(range / res), t += 1.0 / num_bins in float
+        const uint32_t nbins = (uint32_t)round((double)d.range[b] / d.res);
+        const float inc = (float)(1.0 / (double)nbins);
+        // lane l takes the l-th contiguous chunk of the ~nbins + 1 steps (the last lane runs on to
+        // the chain's true end): it first replays the float t chain up to its chunk, then marks
+        const uint32_t chunk = (nbins + kG) / kG;
+        const uint32_t s0 = (uint32_t)lane * chunk, s1 = lane == kG - 1 ? 0xffffffffu : s0 + chunk;
+        uint32_t step = 0;
+        float t = 0.0f;
+        for (; step < s0 && (double)t < 1.0; ++step) t = t + inc;
+        for (; step < s1 && (double)t < 1.0; t = t + inc, ++step) {
+            const float ix = (1 - t) * f.x + t * m.x;
+            const float iy = (1 - t) * f.y + t * m.y;
+            ++ns;
+            if (!cell_of(d, ix, iy, &c)) { ++oob; continue; }
+            mark_cell<MODE>(d, hset, c, false, k, chain_mask, fbit, obit);
         }
     }
-    // getIntermediateFreeCellsInFOV: num_bins = round(range / res), t += 1.0 / num_bins in float
-    const uint32_t nbins = (uint32_t)round((double)d.range[b] / d.res);
-    const float inc = (float)(1.0 / (double)nbins);
-    int64_t last = -1;
-    unsigned long long ns = 0;
-    for (float t = 0.0f; (double)t < 1.0; t = t + inc) {
-        const float ix = (1 - t) * f.x + t * m.x;
-        const float iy = (1 - t) * f.y + t * m.y;
-        ++ns;
-        if (!cell_of(d, ix, iy, &c)) { ++oob; continue; }
-        if (c == last) continue;
-        last = c;
-        if (MODE == 1) {
-            if ((d.grid[c] & chain_mask) && d.first[c] > k) atomicMin(&d.first[c], k);
-        } else if (!(d.grid[c] & fbit)) {
-            atomicOr(&d.grid[c], fbit);
-        }
+    if (ns) atomicAdd(&red[0], ns);
+    if (oob) atomicAdd(&red[1], oob);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (red[0]) atomicAdd(&d.ctl->samples, red[0]);
+        if (MODE == 0 && red[1]) atomicAdd(&d.ctl->oob, red[1]);   // chain grids must fit the window
     }
-    atomicAdd(&d.ctl->samples, ns);
-    if (MODE == 0 && oob) atomicAdd(&d.ctl->oob, oob);   // chain grids must fit the window
 }
 
-// chain cells (the uncovered set at the start) and cells per first coverer
-__global__ __launch_bounds__(kT) void hist_kernel(DS d, int64_t n_cells) {
-    const uint32_t chain_mask = (1u << (2 * d.n_chain)) - 1u;
-    const int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x;
-    bool in = false;
-    if (c < n_cells && (d.grid[c] & chain_mask)) {
-        in = true;
-        const int32_t f = d.first[c];
-        if (f != kInf) atomicAdd(&d.cand_cnt[f], 1);
+// per-call reset of the window and the small scratch (one launch instead of seven memsets)
+__global__ __launch_bounds__(kT) void init_kernel(DS d, int64_t n_cells) {
+    const int64_t stride = (int64_t)gridDim.x * kT;
+    for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
+        d.grid[c] = 0u;
+        d.first[c] = kInf;
     }
-    const int cnt = __syncthreads_count(in);
-    if (threadIdx.x == 0 && cnt) atomicAdd(&d.ctl->chain_cells, (unsigned long long)cnt);
+    if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < d.n_cand; k += kT) { d.cand_cnt[k] = 0; d.acc[k] = 0; }
+        for (int k = threadIdx.x; k < d.n_chain * d.bin_words; k += kT) d.bins[k] = 0u;
+        for (int k = threadIdx.x; k < d.n_chain; k += kT) d.inrange[k] = 0;
+        if (threadIdx.x == 0) memset(d.ctl, 0, sizeof(Ctl));
+    }
+}
+
+// chain cells (the uncovered set at the start) and cells per first coverer: grid-stride blocks
+// with an LDS histogram (up to kHist candidates), flushed once per block
+constexpr int kHist = 1024;
+__global__ __launch_bounds__(kT) void hist_kernel(DS d, int64_t n_cells) {
+    __shared__ int32_t h[kHist];
+    __shared__ unsigned long long tot;
+    const bool lds = d.n_cand <= kHist;
+    for (int q = threadIdx.x; q < kHist; q += kT) h[q] = 0;
+    if (threadIdx.x == 0) tot = 0;
+    __syncthreads();
+    const uint32_t chain_mask = (1u << (2 * d.n_chain)) - 1u;
+    int in = 0;
+    const int64_t stride = (int64_t)gridDim.x * kT;
+    for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
+        if (!(d.grid[c] & chain_mask)) continue;
+        ++in;
+        const int32_t f = d.first[c];
+        if (f != kInf) {
+            if (lds) atomicAdd(&h[f], 1);
+            else atomicAdd(&d.cand_cnt[f], 1);
+        }
+    }
+    if (in) atomicAdd(&tot, (unsigned long long)in);
+    __syncthreads();
+    if (threadIdx.x == 0 && tot) atomicAdd(&d.ctl->chain_cells, tot);
+    if (lds)
+        for (int q = threadIdx.x; q < d.n_cand; q += kT)
+            if (h[q]) atomicAdd(&d.cand_cnt[q], h[q]);
 }
 
 // the greedy walk of getSubMapCoveringCurrPoseChain (:646-695) over the candidates in node order
@@ -320,9 +387,10 @@ __global__ __launch_bounds__(kT) void apply_removed_kernel(DS d) {
 
 // DpgNode::deactivateIntersectingSectors for every past node (dpg_node.cc:28-96), Q8 fix: a point
 // in an already inactive sector is skipped (continue) instead of ending the loop (break)
-__global__ __launch_bounds__(kT) void deactivate_kernel(DS d, int64_t n_removed) {
+__global__ __launch_bounds__(kT) void deactivate_kernel(DS d) {
     const int64_t v = blockIdx.x;
     if (!d.active[v]) return;
+    const int64_t n_removed = (int64_t)d.ctl->n_removed;   // written by apply_removed_kernel
     __shared__ uint32_t mask;
     const uint32_t m0 = d.sect[v];
     if (threadIdx.x == 0) mask = m0;
@@ -454,6 +522,8 @@ struct dpg_dpg {
     std::vector<float> geom;          // [V][4]
     std::vector<float> rmax_beam;     // largest range of each node's beams (window size)
     std::vector<uint8_t> active_h;    // host mirror of the node activity
+    std::vector<float> h_pose;        // [V][3] pose bits the cached frames were computed from (NaN: none)
+    std::vector<float> h_frames;      // [V][8] cached node frames (see upload_frames)
     Buf<int64_t> d_off;
     Buf<float2> d_plaser;
     Buf<float> d_range;
@@ -487,7 +557,7 @@ DS make_ds(dpg_dpg* d) {
     s.cand = d->d_cand.p; s.cand_cnt = d->d_cand_cnt.p; s.acc = d->d_acc.p; s.bins = d->d_bins.p;
     s.inrange = d->d_inrange.p; s.commit = d->d_commit.p; s.added = d->d_added.p; s.rmask = d->d_rmask.p;
     s.removed_xy = d->d_removed.p; s.ctl = d->d_ctl.p;
-    s.res = d->p.occ_grid_resolution; s.max_beams = d->max_beams; s.num_sectors = d->p.num_sectors;
+    s.res = d->p.occ_grid_resolution; s.inv_res = 1.0 / d->p.occ_grid_resolution; s.max_beams = d->max_beams; s.num_sectors = d->p.num_sectors;
     s.total_bins = d->p.num_bins_for_change_detection;
     s.bin_words = (d->p.num_bins_for_change_detection + 2 + 31) / 32;
     s.min_pct = d->p.minimum_percent_active_sectors;
@@ -497,26 +567,31 @@ DS make_ds(dpg_dpg* d) {
 }
 
 // node frames: lidar pose in the map (transformPoint(laser, node pose), dpg_node.cc:34-36) with
-// Rotation2Df(a) and Rotation2Df(-a) coefficients from the host libm
-void node_frames(const dpg_dpg* d, int64_t V, const float* est, std::vector<float>& fr) {
-    fr.assign((size_t)(8 * V), 0.f);
-    for (int64_t v = 0; v < V; ++v) {
-        const float th = est[3 * v + 2];
-        const float c0 = cosf(th), s0 = sinf(th), ns0 = -s0;
-        const float lx = est[3 * v] + (c0 * d->p.laser[0] + ns0 * d->p.laser[1]);
-        const float ly = est[3 * v + 1] + (s0 * d->p.laser[0] + c0 * d->p.laser[1]);
-        const float a = angle_mod_f(th + d->p.laser[2]);
-        float* f = &fr[(size_t)(8 * v)];
-        f[0] = lx; f[1] = ly; f[2] = cosf(a); f[3] = sinf(a); f[4] = cosf(-a); f[5] = sinf(-a);
-    }
+// Rotation2Df(a) and Rotation2Df(-a) coefficients from the host libm.  Cached per node and keyed
+// by the pose bits: only nodes whose estimate changed since the last call are recomputed and
+// uploaded (a call after a re-optimisation refreshes them all).
+void node_frame(const dpg_dpg* d, const float* e, float* f) {
+    const float th = e[2];
+    const float c0 = cosf(th), s0 = sinf(th), ns0 = -s0;
+    const float lx = e[0] + (c0 * d->p.laser[0] + ns0 * d->p.laser[1]);
+    const float ly = e[1] + (s0 * d->p.laser[0] + c0 * d->p.laser[1]);
+    const float a = angle_mod_f(th + d->p.laser[2]);
+    f[0] = lx; f[1] = ly; f[2] = cosf(a); f[3] = sinf(a); f[4] = cosf(-a); f[5] = sinf(-a); f[6] = 0.f; f[7] = 0.f;
 }
 
 int upload_frames(dpg_dpg* d, int64_t V, const float* est) {
-    std::vector<float> fr;
-    node_frames(d, V, est, fr);
-    if (d->d_frame.reserve((size_t)(2 * V))) return dpg_set_error(DPG_ERR_HIP, "hipMalloc(frames) failed");
-    DTRY(hipMemcpyAsync(d->d_frame.p, fr.data(), sizeof(float) * fr.size(), hipMemcpyHostToDevice, d->s));
-    DTRY(hipStreamSynchronize(d->s));   // fr is a stack vector
+    int64_t lo = V, hi = -1;
+    for (int64_t v = 0; v < V; ++v) {
+        float* c = &d->h_pose[(size_t)(3 * v)];
+        if (memcmp(c, est + 3 * v, 3 * sizeof(float)) == 0) continue;
+        memcpy(c, est + 3 * v, 3 * sizeof(float));
+        node_frame(d, est + 3 * v, &d->h_frames[(size_t)(8 * v)]);
+        lo = std::min(lo, v);
+        hi = v;
+    }
+    if (hi >= lo)
+        DTRY(hipMemcpyAsync(d->d_frame.p + 2 * lo, &d->h_frames[(size_t)(8 * lo)], sizeof(float) * 8 * (hi - lo + 1),
+                            hipMemcpyHostToDevice, d->s));
     return DPG_OK;
 }
 
@@ -560,6 +635,8 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
     d->geom.resize((size_t)(4 * V));
     d->rmax_beam.assign((size_t)V, 0.f);
     d->active_h.assign((size_t)V, 1);
+    d->h_pose.assign((size_t)(3 * V), NAN);
+    d->h_frames.assign((size_t)(8 * V), 0.f);
     std::vector<float2> pl((size_t)d->B);
     std::vector<uint8_t> lab((size_t)d->B), sec((size_t)d->B);
     for (int64_t v = 0; v < V; ++v) {
@@ -587,7 +664,8 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
     if (hipSetDevice(d->device) != hipSuccess) return bad("hipSetDevice failed");
     if (d->d_off.reserve((size_t)(V + 1)) || d->d_plaser.reserve((size_t)d->B) || d->d_range.reserve((size_t)d->B) ||
         d->d_label.reserve((size_t)d->B) || d->d_sector.reserve((size_t)d->B) || d->d_geom.reserve((size_t)V) ||
-        d->d_sect.reserve((size_t)V) || d->d_active.reserve((size_t)V) || d->d_ctl.reserve(1))
+        d->d_sect.reserve((size_t)V) || d->d_active.reserve((size_t)V) || d->d_ctl.reserve(1) ||
+        d->d_frame.reserve((size_t)(2 * V)))
         return bad("hipMalloc failed");
     if (hipHostMalloc(reinterpret_cast<void**>(&d->h_ctl), sizeof(Ctl), hipHostMallocDefault) != hipSuccess)
         return bad("hipHostMalloc failed");
@@ -646,14 +724,13 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         DS ds = make_ds(d);
         DTRY(hipEventRecord(d->ev[0], s));
         DTRY(hipMemsetAsync(d->d_ctl.p, 0, sizeof(Ctl), s));
-        if (n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds, 0);
+        if (n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds);
         DTRY(hipGetLastError());
         DTRY(hipEventRecord(d->ev[1], s));
         return finish_call(d, V, 0, t0, st);
     }
     // window: every chain ray stays within its longest range of the lidar
-    std::vector<float> fr;
-    node_frames(d, V, est, fr);
+    const std::vector<float>& fr = d->h_frames;
     double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
     for (int32_t v : chain) {
         const double r = d->rmax_beam[(size_t)v];
@@ -679,13 +756,6 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         d->d_removed.reserve((size_t)(std::max<int64_t>(nc, 1) * d->max_beams)))
         return dpg_set_error(DPG_ERR_HIP, "hipMalloc(change scratch) failed");
     DTRY(hipEventRecord(d->ev[0], s));
-    DTRY(hipMemsetAsync(d->d_grid.p, 0, sizeof(uint32_t) * cells, s));
-    DTRY(hipMemsetAsync(d->d_first.p, 0x7f, sizeof(int32_t) * cells, s));
-    DTRY(hipMemsetAsync(d->d_cand_cnt.p, 0, sizeof(int32_t) * std::max<int64_t>(nc, 1), s));
-    DTRY(hipMemsetAsync(d->d_acc.p, 0, sizeof(int32_t) * std::max<int64_t>(nc, 1), s));
-    DTRY(hipMemsetAsync(d->d_bins.p, 0, sizeof(uint32_t) * chain_n * bin_words, s));
-    DTRY(hipMemsetAsync(d->d_inrange.p, 0, sizeof(int32_t) * chain_n, s));
-    DTRY(hipMemsetAsync(d->d_ctl.p, 0, sizeof(Ctl), s));
     DTRY(hipMemcpyAsync(d->d_chain.p, chain.data(), sizeof(int32_t) * chain_n, hipMemcpyHostToDevice, s));
     if (nc) DTRY(hipMemcpyAsync(d->d_cand.p, cand.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
     DS ds = make_ds(d);
@@ -693,23 +763,20 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     ds.n_cand = (int32_t)nc;
     ds.box = box;
     const unsigned gx = (unsigned)((d->max_beams + kT - 1) / kT);
-    raster_kernel<0><<<dim3(gx, (unsigned)chain_n), kT, 0, s>>>(ds);
-    if (nc) raster_kernel<1><<<dim3(gx, (unsigned)nc), kT, 0, s>>>(ds);
-    hist_kernel<<<(unsigned)((cells + kT - 1) / kT), kT, 0, s>>>(ds, cells);
+    const unsigned gr = (unsigned)((d->max_beams + kT / kG - 1) / (kT / kG));
+    init_kernel<<<(unsigned)std::min<int64_t>((cells + kT - 1) / kT, 2048), kT, 0, s>>>(ds, cells);
+    raster_kernel<0><<<dim3(gr, (unsigned)chain_n), kT, 0, s>>>(ds);
+    if (nc) raster_kernel<1><<<dim3(gr, (unsigned)nc), kT, 0, s>>>(ds);
+    hist_kernel<<<(unsigned)std::min<int64_t>((cells + kT - 1) / kT, 1024), kT, 0, s>>>(ds, cells);
     accept_kernel<<<1, 64, 0, s>>>(ds);
-    if (nc) raster_kernel<2><<<dim3(gx, (unsigned)nc), kT, 0, s>>>(ds);
+    if (nc) raster_kernel<2><<<dim3(gr, (unsigned)nc), kT, 0, s>>>(ds);
     added_kernel<<<dim3(gx, (unsigned)chain_n), kT, 0, s>>>(ds);
     if (nc) removed_kernel<<<dim3(gx, (unsigned)nc), kT, 0, s>>>(ds);
     commit_kernel<<<1, 64, 0, s>>>(ds);
     apply_added_kernel<<<dim3(gx, (unsigned)chain_n), kT, 0, s>>>(ds);
     if (nc) apply_removed_kernel<<<dim3(gx, (unsigned)nc), kT, 0, s>>>(ds);
-    DTRY(hipGetLastError());
-    // the removed count is needed for the deactivation launch: one small read-back
-    DTRY(hipMemcpyAsync(d->h_ctl, d->d_ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, s));
-    DTRY(hipStreamSynchronize(s));
-    const int64_t n_removed = (int64_t)d->h_ctl->n_removed;
     // every active past node re-checks its active-sector fraction, removed points or not (dpg_node.cc:93-95)
-    if (n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds, n_removed);
+    if (n_past > 0) deactivate_kernel<<<(unsigned)n_past, kT, 0, s>>>(ds);
     DTRY(hipGetLastError());
     DTRY(hipEventRecord(d->ev[1], s));
     return finish_call(d, V, chain_n, t0, st);
