@@ -31,6 +31,7 @@
 #include <float.h>
 #include <stdint.h>
 
+#include "dpg_atan2f.h"
 #include "dpg_internal.h"
 #include "dpg_icp_tree.h"
 
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(kThreads) void icp_edges_kernel(const float2* __res
         for (int q = 0; q < 6; ++q) R.T[q] = F[q];
         R.z[0] = F[2];
         R.z[1] = F[5];
-        R.z[2] = (float)atan2((double)F[3], (double)F[0]);
+        R.z[2] = dpg_atan2f(F[3], F[0]);   // Rotation2Df::fromRotationMatrix -> std::atan2(float, float)
         R.converged = converged;
         R.iterations = k;
         R.n_corr = last_cnt;
@@ -345,7 +346,7 @@ __global__ __launch_bounds__(kThreads) void cov_block_kernel(const float2* __res
     const int t = threadIdx.x;
     const dpg_icp_edge E = edges[e];
     const float* T = results[e].T;
-    const double a = (double)(float)atan2((double)T[3], (double)T[0]);
+    const double a = (double)dpg_atan2f(T[3], T[0]);   // yaw = atan2f(T10, T00) (cov :31)
     const double x = T[2], y = T[5];
     const double ca = cos(a), sa = sin(a);
     const int n = min(E.n_src_full, E.n_tgt_full);

@@ -24,6 +24,7 @@
 #include <float.h>
 #include <stdint.h>
 
+#include "dpg_atan2f.h"
 #include "dpg_internal.h"
 #include "dpg_icp_tree.h"
 
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(kT) void icp_kd_kernel(const float2* __restrict__ d
         for (int q = 0; q < 6; ++q) R.T[q] = F[q];
         R.z[0] = F[2];
         R.z[1] = F[5];
-        R.z[2] = (float)atan2((double)F[3], (double)F[0]);
+        R.z[2] = dpg_atan2f(F[3], F[0]);   // Rotation2Df::fromRotationMatrix -> std::atan2(float, float)
         R.converged = converged;
         R.iterations = k;
         R.n_corr = last_cnt;

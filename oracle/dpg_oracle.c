@@ -356,7 +356,7 @@ int oracle_icp_align(const float* src_in, int64_t n_src, const float* tgt, int64
     memcpy(res->T, F, sizeof(F));
     res->z[0] = F[2];
     res->z[1] = F[5];
-    res->z[2] = (float)atan2((double)F[3], (double)F[0]);    /* Rotation2Df::fromRotationMatrix */
+    res->z[2] = atan2f(F[3], F[0]);    /* Rotation2Df::fromRotationMatrix: std::atan2(float, float) */
     res->converged = converged;
     res->iterations = k;
     res->n_corr = last_cnt;
@@ -382,7 +382,7 @@ void oracle_icp_cov(const float* data, int64_t nd, const float* model, int64_t n
     cov[8] = (double)vth;
     if (!hess) return;
     /* :26-35 with T20 = T21 = 0, T22 = 1 (b = c = 0): yaw from the float rotation */
-    double a = (double)(float)atan2((double)T[3], (double)T[0]);
+    double a = (double)atan2f(T[3], T[0]);   /* cov :31 yaw = atan2f(T10, T00) */
     double x = T[2], y = T[5];
     double ca = cos(a), sa = sin(a);
     double h00 = 0, h01 = 0, h02 = 0, h11 = 0, h12 = 0, h22 = 0;
@@ -409,7 +409,7 @@ void oracle_cov_block_literal(const float* data, int64_t nd, const float* model,
                               const float T[6], double hess[9]) {
     /* The reference's generated expressions (cov :133-135, :148-160) with b = c = piz = qiz = 0
      * substituted symbol by symbol (sin(0) = 0, cos(0) = 1), evaluated without simplification. */
-    double a = (double)(float)atan2((double)T[3], (double)T[0]);
+    double a = (double)atan2f(T[3], T[0]);   /* cov :31 yaw = atan2f(T10, T00) */
     double x = T[2], y = T[5];
     double sb = sin(0.0), cb = cos(0.0), sc = sin(0.0), cc = cos(0.0), piz = 0.0;
     double S[6] = {0, 0, 0, 0, 0, 0};
