@@ -255,6 +255,13 @@ def lib() -> C.CDLL:
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is not built; run `make -C dpg-slam_amd` or __graft_entry__.build()")
+        # One HIP runtime per process: PyTorch ships its own libamdhip64 (same soname), so load it
+        # first and libdpg binds to it; loaded the other way round torch would bring a second
+        # runtime that finds no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)
