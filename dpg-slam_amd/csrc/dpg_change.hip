@@ -35,6 +35,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <cmath>
 #include <vector>
 
 #include "dpg_atan2f.h"
@@ -730,6 +731,9 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         return finish_call(d, V, 0, t0, st);
     }
     // window: every chain ray stays within its longest range of the lidar
+    for (int32_t v : chain)
+        if (!std::isfinite(est[3 * v]) || !std::isfinite(est[3 * v + 1]) || !std::isfinite(est[3 * v + 2]))
+            return dpg_set_error(DPG_ERR_ARG, "non-finite pose in the pose chain");
     const std::vector<float>& fr = d->h_frames;
     double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
     for (int32_t v : chain) {

@@ -50,7 +50,8 @@ def test_struct_layouts():
     from dpgslam import _abi
     assert C.sizeof(_abi.IcpResult) == 64 and C.sizeof(_abi.Factor) == 64
     for struct, cls in (("dpg_icp_params", _abi.IcpParams), ("dpg_gn_params", _abi.GnParams),
-                        ("dpg_gn_stats", _abi.GnStats)):
+                        ("dpg_gn_stats", _abi.GnStats), ("dpg_change_params", _abi.ChangeParams),
+                        ("dpg_change_stats", _abi.ChangeStats)):
         names = [f[0] for f in cls._fields_]
         lay = _c_layout(struct, names)
         assert lay[0] == C.sizeof(cls), (struct, lay[0], C.sizeof(cls))
