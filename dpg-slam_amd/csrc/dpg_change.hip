@@ -67,6 +67,11 @@ struct DS {                      // device view of the node store + per-call scr
     uint32_t* grid;
     int32_t* first;
     const int32_t* chain;        // chain node ids
+    const int32_t* slot;         // [chain]: bit-plane slot of chain node k (bits 2 slot, 2 slot + 1)
+    const int32_t* rast;         // chain indices whose grid is (re)rasterised this call
+    uint32_t chain_bits;         // planes of the current chain nodes
+    uint32_t keep_mask;          // planes kept from the previous call (window reused)
+    int32_t rebuild;             // 1: window (re)built, every plane starts empty
     const int32_t* cand;         // candidate node ids, node order
     int32_t* cand_cnt;
     int32_t* acc;
@@ -146,17 +151,27 @@ __device__ __forceinline__ void score_bin(const DS& d, int k, float2 q) {
 // scan.  Near the lidar those rays cross the same cells over and over (hundreds of rays per cell
 // within a metre), so each block first inserts a cell into an LDS hash set and only the first
 // insertion issues the global atomic; the marking is a set union, so dropping repeats is exact.
-constexpr int kG = 8;
-constexpr int kH = 4096;   // LDS hash slots (16 KB)
+#ifndef DPG_RASTER_G
+#define DPG_RASTER_G 32
+#endif
+#ifndef DPG_RASTER_BLOCK
+#define DPG_RASTER_BLOCK 1024
+#endif
+constexpr int kG = DPG_RASTER_G;
+constexpr int kRB = DPG_RASTER_BLOCK;   // raster workgroup: kRB / kG beams
+#ifndef DPG_RASTER_HASH
+#define DPG_RASTER_HASH 16384
+#endif
+constexpr int kH = DPG_RASTER_HASH > 0 ? DPG_RASTER_HASH : 1;   // LDS hash slots (4 B each)
 constexpr uint32_t kEmpty = 0xffffffffu;
 
 template <int MODE>
 __device__ __forceinline__ void mark_cell(const DS& d, uint32_t* hset, int64_t c, bool occ, int k,
                                           uint32_t chain_mask, uint32_t fbit, uint32_t obit) {
     const uint32_t key = ((uint32_t)c << 1) | (occ ? 1u : 0u);      // c < 2^28
-    uint32_t h = (key * 2654435761u) >> 20;                         // 12-bit multiplicative hash
+    uint32_t h = (key * 2654435761u) >> (32 - (kH > 1 ? __builtin_ctz(kH) : 1));   // multiplicative hash
     bool fresh = true;
-    for (int probe = 0; probe < 8; ++probe, h = (h + 1) & (kH - 1)) {
+    for (int probe = 0; DPG_RASTER_HASH > 0 && probe < 8; ++probe, h = (h + 1) & (kH - 1)) {
         const uint32_t old = atomicCAS(&hset[h], kEmpty, key);
         if (old == kEmpty) break;
         if (old == key) { fresh = false; break; }
@@ -169,23 +184,25 @@ __device__ __forceinline__ void mark_cell(const DS& d, uint32_t* hset, int64_t c
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kT) void raster_kernel(DS d) {
+__global__ __launch_bounds__(kRB) void raster_kernel(DS d) {
     __shared__ uint32_t hset[kH];
     __shared__ unsigned long long red[2];
     const int k = blockIdx.y;
     const int lane = threadIdx.x % kG;
-    for (int q = threadIdx.x; q < kH; q += kT) hset[q] = kEmpty;
+    for (int q = threadIdx.x; q < kH; q += kRB) hset[q] = kEmpty;
     if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; }
     __syncthreads();
     bool live = !(MODE == 2 && !d.acc[k]);
-    const int64_t v = MODE == 0 ? d.chain[k] : d.cand[k];
-    const int64_t i = (int64_t)blockIdx.x * (kT / kG) + threadIdx.x / kG;
+    const int kc = MODE == 0 ? d.rast[k] : k;                 // chain index (MODE 0)
+    const int64_t v = MODE == 0 ? d.chain[kc] : d.cand[k];
+    const int64_t i = (int64_t)blockIdx.x * (kRB / kG) + threadIdx.x / kG;
     const int64_t b0 = d.off[v], nb = d.off[v + 1] - b0;
     const int64_t b = b0 + i;
     live = live && i < nb && included(d, v, b);
-    const uint32_t chain_mask = (1u << (2 * d.n_chain)) - 1u;
-    const uint32_t fbit = MODE == 0 ? 1u << (2 * k) : kSubFree;
-    const uint32_t obit = MODE == 0 ? 1u << (2 * k + 1) : kSubOcc;
+    const uint32_t chain_mask = d.chain_bits;
+    const int sl = MODE == 0 ? d.slot[kc] : 0;
+    const uint32_t fbit = MODE == 0 ? 1u << (2 * sl) : kSubFree;
+    const uint32_t obit = MODE == 0 ? 1u << (2 * sl + 1) : kSubOcc;
     unsigned long long oob = 0, ns = 0;
     if (live) {
         const float4 f = d.frame[2 * v];
@@ -226,7 +243,7 @@ __global__ __launch_bounds__(kT) void raster_kernel(DS d) {
 __global__ __launch_bounds__(kT) void init_kernel(DS d, int64_t n_cells) {
     const int64_t stride = (int64_t)gridDim.x * kT;
     for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
-        d.grid[c] = 0u;
+        d.grid[c] = d.rebuild ? 0u : (d.grid[c] & d.keep_mask);
         d.first[c] = kInf;
     }
     if (blockIdx.x == 0) {
@@ -247,7 +264,7 @@ __global__ __launch_bounds__(kT) void hist_kernel(DS d, int64_t n_cells) {
     for (int q = threadIdx.x; q < kHist; q += kT) h[q] = 0;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
-    const uint32_t chain_mask = (1u << (2 * d.n_chain)) - 1u;
+    const uint32_t chain_mask = d.chain_bits;
     int in = 0;
     const int64_t stride = (int64_t)gridDim.x * kT;
     for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
@@ -329,7 +346,7 @@ __global__ __launch_bounds__(kT) void removed_kernel(DS d) {
         if (cell_of(d, m.x, m.y, &c)) {
             const uint32_t w = d.grid[c];
             for (int k = 0; k < d.n_chain; ++k) {
-                if (((w >> (2 * k)) & 3u) == 1u) {     // FREE in chain node k's grid
+                if (((w >> (2 * d.slot[k])) & 3u) == 1u) {     // FREE in chain node k's grid
                     mask |= 1u << k;
                     score_bin(d, k, m);
                 }
@@ -525,13 +542,19 @@ struct dpg_dpg {
     std::vector<uint8_t> active_h;    // host mirror of the node activity
     std::vector<float> h_pose;        // [V][3] pose bits the cached frames were computed from (NaN: none)
     std::vector<float> h_frames;      // [V][8] cached node frames (see upload_frames)
+    // the window kept across calls: chain grids of nodes still in the chain (same pose) stay as
+    // planes; only the new chain node is rasterised (see dpg_execute_dpg)
+    Box win{};
+    bool win_valid = false;
+    int32_t slot_node[15];
+    float slot_pose[15][3];
     Buf<int64_t> d_off;
     Buf<float2> d_plaser;
     Buf<float> d_range;
     Buf<uint8_t> d_label, d_sector;
     Buf<float4> d_geom, d_frame;
     Buf<uint32_t> d_sect, d_active, d_grid, d_bins;
-    Buf<int32_t> d_first, d_chain, d_cand, d_cand_cnt, d_acc, d_inrange, d_commit;
+    Buf<int32_t> d_first, d_chain, d_slot, d_rast, d_cand, d_cand_cnt, d_acc, d_inrange, d_commit;
     Buf<uint8_t> d_added;
     Buf<uint16_t> d_rmask;
     Buf<float2> d_removed, d_map_out;
@@ -638,6 +661,7 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
     d->active_h.assign((size_t)V, 1);
     d->h_pose.assign((size_t)(3 * V), NAN);
     d->h_frames.assign((size_t)(8 * V), 0.f);
+    for (int q = 0; q < 15; ++q) d->slot_node[q] = -1;
     std::vector<float2> pl((size_t)d->B);
     std::vector<uint8_t> lab((size_t)d->B), sec((size_t)d->B);
     for (int64_t v = 0; v < V; ++v) {
@@ -741,17 +765,57 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         xlo = std::min(xlo, fr[(size_t)(8 * v)] - r); xhi = std::max(xhi, fr[(size_t)(8 * v)] + r);
         ylo = std::min(ylo, fr[(size_t)(8 * v + 1)] - r); yhi = std::max(yhi, fr[(size_t)(8 * v + 1)] + r);
     }
-    Box box;
-    box.x0 = (int32_t)floor(xlo / p.occ_grid_resolution) - 4;
-    box.y0 = (int32_t)floor(ylo / p.occ_grid_resolution) - 4;
-    box.w = (int32_t)ceil(xhi / p.occ_grid_resolution) + 4 - box.x0 + 1;
-    box.h = (int32_t)ceil(yhi / p.occ_grid_resolution) + 4 - box.y0 + 1;
+    Box need;
+    need.x0 = (int32_t)floor(xlo / p.occ_grid_resolution) - 4;
+    need.y0 = (int32_t)floor(ylo / p.occ_grid_resolution) - 4;
+    need.w = (int32_t)ceil(xhi / p.occ_grid_resolution) + 4 - need.x0 + 1;
+    need.h = (int32_t)ceil(yhi / p.occ_grid_resolution) + 4 - need.y0 + 1;
+    const Box& w0 = d->win;
+    const bool reuse = d->win_valid && need.x0 >= w0.x0 && need.y0 >= w0.y0 && need.x0 + need.w <= w0.x0 + w0.w &&
+                       need.y0 + need.h <= w0.y0 + w0.h;
+    if (!reuse) {   // new window with a margin, so the next chain nodes usually still fit
+        const int32_t m = (int32_t)ceil(4.0 / p.occ_grid_resolution);
+        Box nw{need.x0 - m, need.y0 - m, need.w + 2 * m, need.h + 2 * m};
+        if ((int64_t)nw.w * nw.h > (int64_t)1 << 28) nw = need;
+        if ((int64_t)nw.w * nw.h > (int64_t)1 << 28)
+            return dpg_set_error(DPG_ERR_SIZE, "change-detection window exceeds 2^28 cells");
+        if (d->d_grid.reserve((size_t)nw.w * nw.h) || d->d_first.reserve((size_t)nw.w * nw.h))
+            return dpg_set_error(DPG_ERR_HIP, "hipMalloc(window) failed");
+        d->win = nw;
+        d->win_valid = true;
+        for (int q = 0; q < 15; ++q) d->slot_node[q] = -1;
+    }
+    const Box box = d->win;
     const int64_t cells = (int64_t)box.w * box.h;
-    if (cells > (int64_t)1 << 28) return dpg_set_error(DPG_ERR_SIZE, "change-detection window exceeds 2^28 cells");
     st->grid_cells = cells;
+    // bit-plane slots: a chain node keeps its plane while it stays in the chain with the same pose
+    std::vector<int32_t> slot((size_t)chain_n, -1), rast;
+    uint32_t keep = 0, chain_bits = 0;
+    for (int q = 0; q < 15; ++q) {
+        const int32_t v = d->slot_node[q];
+        if (v < 0) continue;
+        int64_t k = v - (V - chain_n);
+        if (k >= 0 && k < chain_n && memcmp(d->slot_pose[q], est + 3 * v, 3 * sizeof(float)) == 0) {
+            slot[(size_t)k] = q;
+            keep |= 3u << (2 * q);
+        } else {
+            d->slot_node[q] = -1;
+        }
+    }
+    for (int64_t k = 0; k < chain_n; ++k) {
+        if (slot[(size_t)k] < 0) {
+            int q = 0;
+            while (d->slot_node[q] >= 0) ++q;   // chain_n <= 15 planes: always one free
+            d->slot_node[q] = chain[(size_t)k];
+            memcpy(d->slot_pose[q], est + 3 * chain[(size_t)k], 3 * sizeof(float));
+            slot[(size_t)k] = q;
+            rast.push_back((int32_t)k);
+        }
+        chain_bits |= 3u << (2 * slot[(size_t)k]);
+    }
     const int64_t nc = (int64_t)cand.size();
     const int32_t bin_words = (p.num_bins_for_change_detection + 2 + 31) / 32;
-    if (d->d_grid.reserve((size_t)cells) || d->d_first.reserve((size_t)cells) || d->d_chain.reserve((size_t)chain_n) ||
+    if (d->d_chain.reserve((size_t)chain_n) || d->d_slot.reserve((size_t)chain_n) || d->d_rast.reserve((size_t)chain_n) ||
         d->d_cand.reserve((size_t)std::max<int64_t>(nc, 1)) || d->d_cand_cnt.reserve((size_t)std::max<int64_t>(nc, 1)) ||
         d->d_acc.reserve((size_t)std::max<int64_t>(nc, 1)) || d->d_bins.reserve((size_t)(chain_n * bin_words)) ||
         d->d_inrange.reserve((size_t)chain_n) || d->d_commit.reserve((size_t)chain_n + 1) ||
@@ -761,19 +825,27 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         return dpg_set_error(DPG_ERR_HIP, "hipMalloc(change scratch) failed");
     DTRY(hipEventRecord(d->ev[0], s));
     DTRY(hipMemcpyAsync(d->d_chain.p, chain.data(), sizeof(int32_t) * chain_n, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_slot.p, slot.data(), sizeof(int32_t) * chain_n, hipMemcpyHostToDevice, s));
+    if (!rast.empty())
+        DTRY(hipMemcpyAsync(d->d_rast.p, rast.data(), sizeof(int32_t) * rast.size(), hipMemcpyHostToDevice, s));
     if (nc) DTRY(hipMemcpyAsync(d->d_cand.p, cand.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
     DS ds = make_ds(d);
     ds.n_chain = (int32_t)chain_n;
     ds.n_cand = (int32_t)nc;
     ds.box = box;
+    ds.slot = d->d_slot.p;
+    ds.rast = d->d_rast.p;
+    ds.chain_bits = chain_bits;
+    ds.keep_mask = keep;
+    ds.rebuild = reuse ? 0 : 1;
     const unsigned gx = (unsigned)((d->max_beams + kT - 1) / kT);
-    const unsigned gr = (unsigned)((d->max_beams + kT / kG - 1) / (kT / kG));
+    const unsigned gr = (unsigned)((d->max_beams + kRB / kG - 1) / (kRB / kG));
     init_kernel<<<(unsigned)std::min<int64_t>((cells + kT - 1) / kT, 2048), kT, 0, s>>>(ds, cells);
-    raster_kernel<0><<<dim3(gr, (unsigned)chain_n), kT, 0, s>>>(ds);
-    if (nc) raster_kernel<1><<<dim3(gr, (unsigned)nc), kT, 0, s>>>(ds);
+    if (!rast.empty()) raster_kernel<0><<<dim3(gr, (unsigned)rast.size()), kRB, 0, s>>>(ds);
+    if (nc) raster_kernel<1><<<dim3(gr, (unsigned)nc), kRB, 0, s>>>(ds);
     hist_kernel<<<(unsigned)std::min<int64_t>((cells + kT - 1) / kT, 1024), kT, 0, s>>>(ds, cells);
     accept_kernel<<<1, 64, 0, s>>>(ds);
-    if (nc) raster_kernel<2><<<dim3(gr, (unsigned)nc), kT, 0, s>>>(ds);
+    if (nc) raster_kernel<2><<<dim3(gr, (unsigned)nc), kRB, 0, s>>>(ds);
     added_kernel<<<dim3(gx, (unsigned)chain_n), kT, 0, s>>>(ds);
     if (nc) removed_kernel<<<dim3(gx, (unsigned)nc), kT, 0, s>>>(ds);
     commit_kernel<<<1, 64, 0, s>>>(ds);
@@ -843,6 +915,7 @@ int dpg_dpg_load(dpg_dpg* d, const uint8_t* labels, const uint8_t* sector_active
     if (!d) return dpg_set_error(DPG_ERR_ARG, "bad arguments");
     DTRY(hipSetDevice(d->device));
     DTRY(hipStreamSynchronize(d->s));
+    d->win_valid = false;   // the kept chain planes may no longer match the node state
     if (labels) DTRY(hipMemcpy(d->d_label.p, labels, d->B, hipMemcpyHostToDevice));
     std::vector<uint32_t> t((size_t)d->V);
     if (sector_active) {
