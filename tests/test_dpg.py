@@ -225,3 +225,27 @@ def test_atan2f_restatement_matches_libm(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True)
     assert out.returncode == 0, out.stdout
     assert "mismatches: 0 of" in out.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_pose_updates_between_calls():
+    """Estimates change between calls (as after a re-optimisation): the cached node frames and the
+    kept chain planes must follow -- small perturbations every third call, one large shift that
+    leaves the kept window, identical results to the oracle after every call."""
+    w = _dynamic()
+    o = O.OracleDpgStore(w.ranges, w.geom)
+    ctx, g = _gpu_store(w.ranges, w.geom)
+    rng = np.random.default_rng(11)
+    est = w.est.copy()
+    for n, v in enumerate(range(20, 60)):
+        if n % 3 == 2:
+            est[:v + 1, :2] += rng.normal(0, 0.02, (v + 1, 2)).astype(np.float32)
+            est[:v + 1, 2] += rng.normal(0, 0.005, v + 1).astype(np.float32)
+        if n == 25:
+            est[:v + 1, 0] += np.float32(9.0)          # beyond the window margin: rebuild
+        p = w.pass_of[v]
+        cur = int(v - w.pass_start[p] + 1)
+        so = o.execute_dpg(v + 1, cur, est[:v + 1])
+        sg = g.execute_dpg(v + 1, cur, est[:v + 1])
+        assert sg.counters() == so.counters(), (v, sg.counters(), so.counters())
+        _same_state(g, o)
