@@ -541,7 +541,13 @@ struct dpg_dpg {
     std::vector<float> rmax_beam;     // largest range of each node's beams (window size)
     std::vector<uint8_t> active_h;    // host mirror of the node activity
     std::vector<float> h_pose;        // [V][3] pose bits the cached frames were computed from (NaN: none)
-    std::vector<float> h_frames;      // [V][8] cached node frames (see upload_frames)
+    float* h_frames = nullptr;        // [V][8] cached node frames, pinned (see upload_frames)
+    // pinned staging of the per-call inputs/outputs: one H2D copy of [chain 16 | slot 16 | rast 16 |
+    // candidates], one D2H of the node activity and the commit flags
+    int32_t* h_stage = nullptr;
+    int64_t stage_cap = 0;
+    uint32_t* h_act = nullptr;
+    int32_t* h_commit = nullptr;
     // the window kept across calls: chain grids of nodes still in the chain (same pose) stay as
     // planes; only the new chain node is rasterised (see dpg_execute_dpg)
     Box win{};
@@ -554,7 +560,7 @@ struct dpg_dpg {
     Buf<uint8_t> d_label, d_sector;
     Buf<float4> d_geom, d_frame;
     Buf<uint32_t> d_sect, d_active, d_grid, d_bins;
-    Buf<int32_t> d_first, d_chain, d_slot, d_rast, d_cand, d_cand_cnt, d_acc, d_inrange, d_commit;
+    Buf<int32_t> d_first, d_stage, d_cand_cnt, d_acc, d_inrange, d_commit;
     Buf<uint8_t> d_added;
     Buf<uint16_t> d_rmask;
     Buf<float2> d_removed, d_map_out;
@@ -577,8 +583,9 @@ DS make_ds(dpg_dpg* d) {
     memset(&s, 0, sizeof(s));
     s.off = d->d_off.p; s.plaser = d->d_plaser.p; s.range = d->d_range.p; s.label = d->d_label.p;
     s.sector = d->d_sector.p; s.geom = d->d_geom.p; s.sect = d->d_sect.p; s.active = d->d_active.p;
-    s.frame = d->d_frame.p; s.grid = d->d_grid.p; s.first = d->d_first.p; s.chain = d->d_chain.p;
-    s.cand = d->d_cand.p; s.cand_cnt = d->d_cand_cnt.p; s.acc = d->d_acc.p; s.bins = d->d_bins.p;
+    s.frame = d->d_frame.p; s.grid = d->d_grid.p; s.first = d->d_first.p; s.chain = d->d_stage.p;
+    s.slot = d->d_stage.p ? d->d_stage.p + 16 : nullptr; s.rast = d->d_stage.p ? d->d_stage.p + 32 : nullptr;
+    s.cand = d->d_stage.p ? d->d_stage.p + 48 : nullptr; s.cand_cnt = d->d_cand_cnt.p; s.acc = d->d_acc.p; s.bins = d->d_bins.p;
     s.inrange = d->d_inrange.p; s.commit = d->d_commit.p; s.added = d->d_added.p; s.rmask = d->d_rmask.p;
     s.removed_xy = d->d_removed.p; s.ctl = d->d_ctl.p;
     s.res = d->p.occ_grid_resolution; s.inv_res = 1.0 / d->p.occ_grid_resolution; s.max_beams = d->max_beams; s.num_sectors = d->p.num_sectors;
@@ -660,7 +667,6 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
     d->rmax_beam.assign((size_t)V, 0.f);
     d->active_h.assign((size_t)V, 1);
     d->h_pose.assign((size_t)(3 * V), NAN);
-    d->h_frames.assign((size_t)(8 * V), 0.f);
     for (int q = 0; q < 15; ++q) d->slot_node[q] = -1;
     std::vector<float2> pl((size_t)d->B);
     std::vector<uint8_t> lab((size_t)d->B), sec((size_t)d->B);
@@ -692,8 +698,12 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
         d->d_sect.reserve((size_t)V) || d->d_active.reserve((size_t)V) || d->d_ctl.reserve(1) ||
         d->d_frame.reserve((size_t)(2 * V)))
         return bad("hipMalloc failed");
-    if (hipHostMalloc(reinterpret_cast<void**>(&d->h_ctl), sizeof(Ctl), hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc(reinterpret_cast<void**>(&d->h_ctl), sizeof(Ctl), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&d->h_frames), sizeof(float) * 8 * V, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&d->h_act), sizeof(uint32_t) * V, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&d->h_commit), sizeof(int32_t) * 16, hipHostMallocDefault) != hipSuccess)
         return bad("hipHostMalloc failed");
+    memset(d->h_frames, 0, sizeof(float) * 8 * V);
     hipStream_t s = d->s;
     if (hipMemcpyAsync(d->d_off.p, off, sizeof(int64_t) * (V + 1), hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d->d_plaser.p, pl.data(), sizeof(float2) * d->B, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -714,6 +724,10 @@ void dpg_dpg_destroy(dpg_dpg* d) {
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);
+    if (d->h_frames) (void)hipHostFree(d->h_frames);
+    if (d->h_act) (void)hipHostFree(d->h_act);
+    if (d->h_commit) (void)hipHostFree(d->h_commit);
+    if (d->h_stage) (void)hipHostFree(d->h_stage);
     for (auto& e : d->ev) if (e) (void)hipEventDestroy(e);
     delete d;
 }
@@ -758,7 +772,7 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     for (int32_t v : chain)
         if (!std::isfinite(est[3 * v]) || !std::isfinite(est[3 * v + 1]) || !std::isfinite(est[3 * v + 2]))
             return dpg_set_error(DPG_ERR_ARG, "non-finite pose in the pose chain");
-    const std::vector<float>& fr = d->h_frames;
+    const float* fr = d->h_frames;
     double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
     for (int32_t v : chain) {
         const double r = d->rmax_beam[(size_t)v];
@@ -815,8 +829,16 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     }
     const int64_t nc = (int64_t)cand.size();
     const int32_t bin_words = (p.num_bins_for_change_detection + 2 + 31) / 32;
-    if (d->d_chain.reserve((size_t)chain_n) || d->d_slot.reserve((size_t)chain_n) || d->d_rast.reserve((size_t)chain_n) ||
-        d->d_cand.reserve((size_t)std::max<int64_t>(nc, 1)) || d->d_cand_cnt.reserve((size_t)std::max<int64_t>(nc, 1)) ||
+    if (d->stage_cap < 48 + nc) {
+        if (d->h_stage) (void)hipHostFree(d->h_stage);
+        d->h_stage = nullptr;
+        d->stage_cap = 0;
+        const int64_t cap = 48 + std::max<int64_t>(2 * nc, 256);
+        if (hipHostMalloc(reinterpret_cast<void**>(&d->h_stage), sizeof(int32_t) * cap, hipHostMallocDefault) != hipSuccess)
+            return dpg_set_error(DPG_ERR_HIP, "hipHostMalloc(stage) failed");
+        d->stage_cap = cap;
+    }
+    if (d->d_stage.reserve((size_t)d->stage_cap) || d->d_cand_cnt.reserve((size_t)std::max<int64_t>(nc, 1)) ||
         d->d_acc.reserve((size_t)std::max<int64_t>(nc, 1)) || d->d_bins.reserve((size_t)(chain_n * bin_words)) ||
         d->d_inrange.reserve((size_t)chain_n) || d->d_commit.reserve((size_t)chain_n + 1) ||
         d->d_added.reserve((size_t)(chain_n * d->max_beams)) ||
@@ -824,17 +846,16 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         d->d_removed.reserve((size_t)(std::max<int64_t>(nc, 1) * d->max_beams)))
         return dpg_set_error(DPG_ERR_HIP, "hipMalloc(change scratch) failed");
     DTRY(hipEventRecord(d->ev[0], s));
-    DTRY(hipMemcpyAsync(d->d_chain.p, chain.data(), sizeof(int32_t) * chain_n, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_slot.p, slot.data(), sizeof(int32_t) * chain_n, hipMemcpyHostToDevice, s));
-    if (!rast.empty())
-        DTRY(hipMemcpyAsync(d->d_rast.p, rast.data(), sizeof(int32_t) * rast.size(), hipMemcpyHostToDevice, s));
-    if (nc) DTRY(hipMemcpyAsync(d->d_cand.p, cand.data(), sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
+    int32_t* hs = d->h_stage;   // the previous call ended with a stream synchronisation
+    memcpy(hs, chain.data(), sizeof(int32_t) * chain_n);
+    memcpy(hs + 16, slot.data(), sizeof(int32_t) * chain_n);
+    if (!rast.empty()) memcpy(hs + 32, rast.data(), sizeof(int32_t) * rast.size());
+    if (nc) memcpy(hs + 48, cand.data(), sizeof(int32_t) * nc);
+    DTRY(hipMemcpyAsync(d->d_stage.p, hs, sizeof(int32_t) * (48 + nc), hipMemcpyHostToDevice, s));
     DS ds = make_ds(d);
     ds.n_chain = (int32_t)chain_n;
     ds.n_cand = (int32_t)nc;
     ds.box = box;
-    ds.slot = d->d_slot.p;
-    ds.rast = d->d_rast.p;
     ds.chain_bits = chain_bits;
     ds.keep_mask = keep;
     ds.rebuild = reuse ? 0 : 1;
@@ -866,10 +887,10 @@ namespace {
 int finish_call(dpg_dpg* d, int64_t V, int64_t chain_n, double t0, dpg_change_stats* st) {
     hipStream_t s = d->s;
     DTRY(hipMemcpyAsync(d->h_ctl, d->d_ctl.p, sizeof(Ctl), hipMemcpyDeviceToHost, s));
-    std::vector<uint32_t> act((size_t)V);
-    DTRY(hipMemcpyAsync(act.data(), d->d_active.p, sizeof(uint32_t) * V, hipMemcpyDeviceToHost, s));
-    std::vector<int32_t> cm((size_t)chain_n + 1, 0);
-    if (chain_n) DTRY(hipMemcpyAsync(cm.data(), d->d_commit.p, sizeof(int32_t) * (chain_n + 1), hipMemcpyDeviceToHost, s));
+    uint32_t* act = d->h_act;
+    DTRY(hipMemcpyAsync(act, d->d_active.p, sizeof(uint32_t) * V, hipMemcpyDeviceToHost, s));
+    int32_t* cm = d->h_commit;
+    if (chain_n) DTRY(hipMemcpyAsync(cm, d->d_commit.p, sizeof(int32_t) * (chain_n + 1), hipMemcpyDeviceToHost, s));
     DTRY(hipStreamSynchronize(s));
     for (int64_t v = 0; v < V; ++v) d->active_h[(size_t)v] = act[(size_t)v] ? 1 : 0;
     const Ctl& c = *d->h_ctl;
