@@ -1,0 +1,59 @@
+"""The DpgSLAM host driver (dpgslam/slam.py): the reference's public API (dpg_slam.h:283-335) run
+end to end -- odometry gating, node creation, successive + non-successive ICP factors, the solve
+after every node, executeDPG on later passes, reoptimize between passes, GetPose/GetMap and the
+DPG map lists -- on the oracle backend (CPU) and on the GPU backend against it."""
+import numpy as np
+import pytest
+
+from dpgslam import synth
+from dpgslam.slam import DpgSLAM
+
+
+def _drive(slam, w, nodes_per_pass, rng_seed=3):
+    rng = np.random.default_rng(rng_seed)
+    P = len(w.pass_start) - 1
+    out = []
+    for p in range(P):
+        if p:
+            slam.incrementPassNumber()
+        for v in range(int(w.pass_start[p]), int(w.pass_start[p + 1])):
+            odom = w.est[v].astype(np.float64) + rng.normal(0, [0.01, 0.01, 0.002])
+            slam.ObserveOdometry(odom[:2].astype(np.float32), np.float32(odom[2]))
+            slam.ObserveLaser(w.ranges[v], 0.0, float(w.geom[v, 2]), float(w.geom[v, 0]), float(w.geom[v, 1]))
+            out.append((len(slam.poses), len(slam.factors)))
+    return out
+
+
+def _workload():
+    return synth.make_dynamic(n_passes=2, nodes_per_pass=14, n_beams=360, world_size=16.0, range_max=8.0,
+                              n_boxes=6, seed=9)
+
+
+def test_slam_driver_oracle_backend():
+    w = _workload()
+    s = DpgSLAM(backend="oracle")
+    trace = _drive(s, w, 14)
+    V = len(s.poses)
+    assert V > 10 and s.pass_number == 1
+    assert trace[-1][1] >= V                           # priors + odometry + ICP factors
+    assert len(set(s.node_pass)) == 2 and s.current_pass and s.current_pass[0] < V
+    loc, ang = s.GetPose()
+    assert np.all(np.isfinite(loc)) and np.isfinite(ang)
+    m = s.GetMap()
+    assert m.shape[1] == 2 and len(m) > 0
+    lists = s.GetActiveAndDynamicMapPoints()
+    assert set(lists) == {"active_static", "active_added", "dynamic_removed", "dynamic_added"}
+
+
+@pytest.mark.gpu
+def test_slam_driver_gpu_matches_oracle():
+    w = _workload()
+    so, sg = DpgSLAM(backend="oracle"), DpgSLAM(backend="gpu")
+    to, tg = _drive(so, w, 14), _drive(sg, w, 14)
+    assert to == tg                                    # same nodes and factors after every scan
+    Xo, Xg = np.stack(so.poses), np.stack(sg.poses)
+    assert np.abs(Xo - Xg).max() < 1e-5, np.abs(Xo - Xg).max()
+    lo, _, ao = so._store.fetch()
+    lg, _, ag = sg._store.fetch()
+    assert np.array_equal(ao, ag) and (lo != lg).mean() < 1e-3
+    np.testing.assert_allclose(sg.GetMap(), so.GetMap(), atol=1e-4)
