@@ -15,6 +15,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
@@ -328,8 +329,28 @@ int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const fl
         E.tgt_full_off = (int32_t)c->full_off[(size_t)t];
         E.n_tgt_full = (int32_t)(c->full_off[(size_t)t + 1] - c->full_off[(size_t)t]);
         dpg_icp_guess(poses + 3 * s, poses + 3 * t, E.guess);  // R3 (dpg_slam.cc:364-378)
+        E.pad[0] = (int32_t)e;
         ms = std::max(ms, E.n_src_ds);
         mt = std::max(mt, E.n_tgt_ds);
+    }
+    // Optional dispatch order (DPG_ICP_ORDER=1): one workgroup per edge, so edges that need long
+    // alignments could start first; the predictor is the guess displacement.  Measured on config 4
+    // in bench.py it does not pay (6.55 ms ordered vs 6.49 ms in the caller's order; an oracle order
+    // by the measured iteration counts reached 5.82 ms in tools/icp_order_probe.py), so it is off by
+    // default.  Results are written by pad[0] either way, so the caller's order is unchanged.
+    static const bool order_edges = [] { const char* v = getenv("DPG_ICP_ORDER"); return v && v[0] == '1'; }();
+    if (order_edges && ne > 1) {
+        std::vector<double> key((size_t)ne);
+        for (int64_t e = 0; e < ne; ++e) {
+            const float* g = c->h_edges[(size_t)e].guess;   // [c -s tx; s c ty]
+            key[(size_t)e] = std::hypot((double)g[2], (double)g[5]) + 2.0 * std::fabs(std::atan2((double)g[3], (double)g[0]));
+        }
+        std::vector<int64_t> idx((size_t)ne);
+        for (int64_t e = 0; e < ne; ++e) idx[(size_t)e] = e;
+        std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return key[(size_t)a] > key[(size_t)b]; });
+        std::vector<dpg_icp_edge> sorted((size_t)ne);
+        for (int64_t k = 0; k < ne; ++k) sorted[(size_t)k] = c->h_edges[(size_t)idx[(size_t)k]];
+        std::copy(sorted.begin(), sorted.end(), c->h_edges.begin());
     }
     if (c->edges.reserve((size_t)std::max<int64_t>(ne, 1)) || c->res.reserve((size_t)std::max<int64_t>(ne, 1)) ||
         c->hess.reserve((size_t)(9 * std::max<int64_t>(ne, 1))))
@@ -424,9 +445,9 @@ double dpg_icp_batch_algorithmic_bytes(dpg_ctx* c) {
     if (hipMemcpy(r.data(), c->res.p, sizeof(dpg_icp_result) * r.size(), hipMemcpyDeviceToHost) != hipSuccess) return -1.0;
     double bytes = 0.0;
     for (int64_t e = 0; e < c->n_edges; ++e) {
-        const dpg_icp_edge& E = c->h_edges[(size_t)e];
+        const dpg_icp_edge& E = c->h_edges[(size_t)e];   // dispatch order; its result is r[E.pad[0]]
         // correspondence kernel per edge-iteration: 8N (source xy) + 8M (target xy) + 8N (idx + d^2)
-        bytes += (double)r[(size_t)e].iterations * (16.0 * E.n_src_ds + 8.0 * E.n_tgt_ds);
+        bytes += (double)r[(size_t)E.pad[0]].iterations * (16.0 * E.n_src_ds + 8.0 * E.n_tgt_ds);
     }
     return bytes;
 }

@@ -84,8 +84,8 @@ __global__ __launch_bounds__(kThreads) void icp_edges_kernel(const float2* __res
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = t >> 6;
-    const int e = blockIdx.x;
-    const dpg_icp_edge E = edges[e];
+    const dpg_icp_edge E = edges[blockIdx.x];   // dispatch order (dpg_icp_batch_prepare)
+    const int e = E.pad[0];                     // the edge's index in the caller's list
     const int N = E.n_src_ds;
     const int M = E.n_tgt_ds;
     Lds L = carve(smem, kp.lds_tgt, kp.cells_max);
@@ -342,9 +342,9 @@ __global__ __launch_bounds__(kThreads) void cov_block_kernel(const float2* __res
                                                              const dpg_icp_result* __restrict__ results,
                                                              double* __restrict__ hess) {
     __shared__ double red[kWaves][3];
-    const int e = blockIdx.x;
     const int t = threadIdx.x;
-    const dpg_icp_edge E = edges[e];
+    const dpg_icp_edge E = edges[blockIdx.x];
+    const int e = E.pad[0];   // results / hess by the caller's edge index
     const float* T = results[e].T;
     const double a = (double)dpg_atan2f(T[3], T[0]);   // yaw = atan2f(T10, T00) (cov :31)
     const double x = T[2], y = T[5];

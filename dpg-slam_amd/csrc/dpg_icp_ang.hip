@@ -348,8 +348,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
                                                      int32_t* __restrict__ trace) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int e = blockIdx.x;
-    const dpg_icp_edge E = edges[e];
+    const dpg_icp_edge E = edges[blockIdx.x];   // dispatch order (dpg_icp_batch_prepare)
+    const int e = E.pad[0];                     // the edge's index in the caller's list
     const int N = E.n_src_ds, M = E.n_tgt_ds;
     const int vt = E.tgt_node, vs = E.src_node;
     const int cap = kp.lds_tgt;

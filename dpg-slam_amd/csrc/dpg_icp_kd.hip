@@ -166,8 +166,8 @@ __global__ __launch_bounds__(kT) void icp_kd_kernel(const float2* __restrict__ d
                                                     int32_t* __restrict__ trace) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int e = blockIdx.x;
-    const dpg_icp_edge E = edges[e];
+    const dpg_icp_edge E = edges[blockIdx.x];   // dispatch order (dpg_icp_batch_prepare)
+    const int e = E.pad[0];                     // the edge's index in the caller's list
     const int N = E.n_src_ds, M = E.n_tgt_ds;
     Lds L = carve(smem, kp.lds_tgt);
     for (int i = t; i < M; i += kT) {

@@ -26,7 +26,8 @@ typedef struct dpg_icp_edge {
     int32_t tgt_full_off, n_tgt_full;  /* full node_1 cloud (covariance model_qi) */
     float guess[6];                  /* runIcp transform_guess rows (dpg_slam.cc:374-378) */
     int32_t src_node, tgt_node;      /* cloud ids (angle-index bucket tables) */
-    int32_t pad[2];
+    int32_t pad[2];                  /* pad[0]: index of the edge in the caller's list (results go
+                                        there); the array itself is in dispatch order */
 } dpg_icp_edge;
 
 /* Scalars of the ICP/convergence rule, precomputed on the host in double. */
