@@ -170,6 +170,12 @@ def main():
         cpu = {"value": cb["icp_edges_per_s"], "unit": "edges/s", "cores": 1, "kind": "port",
                "sample": f"oracle (C restatement, grid NN, 1 thread) ICP on {cb['n']} random edges of "
                          f"{args.config} ({cb['icp_s']:.1f} s, mean {cb['iters_mean']:.1f} ICP iterations)"}
+        # the same sample over edges with OpenMP, at most 16 threads (the box's share)
+        nt = max(1, min(16, os.cpu_count() or 1))
+        if nt > 1:
+            cm = cpu_baseline(w, params, args.cpu_sample, threads=nt)
+            cpu["multithread"] = {"value": cm["icp_edges_per_s"], "unit": "edges/s", "cores": nt,
+                                  "sample": f"same sample, OpenMP over edges ({cm['icp_s']:.2f} s)"}
 
     traffic, traffic_src = pmc_traffic(KERNEL_NAME[args.icp_variant])
     if rank == 0:
