@@ -36,6 +36,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <vector>
 
 #include "dpg_atan2f.h"
@@ -717,6 +718,91 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
         return bad("upload of the node store failed");
     for (auto& e : d->ev) (void)hipEventCreate(&e);
     return d;
+}
+
+int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const float* ranges, const float* geom) {
+    if (!d || n_new < 0 || (n_new > 0 && (!off_rel || !ranges || !geom))) return dpg_set_error(DPG_ERR_ARG, "bad arguments");
+    if (n_new == 0) return DPG_OK;
+    DTRY(hipSetDevice(d->device));
+    hipStream_t s = d->s;
+    DTRY(hipStreamSynchronize(s));
+    const int64_t V0 = d->V, B0 = d->B, V1 = V0 + n_new, nb_new = off_rel[n_new] - off_rel[0];
+    std::vector<float2> pl((size_t)nb_new);
+    std::vector<uint8_t> lab((size_t)nb_new), sec((size_t)nb_new);
+    std::vector<float> gm((size_t)(4 * n_new));
+    std::vector<int64_t> off(d->off);
+    for (int64_t k = 0; k < n_new; ++k) {
+        const int64_t nb = off_rel[k + 1] - off_rel[k];
+        if (nb < 2 || nb > 65535) return dpg_set_error(DPG_ERR_SIZE, "beams per scan must be in [2, 65535]");
+        const float amin = geom[3 * k], amax = geom[3 * k + 1], rmax = geom[3 * k + 2];
+        const float ainc = (float)((double)(amax - amin) / ((double)nb - 1.0));   // createNode (dpg_slam.cc:497)
+        const float per_sector = ((float)nb) / (float)d->p.num_sectors;
+        gm[(size_t)(4 * k)] = amin; gm[(size_t)(4 * k + 1)] = amax; gm[(size_t)(4 * k + 2)] = rmax; gm[(size_t)(4 * k + 3)] = ainc;
+        float rm = 0.f;
+        for (int64_t i = 0; i < nb; ++i) {
+            const int64_t b = off_rel[k] - off_rel[0] + i;
+            const float angle = ainc * (float)i + amin;
+            const float r = ranges[b];
+            pl[(size_t)b] = make_float2(r * cosf(angle), r * sinf(angle));
+            lab[(size_t)b] = r >= rmax ? DPG_LABEL_MAX_RANGE : DPG_LABEL_NOT_YET_LABELED;
+            sec[(size_t)b] = (uint8_t)((float)i / per_sector);
+            rm = std::max(rm, r);
+        }
+        off.push_back(off.back() + nb);
+        d->rmax_beam.push_back(rm);
+        d->max_beams = std::max<int32_t>(d->max_beams, (int32_t)nb);
+    }
+    // device arrays grow with their contents kept (amortised x1.5)
+    auto grow = [&](auto& b, size_t used, size_t need) -> int {
+        using T = std::remove_pointer_t<decltype(b.p)>;
+        if (need <= b.cap) return 0;
+        const size_t cap = std::max(need, b.cap + b.cap / 2);
+        T* np = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&np), cap * sizeof(T)) != hipSuccess) return -1;
+        if (used && hipMemcpyAsync(np, b.p, used * sizeof(T), hipMemcpyDeviceToDevice, s) != hipSuccess) { (void)hipFree(np); return -1; }
+        if (hipStreamSynchronize(s) != hipSuccess) { (void)hipFree(np); return -1; }
+        if (b.p) (void)hipFree(b.p);
+        b.p = np;
+        b.cap = cap;
+        return 0;
+    };
+    const size_t B1 = (size_t)(B0 + nb_new);
+    if (grow(d->d_off, 0, (size_t)(V1 + 1)) || grow(d->d_plaser, (size_t)B0, B1) || grow(d->d_range, (size_t)B0, B1) ||
+        grow(d->d_label, (size_t)B0, B1) || grow(d->d_sector, (size_t)B0, B1) || grow(d->d_geom, (size_t)V0, (size_t)V1) ||
+        grow(d->d_sect, (size_t)V0, (size_t)V1) || grow(d->d_active, (size_t)V0, (size_t)V1) ||
+        grow(d->d_frame, (size_t)(2 * V0), (size_t)(2 * V1)))
+        return dpg_set_error(DPG_ERR_HIP, "hipMalloc(node store growth) failed");
+    // pinned host mirrors
+    float* nf = nullptr;
+    uint32_t* na = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&nf), sizeof(float) * 8 * V1, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&na), sizeof(uint32_t) * V1, hipHostMallocDefault) != hipSuccess) {
+        if (nf) (void)hipHostFree(nf);
+        return dpg_set_error(DPG_ERR_HIP, "hipHostMalloc(node store growth) failed");
+    }
+    memcpy(nf, d->h_frames, sizeof(float) * 8 * V0);
+    memset(nf + 8 * V0, 0, sizeof(float) * 8 * n_new);
+    (void)hipHostFree(d->h_frames);
+    (void)hipHostFree(d->h_act);
+    d->h_frames = nf;
+    d->h_act = na;
+    d->h_pose.resize((size_t)(3 * V1), NAN);
+    d->active_h.resize((size_t)V1, 1);
+    d->geom.insert(d->geom.end(), gm.begin(), gm.end());
+    d->off = off;
+    std::vector<uint32_t> sect((size_t)n_new, (1u << d->p.num_sectors) - 1u), act((size_t)n_new, 1u);
+    DTRY(hipMemcpyAsync(d->d_off.p, d->off.data(), sizeof(int64_t) * (V1 + 1), hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_plaser.p + B0, pl.data(), sizeof(float2) * nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_range.p + B0, ranges, sizeof(float) * nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_label.p + B0, lab.data(), nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_sector.p + B0, sec.data(), nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_geom.p + V0, gm.data(), sizeof(float) * 4 * n_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_sect.p + V0, sect.data(), sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_active.p + V0, act.data(), sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
+    DTRY(hipStreamSynchronize(s));
+    d->V = V1;
+    d->B = (int64_t)B1;
+    return DPG_OK;
 }
 
 void dpg_dpg_destroy(dpg_dpg* d) {

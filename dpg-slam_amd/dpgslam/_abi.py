@@ -232,6 +232,7 @@ SIGNATURES = {
     "dpg_change_params_default": (None, [C.POINTER(ChangeParams)]),
     "dpg_dpg_create": (P, [P, C.c_int64, I64P, F32P, F32P, C.POINTER(ChangeParams)]),
     "dpg_dpg_destroy": (None, [P]),
+    "dpg_dpg_append": (C.c_int, [P, C.c_int64, I64P, F32P, F32P]),
     "dpg_execute_dpg": (C.c_int, [P, C.c_int64, C.c_int64, F32P, C.POINTER(ChangeStats)]),
     "dpg_dpg_fetch": (C.c_int, [P, U8P, U8P, U8P]),
     "dpg_dpg_load": (C.c_int, [P, U8P, U8P, U8P]),

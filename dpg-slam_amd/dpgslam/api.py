@@ -379,6 +379,19 @@ class DpgStore:
         except Exception:
             pass
 
+    def append(self, ranges, geom, offsets=None):
+        """Add nodes' scans at the end (dpg_dpg_append); the existing node state is kept."""
+        r = _f32(ranges)
+        if offsets is None:
+            n, nb = r.shape
+            offsets = np.arange(n + 1, dtype=np.int64) * nb
+        off = np.ascontiguousarray(offsets, np.int64)
+        g = _f32(geom).reshape(-1, 3)
+        check(lib().dpg_dpg_append(self.handle, len(off) - 1, ptr(off, C.c_int64), ptr(r.reshape(-1), C.c_float),
+                                   ptr(g, C.c_float)), "dpg_dpg_append")
+        self.V += len(off) - 1
+        self.B += int(off[-1] - off[0])
+
     def execute_dpg(self, n_nodes: int, current_pass_len: int, est) -> "_abi.ChangeStats":
         e = _f32(est).reshape(-1, 3)
         st = _abi.ChangeStats()

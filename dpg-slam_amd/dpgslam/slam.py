@@ -299,18 +299,18 @@ class DpgSLAM:
         self.poses = [np.asarray(x, f32) for x in X]
 
     def _dpg_store(self):
-        """The node store over every node so far; rebuilt (state carried over) when nodes were added."""
+        """The node store over every node so far: created once, then the new nodes' scans are
+        appended (dpg_dpg_append keeps the labels, sectors and activity of the others)."""
         V = len(self.poses)
-        if self._store is None or self._store_V != V:
-            offs = np.zeros(V + 1, np.int64)
-            offs[1:] = np.cumsum([len(r) for r in self.ranges])
-            rng = np.ascontiguousarray(np.concatenate(self.ranges), f32)
-            geom = np.asarray(self.geom, f32)
-            new = self.be.store(rng, geom, offs, self.change_params)
-            if self._store is not None:
-                lab, sec, act = self._store.fetch()
-                lab2, sec2, act2 = new.fetch()
-                lab2[:len(lab)], sec2[:len(sec)], act2[:len(act)] = lab, sec, act
-                new.load(lab2, sec2, act2)
-            self._store, self._store_V = new, V
+        if self._store_V != V:
+            rs = self.ranges[self._store_V:]
+            offs = np.zeros(len(rs) + 1, np.int64)
+            offs[1:] = np.cumsum([len(r) for r in rs])
+            rng = np.ascontiguousarray(np.concatenate(rs), f32)
+            geom = np.asarray(self.geom[self._store_V:], f32)
+            if self._store is None:
+                self._store = self.be.store(rng, geom, offs, self.change_params)
+            else:
+                self._store.append(rng, geom, offs)
+            self._store_V = V
         return self._store

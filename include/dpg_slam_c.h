@@ -352,6 +352,10 @@ void dpg_change_params_default(dpg_change_params* p);
 dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t n_nodes, const int64_t* beam_offsets, const float* ranges,
                         const float* geom /*[V][3]*/, const dpg_change_params* params);
 void dpg_dpg_destroy(dpg_dpg* d);
+/* Add n_new nodes' scans at the end (createNode of each new node, dpg_slam.cc:488-513):
+ * beam_offsets[n_new + 1] relative to ranges[0]; existing labels, sectors and activity are kept. */
+int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* beam_offsets, const float* ranges,
+                   const float* geom /*[n_new][3]*/);
 /* executeDPG after node n_nodes-1 was added: dpg_nodes_ = nodes [0, n_nodes), current_pass_nodes_ =
  * the last current_pass_len of them; est_poses[n_nodes][3] the estimated node poses. */
 int dpg_execute_dpg(dpg_dpg* d, int64_t n_nodes, int64_t current_pass_len, const float* est_poses,

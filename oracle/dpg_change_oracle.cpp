@@ -374,6 +374,13 @@ oracle_dpg* oracle_dpg_create(int64_t V, const int64_t* off, const float* ranges
 
 void oracle_dpg_destroy(oracle_dpg* o) { delete o; }
 
+int oracle_dpg_append(oracle_dpg* o, int64_t n, const int64_t* off, const float* ranges, const float* geom) {
+    oracle_dpg* t = oracle_dpg_create(n, off, ranges + 0, geom, &o->p);   // same per-node construction
+    for (auto& nd : t->nodes) o->nodes.push_back(nd);
+    delete t;
+    return DPG_OK;
+}
+
 int oracle_execute_dpg(oracle_dpg* o, int64_t V, int64_t cur_len, const float* est, dpg_change_stats* st) {
     return o->execute(V, cur_len, est, st);
 }

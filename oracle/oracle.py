@@ -56,6 +56,7 @@ def lib():
             "oracle_gn_delta": (C.c_int, [F64P, C.c_int64, P, C.c_int64, F64P, F64P]),
             "oracle_dpg_create": (P, [C.c_int64, I64P, F32P, F32P, C.POINTER(_abi.ChangeParams)]),
             "oracle_dpg_destroy": (None, [P]),
+            "oracle_dpg_append": (C.c_int, [P, C.c_int64, I64P, F32P, F32P]),
             "oracle_execute_dpg": (C.c_int, [P, C.c_int64, C.c_int64, F32P, C.POINTER(_abi.ChangeStats)]),
             "oracle_dpg_fetch": (None, [P, _abi.U8P, _abi.U8P, _abi.U8P]),
             "oracle_dpg_load": (None, [P, _abi.U8P, _abi.U8P, _abi.U8P]),
@@ -326,6 +327,18 @@ class OracleDpgStore:
         rc = lib().oracle_execute_dpg(self.handle, n_nodes, current_pass_len, _p(e, C.c_float), C.byref(st))
         assert rc == 0, rc
         return st
+
+    def append(self, ranges, geom, offsets=None):
+        r = _f32(ranges)
+        if offsets is None:
+            n, nb = r.shape
+            offsets = np.arange(n + 1, dtype=np.int64) * nb
+        off = np.ascontiguousarray(offsets, np.int64)
+        g = _f32(geom).reshape(-1, 3)
+        lib().oracle_dpg_append(self.handle, len(off) - 1, _p(off, C.c_int64), _p(r.reshape(-1), C.c_float),
+                                _p(g, C.c_float))
+        self.V += len(off) - 1
+        self.B += int(off[-1] - off[0])
 
     def fetch(self):
         lab, sec, act = np.zeros(self.B, np.uint8), np.zeros(self.V, np.uint8), np.zeros(self.V, np.uint8)

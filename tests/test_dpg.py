@@ -249,3 +249,40 @@ def test_gpu_pose_updates_between_calls():
         sg = g.execute_dpg(v + 1, cur, est[:v + 1])
         assert sg.counters() == so.counters(), (v, sg.counters(), so.counters())
         _same_state(g, o)
+
+
+def _append_sequence(store_factory, w):
+    """Create the store over the first pass, then append one node before each call (as the driver
+    does while nodes are added)."""
+    n0 = int(w.pass_start[1])
+    s = store_factory(w.ranges[:n0], w.geom[:n0])
+    out = []
+    for v in range(n0, 60):
+        s.append(w.ranges[v:v + 1], w.geom[v:v + 1])
+        p = w.pass_of[v]
+        st = s.execute_dpg(v + 1, int(v - w.pass_start[p] + 1), w.est[:v + 1])
+        out.append((st.counters(), tuple(x.tobytes() for x in s.fetch())))
+    return out
+
+
+def test_oracle_append_equals_full_store():
+    w = _dynamic()
+    full = O.OracleDpgStore(w.ranges, w.geom)
+    ref = []
+    for v in range(int(w.pass_start[1]), 60):
+        p = w.pass_of[v]
+        st = full.execute_dpg(v + 1, int(v - w.pass_start[p] + 1), w.est[:v + 1])
+        lab, sec, act = full.fetch()
+        ref.append((st.counters(), (lab[:w.ranges[:v + 1].size].tobytes(), sec[:v + 1].tobytes(), act[:v + 1].tobytes())))
+    got = _append_sequence(lambda r, g: O.OracleDpgStore(r, g), w)
+    assert got == ref
+
+
+@pytest.mark.gpu
+def test_gpu_append_matches_oracle():
+    from dpgslam import api
+    w = _dynamic()
+    ctx = api.Context(0)
+    got = _append_sequence(lambda r, g: api.DpgStore(ctx, r, g), w)
+    ref = _append_sequence(lambda r, g: O.OracleDpgStore(r, g), w)
+    assert got == ref
