@@ -178,6 +178,8 @@ def main():
                                   "sample": f"same sample, OpenMP over edges ({cm['icp_s']:.2f} s)"}
 
     traffic, traffic_src = pmc_traffic(KERNEL_NAME[args.icp_variant])
+    if world > 1:   # the PMC pass measured the whole 1-GPU launch; a rank's launch holds only its shard
+        traffic, traffic_src = None, None
     if rank == 0:
         line = {
             "metric": "ICP edges/sec + ms/GN-iter on 5k-node/20k-edge synthetic graph, 1->8 GPU",
