@@ -243,7 +243,19 @@ __global__ __launch_bounds__(kRB) void raster_kernel(DS d) {
 // per-call reset of the window and the small scratch (one launch instead of seven memsets)
 __global__ __launch_bounds__(kT) void init_kernel(DS d, int64_t n_cells) {
     const int64_t stride = (int64_t)gridDim.x * kT;
-    for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
+    const int64_t n4 = n_cells >> 2;   // 16-byte accesses (hipMalloc buffers are 256-B aligned)
+    uint4* g4 = reinterpret_cast<uint4*>(d.grid);
+    int4* f4 = reinterpret_cast<int4*>(d.first);
+    for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n4; c += stride) {
+        uint4 w = make_uint4(0u, 0u, 0u, 0u);
+        if (!d.rebuild) {
+            w = g4[c];
+            w.x &= d.keep_mask; w.y &= d.keep_mask; w.z &= d.keep_mask; w.w &= d.keep_mask;
+        }
+        g4[c] = w;
+        f4[c] = make_int4(kInf, kInf, kInf, kInf);
+    }
+    for (int64_t c = 4 * n4 + (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
         d.grid[c] = d.rebuild ? 0u : (d.grid[c] & d.keep_mask);
         d.first[c] = kInf;
     }
@@ -268,15 +280,25 @@ __global__ __launch_bounds__(kT) void hist_kernel(DS d, int64_t n_cells) {
     const uint32_t chain_mask = d.chain_bits;
     int in = 0;
     const int64_t stride = (int64_t)gridDim.x * kT;
-    for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride) {
-        if (!(d.grid[c] & chain_mask)) continue;
+    auto count = [&](uint32_t w, int32_t f) {
+        if (!(w & chain_mask)) return;
         ++in;
-        const int32_t f = d.first[c];
         if (f != kInf) {
             if (lds) atomicAdd(&h[f], 1);
             else atomicAdd(&d.cand_cnt[f], 1);
         }
+    };
+    const int64_t n4 = n_cells >> 2;   // 16-byte loads; first[] only where a chain cell is
+    const uint4* g4 = reinterpret_cast<const uint4*>(d.grid);
+    const int4* f4 = reinterpret_cast<const int4*>(d.first);
+    for (int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x; c < n4; c += stride) {
+        const uint4 w = g4[c];
+        if (!((w.x | w.y | w.z | w.w) & chain_mask)) continue;
+        const int4 f = f4[c];
+        count(w.x, f.x); count(w.y, f.y); count(w.z, f.z); count(w.w, f.w);
     }
+    for (int64_t c = 4 * n4 + (int64_t)blockIdx.x * kT + threadIdx.x; c < n_cells; c += stride)
+        count(d.grid[c], d.first[c]);
     if (in) atomicAdd(&tot, (unsigned long long)in);
     __syncthreads();
     if (threadIdx.x == 0 && tot) atomicAdd(&d.ctl->chain_cells, tot);
