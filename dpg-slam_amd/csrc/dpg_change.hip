@@ -633,9 +633,13 @@ void node_frame(const dpg_dpg* d, const float* e, float* f) {
     f[0] = lx; f[1] = ly; f[2] = cosf(a); f[3] = sinf(a); f[4] = cosf(-a); f[5] = sinf(-a); f[6] = 0.f; f[7] = 0.f;
 }
 
-int upload_frames(dpg_dpg* d, int64_t V, const float* est) {
+// active_only: executeDPG reads the frames of active nodes only (inactive nodes have no grid and
+// skip the sector update), so after a re-optimisation only those are recomputed; a stale frame of
+// an inactive node keeps its old pose bits in h_pose and is refreshed when the map lists need it
+int upload_frames(dpg_dpg* d, int64_t V, const float* est, bool active_only = false) {
     int64_t lo = V, hi = -1;
     for (int64_t v = 0; v < V; ++v) {
+        if (active_only && !d->active_h[(size_t)v]) continue;
         float* c = &d->h_pose[(size_t)(3 * v)];
         if (memcmp(c, est + 3 * v, 3 * sizeof(float)) == 0) continue;
         memcpy(c, est + 3 * v, 3 * sizeof(float));
@@ -864,7 +868,7 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         }
     }
     st->n_candidates = (int64_t)cand.size();
-    int rc = upload_frames(d, V, est);
+    int rc = upload_frames(d, V, est, true);
     if (rc) return rc;
     if (d->d_ctl.reserve(1)) return dpg_set_error(DPG_ERR_HIP, "hipMalloc(ctl) failed");
     if (chain_n == 0) {   // no pose chain: only the sector/node update of the (empty) removed set runs
