@@ -33,31 +33,65 @@ def log(*a):
 
 
 def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the last committed rocprofv3 PMC pass
-    (profiles/pmc_traffic.json, written by tools/pmc_summary.py: (2 x FETCH_SIZE + WRITE_SIZE) KiB,
-    the gfx950 correction of MI355X_MICROARCH.md "HBM").  None when no pass covers this kernel."""
+    """HBM bytes per launch of `kernel` and its SQ-counter fractions from the last committed
+    rocprofv3 PMC passes (profiles/pmc_traffic.json, written by tools/pmc_summary.py: (2 x
+    FETCH_SIZE + WRITE_SIZE) KiB, the gfx950 correction of MI355X_MICROARCH.md "HBM").  (None, None,
+    {}) when no pass covers this kernel."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None, None
+        return None, None, {}
     d = json.load(open(path))
     for k, v in d.get("traffic_bytes_per_launch", {}).items():
         if k.split("<")[0] == kernel:
-            return float(v), d.get("source")
-    return None, None
+            return float(v), d.get("source"), d.get("sq_fractions", {}).get(k, {})
+    return None, None, {}
 
 
-def cpu_baseline(w, params, sample_edges: int, threads: int = 1) -> dict:
-    """Oracle (CPU restatement, grid NN) timed on this host: ICP on a bounded sample of the same
-    workload + the full-graph GN (block-sparse Cholesky)."""
+def host_cpus() -> dict:
+    """Core count of this host: the CPUs this process may run on, and lscpu's view of the machine."""
+    info = {"affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()}
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("CPU(s)", "Model name", "Thread(s) per core"):
+                info[k.strip()] = v.strip()
+    except Exception:
+        pass
+    return info
+
+
+def _median_time(fn, runs: int) -> tuple:
+    fn()   # warm-up
+    ts = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        out = fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), out
+
+
+def cpu_baseline(w, params, sample_edges: int, threads: int = 1, runs: int = 5) -> dict:
+    """Oracle (CPU restatement, grid NN) timed on this host, median of `runs` after a warm-up:
+    ICP on a bounded random sample of the same workload's edges."""
     from oracle import oracle as O
     rng = np.random.default_rng(0)
     sel = np.sort(rng.choice(w.E, min(sample_edges, w.E), replace=False))
-    O.icp_batch(w.pts, w.offsets, w.edges[sel[:8]], w.est, params, O.NN_GRID, threads)   # warm-up
-    t0 = time.perf_counter()
-    res, _ = O.icp_batch(w.pts, w.offsets, w.edges[sel], w.est, params, O.NN_GRID, threads)
-    t_icp = time.perf_counter() - t0
-    # GN on the full graph needs all ICP measurements: use the GPU's (bit-identical) results
-    return {"icp_edges_per_s": len(sel) / t_icp, "icp_s": t_icp, "n": len(sel), "iters_mean": float(res["iterations"].mean())}
+    t, (res, _) = _median_time(lambda: O.icp_batch(w.pts, w.offsets, w.edges[sel], w.est, params, O.NN_GRID, threads),
+                               runs)
+    return {"icp_edges_per_s": len(sel) / t, "icp_s": t, "n": len(sel), "iters_mean": float(res["iterations"].mean())}
+
+
+def cpu_gn_baseline(w, icp_results, params, runs: int = 5) -> dict:
+    """The oracle's batch Gauss-Newton (block-sparse Cholesky, one thread) on the full graph of the
+    same workload from the same initial poses, fed the step's ICP measurements (bit-identical to
+    the oracle's own), median of `runs` after a warm-up."""
+    from oracle import oracle as O
+    F = w.factors_with_icp(icp_results, params)
+    X0 = w.est.astype(np.float64)
+    t, (_, st) = _median_time(lambda: O.optimize_graph(X0, F), runs)
+    return {"ms_per_gn_iter": t * 1e3 / max(1, st.iterations), "gn_iterations": int(st.iterations), "s": t}
 
 
 def main():
@@ -66,7 +100,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="config4")
-    ap.add_argument("--cpu-sample", type=int, default=1500, help="edges in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=500, help="edges in the CPU-baseline ICP sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse "
@@ -166,20 +200,27 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = host_cpus()
         cb = cpu_baseline(w, params, args.cpu_sample, threads=1)
+        gnb = cpu_gn_baseline(w, res, params)
         cpu = {"value": cb["icp_edges_per_s"], "unit": "edges/s", "cores": 1, "kind": "port",
                "sample": f"oracle (C restatement, grid NN, 1 thread) ICP on {cb['n']} random edges of "
-                         f"{args.config} ({cb['icp_s']:.1f} s, mean {cb['iters_mean']:.1f} ICP iterations)"}
-        # the same sample over edges with OpenMP, at most 16 threads (the box's share)
-        nt = max(1, min(16, os.cpu_count() or 1))
+                         f"{args.config}: median of 5 runs after a warm-up ({cb['icp_s']:.2f} s per run, mean "
+                         f"{cb['iters_mean']:.1f} ICP iterations)",
+               "gn_ms_per_iter": gnb["ms_per_gn_iter"],
+               "gn_sample": f"oracle batch GN (block-sparse Cholesky, 1 thread) on the full {args.config} graph, "
+                            f"{gnb['gn_iterations']} iterations, median of 5 runs ({gnb['s']:.2f} s per solve)",
+               "host": cores}
+        # the same ICP sample over edges with OpenMP, at most 16 threads (the box's share)
+        nt = max(1, min(16, cores.get("affinity") or 1))
         if nt > 1:
             cm = cpu_baseline(w, params, args.cpu_sample, threads=nt)
             cpu["multithread"] = {"value": cm["icp_edges_per_s"], "unit": "edges/s", "cores": nt,
-                                  "sample": f"same sample, OpenMP over edges ({cm['icp_s']:.2f} s)"}
+                                  "sample": f"same sample, OpenMP over edges, median of 5 runs ({cm['icp_s']:.2f} s per run)"}
 
-    traffic, traffic_src = pmc_traffic(KERNEL_NAME[args.icp_variant])
+    traffic, traffic_src, sq = pmc_traffic(KERNEL_NAME[args.icp_variant])
     if world > 1:   # the PMC pass measured the whole 1-GPU launch; a rank's launch holds only its shard
-        traffic, traffic_src = None, None
+        traffic, traffic_src, sq = None, None, {}
     if rank == 0:
         line = {
             "metric": "ICP edges/sec + ms/GN-iter on 5k-node/20k-edge synthetic graph, 1->8 GPU",
@@ -206,10 +247,18 @@ def main():
             "icp_variant": args.icp_variant,
             "icp_edges_per_s_kernel": w.E / world / (stats["icp_kernel_ms"] * 1e-3) * world,
             "icp_iters_mean": stats["icp_iters_mean"],
+            "icp_iters_max": stats["icp_iters_max"],
+            "gn_note": "ms_per_gn_iter averages plain GN steps and chord steps that reuse the last Cholesky "
+                       "factor (gn_factorizations of gn_iterations refactor; DESIGN.md section 3)",
+            # roofline of the dominant kernel against HBM (SURVEY 8d's algorithmic bytes); the counters
+            # say what actually limits it: "limiter" + the SQ fractions of the last committed PMC pass
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": KERNEL_NAME[args.icp_variant] + " (correspondence search + fit, fused)",
-                         "bytes_per_launch": algo_bytes},
+                         "bytes_per_launch": algo_bytes,
+                         "limiter": "VALU issue + LDS latency with per-iteration workgroup barriers, not HBM: "
+                                    "the clouds stay in LDS for all iterations (traffic << algorithmic bytes)",
+                         **({"sq": sq} if sq else {})},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

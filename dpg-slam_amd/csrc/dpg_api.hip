@@ -83,6 +83,7 @@ struct dpg_ctx {
     bool own_stream = false;
     hipEvent_t ev[8] = {};
     int32_t icp_variant = DPG_ICP_ANGULAR;
+    int32_t defer_cap = 256;        // angular ICP: cooperative-queue threshold (dpg_ctx_set_icp_defer_cap)
     float map_ms = 0.f;             // last dpg_get_map kernel (HIP events map_ev)
     hipEvent_t map_ev[2] = {};
     // scan store (batch form)
@@ -168,6 +169,7 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (c->icp_variant == DPG_ICP_ANGULAR) {
         kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 16);   // LDS record capacity
+        kp.defer_cap = c->defer_cap;
         rc = dpg_launch_icp_ang(ds_dev, tree_pts, tree_idx, buckets, edges_dev, ne, &kp, maxp, res_dev, trace_dev,
                                 c->stream);
     } else if (c->icp_variant == DPG_ICP_KDTREE) {
@@ -389,6 +391,12 @@ int dpg_ctx_set_icp_variant(dpg_ctx* c, int32_t variant) {
     if (!c || (variant != DPG_ICP_ANGULAR && variant != DPG_ICP_KDTREE && variant != DPG_ICP_GRID))
         return fail(DPG_ERR_ARG, "bad ICP variant");
     c->icp_variant = variant;
+    return DPG_OK;
+}
+
+int dpg_ctx_set_icp_defer_cap(dpg_ctx* c, int32_t cap) {
+    if (!c || cap < 0) return fail(DPG_ERR_ARG, "bad defer cap");
+    c->defer_cap = cap;
     return DPG_OK;
 }
 

@@ -27,6 +27,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "dpg_atan2f.h"
 #include "dpg_internal.h"
 #include "dpg_icp_tree.h"
@@ -39,9 +41,11 @@
 // of all waves' trips (imbalance = 8 [14] / [15]).  DPG_ICP_TIMING
 // (per-wave s_memtime cycles summed over waves and iterations, last iteration excluded):
 // [8] search, [9] sums + fold, [10] arrival + fit + publish barrier, [11] move + barrier,
-// [12] wave-iterations
+// [12] wave-iterations, [45] queue phase (barrier, cooperative scans, barrier, finalize).
+// DPG_ICP_STATS also: [40] queued forward windows, [41] their candidates, [42] cooperative
+// reciprocal scans, [43] their candidates, [44] workgroup-iterations with a non-empty queue
 #define DPG_ICP_DIAG 1
-__device__ unsigned long long g_icp_stats[40];
+__device__ unsigned long long g_icp_stats[48];
 #define ICP_STAT_ADD(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
 #endif
 #ifdef DPG_ICP_STATS
@@ -172,18 +176,26 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 
 // Workgroup shape: kT = 512 threads (8 waves; 4 workgroups = 32 waves per CU at <= 64 VGPRs and
 // ~38 KB of LDS each), thread t owns the source points i = t + kT m and is lane t of the fp64
-// reduction tree (dpg_icp_tree.h, DPG_ICP_LANES = 512): it sums its own accepted pairs right after
-// its searches, the wave folds by DPP/swizzle, and the LAST wave to arrive (LDS counter) combines
-// the eight partials, fits and decides convergence, then one barrier publishes the result.
-// Per iteration: search + sums + fold, fit by one wave, barrier, move the source, barrier.
+// reduction tree (dpg_icp_tree.h, DPG_ICP_LANES = 512).  Per iteration:
+//   1. search: each thread runs the forward and reciprocal windows of its points in its own lane;
+//      a window of more than kp.defer_cap candidates goes to the workgroup's cooperative queue
+//      instead (a point near the sensor origin can span the whole cloud, and one such lane used to
+//      hold its wave -- and the other seven at the fit -- for a full scan);
+//   2. barrier; the waves drain the queue, one item per wave at a time, 64 candidates per trip,
+//      wave-wide argmin / any (same exact result as the lane's own scan); barrier (only when the
+//      queue was not empty);
+//   3. each thread finalizes its points, sums its accepted pairs (tree lane t), the wave folds by
+//      DPP/swizzle, and the LAST wave to arrive (LDS counter) combines the eight partials, fits
+//      and decides convergence; one barrier publishes the result; the source moves; barrier.
 //
-// Candidate loops (R4) visit kU records per trip, wave-uniformly, with no per-candidate bounds
-// test: a lane whose own window is exhausted keeps evaluating the records that follow it.  That
-// is exact -- every record visited is a real point of the cloud, so the forward argmin over a
+// In-lane candidate loops (R4) visit kU records per trip, wave-uniformly, with no per-candidate
+// bounds test: a lane whose own window is exhausted keeps evaluating the records that follow it.
+// That is exact -- every record visited is a real point of the cloud, so the forward argmin over a
 // superset of the window that contains the true nearest neighbour is the same (distance, lowest
 // original index) minimum, and any extra source record that beats i at t_j is a genuine
 // reciprocity violation.  Records [n, n + kU) repeat [0, kU) mod n so that a trip never wraps
-// inside itself; the trip start advances by kU mod n.
+// inside itself; the trip start advances by kU mod n.  The cooperative scan visits the window
+// exactly.
 constexpr int kWaves = kT / 64;
 static_assert(kT == dpg_tree::kLanes, "one tree lane per thread");
 #ifndef DPG_ANG_KU
@@ -196,6 +208,17 @@ constexpr int kU = DPG_ANG_KU;   // candidates per trip
 // an unmatched point searches kClear beyond r once; while the distance it has moved since stays
 // below the margin found, it provably has no target within r and skips its forward search
 constexpr float kClear = 0.1f;
+constexpr int kQCap = 64;        // cooperative queue items per iteration (a full queue: in-lane scan)
+
+// One queued window (16 B), as indices only: the wave that takes it recomputes the window from
+// LDS, with the same float expressions the owner would have used.  w0 = i | sp << 16 (source
+// original index, sorted position); w1 = kind (0 forward, 1 reciprocal) | v << 1 with v = the
+// point's seed + 1 (forward) or its forward match position (reciprocal); w2, w3 = result: the
+// best key of a forward item (lo, hi) and, in bit 0 of w1 after the scan, whether the point has a
+// (reciprocal) correspondence.
+struct QItem {
+    uint32_t w[4];
+};
 
 // what the fitting wave hands every wave after the fit of an iteration
 struct Bcast {
@@ -206,6 +229,9 @@ struct Bcast {
     float r[4];      // this iteration's (cos, sin, tx, ty)
     int code;        // 0 continue, 1 converged (stop), 2 too few correspondences (stop)
     int cnt;
+    int qtail;       // cooperative queue: items pushed this iteration (may exceed kQCap)
+    int qhead;       // unused
+    int iter;        // iterations fitted so far (every wave checks it after the publish barrier)
 };
 
 // fp64 inverse of the 2x2 block of a 2x3 float transform (same expressions every time)
@@ -220,7 +246,8 @@ __device__ __forceinline__ void inverse2(const float F[6], double inv[4]) {
 struct Lds {
     Rec* tp;          // target points in angle order, [cap + kU]
     Rec* scs;         // current (moved) source points in the source's angle order, [cap + kU]
-    uint16_t* spos;   // source original index -> sorted position
+    uint16_t* spos;   // source original index -> sorted position (setup only)
+    QItem* q;         // cooperative queue [kQCap] (aliases spos after the setup)
     uint16_t* tb;     // target bucket starts [kB+1]
     uint16_t* sb;     // source bucket starts [kB+1]
     double* wpart;    // [kWaves][kSums + 2] wave partials of the tree
@@ -230,9 +257,10 @@ struct Lds {
 
 __host__ __device__ inline size_t ang_lds_layout(int cap, size_t* off /* [7] or null */) {
     size_t o = 0, p[7];
+    const size_t spos_q = 2 * (size_t)cap > sizeof(QItem) * kQCap ? 2 * (size_t)cap : sizeof(QItem) * kQCap;
     p[0] = o; o = (o + 16 * (size_t)(cap + kU) + 15) & ~size_t(15);
     p[1] = o; o = (o + 16 * (size_t)(cap + kU) + 15) & ~size_t(15);
-    p[2] = o; o = (o + 2 * (size_t)cap + 15) & ~size_t(15);
+    p[2] = o; o = (o + spos_q + 15) & ~size_t(15);
     p[3] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
     p[4] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
     p[5] = o; o = (o + sizeof(double) * kWaves * (kSums + 2) + 15) & ~size_t(15);
@@ -249,6 +277,7 @@ __device__ Lds carve(unsigned char* base, int cap) {
     L.tp = reinterpret_cast<Rec*>(base + p[0]);
     L.scs = reinterpret_cast<Rec*>(base + p[1]);
     L.spos = reinterpret_cast<uint16_t*>(base + p[2]);
+    L.q = reinterpret_cast<QItem*>(base + p[2]);
     L.tb = reinterpret_cast<uint16_t*>(base + p[3]);
     L.sb = reinterpret_cast<uint16_t*>(base + p[4]);
     L.wpart = reinterpret_cast<double*>(base + p[5]);
@@ -302,6 +331,7 @@ __device__ __forceinline__ double uni(double x) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b), hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane(x); }
 
 // squared distance, (ax - bx)^2 + (ay - by)^2 in float: packed subtract / multiply (v_pk_*_f32,
 // the same IEEE operations lane by lane), then one add -- bit-identical to the scalar form.
@@ -338,6 +368,68 @@ __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float
     return cnt;
 }
 
+// Wave-level reservation of queue slots for the lanes that want one: one LDS atomic per wave.
+// Returns the lane's slot, or -1 (no request, or the queue is full: the lane scans in-lane).
+// Called by all 64 lanes.
+__device__ __forceinline__ int queue_push(bool want, int* tail) {
+    const uint64_t mask = __ballot(want);
+    if (mask == 0) return -1;
+    int base = 0;
+    if ((threadIdx.x & 63) == 0) base = atomicAdd(tail, __popcll(mask));
+    base = __builtin_amdgcn_readfirstlane(base);
+    const int idx = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    return (want && idx < kQCap) ? idx : -1;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, off, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), off, 64);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// The forward search's starting point for a point at q (R4 seeding): seed >= 0 is the last
+// match (its distance bounds the radius), -1 means no knowledge (search r + kClear, probing the
+// target at q's own bearing first).  Returns the initial best key and sets the radius.  Used by
+// the owner lane and by the cooperative scan with identical arithmetic.
+__device__ __forceinline__ uint64_t forward_init(const Lds& L, int M, int sd, float qx, float qy, float r2f, float rmax,
+                                                 float rext, float r2ext, float& rad) {
+    uint64_t best = dkey(r2f, 0xffffffffu);   // "none": every candidate with d <= r beats it
+    rad = rmax;
+    if (sd == -1) {
+        rad = rext;
+        best = dkey(r2ext, 0xffffffffu);
+        int p0 = L.tb[bucket_of(pseudo_angle(qx, qy))];
+        p0 = p0 >= M ? 0 : p0;
+        if (M > 0) {
+            const Rec r = L.tp[p0];
+            const float d = sqd(qx, qy, r.x, r.y);
+            if (d <= r2ext) {
+                best = dkey(d, r.key);
+                rad = sqrtf(d) * 1.0001f + 1e-6f;
+            }
+        }
+    } else {
+        const Rec r = L.tp[sd];
+        const float d = sqd(qx, qy, r.x, r.y);
+        if (d <= r2f) {
+            best = dkey(d, r.key);
+            rad = sqrtf(d) * 1.0001f + 1e-6f;
+        }
+    }
+    return best;
+}
+
+// per-point state, one register: sorted position << 16 | seed (int16: >= 0 last match, -1 no
+// knowledge, < -1 clearance in 1e-4 m)
+__device__ __forceinline__ int st_seed(uint32_t st) { return (int)(int16_t)(uint16_t)(st & 0xffffu); }
+__device__ __forceinline__ int st_sp(uint32_t st) { return (int)(st >> 16); }
+__device__ __forceinline__ uint32_t st_with_seed(uint32_t st, int seed) { return (st & 0xffff0000u) | (uint32_t)(uint16_t)(int16_t)seed; }
+
 template <int PPT>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE, DPG_ANG_WPE))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
                                                      const float2* __restrict__ idx_pts,
@@ -353,6 +445,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
     const int N = E.n_src_ds, M = E.n_tgt_ds;
     const int vt = E.tgt_node, vs = E.src_node;
     const int cap = kp.lds_tgt;
+    const int dcap = kp.defer_cap > 0 ? kp.defer_cap : 0x7fffffff;   // windows above it are queued
 #ifdef DPG_ICP_STATS
     __shared__ unsigned st_wmax;
     if (t == 0) st_wmax = 0;
@@ -389,18 +482,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
         B.r[0] = B.r[1] = B.r[2] = B.r[3] = 0.f;
         B.code = 0;
         B.cnt = 0;
+        B.qtail = 0;
+        B.qhead = 0;
+        B.iter = 0;
         *L.bc = B;
         *L.arrive = 0;
     }
     __syncthreads();
     float sx[PPT], sy[PPT];
-    int seed[PPT], sp[PPT];
+    uint32_t st[PPT];
     // store the moved source point at its sorted position (and its repeat past n)
     auto put = [&](int m) {
-        L.scs[sp[m]].x = sx[m];
-        L.scs[sp[m]].y = sy[m];
-        if (sp[m] < kU)
-            for (int r = N + sp[m]; r < N + kU; r += N) {
+        const int sp = st_sp(st[m]);
+        L.scs[sp].x = sx[m];
+        L.scs[sp].y = sy[m];
+        if (sp < kU)
+            for (int r = N + sp; r < N + kU; r += N) {
                 L.scs[r].x = sx[m];
                 L.scs[r].y = sy[m];
             }
@@ -408,19 +505,18 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
 #pragma unroll
     for (int m = 0; m < PPT; ++m) {
         const int i = t + kT * m;
-        seed[m] = -1;
-        sp[m] = 0;
+        st[m] = st_with_seed(0u, -1);
         sx[m] = 0.f;
         sy[m] = 0.f;
         if (i < N) {
             const float2 p = ds_pts[E.src_ds_off + i];
             sx[m] = (F[0] * p.x + F[1] * p.y) + F[2];
             sy[m] = (F[3] * p.x + F[4] * p.y) + F[5];
-            sp[m] = L.spos[i];
+            st[m] = ((uint32_t)L.spos[i] << 16) | (st[m] & 0xffffu);
             put(m);
         }
     }
-    __syncthreads();
+    __syncthreads();   // spos is dead from here on: its LDS holds the queue
 
     const float r2f = kp.r2_f;
     const float rmax = sqrtf(r2f) * 1.0001f + 1e-5f;
@@ -428,18 +524,39 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
     const float rext = rmax + kClear, r2ext = rext * rext;
     int k = 0, converged = 0, status = DPG_ICP_OK;
 #ifdef DPG_ICP_TIMING
-    unsigned long long ph[4] = {0, 0, 0, 0}, nit = 0;
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, nit = 0;
 #endif
+    // the forward result of a point (best key) -> its match position (-1: none) and next seed
+    auto forward_done = [&](int m, uint64_t best, bool ext) -> int {
+        const uint32_t bkey = (uint32_t)best;
+        const float bd = __uint_as_float((uint32_t)(best >> 32));
+        const int bp = (bkey == 0xffffffffu || bd > r2f) ? -1 : (int)(bkey & 0xffffu);   // R4: d > r^2 rejected
+        int nsd = bp;
+        if (bp < 0 && ext) {   // nothing within r: the nearest target is >= min(sqrt(bd), rext) away
+            const float clr = fminf(sqrtf(bd), rext) * 0.99999f - rmax_hi;
+            const int q = clr > 0.f ? (int)(clr * 1e4f) : 0;   // units of 1e-4 m, rounded down
+            nsd = -1 - q;
+        }
+        st[m] = st_with_seed(st[m], nsd);
+        return bp;
+    };
     for (;;) {
         ICP_STAMP(c0);
         const float i00 = uni((float)L.bc->inv[0]), i01 = uni((float)L.bc->inv[1]);
         const float i10 = uni((float)L.bc->inv[2]), i11 = uni((float)L.bc->inv[3]);
         const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
         const float drift = 1e-4f + 5e-5f * (float)(k + 1);
-        uint32_t okm = 0;   // bit m: point t + 512 m has a (reciprocal) correspondence
+        // bit m: point t + 512 m has a (reciprocal) correspondence; bits 8 + 7 m ..: queue slot + 1
+        uint32_t okq = 0;
+        static_assert(PPT <= 3 || sizeof(okq) == 4, "");
+        uint32_t qhi = 0;   // PPT > 3: slots of points 3.. (7 bits each)
 #ifdef DPG_ICP_STATS
         unsigned wtrips = 0;
 #endif
+        auto set_slot = [&](int m, int slot) {
+            if (m < 3) okq |= (uint32_t)(slot + 1) << (8 + 7 * m);
+            else qhi |= (uint32_t)(slot + 1) << (7 * (m - 3));
+        };
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
             // every lane runs every trip (dead lanes included): the candidate loops are
@@ -447,40 +564,23 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             const int i = t + kT * m;
             const bool live = i < N;
             const float qx = sx[m], qy = sy[m];
+            const int sd = st_seed(st[m]);
             // ---- forward 1-NN (target index), seeded radius ----
-            // seed[m] >= 0: last match (its distance seeds the radius); -1: no knowledge;
-            // < -1: clearance -- provably no target within r of this point -- so no search
-            uint64_t best = dkey(r2f, 0xffffffffu);   // "none": every candidate with d <= r beats it
-            float rad = rmax;
-            const int sd = seed[m];
-            const bool search = live && sd >= -1;
-            const bool ext = search && sd == -1;   // unseeded: search r + kClear to learn a clearance
-            if (ext) {
-                // unseeded: the target at q's own bearing (first point of q's bucket) bounds the
-                // nearest distance -- on a surface both scans see it is a few cm away
-                rad = rext;
-                best = dkey(r2ext, 0xffffffffu);
-                int p0 = L.tb[bucket_of(pseudo_angle(qx, qy))];
-                p0 = p0 >= M ? 0 : p0;
-                if (M > 0) {
-                    const Rec r = L.tp[p0];
-                    const float d = sqd(qx, qy, r.x, r.y);
-                    if (d <= r2ext) {
-                        best = dkey(d, r.key);
-                        rad = sqrtf(d) * 1.0001f + 1e-6f;
-                    }
-                }
-            } else if (search) {
-                const Rec r = L.tp[sd];
-                const float d = sqd(qx, qy, r.x, r.y);
-                if (d <= r2f) {
-                    best = dkey(d, r.key);
-                    rad = sqrtf(d) * 1.0001f + 1e-6f;
-                }
-            }
+            const bool search = live && sd >= -1;   // < -1: clearance, provably no target within r
+            float rad;
+            uint64_t best = forward_init(L, M, search ? sd : 0, qx, qy, r2f, rmax, rext, r2ext, rad);
+            bool pend;   // this point's forward window went to the queue
             {
                 int s = 0;
-                const int fc = search ? window(L.tb, M, qx, qy, rad, s) : 0;
+                int fc = search ? window(L.tb, M, qx, qy, rad, s) : 0;
+                const int slot = queue_push(fc > dcap, &L.bc->qtail);
+                pend = slot >= 0;
+                if (pend) {
+                    *reinterpret_cast<uint2*>(&L.q[slot].w[0]) =
+                        make_uint2((uint32_t)i | ((uint32_t)st_sp(st[m]) << 16), (uint32_t)(sd + 1) << 1);
+                    set_slot(m, slot);
+                    fc = 0;
+                }
 #ifdef DPG_ICP_STATS
                 {
                     int trips = 0;
@@ -501,22 +601,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
                     s = advance(s, stepM, M);
                 }
             }
-            const uint32_t bkey = (uint32_t)best;
-            const float bd = __uint_as_float((uint32_t)(best >> 32));
-            const int bp = (bkey == 0xffffffffu || bd > r2f) ? -1 : (int)(bkey & 0xffffu);   // R4: d > r^2 rejected
-            const int bi = (int)(bkey >> 16);
-            if (search) {
-                int nsd = bp;
-                if (bp < 0 && ext) {   // nothing within r: the nearest target is >= min(sqrt(bd), rext) away
-                    const float clr = fminf(sqrtf(bd), rext) * 0.99999f - rmax_hi;
-                    const int q = clr > 0.f ? (int)(clr * 1e4f) : 0;   // units of 1e-4 m, rounded down
-                    nsd = -1 - q;
-                }
-                seed[m] = nsd;
-            }
+            int bp = -1;
+            if (search && !pend) bp = forward_done(m, best, sd == -1);
             bool ok = live && bp >= 0;
             // ---- reciprocal test in the static source index ----
             if (kp.reciprocal) {
+                const float bd = __uint_as_float((uint32_t)(best >> 32));
                 float2 tj = make_float2(0.f, 0.f);
                 int s = 0, rc = 0;
                 if (ok) {
@@ -527,15 +617,23 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
                     const float px = i00 * ux + i01 * uy, py = i10 * ux + i11 * uy;
                     rc = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
                 }
+                const int slot = queue_push(ok && rc > dcap, &L.bc->qtail);
+                if (slot >= 0) {
+                    *reinterpret_cast<uint2*>(&L.q[slot].w[0]) =
+                        make_uint2((uint32_t)i | ((uint32_t)st_sp(st[m]) << 16), 1u | ((uint32_t)bp << 1));
+                    set_slot(m, slot);
+                    ok = false;
+                    rc = 0;
+                }
                 // i's own word: any other current source with a smaller (d, original index) word
                 // is closer to t_j (or tied with a lower index) and breaks reciprocity
-                const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)sp[m]);
+                const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)st_sp(st[m]));
 #ifdef DPG_ICP_STATS
                 {
                     int trips = 0;
                     for (int c = 0; __any(ok & (c < rc)); c += kU) ++trips;
                     if (ok) { ICP_STAT(3, rc); if (rc >= N) ICP_STAT(13, 1); }
-                    if (live && !ok) ICP_STAT(6, 1);
+                    if (live && !ok && !pend && slot < 0) ICP_STAT(6, 1);
                     if (lane == 0) { ICP_STAT(4, trips); ICP_STAT(28 + trip_bin(trips), trips); }
                     wtrips += trips;
                 }
@@ -556,11 +654,87 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
 #ifdef DPG_ICP_STATS
             if (ok) ICP_STAT(5, 1);
 #endif
-            if (live && trace && k < kp.trace_iters)
-                trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] = ok ? bi : -1;
-            okm |= (ok ? 1u : 0u) << m;
+            okq |= (ok ? 1u : 0u) << m;
         }
         ICP_STAMP(c1);
+        // ---- the cooperative queue: windows too wide for one lane, 64 candidates per trip ----
+        __syncthreads();
+        const int nq = min((int)uni((uint32_t)L.bc->qtail), kQCap);
+        if (nq > 0) {   // nq is the same in every wave (read after the barrier)
+            const int w0q = __builtin_amdgcn_readfirstlane(wave);
+            for (int h = w0q; h < nq; h += kWaves) {   // items dealt round-robin to the waves
+                QItem* it = L.q + h;
+                const uint32_t w0 = uni(it->w[0]), w1 = uni(it->w[1]);
+                const int i = (int)(w0 & 0xffffu), ps = (int)(w0 >> 16);
+                const float qx = uni(L.scs[ps].x), qy = uni(L.scs[ps].y);   // the point as the owner saw it
+                bool okw = true;
+                int bp, s = 0, cnt = 0;
+                uint64_t best = 0;
+                if ((w1 & 1u) == 0u) {   // forward argmin over the window, then the reciprocal test
+                    float rad;
+                    const uint64_t b0 = forward_init(L, M, (int)(w1 >> 1) - 1, qx, qy, r2f, rmax, rext, r2ext, rad);
+                    const int fc = window(L.tb, M, qx, qy, rad, s);
+                    best = lane == 0 ? b0 : ~0ull;
+                    for (int c = lane; c < fc; c += 64) {
+                        const int p = s + c >= M ? s + c - M : s + c;
+                        const Rec r = ld_rec(L.tp + p);
+                        const uint64_t kd = dkey(sqd(qx, qy, r.x, r.y), r.key);
+                        best = kd < best ? kd : best;
+                    }
+                    best = wave_min_u64(best);
+#ifdef DPG_ICP_STATS
+                    if (lane == 0) { ICP_STAT(40, 1); ICP_STAT(41, fc); }
+#endif
+                    const uint32_t bkey = (uint32_t)best;
+                    const float bd = __uint_as_float((uint32_t)(best >> 32));
+                    bp = (bkey == 0xffffffffu || bd > r2f) ? -1 : (int)(bkey & 0xffffu);
+                    okw = bp >= 0;
+                } else {
+                    bp = (int)(w1 >> 1);
+                }
+                if (okw && kp.reciprocal) {   // does any current source point beat i at t_j?
+                    const Rec r = L.tp[bp];
+                    const float tjx = r.x, tjy = r.y;
+                    const float bd = sqd(qx, qy, tjx, tjy);   // the same float the forward search kept
+                    const float ux = tjx - ftx, uy = tjy - fty;
+                    const float px = i00 * ux + i01 * uy, py = i10 * ux + i11 * uy;
+                    cnt = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
+                    const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)ps);
+                    bool beat = false;
+                    for (int c = lane; c < cnt; c += 64) {
+                        const int p = s + c >= N ? s + c - N : s + c;
+                        const Rec q = ld_rec(L.scs + p);
+                        beat = beat | (dkey(sqd(q.x, q.y, tjx, tjy), q.key) < mine);
+                    }
+                    okw = !__any(beat);
+                }
+#ifdef DPG_ICP_STATS
+                if (lane == 0) { ICP_STAT(42, 1); ICP_STAT(43, cnt); }
+#endif
+                if (lane == 0) *reinterpret_cast<uint4*>(it) = make_uint4(w0, (w1 & ~1u) | (okw ? 1u : 0u) | ((w1 & 1u) << 31),
+                                                                            (uint32_t)best, (uint32_t)(best >> 32));
+            }
+#ifdef DPG_ICP_STATS
+            if (t == 0) ICP_STAT(44, 1);
+#endif
+            __syncthreads();
+        }
+        // finalize the points whose windows were queued
+#pragma unroll
+        for (int m = 0; m < PPT; ++m) {
+            const int slot = (int)(m < 3 ? (okq >> (8 + 7 * m)) & 0x7fu : (qhi >> (7 * (m - 3))) & 0x7fu) - 1;
+            if (slot >= 0) {
+                const uint4 it = *reinterpret_cast<const uint4*>(L.q + slot);
+                if ((it.y >> 31) == 0u)   // forward item: its best key -> match, next seed
+                    (void)forward_done(m, ((uint64_t)it.w << 32) | it.z, st_seed(st[m]) == -1);
+                okq |= (it.y & 1u) << m;
+            }
+            const int i = t + kT * m;
+            if (i < N && trace && k < kp.trace_iters)
+                trace[((size_t)e * kp.trace_iters + k) * kp.trace_stride + i] =
+                    ((okq >> m) & 1u) ? (int)(L.tp[st_seed(st[m])].key >> 16) : -1;
+        }
+        ICP_STAMP(c2);
         // ---- R5 sums: this thread is tree lane t (points t + 512 m, m ascending) ----
         {
             double acc[kSums];
@@ -568,22 +742,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             for (int q = 0; q < kSums; ++q) acc[q] = 0.0;
 #pragma unroll
             for (int m = 0; m < PPT; ++m) {
-                if ((okm >> m) & 1u) {
-                    const Rec tq = ld_rec(L.tp + seed[m]);
+                if ((okq >> m) & 1u) {
+                    const Rec tq = ld_rec(L.tp + st_seed(st[m]));
                     dpg_tree::add_pair(acc, sx[m], sy[m], tq.x, tq.y, sqd(sx[m], sy[m], tq.x, tq.y));
                 }
             }
-            dpg_tree::wave_fold<1>(acc);   // the count is an integer: ballots instead
+            acc[0] = 0.0;   // the count is an integer: ballots instead
+            const double wf = dpg_tree::wave_fold_t(acc);
             int cnt = 0;
 #pragma unroll
-            for (int m = 0; m < PPT; ++m) cnt += __popcll(__ballot((okm >> m) & 1u));
-            acc[0] = (double)cnt;
-            if (lane == 0) {
-#pragma unroll
-                for (int q = 0; q < kSums; ++q) L.wpart[wave * (kSums + 2) + q] = acc[q];
+            for (int m = 0; m < PPT; ++m) cnt += __popcll(__ballot((okq >> m) & 1u));
+            if ((lane & 7) == 0) {
+                const int q = dpg_tree::fold_sum(lane >> 3);
+                L.wpart[wave * (kSums + 2) + q] = q == 0 ? (double)cnt : wf;
             }
         }
-        ICP_STAMP(c2);
+        ICP_STAMP(c3);
         // ---- the last wave to arrive combines the partials, fits (R5) and decides (R6) ----
         int last = 0;
 #ifdef DPG_ICP_STATS
@@ -604,6 +778,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             for (int q = 0; q < 6; ++q) F[q] = uni(B.F[q]);
             const double prev_mse = uni(B.prev_mse);
             B.cnt = (int)S[0];
+            B.qtail = 0;   // every wave is past the queue of this iteration
+            B.qhead = 0;
+            B.iter = k + 1;
             if (B.cnt < kp.min_corr) {
                 B.code = 2;   // stop, "Not enough correspondences found" (transform unchanged)
             } else {
@@ -647,8 +824,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             }
         }
         __syncthreads();
-        ICP_STAMP(c3);
+        ICP_STAMP(c4);
         const int code = __builtin_amdgcn_readfirstlane(L.bc->code);
+        if (__builtin_amdgcn_readfirstlane(L.bc->iter) != k + 1) {   // no fit this iteration: internal error
+            converged = 0; status = DPG_ICP_INTERNAL; break;
+        }
         if (code == 2) { converged = 0; status = DPG_ICP_TOO_FEW_CORR; break; }
         const float cf = uni(L.bc->r[0]), sf = uni(L.bc->r[1]), txf = uni(L.bc->r[2]), tyf = uni(L.bc->r[3]);
         const float nsf = -sf;
@@ -659,15 +839,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             sx[m] = (cf * x + nsf * y) + txf;
             sy[m] = (sf * x + cf * y) + tyf;
             if (i < N) put(m);
-            if (seed[m] < -1) {   // the clearance shrinks by the distance the point just moved
+            const int sd = st_seed(st[m]);
+            if (sd < -1) {   // the clearance shrinks by the distance the point just moved
                 const float dx = sx[m] - x, dy = sy[m] - y;
                 const float mv = sqrtf(dx * dx + dy * dy) * 1.0001f + 1e-6f;
-                const int q = (-1 - seed[m]) - (int)ceilf(mv * 1e4f);
-                seed[m] = q > 0 ? -1 - q : -1;
+                const int q = (-1 - sd) - (int)ceilf(mv * 1e4f);
+                st[m] = st_with_seed(st[m], q > 0 ? -1 - q : -1);
             }
         }
         ++k;
         if (code == 1) { converged = 1; break; }
+        if (k >= kp.max_iter) { converged = 0; status = DPG_ICP_INTERNAL; break; }   // unreachable (the fit stops it)
         if (__builtin_amdgcn_readlane(last, 0)) {   // off the publish path: the next reciprocal
             double inv[4];                          // tests' inverse, while the others move points
             float Fn[6];
@@ -681,15 +863,15 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
         __syncthreads();   // moved source complete before the next reciprocal tests
 #ifdef DPG_ICP_TIMING
         {
-            ICP_STAMP(c4);
-            ph[0] += c1 - c0; ph[1] += c2 - c1; ph[2] += c3 - c2; ph[3] += c4 - c3; ++nit;
+            ICP_STAMP(c5);
+            ph[0] += c1 - c0; ph[1] += c3 - c2; ph[2] += c4 - c3; ph[3] += c5 - c4; ph[4] += c2 - c1; ++nit;
         }
 #endif
     }
 #ifdef DPG_ICP_TIMING
     if (lane == 0) {
         ICP_STAT_ADD(8, ph[0]); ICP_STAT_ADD(9, ph[1]); ICP_STAT_ADD(10, ph[2]); ICP_STAT_ADD(11, ph[3]);
-        ICP_STAT_ADD(12, nit);
+        ICP_STAT_ADD(12, nit); ICP_STAT_ADD(45, ph[4]);
     }
 #endif
     if (t == 0) {
@@ -720,9 +902,9 @@ extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 
 #ifdef DPG_ICP_DIAG
 extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 40 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 48 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[40] = {0};
+        unsigned long long z[48] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_icp_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

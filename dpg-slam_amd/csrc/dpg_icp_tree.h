@@ -59,6 +59,59 @@ __device__ __forceinline__ void wave_fold(double (&acc)[kSums]) {
     for (int q = FIRST; q < kSums; ++q) acc[q] = acc[q] + down<1>(acc[q]);
 }
 
+namespace detail {
+__device__ __forceinline__ uint32_t lo32(double v) { return (uint32_t)(uint64_t)__double_as_longlong(v); }
+__device__ __forceinline__ uint32_t hi32(double v) { return (uint32_t)((uint64_t)__double_as_longlong(v) >> 32); }
+__device__ __forceinline__ double mk(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// v_permlane32_swap / v_permlane16_swap on a pair of doubles: a keeps its own lower part (lanes
+// 0-31, resp. rows 0 and 2) and receives b's, b the mirror -- then a + b is the tree's sum
+// "lower lane + upper lane" of a in the lower part and of b in the upper part
+template <int W>
+__device__ __forceinline__ double swap_add(double a, double b) {
+    uint32_t al = lo32(a), ah = hi32(a), bl = lo32(b), bh = hi32(b);
+    if constexpr (W == 32) {
+        const auto l = __builtin_amdgcn_permlane32_swap(al, bl, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(ah, bh, false, false);
+        al = l[0]; bl = l[1]; ah = h[0]; bh = h[1];
+    } else {
+        const auto l = __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+        al = l[0]; bl = l[1]; ah = h[0]; bh = h[1];
+    }
+    return mk(al, ah) + mk(bl, bh);
+}
+}  // namespace detail
+
+// The same in-wave tree as wave_fold for all eight sums, with the work of each level spread
+// over the lanes: at off = 32 the lower half adds sums 0-3 and the upper half sums 4-7 (one
+// permlane32 swap per pair instead of a shuffle per sum), at off = 16 the rows split them again,
+// at off = 8 the half-rows, and the last three levels fold one sum per 8-lane group.  Every
+// partial is the same two operands added in the same order as in wave_fold, so the results are
+// bit-identical.  Lane 8 g ends with W_w[fold_sum(g)]; the other lanes' values are not used.
+__device__ __forceinline__ int fold_sum(int g) { return 4 * (g >> 2) + 2 * (g & 1) + ((g >> 1) & 1); }
+__device__ __forceinline__ double wave_fold_t(const double (&acc)[kSums]) {
+    static_assert(kSums == 8, "the transposed fold is written for eight sums");
+    const int lane = threadIdx.x & 63;
+    double u0 = detail::swap_add<32>(acc[0], acc[4]);
+    double u1 = detail::swap_add<32>(acc[1], acc[5]);
+    double u2 = detail::swap_add<32>(acc[2], acc[6]);
+    double u3 = detail::swap_add<32>(acc[3], acc[7]);
+    const double s0 = detail::swap_add<16>(u0, u1);
+    const double s1 = detail::swap_add<16>(u2, u3);
+    // off = 8 inside each 16-lane row: lanes 0-7 add s0, lanes 8-15 add s1
+    const bool lo8 = (lane & 15) < 8;
+    const double t = lo8 ? s1 : s0;
+    const double r = detail::mk((uint32_t)__builtin_amdgcn_update_dpp(0, (int)detail::lo32(t), 0x128, 0xF, 0xF, false),
+                                (uint32_t)__builtin_amdgcn_update_dpp(0, (int)detail::hi32(t), 0x128, 0xF, 0xF, false));
+    double z = lo8 ? s0 + r : r + s1;
+    z = z + down<4>(z);
+    z = z + down<2>(z);
+    z = z + down<1>(z);
+    return z;
+}
+
 // the cross-wave part: W[w * stride + q] -> S[q]
 __device__ __forceinline__ double combine(const double* W, int stride, int q) {
     return ((W[0 * stride + q] + W[1 * stride + q]) + (W[2 * stride + q] + W[3 * stride + q])) +

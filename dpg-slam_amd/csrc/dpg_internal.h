@@ -45,7 +45,8 @@ typedef struct dpg_icp_kparams {
     int32_t lds_tgt;    /* LDS target capacity (points) */
     int32_t trace_iters;
     int32_t trace_stride;
-    int32_t pad;
+    int32_t defer_cap;  /* angular kernel: windows of more candidates go to the workgroup's
+                           cooperative queue (0: never) */
 } dpg_icp_kparams;
 
 /* Launchers (defined in dpg_icp.hip).  Return 0 or a negative DPG_ERR_*. */

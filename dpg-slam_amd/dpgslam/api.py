@@ -172,6 +172,11 @@ class Context:
         v = {"angular": 3, "kdtree": 2, "grid": 1}[variant]
         check(lib().dpg_ctx_set_icp_variant(self.handle, v), "dpg_ctx_set_icp_variant")
 
+    def set_icp_defer_cap(self, cap: int):
+        """Angular ICP: windows of more than `cap` candidates are scanned by a whole wave (0: never);
+        results are identical for every value."""
+        check(lib().dpg_ctx_set_icp_defer_cap(self.handle, int(cap)), "dpg_ctx_set_icp_defer_cap")
+
     def kdtree_build_ms(self) -> float:
         return float(lib().dpg_kdtree_build_ms(self.handle))
 

@@ -71,6 +71,7 @@ typedef struct dpg_icp_result {
 #define DPG_ICP_TOO_FEW_CORR 1   /* fewer than min_number_correspondences -> converged = 0 */
 #define DPG_ICP_NON_PLANAR 2     /* est_transform(2,2) != 1 (dpg_slam.cc:422-426); never produced by
                                     the planar closed form, kept for ABI parity */
+#define DPG_ICP_INTERNAL 3       /* kernel self-check failed (a bug: never expected) */
 
 /* Factors (R9/R10).  info = diagonal information (1/sigma^2 for noiseModel::Diagonal::Sigmas,
  * 1/variance for noiseModel::Gaussian::Covariance of a diagonal matrix, dpg_slam.cc:335). */
@@ -206,6 +207,10 @@ float dpg_kdtree_build_ms(dpg_ctx* ctx);
 #define DPG_ICP_KDTREE 2   /* per-node k-d trees, seeded search, static-frame reciprocal test */
 #define DPG_ICP_GRID 1     /* uniform LDS grid, all-pairs reverse keys by LDS atomics */
 int dpg_ctx_set_icp_variant(dpg_ctx* ctx, int32_t variant);
+/* Angular variant tuning (results are identical for every value): a point whose search window
+ * holds more than `cap` candidates is handed to the workgroup's cooperative queue, where a whole
+ * wave scans it; 0 scans every window in its own lane.  Default 256. */
+int dpg_ctx_set_icp_defer_cap(dpg_ctx* ctx, int32_t cap);
 /* Sum over edges of iterations x (8N + 8M + 8N) -- algorithmic bytes of the correspondence
  * search for the last run, computed on device and copied back. */
 double dpg_icp_batch_algorithmic_bytes(dpg_ctx* ctx);

@@ -17,8 +17,10 @@ w = synth.generate(sys.argv[1] if len(sys.argv) > 1 else "config4")
 p = _abi.default_icp_params()
 L = _abi.lib()
 L.dpg_icp_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-st = (C.c_ulonglong * 40)()
+st = (C.c_ulonglong * 48)()
 with api.Context(0) as ctx:
+    if os.environ.get("DPG_DEFER_CAP"):
+        ctx.set_icp_defer_cap(int(os.environ["DPG_DEFER_CAP"]))
     ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
     ctx.icp_prepare(w.edges, w.est, p)
     L.dpg_icp_stats(st, 1)
@@ -38,14 +40,17 @@ if s[0]:
   print(f"full-scan reciprocal windows {s[13]}  wave imbalance (slowest wave trips x 8 / all trips) {8 * s[14] / max(1, s[15]):.2f}")
   print(f"reciprocal: candidates/matched {s[3] / max(1, s[5]):.1f}  wave-level candidates/point-slot {KU * s[4] * 64 / s[0]:.1f}")
 if s[0]:
+  print(f"queue: forward items {s[40]} (candidates/item {s[41] / max(1, s[40]):.0f}), cooperative reciprocal scans {s[42]}"
+        f" (candidates/scan {s[43] / max(1, s[42]):.0f}), workgroup-iterations with a queue {s[44]}")
+if s[0]:
   bins = ["0", "1", "2", "3", "4", "5-8", "9-16", "17-32", "33-64", "65-128", "129-256", ">256"]
   for name, o in (("forward", 16), ("reciprocal", 28)):
     t = sum(s[o:o + 12])
     print(f"{name} wave trips by trips-per-slot bin (share of all {name} trips): " +
           " ".join(f"{b}:{s[o + k] / max(1, t):.1%}" for k, b in enumerate(bins)))
-tot = sum(s[8:12])
+tot = sum(s[8:12]) + s[45]
 if s[12]:
-    names = ["search", "sums+fold", "arrive+fit+barrier", "move+barrier"]
+    names = ["search", "sums+fold", "arrive+fit+barrier", "move+barrier", "queue (barriers, scans)"]
     print(f"per wave-iteration clock (s_memtime ticks, {s[12]} wave-iterations):")
-    for n, v in zip(names, s[8:12]):
+    for n, v in zip(names, s[8:12] + [s[45]]):
         print(f"  {n:22s} {v / s[12]:9.0f}  ({v / tot:.1%})")

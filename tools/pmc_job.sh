@@ -9,14 +9,13 @@ mkdir -p "$OUT"
 cd "$ROOT"
 export PYTHONPATH=$ROOT:$ROOT/dpg-slam_amd
 export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 run() {   # name, counters...
     local name=$1; shift
-    timeout -k 10 400 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- \
-        python bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv -- \
+        python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/$name.log" 2>&1
     local rc=$?
     echo "$name exit $rc"
     return $rc
 }
 run fetch FETCH_SIZE && run write WRITE_SIZE && \
-run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES
+run sq SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES GRBM_GUI_ACTIVE
