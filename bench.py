@@ -94,6 +94,114 @@ def cpu_gn_baseline(w, icp_results, params, runs: int = 5) -> dict:
     return {"ms_per_gn_iter": t * 1e3 / max(1, st.iterations), "gn_iterations": int(st.iterations), "s": t}
 
 
+def rel_factors(w, V):
+    """The graph's factors up to node V with BetweenFactor measurements taken from the estimates
+    (est_j in the frame of est_i) -- inputs for TIMING the from-scratch and CPU solves only."""
+    from dpgslam import _abi, synth
+    E = w.edges[w.edges[:, 1] < V]
+    F = np.zeros(V + len(E), _abi.FACTOR_DTYPE)
+    F[:V] = w.base_factors[:V]
+    F["kind"][V:] = _abi.DPG_FACTOR_BETWEEN
+    F["i"][V:], F["j"][V:] = E[:, 0], E[:, 1]
+    F["z"][V:] = synth._relative(w.est[E[:, 1]].astype(np.float64), w.est[E[:, 0]].astype(np.float64))
+    p = _abi.default_icp_params()
+    F["info"][V:] = [1.0 / float(np.float32(p.laser_x_variance)), 1.0 / float(np.float32(p.laser_y_variance)),
+                     1.0 / float(np.float32(p.laser_theta_variance))]
+    return F
+
+
+def main_incremental(args):
+    """--workload incremental: per-node latency of the incremental path (SURVEY 8f rank 3;
+    updatePoseGraphObsConstraints -> optimizeGraph, dpg_slam.cc:255-329) at V = 5000: config 4's
+    graph fed node by node.  Node v arrives with its prior/odometry factor, the successive alignment
+    (v-1, v) and config 4's loop closures (j, v); each call is ONE dpg_add_node_pairs: the node's
+    cloud joins the device scan store, its alignments run as one batched ICP, the factors go into
+    the device-resident graph (dpg_inc) and the ISAM2-semantics update runs.  Beside it: round 1's
+    per-node cost (dpg_optimize_graph from scratch on the same graph) and the oracle (CPU) per-node
+    update on the same call mix at the same size."""
+    from dpgslam import _abi, api, synth
+
+    t0 = time.time()
+    w = synth.generate(args.config)
+    V = min(args.inc_nodes, w.V)
+    p = _abi.default_icp_params()
+    lc = w.edges[w.n_successive:]
+    by_node = [[] for _ in range(V)]
+    for k, (j, i) in enumerate(lc):
+        if i < V:
+            by_node[int(i)].append((int(j), int(i)))
+    print(f"generated {args.config} in {time.time() - t0:.1f}s; {sum(len(b) for b in by_node)} loop closures", file=sys.stderr,
+          flush=True)
+
+    lat, icp_ms, sym_ms, num_ms, reord, relin = [], [], [], [], 0, 0
+    with api.Context(0) as ctx:
+        g = api.IncGraph(ctx, mode=args.inc_mode)
+        for v in range(V):
+            extra = w.base_factors[v:v + 1]
+            ts = time.perf_counter()
+            st = g.add_node_pairs(w.cloud(v), w.est[v], np.asarray(by_node[v], np.int32).reshape(-1, 2), extra=extra,
+                                  successive=v >= 1, icp_params=p)
+            lat.append((time.perf_counter() - ts) * 1e3)
+            icp_ms.append(st.ms_icp)
+            sym_ms.append(st.update.ms_symbolic)
+            num_ms.append(st.update.ms_numeric)
+            reord += st.update.reordered
+            relin += st.update.relinearized
+            if v % 1000 == 999:
+                print(f"node {v + 1}: last latency {lat[-1]:.2f} ms", file=sys.stderr, flush=True)
+        X_inc = g.poses()
+        nnz = int(st.update.nnz_l)
+        n_fac = int(st.update.n_factors)
+        # round 1's per-node cost: the whole graph set up and solved from scratch (dpg_optimize_graph)
+        ts = time.perf_counter()
+        _, gst = ctx.optimize_graph(w.est[:V].astype(np.float64), rel_factors(w, V))
+        scratch_ms = (time.perf_counter() - ts) * 1e3
+        g.close()
+
+    tail = np.asarray(lat[-500:])
+    line = {
+        "metric": f"per-node latency of the incremental path at V={V} ({args.config} graph node by node, {args.inc_mode})",
+        "unit": "ms/node",
+        "p50_ms": float(np.median(tail)), "p90_ms": float(np.percentile(tail, 90)), "mean_ms_all": float(np.mean(lat)),
+        "nodes_per_s_tail": float(1e3 / np.mean(tail)),
+        "tail_breakdown_ms": {"icp": float(np.mean(icp_ms[-500:])), "symbolic_host": float(np.mean(sym_ms[-500:])),
+                              "numeric": float(np.mean(num_ms[-500:]))},
+        "reorders": reord, "relinearized_total": relin, "nnz_L_blocks": nnz, "factors": n_fac,
+        "round1_per_node_from_scratch_ms": scratch_ms, "round1_from_scratch_gn_iterations": int(gst.iterations),
+    }
+
+    # CPU baseline: the oracle's per-node update at the same size on the same call mix (the graph up to
+    # node V - k built in one update, then k single-node updates each with the node's own alignments)
+    if args.cpu_nodes > 0:
+        from oracle import oracle as O
+        k = args.cpu_nodes
+        V0 = V - k
+        og = O.OracleIncGraph(mode=args.inc_mode)
+        og.update(w.est[:V0].astype(np.float64), rel_factors(w, V0))
+        cpu = []
+        for v in range(V0, V):
+            ts = time.perf_counter()
+            pf = np.concatenate([og.poses().astype(np.float32), w.est[v:v + 1]])
+            pairs = ([(v - 1, v)] if v >= 1 else []) + by_node[v]
+            Fv = [w.base_factors[v:v + 1]]
+            for q, (a, b) in enumerate(pairs):
+                r, _, _ = O.run_icp(w.cloud(b), w.cloud(a), pf[b], pf[a], p, O.NN_GRID)
+                if q == 0 or (r.converged and r.status == _abi.DPG_ICP_OK):
+                    f = np.zeros(1, _abi.FACTOR_DTYPE)
+                    f["kind"], f["i"], f["j"] = _abi.DPG_FACTOR_BETWEEN, a, b
+                    f["z"] = np.asarray(r.z, np.float64)
+                    f["info"] = [1.0 / float(np.float32(p.laser_x_variance)), 1.0 / float(np.float32(p.laser_y_variance)),
+                                 1.0 / float(np.float32(p.laser_theta_variance))]
+                    Fv.append(f)
+            og.update(w.est[v:v + 1].astype(np.float64), np.concatenate(Fv))
+            cpu.append((time.perf_counter() - ts) * 1e3)
+        line["cpu_baseline"] = {"value": float(np.median(cpu)), "unit": "ms/node", "cores": 1, "kind": "port",
+                                "sample": f"oracle per-node update (ICP grid NN + block-sparse Cholesky, 1 thread) of "
+                                          f"nodes {V0}..{V - 1} of the same sequence (graph up to node {V0} built in "
+                                          f"one update from estimate-relative measurements), median of {k}"}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,7 +215,15 @@ def main():
                          "the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--icp-variant", default="angular", choices=["angular", "kdtree", "grid"],
                     help="nearest-neighbour machinery of the ICP kernel (results are identical)")
+    ap.add_argument("--workload", default="batch", choices=["batch", "incremental"],
+                    help="batch: the headline step (all edges + GN); incremental: per-node latency of "
+                         "dpg_add_node_pairs at V = 5000 (1 GPU)")
+    ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
+    ap.add_argument("--inc-nodes", type=int, default=5000)
+    ap.add_argument("--cpu-nodes", type=int, default=8, help="nodes in the incremental CPU-baseline sample")
     args = ap.parse_args()
+    if args.workload == "incremental":
+        return main_incremental(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

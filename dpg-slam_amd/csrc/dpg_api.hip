@@ -73,6 +73,22 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
     }
+    // grow to n elements keeping the first `keep` (stream-ordered copy, synchronised)
+    int grow(size_t n, size_t keep, hipStream_t s) {
+        if (n <= cap) return 0;
+        const size_t nc = std::max(n, cap + cap / 2);
+        T* q = nullptr;
+        if (hipMalloc(reinterpret_cast<void**>(&q), nc * sizeof(T)) != hipSuccess) return -1;
+        if (p && keep && (hipMemcpyAsync(q, p, std::min(keep, cap) * sizeof(T), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+                          hipStreamSynchronize(s) != hipSuccess)) {
+            (void)hipFree(q);
+            return -1;
+        }
+        if (p) (void)hipFree(p);
+        p = q;
+        cap = nc;
+        return 0;
+    }
 };
 
 }  // namespace
@@ -153,7 +169,8 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
                  int64_t n_tree_nodes, int32_t max_node_pts, float* tree_pts, uint16_t* tree_idx,
                  uint16_t* buckets, const dpg_icp_edge* edges_dev, int64_t ne, dpg_icp_kparams kp,
                  int32_t max_src, int32_t max_tgt, dpg_icp_result* res_dev, double* hess_dev, int32_t* trace_dev,
-                 bool timed) {
+                 bool timed, int64_t tree_from = 0) {
+    if (c->icp_variant != DPG_ICP_ANGULAR) tree_from = 0;   // the other variants rebuild everything
     const int32_t maxp = std::max(max_src, max_tgt);
     if (maxp > 4096) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 4096", maxp);
     int rc = 0;
@@ -162,8 +179,8 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
         rc = dpg_launch_kdtree_build(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, c->stream);
         if (rc) return fail(rc, "k-d tree build launch failed (%d)", rc);
     } else if (c->icp_variant == DPG_ICP_ANGULAR) {
-        rc = dpg_launch_angle_index(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, buckets,
-                                    c->stream);
+        rc = dpg_launch_angle_index(ds_dev, ds_off_dev + tree_from, n_tree_nodes - tree_from, max_node_pts, tree_pts,
+                                    tree_idx, buckets + tree_from * (int64_t)(dpg_angle_buckets() + 1), c->stream);
         if (rc) return fail(rc, "angle index build launch failed (%d)", rc);
     }
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -304,6 +321,53 @@ int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V
     return DPG_OK;
 }
 
+int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k, int32_t ratio) {
+    if (!c || !pts || !off || k <= 0) return fail(DPG_ERR_ARG, "dpg_scans_append: bad arguments");
+    if (ratio < 1) ratio = 1;
+    if (c->n_nodes == 0) return dpg_scans_upload(c, pts, off, k, ratio);
+    if (ratio != c->ratio) return fail(DPG_ERR_STATE, "scans were uploaded with downsample ratio %d", c->ratio);
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t V0 = c->n_nodes, V1 = V0 + k;
+    const int64_t P0 = c->full_off[(size_t)V0], D0 = c->ds_off[(size_t)V0];
+    const int64_t add = off[k] - off[0];
+    if (P0 + add >= ((int64_t)1 << 31)) return fail(DPG_ERR_SIZE, "too many points");
+    std::vector<int64_t> foff((size_t)k + 1), doff((size_t)k + 1);
+    foff[0] = P0;
+    doff[0] = D0;
+    int64_t mx = c->max_ds;
+    for (int64_t v = 0; v < k; ++v) {
+        const int64_t n = off[v + 1] - off[v];
+        if (n < 0) return fail(DPG_ERR_ARG, "node offsets must be non-decreasing");
+        foff[(size_t)v + 1] = foff[(size_t)v] + n;
+        doff[(size_t)v + 1] = doff[(size_t)v] + (n + ratio - 1) / ratio;
+        mx = std::max(mx, (n + ratio - 1) / ratio);
+    }
+    if (mx > 4096) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 4096)", (long long)mx);
+    const int64_t nds = doff[(size_t)k] - D0;
+    std::vector<float> ds((size_t)(2 * std::max<int64_t>(nds, 1)));
+    for (int64_t v = 0; v < k; ++v)
+        dpg_downsample_cloud(pts + 2 * (off[v] - off[0]), off[v + 1] - off[v], ratio, ds.data() + 2 * (doff[(size_t)v] - D0));
+    const size_t B = (size_t)(dpg_angle_buckets() + 1);
+    if (c->full.grow((size_t)(2 * (P0 + add)), (size_t)(2 * P0), c->stream) ||
+        c->ds.grow((size_t)(2 * (D0 + nds)), (size_t)(2 * D0), c->stream) ||
+        c->ds_off_dev.grow((size_t)V1 + 1, (size_t)V0 + 1, c->stream) ||
+        c->tree_pts.grow((size_t)(2 * (D0 + nds)), (size_t)(2 * D0), c->stream) ||
+        c->tree_idx.grow((size_t)(D0 + nds), (size_t)D0, c->stream) ||
+        c->buckets.grow((size_t)V1 * B, (size_t)V0 * B, c->stream))
+        return fail(DPG_ERR_HIP, "out of device memory for scans");
+    HIP_TRY(hipMemcpyAsync(c->full.p + 2 * P0, pts, sizeof(float) * 2 * (size_t)add, hipMemcpyHostToDevice, c->stream));
+    if (nds > 0)
+        HIP_TRY(hipMemcpyAsync(c->ds.p + 2 * D0, ds.data(), sizeof(float) * 2 * (size_t)nds, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->ds_off_dev.p + V0 + 1, doff.data() + 1, sizeof(int64_t) * (size_t)k, hipMemcpyHostToDevice,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->full_off.insert(c->full_off.end(), foff.begin() + 1, foff.end());
+    c->ds_off.insert(c->ds_off.end(), doff.begin() + 1, doff.end());
+    c->n_nodes = V1;
+    c->max_ds = (int32_t)mx;
+    return DPG_OK;
+}
+
 int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
     if (!c || (!edges && ne > 0) || !poses) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
     if (c->n_nodes <= 0) return fail(DPG_ERR_STATE, "no scans uploaded");
@@ -385,6 +449,17 @@ int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
     return launch_batch(c, c->ds.p, c->full.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
                         c->buckets.p, c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
                         compute_cov ? c->hess.p : nullptr, tr, true);
+}
+
+// the staged batch, building only the indexes of nodes [tree_from, n_nodes) (nodes appended since
+// the last run: the others' indexes are still in place)
+static int icp_batch_run_from(dpg_ctx* c, int64_t tree_from) {
+    HIP_TRY(hipSetDevice(c->device));
+    c->trace_iters = 0;
+    c->have_cov = false;
+    return launch_batch(c, c->ds.p, c->full.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
+                        c->buckets.p, c->edges.p, c->n_edges, c->kp, c->max_src, c->max_tgt, c->res.p, nullptr,
+                        nullptr, true, tree_from);
 }
 
 int dpg_ctx_set_icp_variant(dpg_ctx* c, int32_t variant) {
@@ -913,6 +988,97 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
     S.ms_gn = t3 - t2;
     if (st) *st = S;
     return DPG_OK;
+}
+
+int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const float init_pose[3], const dpg_factor* extra,
+                       int64_t n_extra, const int32_t* pairs, int64_t n_pairs, int32_t successive,
+                       const dpg_icp_params* ip, dpg_add_node_stats* st) {
+    if (!g || (!cloud && n_pts > 0) || n_pts < 0 || !init_pose || (n_extra > 0 && !extra) || n_extra < 0 ||
+        n_pairs < 0 || (n_pairs > 0 && !pairs))
+        return fail(DPG_ERR_ARG, "dpg_add_node_pairs: bad arguments");
+    dpg_ctx* c = dpg_inc_ctx(g);
+    dpg_icp_params I;
+    if (ip) I = *ip;
+    else dpg_icp_params_default(&I);
+    dpg_add_node_stats S;
+    memset(&S, 0, sizeof(S));
+    const int64_t V = dpg_inc_num_nodes(g);
+    if (c->n_nodes != V) return fail(DPG_ERR_STATE, "scan store holds %lld nodes, graph %lld", (long long)c->n_nodes,
+                                     (long long)V);
+    for (int64_t e = 0; e < n_pairs; ++e)
+        if (pairs[2 * e] < 0 || pairs[2 * e + 1] < 0 || pairs[2 * e] > V || pairs[2 * e + 1] > V || pairs[2 * e] == pairs[2 * e + 1])
+            return fail(DPG_ERR_ARG, "dpg_add_node_pairs: pair %lld references a missing node", (long long)e);
+    // createNode: the node's cloud joins the store (node id V)
+    const int64_t offs[2] = {0, n_pts};
+    const float dummy[2] = {0.f, 0.f};
+    int rc = dpg_scans_append(c, n_pts > 0 ? cloud : dummy, offs, 1, I.downsample_icp_points_ratio);
+    if (rc) return rc;
+    // estimates as float (dpg_nodes_ positions), the new node's initial pose last
+    std::vector<double> est((size_t)(3 * std::max<int64_t>(V, 1)));
+    if (V > 0 && (rc = dpg_inc_get_poses(g, est.data(), V))) return rc;
+    std::vector<float> pf((size_t)(3 * (V + 1)));
+    for (int64_t q = 0; q < 3 * V; ++q) pf[(size_t)q] = (float)est[(size_t)q];
+    for (int k = 0; k < 3; ++k) pf[(size_t)(3 * V + k)] = init_pose[k];
+    std::vector<int32_t> edges;
+    if (successive && V >= 1) { edges.push_back((int32_t)(V - 1)); edges.push_back((int32_t)V); }
+    edges.insert(edges.end(), pairs, pairs + 2 * n_pairs);
+    const int64_t n_succ = (successive && V >= 1) ? 1 : 0;
+    const int64_t E = (int64_t)edges.size() / 2;
+    std::vector<dpg_factor> F(extra, extra + n_extra);
+    if (E > 0) {
+        const double t0 = now_ms();
+        if ((rc = dpg_icp_batch_prepare(c, edges.data(), E, pf.data(), &I))) return rc;
+        if ((rc = icp_batch_run_from(c, V))) return rc;
+        std::vector<dpg_icp_result> res((size_t)E);
+        if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+        S.ms_icp = now_ms() - t0;
+        S.n_icp_edges = E;
+        for (int64_t e = 0; e < E; ++e) {
+            const dpg_icp_result& r = res[(size_t)e];
+            const bool ok = r.converged && r.status == DPG_ICP_OK;
+            if (e < n_succ || ok) {   // successive: always (dpg_slam.cc:263-267); loop closures when converged (:295-301)
+                dpg_factor f;
+                dpg_icp_factor(&r, edges[(size_t)(2 * e)], edges[(size_t)(2 * e + 1)], &I, &f);
+                F.push_back(f);
+                if (e >= n_succ) ++S.n_loop_closures;
+            }
+        }
+    } else if (c->icp_variant == DPG_ICP_ANGULAR && n_pts > 0) {   // no alignment: only the new node's index
+        rc = dpg_launch_angle_index(c->ds.p, c->ds_off_dev.p + V, 1, c->max_ds, c->tree_pts.p, c->tree_idx.p,
+                                    c->buckets.p + V * (int64_t)(dpg_angle_buckets() + 1), c->stream);
+        if (rc) return fail(rc, "angle index build failed");
+    }
+    const double init[3] = {(double)init_pose[0], (double)init_pose[1], (double)init_pose[2]};
+    if ((rc = dpg_inc_update(g, 1, init, F.data(), (int64_t)F.size(), &S.update))) return rc;
+    if (st) *st = S;
+    return DPG_OK;
+}
+
+int dpg_add_node(dpg_inc* g, const float* cloud, int64_t n_pts, const int32_t* pass, const float init_pose[3],
+                 const dpg_factor* extra, int64_t n_extra, const dpg_icp_params* ip, const dpg_reopt_params* rp,
+                 int32_t non_successive, dpg_add_node_stats* st) {
+    if (!g || !pass || !init_pose) return fail(DPG_ERR_ARG, "dpg_add_node: bad arguments");
+    dpg_reopt_params R;
+    if (rp) R = *rp;
+    else dpg_reopt_params_default(&R);
+    const int64_t V = dpg_inc_num_nodes(g);
+    // updatePoseGraphObsConstraints (dpg_slam.cc:273-304): loop-closure candidates (i, prev), i < V - 2,
+    // by the float distance of the estimates (dpg_nodes_ positions are float), ascending i
+    std::vector<int32_t> lc;
+    if (non_successive && V > 1) {
+        std::vector<double> est((size_t)(3 * V));
+        int rc = dpg_inc_get_poses(g, est.data(), V);
+        if (rc) return rc;
+        const int64_t pv = V - 1;
+        const float px = (float)est[(size_t)(3 * pv)], py = (float)est[(size_t)(3 * pv + 1)];
+        for (int64_t i = 0; i < V - 2; ++i) {
+            const float dx = (float)est[(size_t)(3 * i)] - px, dy = (float)est[(size_t)(3 * i + 1)] - py;
+            const float dist = sqrtf(dx * dx + dy * dy);   // Eigen Vector2f::norm
+            const float thr = pass[i] == pass[pv] ? R.max_node_dist_within_pass : R.max_node_dist_across_passes;
+            if (dist <= thr) { lc.push_back((int32_t)i); lc.push_back((int32_t)pv); }
+        }
+    }
+    return dpg_add_node_pairs(g, cloud, n_pts, init_pose, extra, n_extra, lc.data(), (int64_t)lc.size() / 2, 1, ip, st);
 }
 
 }  // extern "C"

@@ -37,5 +37,36 @@ struct dpg_chol_sym {
 
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                       const dpg_chol_opts* opts, dpg_chol_sym* S);
+// the two halves of dpg_chol_symbolic: the minimum-degree order with the column patterns of L
+// (in elimination positions, sorted), and everything derived from an order + patterns
+int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                   std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
+int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
+                               const dpg_chol_opts* opts, dpg_chol_sym* S);
+
+// Incremental symbolic state of a growing pose graph (dpg_inc.hip): the elimination order is kept
+// and new nodes are appended at its end; the column patterns of L are bitsets over positions,
+// updated along the elimination-tree paths a new edge touches (no re-ordering).
+struct dpg_chol_incsym {
+    int64_t n = 0, words = 0;               // nodes, 64-bit words per pattern row (capacity)
+    std::vector<int32_t> perm, pos;         // elimination order
+    std::vector<uint64_t> bits;             // [n][words]: later positions in column p's pattern
+    std::vector<int32_t> parent;            // elimination-tree parent position (-1: root)
+    int64_t nnz = 0;                        // pattern entries (blocks below the diagonal)
+};
+// a fresh minimum-degree order of the graph (pairs) -> state
+int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+// nodes n .. n + k - 1 appended at the end of the order
+void dpg_incsym_append(dpg_chol_incsym* I, int64_t k);
+// edge (a, b) of the graph (nodes); returns the number of pattern entries it added (fill)
+int64_t dpg_incsym_add_edge(dpg_chol_incsym* I, int32_t a, int32_t b);
+// the derived structures of the current state
+int dpg_incsym_derive(const dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S);
+
+
+// GPU solver structures (dpg_chol.hip) for a given symbolic analysis; *h is reused -- its device
+// buffers grow only when needed -- or created when NULL.  On error *h is destroyed and NULL.
+int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                        const dpg_chol_sym* S);
 
 #endif

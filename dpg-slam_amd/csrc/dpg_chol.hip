@@ -1332,10 +1332,23 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
                     ftasks, fchild, hb, g, perm, fronts, ysol, acc, sm, db);
 }
 
+// device buffers are kept between rebuilds of the same solver (an incremental graph re-derives its
+// structures every update): a buffer is re-allocated only when it must grow (by 1.5x at least)
 template <typename T>
-int dalloc_copy(T** d, const std::vector<T>& h) {
-    const size_t n = std::max<size_t>(h.size(), 1);
-    if (hipMalloc(reinterpret_cast<void**>(d), n * sizeof(T)) != hipSuccess) return DPG_ERR_HIP;
+int dreserve(T** d, size_t* cap, size_t n) {
+    n = std::max<size_t>(n, 1);
+    if (*d && n <= *cap) return DPG_OK;
+    if (*d) (void)hipFree(*d);
+    *d = nullptr;
+    const size_t nc = std::max(n, *cap + *cap / 2);
+    *cap = 0;
+    if (hipMalloc(reinterpret_cast<void**>(d), nc * sizeof(T)) != hipSuccess) return DPG_ERR_HIP;
+    *cap = nc;
+    return DPG_OK;
+}
+template <typename T>
+int dalloc_copy(T** d, size_t* cap, const std::vector<T>& h) {
+    if (dreserve(d, cap, h.size())) return DPG_ERR_HIP;
     if (!h.empty() && hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
         return DPG_ERR_HIP;
     return DPG_OK;
@@ -1382,6 +1395,10 @@ struct CholDev {
     bool fused = false;
     size_t lds_fused = 0;
     bool fused_db = true;
+    // capacities (elements) of the device buffers above, for rebuilds
+    size_t c_sns = 0, c_omap = 0, c_child = 0, c_relmap = 0, c_rows = 0, c_level = 0, c_perm = 0, c_pos = 0,
+           c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_asm_t = 0, c_asm_c = 0, c_panel = 0,
+           c_upd = 0, c_fwd = 0, c_fac = 0, c_ftasks = 0, c_fchild = 0, c_bwd = 0, c_sync = 0;
 };
 
 }  // namespace
@@ -1397,6 +1414,11 @@ extern "C" void dpg_chol_destroy(void* h) {
     delete c;
 }
 
+namespace {
+// Device structures of the factorization for the symbolic analysis in c->sym (reusing c's buffers).
+int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+}  // namespace
+
 extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
                                int64_t n_pairs) {
     *out = nullptr;
@@ -1406,7 +1428,28 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         delete c;
         return DPG_ERR_NUMERIC;
     }
+    const int rc = chol_build(c, n, pair_lo, pair_hi, n_pairs);
+    if (rc) { dpg_chol_destroy(c); return rc; }
+    *out = c;
+    return DPG_OK;
+}
+
+// The same from a given symbolic analysis; *h is reused (its buffers grow when needed) or created.
+int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                        const dpg_chol_sym* S) {
+    CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
+    c->sym = *S;
+    const int rc = chol_build(c, n, pair_lo, pair_hi, n_pairs);
+    if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
+    *h = c;
+    return DPG_OK;
+}
+
+namespace {
+int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
     const dpg_chol_sym& S = c->sym;
+    c->lds_fused = 0;
+    c->n_launches = 0;
     c->n = n;
     c->nnzb_upper = n + n_pairs;
     // omap: every upper block of H -> (front, local block row, local block col, transpose)
@@ -1431,7 +1474,7 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
         const int32_t later = plo > phi ? plo : phi, earlier = plo > phi ? phi : plo;
         const int32_t s = S.sn_of[(size_t)earlier];
         const int32_t a = local_index(s, later), b = local_index(s, earlier);
-        if (a < 0 || b < 0) { delete c; return DPG_ERR_NUMERIC; }
+        if (a < 0 || b < 0) return DPG_ERR_NUMERIC;
         // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
         per[(size_t)s].push_back(OEnt{(int32_t)(n + q), (int16_t)a, (int16_t)b, plo > phi ? 0 : 1, 0});
     }
@@ -1601,51 +1644,51 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
             st.upd_cnt = (int32_t)upd_t.size() - st.upd_off;
             st.max_rows = maxR;
             st.rpt = maxR <= kT ? 1 : maxR <= 2 * kT ? 2 : maxR <= 4 * kT ? 4 : 0;
-            if (st.rpt == 0) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
+            if (st.rpt == 0) return DPG_ERR_SIZE;
             L.steps.push_back(st);
             c->n_launches += 1 + (st.upd_cnt > 0);
         }
         c->lds_solve[(size_t)l] = ms;
         L.lds_asm = lds_asm[(size_t)l];
-        if (ms > 160 * 1024 || L.lds_asm > 160 * 1024) { dpg_chol_destroy(c); return DPG_ERR_SIZE; }
+        if (ms > 160 * 1024 || L.lds_asm > 160 * 1024) return DPG_ERR_SIZE;
     }
     int rc = 0;
-    rc |= dalloc_copy(&c->sns, sns);
-    rc |= dalloc_copy(&c->omap, omap);
-    rc |= dalloc_copy(&c->child_list, S.child_list);
-    rc |= dalloc_copy(&c->relmap, S.relmap);
-    rc |= dalloc_copy(&c->rows, S.sn_rows);
-    rc |= dalloc_copy(&c->level_list, S.level_list);
-    rc |= dalloc_copy(&c->perm, S.perm);
-    rc |= dalloc_copy(&c->pos, S.pos);
-    rc |= dalloc_copy(&c->asm_tasks, asm_t);
+    rc |= dalloc_copy(&c->sns, &c->c_sns, sns);
+    rc |= dalloc_copy(&c->omap, &c->c_omap, omap);
+    rc |= dalloc_copy(&c->child_list, &c->c_child, S.child_list);
+    rc |= dalloc_copy(&c->relmap, &c->c_relmap, S.relmap);
+    rc |= dalloc_copy(&c->rows, &c->c_rows, S.sn_rows);
+    rc |= dalloc_copy(&c->level_list, &c->c_level, S.level_list);
+    rc |= dalloc_copy(&c->perm, &c->c_perm, S.perm);
+    rc |= dalloc_copy(&c->pos, &c->c_pos, S.pos);
+    rc |= dalloc_copy(&c->asm_tasks, &c->c_asm_t, asm_t);
     {
         // solves: the critical-path order (children first), and its reverse (parents first)
         std::vector<int32_t> bwd(fo.rbegin(), fo.rend());
-        rc |= dalloc_copy(&c->order_fwd, fo);
-        rc |= dalloc_copy(&c->order_fac, order_fac);
-        rc |= dalloc_copy(&c->ftasks, ftasks);
-        rc |= dalloc_copy(&c->fchild, fchild);
-        rc |= dalloc_copy(&c->order_bwd, bwd);
+        rc |= dalloc_copy(&c->order_fwd, &c->c_fwd, fo);
+        rc |= dalloc_copy(&c->order_fac, &c->c_fac, order_fac);
+        rc |= dalloc_copy(&c->ftasks, &c->c_ftasks, ftasks);
+        rc |= dalloc_copy(&c->fchild, &c->c_fchild, fchild);
+        rc |= dalloc_copy(&c->order_bwd, &c->c_bwd, bwd);
         // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
         //  pivot-tile hand-off flags [per large-front tile]]
         c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
-        rc |= hipMalloc(reinterpret_cast<void**>(&c->sync), c->sync_bytes) != hipSuccess;
+        rc |= dreserve(&c->sync, &c->c_sync, c->sync_bytes / sizeof(int32_t));
+        c->lds_solve_max = 0;
         for (size_t v : c->lds_solve) c->lds_solve_max = std::max(c->lds_solve_max, v);
     }
-    rc |= dalloc_copy(&c->asm_child, asm_c);
-    rc |= dalloc_copy(&c->panel_tasks, panel_t);
-    rc |= dalloc_copy(&c->upd_tasks, upd_t);
-    rc |= hipMalloc(reinterpret_cast<void**>(&c->fronts), std::max<size_t>((size_t)S.front_off[(size_t)S.ns], 1) * 8) != hipSuccess;
-    rc |= hipMalloc(reinterpret_cast<void**>(&c->acc), std::max<size_t>((size_t)acc_total, 1) * 8) != hipSuccess;
-    rc |= hipMalloc(reinterpret_cast<void**>(&c->ysol), (size_t)(3 * n) * 8) != hipSuccess;
-    rc |= hipMalloc(reinterpret_cast<void**>(&c->xsol), (size_t)(3 * n) * 8) != hipSuccess;
-    rc |= hipMalloc(reinterpret_cast<void**>(&c->status), sizeof(int32_t)) != hipSuccess;
+    rc |= dalloc_copy(&c->asm_child, &c->c_asm_c, asm_c);
+    rc |= dalloc_copy(&c->panel_tasks, &c->c_panel, panel_t);
+    rc |= dalloc_copy(&c->upd_tasks, &c->c_upd, upd_t);
+    rc |= dreserve(&c->fronts, &c->c_fronts, (size_t)S.front_off[(size_t)S.ns]);
+    rc |= dreserve(&c->acc, &c->c_acc, (size_t)acc_total);
+    rc |= dreserve(&c->ysol, &c->c_ysol, (size_t)(3 * n));
+    rc |= dreserve(&c->xsol, &c->c_xsol, (size_t)(3 * n));
+    rc |= dreserve(&c->status, &c->c_status, 1);
     if (!rc) rc |= hipMemset(c->status, 0, sizeof(int32_t)) != hipSuccess;
-    if (rc) { dpg_chol_destroy(c); return DPG_ERR_HIP; }
-    *out = c;
-    return DPG_OK;
+    return rc ? DPG_ERR_HIP : DPG_OK;
 }
+}  // namespace
 
 extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);

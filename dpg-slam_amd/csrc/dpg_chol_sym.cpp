@@ -74,8 +74,8 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
 
 }  // namespace
 
-int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                      const dpg_chol_opts* opts, dpg_chol_sym* S) {
+int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                   std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
     if (n <= 0) return -1;
     // ---- graph
     std::vector<int64_t> aptr((size_t)n + 1, 0);
@@ -90,8 +90,6 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
         }
     }
     // ---- ordering + column patterns (in positions)
-    std::vector<int32_t> perm;
-    std::vector<std::vector<int32_t>> pat;
     min_degree(n, aptr, adj, perm, pat);
     std::vector<int32_t> pos((size_t)n);
     for (int64_t p = 0; p < n; ++p) pos[(size_t)perm[(size_t)p]] = (int32_t)p;
@@ -99,6 +97,22 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
         for (int32_t& u : pat[(size_t)p]) u = pos[(size_t)u];
         std::sort(pat[(size_t)p].begin(), pat[(size_t)p].end());
     }
+    return 0;
+}
+
+int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                      const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    std::vector<int32_t> perm;
+    std::vector<std::vector<int32_t>> pat;
+    if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+    return dpg_chol_sym_from_patterns(n, perm, pat, opts, S);
+}
+
+int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
+                               const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    if (n <= 0 || (int64_t)perm.size() != n || (int64_t)pat.size() != n) return -1;
+    std::vector<int32_t> pos((size_t)n);
+    for (int64_t p = 0; p < n; ++p) pos[(size_t)perm[(size_t)p]] = (int32_t)p;
     std::vector<int32_t> parent((size_t)n, -1), nchild((size_t)n, 0);
     for (int64_t p = 0; p < n; ++p)
         if (!pat[(size_t)p].empty()) { parent[(size_t)p] = pat[(size_t)p][0]; nchild[(size_t)parent[(size_t)p]]++; }
@@ -223,4 +237,114 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
     S->max_front = maxm;
     S->flops = flops;
     return 0;
+}
+
+// ---------------------------------------------------------------- incremental symbolic state
+namespace {
+
+void incsym_grow_words(dpg_chol_incsym* I, int64_t need_bits) {
+    if (need_bits <= I->words * 64) return;
+    int64_t w = std::max<int64_t>(64, I->words * 2);
+    while (w * 64 < need_bits) w *= 2;
+    std::vector<uint64_t> nb((size_t)(I->n * w), 0ull);
+    for (int64_t p = 0; p < I->n; ++p)
+        memcpy(&nb[(size_t)(p * w)], &I->bits[(size_t)(p * I->words)], sizeof(uint64_t) * (size_t)I->words);
+    I->bits.swap(nb);
+    I->words = w;
+}
+
+inline bool has(const dpg_chol_incsym* I, int64_t j, int64_t r) {
+    return (I->bits[(size_t)(j * I->words + r / 64)] >> (r % 64)) & 1ull;
+}
+
+}  // namespace
+
+int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
+    std::vector<int32_t> perm;
+    std::vector<std::vector<int32_t>> pat;
+    if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+    I->n = n;
+    I->words = std::max<int64_t>(64, (n + 63) / 64 * 2);
+    I->perm = perm;
+    I->pos.assign((size_t)n, 0);
+    for (int64_t p = 0; p < n; ++p) I->pos[(size_t)perm[(size_t)p]] = (int32_t)p;
+    I->bits.assign((size_t)(n * I->words), 0ull);
+    I->parent.assign((size_t)n, -1);
+    I->nnz = 0;
+    for (int64_t p = 0; p < n; ++p) {
+        for (int32_t r : pat[(size_t)p]) I->bits[(size_t)(p * I->words + r / 64)] |= 1ull << (r % 64);
+        if (!pat[(size_t)p].empty()) I->parent[(size_t)p] = pat[(size_t)p][0];
+        I->nnz += (int64_t)pat[(size_t)p].size();
+    }
+    return 0;
+}
+
+void dpg_incsym_append(dpg_chol_incsym* I, int64_t k) {
+    if (k <= 0) return;
+    incsym_grow_words(I, I->n + k);
+    for (int64_t q = 0; q < k; ++q) {
+        I->perm.push_back((int32_t)(I->n + q));   // new node n + q (ids are dense) -> the next position
+        I->pos.push_back((int32_t)(I->n + q));
+        I->parent.push_back(-1);
+    }
+    I->n += k;
+    I->bits.resize((size_t)(I->n * I->words), 0ull);
+}
+
+// Row r enters column j's pattern (j < r, positions) and everything the elimination implies: it
+// propagates up the elimination tree, and when r becomes a column's new parent, that column's
+// other rows above r enter column r as well.
+int64_t dpg_incsym_add_edge(dpg_chol_incsym* I, int32_t a, int32_t b) {
+    int64_t pa = I->pos[(size_t)a], pb = I->pos[(size_t)b];
+    if (pa == pb) return 0;
+    if (pa > pb) std::swap(pa, pb);
+    int64_t added = 0;
+    std::vector<std::pair<int64_t, int64_t>> work{{pa, pb}};
+    while (!work.empty()) {
+        int64_t j = work.back().first;
+        const int64_t r = work.back().second;
+        work.pop_back();
+        while (j >= 0 && j < r) {
+            if (has(I, j, r)) break;
+            I->bits[(size_t)(j * I->words + r / 64)] |= 1ull << (r % 64);
+            ++added;
+            const int64_t p_old = I->parent[(size_t)j];
+            if (p_old < 0 || r < p_old) {
+                I->parent[(size_t)j] = (int32_t)r;
+                // column r inherits column j's rows above r
+                const uint64_t* row = &I->bits[(size_t)(j * I->words)];
+                for (int64_t w = (r + 1) / 64; w < I->words; ++w) {
+                    uint64_t m = row[w];
+                    if (w == (r + 1) / 64) m &= ~0ull << ((r + 1) % 64);
+                    while (m) {
+                        const int t = __builtin_ctzll(m);
+                        m &= m - 1;
+                        work.emplace_back(r, w * 64 + t);
+                    }
+                }
+                break;
+            }
+            j = p_old;
+        }
+    }
+    I->nnz += added;
+    return added;
+}
+
+int dpg_incsym_derive(const dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    const int64_t n = I->n;
+    std::vector<std::vector<int32_t>> pat((size_t)n);
+    for (int64_t p = 0; p < n; ++p) {
+        const uint64_t* row = &I->bits[(size_t)(p * I->words)];
+        auto& v = pat[(size_t)p];
+        for (int64_t w = (p + 1) / 64; w < I->words; ++w) {
+            uint64_t m = row[w];
+            while (m) {
+                const int t = __builtin_ctzll(m);
+                m &= m - 1;
+                v.push_back((int32_t)(w * 64 + t));
+            }
+        }
+    }
+    return dpg_chol_sym_from_patterns(n, I->perm, pat, opts, S);
 }

@@ -1,0 +1,419 @@
+// dpg_inc.hip -- the incremental pose-graph solver: DpgSLAM::optimizeGraph as the reference runs
+// it once per new node (dpg_slam.cc:255-329, isam_->update at :320, ISAM2 built with default
+// parameters at :22/:38), on a device-resident graph that grows node by node.  SURVEY 8f rank 3.
+//
+// Structure (kept across updates, nothing re-allocated unless it must grow):
+//   * the factor list and its unique node pairs (arrival order) -- the block pattern of H;
+//   * the incremental symbolic state (dpg_chol_incsym, dpg_chol_sym.cpp): the elimination order
+//     is KEPT and each new node is appended at its end; a new edge adds its fill along the
+//     elimination-tree path it touches.  A fresh minimum-degree order is computed only every
+//     `reorder_every` nodes or when the fill has grown 1.5x past the last ordering's;
+//   * the supernodal structures and device buffers of the GPU Cholesky (dpg_chol.hip), re-derived
+//     from that state each update in linear time into the same buffers.
+//
+// Update semantics (dpg_inc_params.mode):
+//   DPG_INC_ISAM2 (default) -- GTSAM ISAM2 with its default parameters: a
+//     linearization point theta per variable, relinearized (theta_k <- theta_k (+) delta_k) only
+//     for variables whose max |delta_k| >= relinearize_threshold (0.1), and only on updates whose
+//     count before the update is a multiple of relinearize_skip (10) -- GTSAM 4.0's
+//     UpdateImpl::relinarizationNeeded; every update re-linearizes every factor at theta, solves
+//     H(theta) delta = -g(theta) by Cholesky and returns the estimate theta (+) delta, one
+//     Gauss-Newton step from a lagging linearization point.  Deviation, documented: the solve is
+//     exact (ISAM2's back-substitution stops at the wildfire threshold 0.001).
+//   DPG_INC_BATCH -- Gauss-Newton to convergence from the current estimates on every update (the
+//     batch optimum of the accumulated graph; what round 1's driver computed from scratch).
+//   duplicate_factors = 1 reproduces SURVEY Q1: the reference passes the whole accumulated graph_
+//     to every isam_->update, so a factor added u updates ago is in ISAM2 u + 1 times -- exactly
+//     its information scaled by u + 1.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+#include <time.h>
+
+#include <algorithm>
+#include <unordered_map>
+#include <vector>
+
+#include "dpg_chol.h"
+#include "dpg_internal.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+double now_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
+template <typename T>
+int dgrow(T** d, size_t* cap, size_t n, hipStream_t s, size_t keep) {
+    n = std::max<size_t>(n, 1);
+    if (*d && n <= *cap) return DPG_OK;
+    const size_t nc = std::max(n, *cap + *cap / 2);
+    T* p = nullptr;
+    if (hipMalloc(reinterpret_cast<void**>(&p), nc * sizeof(T)) != hipSuccess) return DPG_ERR_HIP;
+    if (*d && keep) {
+        if (hipMemcpyAsync(p, *d, std::min(keep, *cap) * sizeof(T), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            (void)hipFree(p);
+            return DPG_ERR_HIP;
+        }
+    }
+    if (*d) (void)hipFree(*d);
+    *d = p;
+    *cap = nc;
+    return DPG_OK;
+}
+
+// est = theta (+) x (Pose2 ChartAtOrigin retraction, as retract_kernel), x indexed by elimination
+// position; maxd[v] = max |x_v|; atomicMax of the largest into maxall
+__global__ void inc_estimate_kernel(const double* __restrict__ theta, const double* __restrict__ x,
+                                    const int32_t* __restrict__ pos, int64_t n, double* __restrict__ est,
+                                    double* __restrict__ maxd, double* __restrict__ maxall) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double m = 0.0;
+    if (v < n) {
+        const int64_t di = 3 * (int64_t)pos[v];
+        const double c = cos(theta[3 * v + 2]), s = sin(theta[3 * v + 2]);
+        const double d0 = x[di], d1 = x[di + 1], d2 = x[di + 2];
+        const double cd = cos(d2), sd = sin(d2);
+        est[3 * v] = theta[3 * v] + (c * d0 - s * d1);
+        est[3 * v + 1] = theta[3 * v + 1] + (s * d0 + c * d1);
+        est[3 * v + 2] = atan2(s * cd + c * sd, c * cd - s * sd);
+        m = fmax(fabs(d0), fmax(fabs(d1), fabs(d2)));
+        if (!(m == m)) m = __longlong_as_double(0x7ff0000000000000ll);
+        maxd[v] = m;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+    if ((threadIdx.x & 63) == 0)
+        atomicMax(reinterpret_cast<unsigned long long*>(maxall), (unsigned long long)__double_as_longlong(m));
+}
+
+// ISAM2 relinearization of the variables [0, n): theta_v <- est_v (= theta_v (+) delta_v) where
+// max |delta_v| >= thr; counts them
+__global__ void inc_relin_kernel(double* __restrict__ theta, const double* __restrict__ est,
+                                 const double* __restrict__ maxd, int64_t n, double thr, int32_t* __restrict__ count) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n || !(maxd[v] >= thr)) return;
+    theta[3 * v] = est[3 * v];
+    theta[3 * v + 1] = est[3 * v + 1];
+    theta[3 * v + 2] = est[3 * v + 2];
+    atomicAdd(count, 1);
+}
+
+inline unsigned nblk(int64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
+inline uint64_t pkey(int32_t lo, int32_t hi) { return ((uint64_t)(uint32_t)lo << 32) | (uint32_t)hi; }
+
+}  // namespace
+
+struct dpg_inc {
+    dpg_ctx* ctx = nullptr;
+    dpg_inc_params P{};
+    int64_t V = 0;
+    int64_t updates = 0;                       // isam_->update calls since the last reset
+    std::vector<dpg_factor> F;                 // as given (base information)
+    std::vector<int32_t> f_created;            // update that added each factor (Q1 multiplicity)
+    std::vector<int32_t> f_pair;               // unique pair of a Between factor, -1 for a prior
+    std::unordered_map<uint64_t, int32_t> pair_id;
+    std::vector<int32_t> plo, phi;             // unique pairs (lo < hi) in arrival order
+    dpg_chol_incsym I;
+    int64_t V_at_order = 0, nnz_at_order = 0;  // size of the graph at the last full ordering
+    dpg_chol_sym S;
+    dpg_chol_opts opts{64, 0.3};
+    int64_t reorders = 0;
+    // device
+    dpg_gn_dev g{};                            // assembly buffers + the Cholesky (g.chol)
+    size_t c_factors = 0, c_cptr = 0, c_clist = 0, c_hb = 0, c_contrib = 0, c_partials = 0;
+    double* theta = nullptr;                   // [V][3] linearization points (g.poses aliases it)
+    double* est = nullptr;                     // [V][3] current estimate
+    double* maxd = nullptr;                    // [V] max |delta_v| of the last update
+    int32_t* cnt = nullptr;                    // relinearized variables of the last update
+    size_t c_theta = 0, c_est = 0, c_maxd = 0;
+    std::vector<dpg_factor> h_dev_factors;     // staging (Q1 scaling)
+};
+
+namespace {
+
+// contribution lists (gather_kernel) of every upper block, in factor order, and the device copies
+int inc_rebuild(dpg_inc* q, hipStream_t s) {
+    dpg_gn_dev& g = q->g;
+    const int64_t n = q->V, nf = (int64_t)q->F.size(), P = (int64_t)q->plo.size();
+    const int64_t nu = n + P;
+    std::vector<int32_t> cnt((size_t)nu + 1, 0);
+    for (int64_t k = 0; k < nf; ++k) {
+        const dpg_factor& f = q->F[(size_t)k];
+        cnt[(size_t)f.i + 1]++;
+        if (f.kind == DPG_FACTOR_BETWEEN) {
+            cnt[(size_t)f.j + 1]++;
+            cnt[(size_t)(n + q->f_pair[(size_t)k]) + 1]++;
+        }
+    }
+    for (int64_t u = 0; u < nu; ++u) cnt[(size_t)u + 1] += cnt[(size_t)u];
+    std::vector<int32_t> clist((size_t)cnt[(size_t)nu]);
+    std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
+    for (int64_t k = 0; k < nf; ++k) {
+        const dpg_factor& f = q->F[(size_t)k];
+        clist[(size_t)cur[(size_t)f.i]++] = (int32_t)(k << 2 | 0);
+        if (f.kind == DPG_FACTOR_BETWEEN) {
+            clist[(size_t)cur[(size_t)f.j]++] = (int32_t)(k << 2 | 1);
+            clist[(size_t)cur[(size_t)(n + q->f_pair[(size_t)k])]++] = (int32_t)(k << 2 | (f.i < f.j ? 2 : 3));
+        }
+    }
+    // factors as the device sees them: Q1 multiplicity folded into the information
+    q->h_dev_factors = q->F;
+    if (q->P.duplicate_factors)
+        for (int64_t k = 0; k < nf; ++k) {
+            const double mult = (double)(q->updates - q->f_created[(size_t)k] + 1);
+            for (int c = 0; c < 3; ++c) q->h_dev_factors[(size_t)k].info[c] *= mult;
+        }
+    g.n_nodes = n;
+    g.n_factors = nf;
+    g.nnzb_upper = nu;
+    g.shard_begin = 0;
+    g.shard_end = nf;
+    g.n_blocks_rows = (int32_t)nblk(n);
+    int rc = 0;
+    rc |= dgrow(&g.factors, &q->c_factors, (size_t)nf, s, 0);
+    rc |= dgrow(&g.up_cptr, &q->c_cptr, cnt.size(), s, 0);
+    rc |= dgrow(&g.up_clist, &q->c_clist, clist.size(), s, 0);
+    rc |= dgrow(&g.hb_own, &q->c_hb, (size_t)(9 * nu + 3 * n + 2), s, 0);
+    rc |= dgrow(&g.contrib, &q->c_contrib, (size_t)(25 * nf), s, 0);
+    rc |= dgrow(&g.partials, &q->c_partials, (size_t)(6 * g.n_blocks_rows + n), s, 0);
+    if (!g.scal3) {
+        rc |= hipMalloc(reinterpret_cast<void**>(&g.scal3), 4 * sizeof(double)) != hipSuccess;
+        if (!rc) rc |= hipHostMalloc(reinterpret_cast<void**>(&g.scal3_host), 4 * sizeof(double)) != hipSuccess;
+    }
+    if (rc) return DPG_ERR_HIP;
+    if (nf && hipMemcpyAsync(g.factors, q->h_dev_factors.data(), sizeof(dpg_factor) * (size_t)nf, hipMemcpyHostToDevice,
+                             s) != hipSuccess)
+        return DPG_ERR_HIP;
+    if (hipMemcpyAsync(g.up_cptr, cnt.data(), sizeof(int32_t) * cnt.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+        return DPG_ERR_HIP;
+    if (!clist.empty() &&
+        hipMemcpyAsync(g.up_clist, clist.data(), sizeof(int32_t) * clist.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+        return DPG_ERR_HIP;
+    // the host vectors above must outlive the async copies
+    if (hipStreamSynchronize(s) != hipSuccess) return DPG_ERR_HIP;
+    return dpg_chol_create_sym(&g.chol, n, q->plo.data(), q->phi.data(), P, &q->S);
+}
+
+int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
+
+}  // namespace
+
+extern "C" {
+
+void dpg_inc_params_default(dpg_inc_params* p) {
+    if (!p) return;
+    memset(p, 0, sizeof(*p));
+    p->mode = DPG_INC_ISAM2;
+    p->relinearize_skip = 10;
+    p->relinearize_threshold = 0.1;
+    p->duplicate_factors = 0;
+    p->reorder_every = 64;
+    dpg_gn_params_default(&p->gn);
+}
+
+dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
+    if (!ctx) {
+        set_err(DPG_ERR_ARG, "dpg_inc_create: ctx is NULL");
+        return nullptr;
+    }
+    dpg_inc* q = new dpg_inc();
+    q->ctx = ctx;
+    if (p) q->P = *p;
+    else dpg_inc_params_default(&q->P);
+    if (q->P.relinearize_skip < 1) q->P.relinearize_skip = 1;
+    if (q->P.reorder_every < 1) q->P.reorder_every = 1;
+    q->P.gn.linear_solver = DPG_SOLVER_CHOLESKY;
+    return q;
+}
+
+int dpg_inc_reset(dpg_inc* q) {
+    if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_reset: NULL");
+    q->V = 0;
+    q->updates = 0;
+    q->F.clear();
+    q->f_created.clear();
+    q->f_pair.clear();
+    q->pair_id.clear();
+    q->plo.clear();
+    q->phi.clear();
+    q->I = dpg_chol_incsym();
+    q->V_at_order = q->nnz_at_order = 0;
+    return DPG_OK;
+}
+
+void dpg_inc_destroy(dpg_inc* q) {
+    if (!q) return;
+    hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
+    (void)hipStreamSynchronize(s);
+    void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.contrib, q->g.partials, q->g.scal3,
+                    q->theta, q->est, q->maxd, q->cnt};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (q->g.scal3_host) (void)hipHostFree(q->g.scal3_host);
+    if (q->g.chol) dpg_chol_destroy(q->g.chol);
+    delete q;
+}
+
+int64_t dpg_inc_num_nodes(const dpg_inc* q) { return q ? q->V : -1; }
+dpg_ctx* dpg_inc_ctx(dpg_inc* q) { return q ? q->ctx : nullptr; }
+
+int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_factor* factors, int64_t n_factors,
+                   dpg_inc_stats* st) {
+    if (!q || n_new < 0 || n_factors < 0 || (n_new > 0 && !init) || (n_factors > 0 && !factors))
+        return set_err(DPG_ERR_ARG, "dpg_inc_update: bad arguments");
+    const double t0 = now_ms();
+    hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
+    if (hipSetDevice(dpg_ctx_device_of(q->ctx)) != hipSuccess) return set_err(DPG_ERR_HIP, "hipSetDevice failed");
+    const int64_t V0 = q->V, V1 = V0 + n_new;
+    // validate before touching any state
+    for (int64_t k = 0; k < n_factors; ++k) {
+        const dpg_factor& f = factors[k];
+        const bool ok = (f.kind == DPG_FACTOR_PRIOR && f.i >= 0 && f.i < V1) ||
+                        (f.kind == DPG_FACTOR_BETWEEN && f.i >= 0 && f.j >= 0 && f.i < V1 && f.j < V1 && f.i != f.j);
+        if (!ok) return set_err(DPG_ERR_ARG, "dpg_inc_update: a factor references a missing node");
+    }
+    if (V1 == 0) return set_err(DPG_ERR_STATE, "dpg_inc_update: empty graph");
+    // device state for the new nodes (theta and the estimate start at the initial values)
+    int rc = 0;
+    rc |= dgrow(&q->theta, &q->c_theta, (size_t)(3 * V1), s, (size_t)(3 * V0));
+    rc |= dgrow(&q->est, &q->c_est, (size_t)(3 * V1), s, (size_t)(3 * V0));
+    rc |= dgrow(&q->maxd, &q->c_maxd, (size_t)V1, s, (size_t)V0);
+    if (!q->cnt) rc |= hipMalloc(reinterpret_cast<void**>(&q->cnt), sizeof(int32_t)) != hipSuccess;
+    if (rc) return set_err(DPG_ERR_HIP, "dpg_inc_update: out of device memory");
+    if (n_new > 0) {
+        if (hipMemcpyAsync(q->theta + 3 * V0, init, sizeof(double) * 3 * (size_t)n_new, hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipMemcpyAsync(q->est + 3 * V0, init, sizeof(double) * 3 * (size_t)n_new, hipMemcpyHostToDevice, s) !=
+                hipSuccess ||
+            hipMemsetAsync(q->maxd + V0, 0, sizeof(double) * (size_t)n_new, s) != hipSuccess)
+            return set_err(DPG_ERR_HIP, "dpg_inc_update: upload failed");
+    }
+    // graph + symbolic state
+    const bool relin = q->P.mode == DPG_INC_ISAM2 && (q->updates % q->P.relinearize_skip) == 0 && V0 > 0;
+    q->updates += 1;
+    q->V = V1;
+    if (q->I.n > 0) dpg_incsym_append(&q->I, n_new);
+    std::vector<std::pair<int32_t, int32_t>> new_pairs;
+    for (int64_t k = 0; k < n_factors; ++k) {
+        const dpg_factor& f = factors[k];
+        int32_t pid = -1;
+        if (f.kind == DPG_FACTOR_BETWEEN) {
+            const int32_t lo = std::min(f.i, f.j), hi = std::max(f.i, f.j);
+            auto it = q->pair_id.find(pkey(lo, hi));
+            if (it == q->pair_id.end()) {
+                pid = (int32_t)q->plo.size();
+                q->pair_id.emplace(pkey(lo, hi), pid);
+                q->plo.push_back(lo);
+                q->phi.push_back(hi);
+                new_pairs.emplace_back(lo, hi);
+            } else {
+                pid = it->second;
+            }
+        }
+        q->F.push_back(f);
+        q->f_created.push_back((int32_t)q->updates);
+        q->f_pair.push_back(pid);
+    }
+    const double t1 = now_ms();
+    // ordering: extended, or fresh every reorder_every nodes / after 1.5x fill growth
+    bool reordered = false;
+    const double expect = q->V_at_order > 0 ? (double)q->nnz_at_order * (double)V1 / (double)q->V_at_order : 0.0;
+    if (q->I.n == 0 || V1 - q->V_at_order >= q->P.reorder_every) {
+        reordered = true;
+    } else {
+        for (auto& pr : new_pairs) dpg_incsym_add_edge(&q->I, pr.first, pr.second);
+        if ((double)q->I.nnz > 1.5 * expect + 64.0) reordered = true;
+    }
+    if (reordered) {
+        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size()))
+            return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: symbolic analysis failed");
+        q->V_at_order = V1;
+        q->nnz_at_order = q->I.nnz;
+        q->reorders += 1;
+    }
+    if (dpg_incsym_derive(&q->I, &q->opts, &q->S))
+        return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: symbolic derivation failed");
+    if ((rc = inc_rebuild(q, s))) return set_err(rc, "dpg_inc_update: solver rebuild failed");
+    const double t2 = now_ms();
+    dpg_inc_stats S;
+    memset(&S, 0, sizeof(S));
+    S.reordered = reordered ? 1 : 0;
+    if (q->P.mode == DPG_INC_ISAM2) {
+        // 1. relinearize the variables whose delta passed the threshold (before the new factors)
+        if (relin) {
+            if (hipMemsetAsync(q->cnt, 0, sizeof(int32_t), s) != hipSuccess) return set_err(DPG_ERR_HIP, "memset");
+            hipLaunchKernelGGL(inc_relin_kernel, dim3(nblk(V0)), dim3(kThreads), 0, s, q->theta, q->est, q->maxd, V0,
+                               q->P.relinearize_threshold, q->cnt);
+        }
+        // 2. linearize everything at theta, factor, solve, estimate = theta (+) delta
+        q->g.poses = q->theta;
+        if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return set_err(rc, "assembly failed");
+        if ((rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s))) return set_err(rc, "Cholesky launch failed");
+        if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return set_err(DPG_ERR_HIP, "memset");
+        hipLaunchKernelGGL(inc_estimate_kernel, dim3(nblk(V1)), dim3(kThreads), 0, s, q->theta, dpg_chol_x_dev(q->g.chol),
+                           dpg_chol_pos_dev(q->g.chol), V1, q->est, q->maxd, q->g.scal3);
+        double sc[3];
+        q->g.last_used_chol = 1;
+        if ((rc = dpg_gn_dev_fetch(&q->g, q->g.hb_own, s, sc))) return set_err(rc, "fetch failed");
+        if (sc[2] != 0.0) return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed (H not positive definite)");
+        int32_t nrel = 0;
+        if (relin && hipMemcpy(&nrel, q->cnt, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return set_err(DPG_ERR_HIP, "read-back failed");
+        S.relinearized = nrel;
+        S.gn_iterations = 1;
+        S.error = sc[1];
+        S.last_delta_inf = sc[0];
+    } else {
+        // batch Gauss-Newton to convergence from the current estimates
+        q->g.poses = q->est;
+        q->g.have_factor = 0;
+        q->g.last_delta_inf = 1e300;
+        q->g.n_factorizations = 0;
+        const dpg_gn_params& gp = q->P.gn;
+        double sc[3] = {0, 0, 0};
+        int it = 0;
+        if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return set_err(rc, "assembly failed");
+        for (; it < gp.max_iterations;) {
+            if ((rc = dpg_gn_dev_solve_async(&q->g, q->g.hb_own, &gp, s)) ||
+                (rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s)) || (rc = dpg_gn_dev_fetch(&q->g, q->g.hb_own, s, sc)))
+                return set_err(rc, "Gauss-Newton step failed");
+            if (sc[2] != 0.0) return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed");
+            ++it;
+            if (sc[0] < gp.delta_tol) break;
+        }
+        // theta follows the estimate (a batch solve relinearizes everything)
+        if (hipMemcpyAsync(q->theta, q->est, sizeof(double) * 3 * (size_t)V1, hipMemcpyDeviceToDevice, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return set_err(DPG_ERR_HIP, "copy failed");
+        S.gn_iterations = it;
+        S.error = sc[1];
+        S.last_delta_inf = sc[0];
+    }
+    const double t3 = now_ms();
+    S.n_nodes = V1;
+    S.n_factors = (int64_t)q->F.size();
+    S.nnz_l = q->I.nnz;
+    S.ms_total = t3 - t0;
+    S.ms_symbolic = t2 - t1;
+    S.ms_numeric = t3 - t2;
+    if (st) *st = S;
+    return DPG_OK;
+}
+
+int dpg_inc_get_poses(dpg_inc* q, double* poses, int64_t n) {
+    if (!q || !poses || n < 0 || n > q->V) return set_err(DPG_ERR_ARG, "dpg_inc_get_poses: bad arguments");
+    if (n == 0) return DPG_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
+    if (hipMemcpyAsync(poses, q->est, sizeof(double) * 3 * (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return set_err(DPG_ERR_HIP, "dpg_inc_get_poses: copy failed");
+    return DPG_OK;
+}
+
+}  // extern "C"

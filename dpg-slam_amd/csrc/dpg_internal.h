@@ -15,6 +15,7 @@ extern "C" {
 
 /* error message + code for dpg_last_error; the context's stream / device (dpg_api.hip) */
 int dpg_set_error(int code, const char* msg);
+dpg_ctx* dpg_inc_ctx(dpg_inc* g);   /* the context an incremental graph runs on (dpg_inc.hip) */
 void* dpg_ctx_stream_of(dpg_ctx* c);
 int dpg_ctx_device_of(dpg_ctx* c);
 

@@ -119,6 +119,49 @@ class ReoptStats(C.Structure):
     ]
 
 
+DPG_INC_ISAM2 = 0
+DPG_INC_BATCH = 1
+
+
+class IncParams(C.Structure):
+    """dpg_inc_params -- the incremental per-node solve (ISAM2 defaults)."""
+
+    _fields_ = [
+        ("mode", C.c_int32),
+        ("relinearize_skip", C.c_int32),
+        ("relinearize_threshold", C.c_double),
+        ("duplicate_factors", C.c_int32),
+        ("reorder_every", C.c_int32),
+        ("gn", GnParams),
+    ]
+
+
+class IncStats(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int64),
+        ("n_factors", C.c_int64),
+        ("nnz_l", C.c_int64),
+        ("reordered", C.c_int32),
+        ("relinearized", C.c_int32),
+        ("gn_iterations", C.c_int32),
+        ("pad", C.c_int32),
+        ("error", C.c_double),
+        ("last_delta_inf", C.c_double),
+        ("ms_total", C.c_double),
+        ("ms_symbolic", C.c_double),
+        ("ms_numeric", C.c_double),
+    ]
+
+
+class AddNodeStats(C.Structure):
+    _fields_ = [
+        ("n_icp_edges", C.c_int64),
+        ("n_loop_closures", C.c_int64),
+        ("ms_icp", C.c_double),
+        ("update", IncStats),
+    ]
+
+
 # numpy mirrors of the array-of-struct types (same layout as the C structs)
 RESULT_DTYPE = np.dtype(
     [("T", "<f4", (6,)), ("z", "<f4", (3,)), ("converged", "<i4"), ("iterations", "<i4"),
@@ -240,7 +283,25 @@ SIGNATURES = {
     "dpg_active_dynamic_points": (C.c_int64, [P, C.c_int64, F32P, F32P, C.c_int64, I64P]),
     "dpg_reoptimize": (C.c_int, [P, C.c_int64, I32P, F32P, F32P, C.POINTER(IcpParams), C.POINTER(GnParams),
                                  C.POINTER(ReoptParams), F64P, C.POINTER(ReoptStats)]),
+    "dpg_inc_params_default": (None, [C.POINTER(IncParams)]),
+    "dpg_inc_create": (P, [P, C.POINTER(IncParams)]),
+    "dpg_inc_destroy": (None, [P]),
+    "dpg_inc_reset": (C.c_int, [P]),
+    "dpg_inc_update": (C.c_int, [P, C.c_int64, F64P, P, C.c_int64, C.POINTER(IncStats)]),
+    "dpg_inc_num_nodes": (C.c_int64, [P]),
+    "dpg_inc_get_poses": (C.c_int, [P, F64P, C.c_int64]),
+    "dpg_scans_append": (C.c_int, [P, F32P, I64P, C.c_int64, C.c_int32]),
+    "dpg_add_node": (C.c_int, [P, F32P, C.c_int64, I32P, F32P, P, C.c_int64, C.POINTER(IcpParams),
+                               C.POINTER(ReoptParams), C.c_int32, C.POINTER(AddNodeStats)]),
+    "dpg_add_node_pairs": (C.c_int, [P, F32P, C.c_int64, F32P, P, C.c_int64, I32P, C.c_int64, C.c_int32,
+                                     C.POINTER(IcpParams), C.POINTER(AddNodeStats)]),
 }
+
+
+def default_inc_params() -> IncParams:
+    p = IncParams()
+    lib().dpg_inc_params_default(C.byref(p))
+    return p
 
 
 def default_reopt_params() -> ReoptParams:

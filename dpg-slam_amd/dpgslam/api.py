@@ -435,3 +435,88 @@ class DpgStore:
             res[name] = out[k:k + c].copy()
             k += int(c)
         return res
+
+
+class IncGraph:
+    """The incremental per-node pose graph (dpg_inc): isam_->update once per new node
+    (dpg_slam.cc:255-329), device-resident, growing in place.  mode: "isam2" (ISAM2 defaults: partial
+    relinearization, threshold 0.1, skip 10) or "batch" (Gauss-Newton to convergence per update)."""
+
+    def __init__(self, ctx: Context, mode: str = "isam2", duplicate_factors: bool = False, reorder_every: int = 64,
+                 gn_params=None):
+        self.ctx = ctx
+        p = _abi.default_inc_params()
+        p.mode = {"isam2": _abi.DPG_INC_ISAM2, "batch": _abi.DPG_INC_BATCH}[mode]
+        p.duplicate_factors = 1 if duplicate_factors else 0
+        p.reorder_every = int(reorder_every)
+        if gn_params is not None:
+            p.gn = gn_params
+        self.params = p
+        self.handle = lib().dpg_inc_create(ctx.handle, C.byref(p))
+        if not self.handle:
+            raise _abi.DpgError("dpg_inc_create failed: " + (lib().dpg_last_error() or b"").decode())
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().dpg_inc_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def V(self) -> int:
+        return int(lib().dpg_inc_num_nodes(self.handle))
+
+    def reset(self):
+        check(lib().dpg_inc_reset(self.handle), "dpg_inc_reset")
+
+    def update(self, init: np.ndarray, factors: np.ndarray) -> "_abi.IncStats":
+        """isam_->update(new factors, new values): init [n_new, 3] initial values of the new nodes."""
+        X = np.ascontiguousarray(np.asarray(init, np.float64).reshape(-1, 3))
+        F = np.ascontiguousarray(factors, FACTOR_DTYPE) if factors is not None and len(factors) else \
+            np.zeros(0, FACTOR_DTYPE)
+        st = _abi.IncStats()
+        check(lib().dpg_inc_update(self.handle, len(X), ptr(X, C.c_double) if len(X) else None,
+                                   vptr(F) if len(F) else None, len(F), C.byref(st)), "dpg_inc_update")
+        return st
+
+    def poses(self, n: int | None = None) -> np.ndarray:
+        n = self.V if n is None else int(n)
+        X = np.zeros((max(n, 1), 3), np.float64)
+        check(lib().dpg_inc_get_poses(self.handle, ptr(X, C.c_double), n), "dpg_inc_get_poses")
+        return X[:n]
+
+    def add_node(self, cloud, passes, init_pose, extra=None, icp_params=None, reopt_params=None,
+                 non_successive=True) -> "_abi.AddNodeStats":
+        """dpg_add_node: the node's cloud joins the device scan store, its successive + loop-closure
+        alignments run as ONE batched ICP, and the factors (+ extra: pass prior / odometry) go into
+        one update.  passes: pass number of every node, the new one last."""
+        cl = _f32(cloud).reshape(-1, 2)
+        ps = np.ascontiguousarray(passes, np.int32)
+        ip = _f32(init_pose).reshape(3)
+        E = np.ascontiguousarray(extra, FACTOR_DTYPE) if extra is not None and len(extra) else np.zeros(0, FACTOR_DTYPE)
+        st = _abi.AddNodeStats()
+        check(lib().dpg_add_node(self.handle, ptr(cl, C.c_float) if len(cl) else None, len(cl), ptr(ps, C.c_int32),
+                                 ptr(ip, C.c_float), vptr(E) if len(E) else None, len(E),
+                                 C.byref(icp_params or _abi.default_icp_params()),
+                                 C.byref(reopt_params or _abi.default_reopt_params()), 1 if non_successive else 0,
+                                 C.byref(st)), "dpg_add_node")
+        return st
+
+    def add_node_pairs(self, cloud, init_pose, pairs, extra=None, successive=True, icp_params=None) -> "_abi.AddNodeStats":
+        """dpg_add_node_pairs: as add_node, with the loop-closure alignments given (pairs [k, 2] =
+        (node_1 target, node_2 source), keys <= the new node's id)."""
+        cl = _f32(cloud).reshape(-1, 2)
+        ip = _f32(init_pose).reshape(3)
+        pr = np.ascontiguousarray(np.asarray(pairs, np.int32).reshape(-1, 2))
+        E = np.ascontiguousarray(extra, FACTOR_DTYPE) if extra is not None and len(extra) else np.zeros(0, FACTOR_DTYPE)
+        st = _abi.AddNodeStats()
+        check(lib().dpg_add_node_pairs(self.handle, ptr(cl, C.c_float) if len(cl) else None, len(cl), ptr(ip, C.c_float),
+                                       vptr(E) if len(E) else None, len(E), ptr(pr, C.c_int32) if len(pr) else None,
+                                       len(pr), 1 if successive else 0, C.byref(icp_params or _abi.default_icp_params()),
+                                       C.byref(st)), "dpg_add_node_pairs")
+        return st

@@ -5,10 +5,10 @@ reoptimize, GetPose, GetMap, getActiveAndDynamicMapPoints).
 
 The bookkeeping (odometry thresholds, node creation, which scans are aligned, which factors are
 added) follows dpg_slam.cc line by line in float32 where the reference is float; every numeric
-step runs through a backend: "gpu" (the HIP kernels, dpgslam.api) or "oracle" (the CPU
-restatement, test infrastructure), so tests can run the same driver on both and compare.
-optimizeGraph runs batch Gauss-Newton to convergence over the accumulated graph instead of ISAM2's
-single incremental update.
+step runs through a backend: GpuBackend (the HIP kernels, dpgslam.api) by default, or any object
+with the same methods (tests/slam_oracle.py holds the CPU restatement the tests compare against).
+optimizeGraph is the incremental graph (dpg_inc): one ISAM2-semantics update per node by default
+(inc_mode="isam2"), or Gauss-Newton to convergence per node (inc_mode="batch"); SURVEY Q1/Q6.
 """
 from __future__ import annotations
 
@@ -38,13 +38,19 @@ def _icp_factor(res, i, j, p) -> np.ndarray:
     return np.frombuffer(bytes(f), FACTOR_DTYPE).copy()
 
 
-class _GpuBackend:
-    def __init__(self, ctx: api.Context):
-        self.ctx = ctx
+class GpuBackend:
+    """The numeric steps of DpgSLAM on the MI355X (dpgslam.api over the C ABI).  Per node ONE call,
+    dpg_add_node: the node's cloud joins the device scan store, its successive and loop-closure
+    alignments run as one batched ICP, and the factors go into the incremental graph (dpg_inc)."""
 
-    def run_icp(self, pose_1, cloud_1, pose_2, cloud_2, p):
-        ok, z, cov, res, _ = self.ctx.run_icp(api.Node(pose_1, cloud_1), api.Node(pose_2, cloud_2), p)
-        return bool(ok), res
+    def __init__(self, ctx: api.Context, inc_mode: str = "isam2"):
+        self.ctx = ctx
+        self.inc = api.IncGraph(ctx, mode=inc_mode)
+
+    def add_node(self, cloud, passes, init_pose, extra, icp_params, reopt_params, non_successive):
+        st = self.inc.add_node(cloud, passes, init_pose, extra, icp_params, reopt_params, non_successive)
+        n_icp = (1 if len(passes) > 1 else 0) + int(st.n_loop_closures)
+        return n_icp, self.inc.poses()
 
     def icp_batch(self, pts, offsets, edges, est, p):
         self.ctx.upload_scans(pts, offsets, p.downsample_icp_points_ratio)
@@ -54,8 +60,12 @@ class _GpuBackend:
     def candidates(self, est, passes, within, across):
         return self.ctx.loop_closure_candidates(est, passes, within, across)
 
-    def optimize(self, X0, F, gp):
-        return self.ctx.optimize_graph(X0, F, gp)[0]
+    def rebuild_graph(self, est, F):
+        """reoptimize's new ISAM2 + new graph and its one update (dpg_slam.cc:36-39,111-119); the
+        scan store holds every node's cloud (icp_batch uploaded them)."""
+        self.inc.reset()
+        self.inc.update(np.asarray(est, np.float64), F)
+        return self.inc.poses()
 
     def store(self, ranges, geom, offsets, params):
         return api.DpgStore(self.ctx, ranges, geom, offsets=offsets, params=params)
@@ -63,31 +73,6 @@ class _GpuBackend:
     def get_map(self, pts, offsets, est, fraction, ratio):
         self.ctx.upload_scans(pts, offsets, ratio)
         return self.ctx.get_map(est, fraction)
-
-
-class _OracleBackend:
-    def __init__(self):
-        from oracle import oracle as O   # test infrastructure: the CPU restatement
-        self.O = O
-
-    def run_icp(self, pose_1, cloud_1, pose_2, cloud_2, p):
-        res, _, _ = self.O.run_icp(cloud_2, cloud_1, pose_2, pose_1, p, self.O.NN_GRID)
-        return bool(res.converged) and res.status == _abi.DPG_ICP_OK, res
-
-    def icp_batch(self, pts, offsets, edges, est, p):
-        return self.O.icp_batch(pts, offsets, edges, est, p, self.O.NN_GRID)[0]
-
-    def candidates(self, est, passes, within, across):
-        return self.O.loop_closure_candidates(est, passes, within, across)
-
-    def optimize(self, X0, F, gp):
-        return self.O.optimize_graph(X0, F, gp)[0]
-
-    def store(self, ranges, geom, offsets, params):
-        return self.O.OracleDpgStore(ranges, geom, offsets=offsets, params=params)
-
-    def get_map(self, pts, offsets, est, fraction, ratio):
-        return self.O.get_map(pts, offsets, est, fraction)
 
 
 class DpgSLAM:
@@ -98,14 +83,14 @@ class DpgSLAM:
                  change_params=None, min_dist_between_nodes=1.0, min_angle_between_nodes=math.pi / 6.0,
                  non_successive_scan_constraints=True, odometry_constraints=True,
                  max_dist_within_pass=5.0, max_dist_across_passes=2.0, new_pass_std_dev=(0.2, 0.2, 0.15),
-                 motion_model=(0.4, 0.4, 0.4, 0.4), display_points_fraction=10):
+                 motion_model=(0.4, 0.4, 0.4, 0.4), display_points_fraction=10, inc_mode="isam2"):
         if backend == "gpu":
             self.ctx = ctx or api.Context(0)
-            self.be = _GpuBackend(self.ctx)
-        elif backend == "oracle":
-            self.be = _OracleBackend()
+            self.be = GpuBackend(self.ctx, inc_mode)
+        elif isinstance(backend, str):
+            raise ValueError(f"unknown backend {backend!r} (pass a backend object for anything but 'gpu')")
         else:
-            raise ValueError(backend)
+            self.be = backend
         self.icp_params = icp_params or _abi.default_icp_params()
         self.gn_params = gn_params or _abi.default_gn_params()
         self.change_params = change_params or _abi.default_change_params()
@@ -132,7 +117,8 @@ class DpgSLAM:
         self.clouds: list[np.ndarray] = []
         self.odom_only: list[np.ndarray] = []
         self.current_pass: list[int] = []
-        self.factors: list[np.ndarray] = []
+        self.factors: list[np.ndarray] = []             # reoptimize's graph (the per-node factors live in the backend)
+        self.n_factors = 0                              # graph_->size()
         self._store = None
         self._store_V = 0
 
@@ -191,7 +177,8 @@ class DpgSLAM:
     def reoptimize(self):
         """dpg_slam.cc:35-120: a fresh graph -- per node the pass prior or the odometry Between, the
         successive alignment (always a factor) and every loop-closure candidate (a factor when
-        converged), all aligned in one batch from the current estimates -- then the solve."""
+        converged), all aligned in one batch from the current estimates -- then one update of a new
+        graph from the current estimates."""
         V = len(self.poses)
         if V == 0:
             return
@@ -216,7 +203,9 @@ class DpgSLAM:
             if k < len(succ) or ok:
                 F.append(_icp_factor(res[k:k + 1], int(a), int(b), self.icp_params))
         self.factors = F
-        self._optimize()
+        self.n_factors = len(F)
+        X = self.be.rebuild_graph(est.astype(np.float64), np.concatenate(F))
+        self.poses = [np.asarray(x, f32) for x in X]
 
     # ------------------------------------------------------------------ internals
     def _odometry_factor(self, prev, cur, i, j):
@@ -252,51 +241,42 @@ class DpgSLAM:
         if self.first_scan_for_pass:
             self.first_scan_for_pass = False
             n = self._create_node(ranges, range_max, angle_min, angle_max, (0.0, 0.0, 0.0))
-            self.factors.append(api.prior_factor(n, sigmas=self.prior_sigmas))
+            extra = api.prior_factor(n, sigmas=self.prior_sigmas)
             self.odom_only.append(self.prev_odom.copy())
             self.odom_at_last_align = self.prev_odom.copy()
-            if self.pass_number == 0:
-                self.current_pass.append(n)
-                self._optimize()
+            if self.pass_number == 0:   # the first node: the prior only, then optimizeGraph (:189-202)
+                self._add_node(n, extra, aligned=False)
                 return False
-            self._obs_constraints(n)
+            self._add_node(n, extra)
             return True
         if not self._should_process_laser():
             return False
         rel = api.inverse_transform_point(self.prev_odom, self.odom_at_last_align)   # displacement since the last node
         pose = api.transform_point(rel, self.poses[-1])                                # createRelativePositionedNode
         n = self._create_node(ranges, range_max, angle_min, angle_max, pose)
-        if self.odometry_constraints:
-            self.factors.append(self._odometry_factor(self.odom_at_last_align, self.prev_odom, n - 1, n))
+        extra = self._odometry_factor(self.odom_at_last_align, self.prev_odom, n - 1, n) if self.odometry_constraints \
+            else np.zeros(0, FACTOR_DTYPE)
         self.odom_only.append(self.prev_odom.copy())
         self.odom_at_last_align = self.prev_odom.copy()
-        self._obs_constraints(n)
+        self._add_node(n, extra)
         return True
 
-    def _obs_constraints(self, n):
-        """updatePoseGraphObsConstraints (dpg_slam.cc:255-314); the new node n is already stored,
-        so dpg_nodes_ of the reference is nodes [0, n)."""
-        prev = n - 1
-        ok, res = self.be.run_icp(self.poses[prev], self.clouds[prev], self.poses[n], self.clouds[n], self.icp_params)
-        self.factors.append(_icp_factor(res, prev, n, self.icp_params))
-        if self.non_successive and n > 1:
-            pp = self.poses[prev]
-            for i in range(max(0, n - 2)):
-                d = self.poses[i][:2] - pp[:2]
-                dist = f32(np.sqrt(f32(d[0] * d[0]) + f32(d[1] * d[1])))
-                thr = self.within if self.node_pass[i] == self.node_pass[prev] else self.across
-                if dist <= thr:
-                    ok, res = self.be.run_icp(self.poses[i], self.clouds[i], pp, self.clouds[prev], self.icp_params)
-                    if ok:
-                        self.factors.append(_icp_factor(res, i, prev, self.icp_params))
+    def _add_node(self, n, extra, aligned=True):
+        """updatePoseGraphObsConstraints (dpg_slam.cc:255-314) + optimizeGraph: the backend aligns the
+        new node n with the preceding one and the preceding one with every earlier node within the
+        distance rule (one batch), adds the factors and updates the graph."""
+        extra = np.asarray(extra, FACTOR_DTYPE).reshape(-1)
+        n_icp, X = self.be.add_node(self.clouds[n], np.asarray(self.node_pass, np.int32), self.poses[n], extra,
+                                    self.icp_params, self._reopt_params(), aligned and self.non_successive)
+        self.n_factors += len(extra) + n_icp
         self.current_pass.append(n)
-        self._optimize()
-
-    def _optimize(self):
-        """optimizeGraph (dpg_slam.cc:316-329): batch GN from the current estimates."""
-        X0 = np.stack(self.poses).astype(np.float64)
-        X = self.be.optimize(X0, np.concatenate(self.factors), self.gn_params)
         self.poses = [np.asarray(x, f32) for x in X]
+
+    def _reopt_params(self):
+        rp = _abi.default_reopt_params()
+        rp.max_node_dist_within_pass = float(self.within)
+        rp.max_node_dist_across_passes = float(self.across)
+        return rp
 
     def _dpg_store(self):
         """The node store over every node so far: created once, then the new nodes' scans are

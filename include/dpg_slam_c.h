@@ -305,6 +305,90 @@ int dpg_reoptimize(dpg_ctx* ctx, int64_t n_nodes, const int32_t* pass_numbers, c
                    const float* odom_only, const dpg_icp_params* icp_params, const dpg_gn_params* gn_params,
                    const dpg_reopt_params* params, double* poses_out, dpg_reopt_stats* stats);
 
+/* ---- incremental per-node solve (updatePoseGraphObsConstraints -> optimizeGraph -> isam_->update,
+ *      dpg_slam.cc:255-329, ISAM2 built at :22 with default parameters) ----
+ * A device-resident pose graph that grows by one isam_->update per call.  The elimination order of
+ * the Cholesky is kept and extended (new nodes at its end, new edges add their fill along the
+ * elimination tree); a fresh minimum-degree order is computed every reorder_every nodes or when the
+ * fill grows 1.5x.  DPG_INC_ISAM2: ISAM2 semantics with its defaults (relinearize variables whose
+ * max |delta| >= 0.1 on every 10th update, one Gauss-Newton step from the linearization point per
+ * update; exact solve instead of the 0.001 wildfire threshold).  DPG_INC_BATCH: Gauss-Newton to
+ * convergence on every update.  duplicate_factors = 1 reproduces SURVEY Q1 (the reference re-adds
+ * the whole accumulated graph_ on every update: a factor's information is scaled by the number of
+ * updates it has been part of). */
+#define DPG_INC_ISAM2 0
+#define DPG_INC_BATCH 1
+typedef struct dpg_inc_params {
+    int32_t mode;                    /* DPG_INC_ISAM2 | DPG_INC_BATCH */
+    int32_t relinearize_skip;        /* 10 (ISAM2Params::relinearizeSkip) */
+    double relinearize_threshold;    /* 0.1 (ISAM2Params::relinearizeThreshold) */
+    int32_t duplicate_factors;       /* 0; 1: SURVEY Q1 */
+    int32_t reorder_every;           /* 64: a fresh fill-reducing order every this many new nodes */
+    dpg_gn_params gn;                /* DPG_INC_BATCH: the Gauss-Newton loop (Cholesky) */
+} dpg_inc_params;
+
+typedef struct dpg_inc_stats {
+    int64_t n_nodes, n_factors;
+    int64_t nnz_l;                   /* 3x3 blocks below the diagonal of L */
+    int32_t reordered;               /* 1: this update computed a fresh order */
+    int32_t relinearized;            /* ISAM2: variables relinearized by this update */
+    int32_t gn_iterations;           /* ISAM2: 1 */
+    int32_t pad;
+    double error;                    /* 0.5 chi2 at the last linearization point */
+    double last_delta_inf;
+    double ms_total, ms_symbolic, ms_numeric;
+} dpg_inc_stats;
+
+typedef struct dpg_inc dpg_inc;
+void dpg_inc_params_default(dpg_inc_params* p);
+dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* params);
+void dpg_inc_destroy(dpg_inc* g);
+/* reoptimize() (dpg_slam.cc:36-39): a new ISAM2 and a new graph */
+int dpg_inc_reset(dpg_inc* g);
+/* isam_->update(new factors, new values): n_new nodes appended (keys V .. V+n_new-1, initial values
+ * init[n_new][3]) and the factors added since the last update (keys < V + n_new). */
+int dpg_inc_update(dpg_inc* g, int64_t n_new, const double* init, const dpg_factor* factors, int64_t n_factors,
+                   dpg_inc_stats* stats);
+int64_t dpg_inc_num_nodes(const dpg_inc* g);
+/* calculateEstimate() of the first n nodes: poses[n][3] */
+int dpg_inc_get_poses(dpg_inc* g, double* poses, int64_t n);
+
+/* Append nodes to the uploaded scan store (dpg_scans_upload's layout): pts_xy = the new nodes' full
+ * clouds concatenated, node_offsets[n_new + 1] relative to pts_xy; the downsample ratio must match
+ * the store's.  Only the new nodes' neighbour indexes are built. */
+int dpg_scans_append(dpg_ctx* ctx, const float* pts_xy, const int64_t* node_offsets, int64_t n_new,
+                     int32_t downsample_ratio);
+
+typedef struct dpg_add_node_stats {
+    int64_t n_icp_edges;             /* successive + loop-closure alignments run for this node */
+    int64_t n_loop_closures;         /* loop-closure factors added (converged alignments) */
+    double ms_icp;                   /* batched ICP of the node's edges (incl. its index build) */
+    dpg_inc_stats update;
+} dpg_add_node_stats;
+
+/* One new node (id V = dpg_inc_num_nodes(g)) with explicit alignments: the node's base_link cloud
+ * joins the scan store; ONE batched ICP aligns the successive pair (V-1, V) when `successive` and
+ * every pair in pairs[n_pairs][2] = {node_1 (target), node_2 (source)}, keys <= V; the successive
+ * factor always joins the graph, the other pairs' factors when converged (dpg_slam.cc:263-267,
+ * 295-301), after the caller's `extra` factors, in one dpg_inc_update (initial pose init_pose). */
+int dpg_add_node_pairs(dpg_inc* g, const float* cloud_xy, int64_t n_pts, const float init_pose[3],
+                       const dpg_factor* extra, int64_t n_extra, const int32_t* pairs, int64_t n_pairs,
+                       int32_t successive, const dpg_icp_params* icp_params, dpg_add_node_stats* stats);
+/* One new node, as updatePoseGraphObsConstraints + optimizeGraph run it (dpg_slam.cc:255-314):
+ * the node's base_link cloud is appended to the scan store (node id = dpg_inc_num_nodes(g)); ONE
+ * batched ICP aligns the successive pair (prev, new) and every loop-closure candidate (i, prev),
+ * i < V - 2 (V = nodes before this one), whose float distance to prev's estimate is within
+ * max_node_dist_within_pass (same pass_numbers) or max_node_dist_across_passes; the successive
+ * factor is always added, loop closures when converged; together with the caller's `extra`
+ * factors (the pass prior or the odometry Between) they go into one dpg_inc_update with the node's
+ * initial pose init_pose (createRelativePositionedNode, float).  pass_numbers[V + 1]: every node's
+ * pass, the new one last.  non_successive = 0 skips the loop closures
+ * (non_successive_scan_constraints_, parameters.h:349-354).  The ICP guesses use the estimates of
+ * dpg_inc_get_poses rounded to float (the reference's dpg_nodes_ positions are float). */
+int dpg_add_node(dpg_inc* g, const float* cloud_xy, int64_t n_pts, const int32_t* pass_numbers, const float init_pose[3],
+                 const dpg_factor* extra, int64_t n_extra, const dpg_icp_params* icp_params,
+                 const dpg_reopt_params* params, int32_t non_successive, dpg_add_node_stats* stats);
+
 /* ---- DPG change detection (DpgSLAM::executeDPG, dpg_slam.cc:865-886) ----
  * The dynamic node state (DpgNode/Measurement: per-beam label and sector, per-node sector
  * activation and active flag) lives on the device in a dpg_dpg store; executeDPG runs on it.

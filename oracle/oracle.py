@@ -362,3 +362,80 @@ class OracleDpgStore:
             res[name] = out[k:k + c].copy()
             k += int(c)
         return res
+
+
+def retract(X, d):
+    """Pose2 retraction X (+) d, ChartAtOrigin (dpg_oracle.c retract, GTSAM Values::retract)."""
+    X = np.asarray(X, np.float64).reshape(-1, 3)
+    d = np.asarray(d, np.float64).reshape(-1, 3)
+    c, s = np.cos(X[:, 2]), np.sin(X[:, 2])
+    cd, sd = np.cos(d[:, 2]), np.sin(d[:, 2])
+    out = np.empty_like(X)
+    out[:, 0] = X[:, 0] + (c * d[:, 0] - s * d[:, 1])
+    out[:, 1] = X[:, 1] + (s * d[:, 0] + c * d[:, 1])
+    out[:, 2] = np.arctan2(s * cd + c * sd, c * cd - s * sd)
+    return out
+
+
+class OracleIncGraph:
+    """CPU restatement of the incremental per-node solve (dpg_inc.hip; optimizeGraph per node,
+    dpg_slam.cc:255-329, isam_->update at :320 with ISAM2's defaults):
+      isam2 -- linearization points theta; on updates whose count before the update is a multiple
+               of relinearize_skip, variables with max |delta| >= relinearize_threshold take
+               theta (+) delta; then every factor is linearized at theta, H delta = -g is solved
+               (block-sparse Cholesky, oracle_gn_delta) and the estimate is theta (+) delta;
+      batch -- Gauss-Newton to convergence from the current estimates (oracle_optimize_graph).
+    duplicate_factors reproduces SURVEY Q1 (information x number of updates a factor has been in)."""
+
+    def __init__(self, mode="isam2", relinearize_skip=10, relinearize_threshold=0.1, duplicate_factors=False,
+                 gn_params=None):
+        from dpgslam import _abi
+        self._abi = _abi
+        self.mode = mode
+        self.skip = int(relinearize_skip)
+        self.thr = float(relinearize_threshold)
+        self.dup = bool(duplicate_factors)
+        self.gn_params = gn_params
+        self.reset()
+
+    def reset(self):
+        self.updates = 0
+        self.F = np.zeros(0, self._abi.FACTOR_DTYPE)
+        self.created = np.zeros(0, np.int64)
+        self.theta = np.zeros((0, 3))
+        self.est = np.zeros((0, 3))
+        self.maxd = np.zeros(0)
+
+    @property
+    def V(self):
+        return len(self.est)
+
+    def update(self, init, factors):
+        init = np.asarray(init, np.float64).reshape(-1, 3)
+        V0 = self.V
+        relin = self.mode == "isam2" and self.updates % self.skip == 0 and V0 > 0
+        self.updates += 1
+        if relin:
+            sel = self.maxd >= self.thr
+            self.theta[sel] = self.est[sel]
+        self.theta = np.concatenate([self.theta, init])
+        self.est = np.concatenate([self.est, init])
+        self.maxd = np.concatenate([self.maxd, np.zeros(len(init))])
+        f = np.asarray(factors, self._abi.FACTOR_DTYPE).reshape(-1)
+        self.F = np.concatenate([self.F, f])
+        self.created = np.concatenate([self.created, np.full(len(f), self.updates, np.int64)])
+        F = self.F.copy()
+        if self.dup:
+            F["info"] *= (self.updates - self.created + 1).astype(np.float64)[:, None]
+        if self.mode == "isam2":
+            d, err = gn_delta(self.theta, F)
+            self.est = retract(self.theta, d)
+            self.maxd = np.abs(d).max(1)
+            return err
+        X, st = optimize_graph(self.est, F, self.gn_params)
+        self.est = X.copy()
+        self.theta = X.copy()
+        return st.final_error
+
+    def poses(self):
+        return self.est.copy()

@@ -7,6 +7,7 @@ import pytest
 
 from dpgslam import synth
 from dpgslam.slam import DpgSLAM
+from slam_oracle import OracleSlamBackend
 
 
 def _drive(slam, w, nodes_per_pass, rng_seed=3):
@@ -20,7 +21,7 @@ def _drive(slam, w, nodes_per_pass, rng_seed=3):
             odom = w.est[v].astype(np.float64) + rng.normal(0, [0.01, 0.01, 0.002])
             slam.ObserveOdometry(odom[:2].astype(np.float32), np.float32(odom[2]))
             slam.ObserveLaser(w.ranges[v], 0.0, float(w.geom[v, 2]), float(w.geom[v, 0]), float(w.geom[v, 1]))
-            out.append((len(slam.poses), len(slam.factors)))
+            out.append((len(slam.poses), slam.n_factors))
     return out
 
 
@@ -31,7 +32,7 @@ def _workload():
 
 def test_slam_driver_oracle_backend():
     w = _workload()
-    s = DpgSLAM(backend="oracle")
+    s = DpgSLAM(backend=OracleSlamBackend())
     trace = _drive(s, w, 14)
     V = len(s.poses)
     assert V > 10 and s.pass_number == 1
@@ -47,8 +48,15 @@ def test_slam_driver_oracle_backend():
 
 @pytest.mark.gpu
 def test_slam_driver_gpu_matches_oracle():
+    """Same nodes and factors after every scan, exactly.  Poses to 1e-5, labels to 0.1 %: the two
+    incremental solves agree to ~1e-13 relative (their Cholesky factors sum in different orders),
+    and the driver keeps float32 poses (dpg_nodes_ positions are float); a double that differs in
+    its last bits across a float rounding boundary moves an ICP guess by one float ulp, which can
+    change that alignment's last iterations (bit-exact ICP parity holds for equal inputs,
+    tests/test_gpu_parity.py) and, through the graph, later poses by ~1e-6 and the occupancy cell
+    of a point on a cell boundary."""
     w = _workload()
-    so, sg = DpgSLAM(backend="oracle"), DpgSLAM(backend="gpu")
+    so, sg = DpgSLAM(backend=OracleSlamBackend()), DpgSLAM(backend="gpu")
     to, tg = _drive(so, w, 14), _drive(sg, w, 14)
     assert to == tg                                    # same nodes and factors after every scan
     Xo, Xg = np.stack(so.poses), np.stack(sg.poses)
