@@ -17,6 +17,8 @@ timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/
 rc=$?; echo "smoke exit $rc"; tail -2 "$OUT/smoke.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench exit $rc"; cat "$OUT/bench.json"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py --workload incremental > "$OUT/inc.json" 2> "$OUT/inc.err"
+rc=$?; echo "inc bench exit $rc"; cat "$OUT/inc.json"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err"
 rc=$?; echo "prof exit $rc"; [ $rc -eq 0 ] || exit $rc
