@@ -133,6 +133,9 @@ def main_incremental(args):
     print(f"generated {args.config} in {time.time() - t0:.1f}s; {sum(len(b) for b in by_node)} loop closures", file=sys.stderr,
           flush=True)
 
+    import ctypes as C
+    L = _abi.lib()
+    prof, pbuf = [], (C.c_double * 8)()
     lat, icp_ms, sym_ms, num_ms, reord, relin = [], [], [], [], 0, 0
     with api.Context(0) as ctx:
         g = api.IncGraph(ctx, mode=args.inc_mode)
@@ -147,6 +150,8 @@ def main_incremental(args):
             num_ms.append(st.update.ms_numeric)
             reord += st.update.reordered
             relin += st.update.relinearized
+            L.dpg_inc_last_profile(C.c_void_p(g.handle), pbuf, 8)
+            prof.append(list(pbuf)[:6])
             if v % 1000 == 999:
                 print(f"node {v + 1}: last latency {lat[-1]:.2f} ms", file=sys.stderr, flush=True)
         X_inc = g.poses()
@@ -165,7 +170,10 @@ def main_incremental(args):
         "p50_ms": float(np.median(tail)), "p90_ms": float(np.percentile(tail, 90)), "mean_ms_all": float(np.mean(lat)),
         "nodes_per_s_tail": float(1e3 / np.mean(tail)),
         "tail_breakdown_ms": {"icp": float(np.mean(icp_ms[-500:])), "symbolic_host": float(np.mean(sym_ms[-500:])),
-                              "numeric": float(np.mean(num_ms[-500:]))},
+                              "numeric": float(np.mean(num_ms[-500:])),
+                              "symbolic_parts": dict(zip(["incsym", "derive", "lists_upload", "chol_build",
+                                                          "chol_host", "chol_upload"],
+                                                         np.mean(np.asarray(prof[-500:]), 0).round(4).tolist()))},
         "reorders": reord, "relinearized_total": relin, "nnz_L_blocks": nnz, "factors": n_fac,
         "round1_per_node_from_scratch_ms": scratch_ms, "round1_from_scratch_gn_iterations": int(gst.iterations),
     }

@@ -43,6 +43,9 @@ int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, in
                    std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
                                const dpg_chol_opts* opts, dpg_chol_sym* S);
+// the same from patterns in CSR form: column p's rows are prow[cp[p] .. cp[p + 1]) (sorted)
+int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow,
+                          const dpg_chol_opts* opts, dpg_chol_sym* S);
 
 // Incremental symbolic state of a growing pose graph (dpg_inc.hip): the elimination order is kept
 // and new nodes are appended at its end; the column patterns of L are bitsets over positions,
@@ -68,5 +71,7 @@ int dpg_incsym_derive(const dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_c
 // buffers grow only when needed -- or created when NULL.  On error *h is destroyed and NULL.
 int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                         const dpg_chol_sym* S);
+// host time (ms) of the last build of h: structures, uploads
+void dpg_chol_build_times(void* h, double out[2]);
 
 #endif

@@ -20,6 +20,7 @@
 // factorization stay resident in HBM (tens of MB).
 
 #include <hip/hip_runtime.h>
+#include <time.h>
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -1399,6 +1400,7 @@ struct CholDev {
     size_t c_sns = 0, c_omap = 0, c_child = 0, c_relmap = 0, c_rows = 0, c_level = 0, c_perm = 0, c_pos = 0,
            c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_asm_t = 0, c_asm_c = 0, c_panel = 0,
            c_upd = 0, c_fwd = 0, c_fac = 0, c_ftasks = 0, c_fchild = 0, c_bwd = 0, c_sync = 0;
+    double t_build[2] = {0, 0};   // last chol_build: host structures, uploads (ms)
 };
 
 }  // namespace
@@ -1446,14 +1448,21 @@ int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32
 }
 
 namespace {
+double wall_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
 int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
+    const double t_b0 = wall_ms();
     const dpg_chol_sym& S = c->sym;
     c->lds_fused = 0;
     c->n_launches = 0;
     c->n = n;
     c->nnzb_upper = n + n_pairs;
-    // omap: every upper block of H -> (front, local block row, local block col, transpose)
-    std::vector<std::vector<OEnt>> per((size_t)S.ns);
+    // omap: every upper block of H -> (front, local block row, local block col, transpose), grouped
+    // by front (counting sort), each front's entries by (column, row)
     auto local_index = [&](int32_t s, int32_t p) -> int32_t {
         const int32_t c0 = S.sn_c0[(size_t)s], k = S.sn_c0[(size_t)s + 1] - c0;
         if (p >= c0 && p < c0 + k) return p - c0;
@@ -1463,24 +1472,32 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
         if (it == e || *it != p) return -1;
         return k + (int32_t)(it - b);
     };
-    for (int64_t v = 0; v < n; ++v) {
-        const int32_t p = S.pos[(size_t)v], s = S.sn_of[(size_t)p];
-        const int32_t l = local_index(s, p);
-        per[(size_t)s].push_back(OEnt{(int32_t)v, (int16_t)l, (int16_t)l, 0, 0});
+    auto front_of_pair = [&](int64_t q) { return S.sn_of[(size_t)std::min(S.pos[(size_t)pair_lo[q]], S.pos[(size_t)pair_hi[q]])]; };
+    std::vector<int64_t> om_ptr((size_t)S.ns + 1, 0);
+    for (int64_t v = 0; v < n; ++v) om_ptr[(size_t)S.sn_of[(size_t)S.pos[(size_t)v]] + 1]++;
+    for (int64_t q = 0; q < n_pairs; ++q) om_ptr[(size_t)front_of_pair(q) + 1]++;
+    for (int32_t s = 0; s < S.ns; ++s) om_ptr[(size_t)s + 1] += om_ptr[(size_t)s];
+    std::vector<OEnt> omap((size_t)om_ptr[(size_t)S.ns]);
+    {
+        std::vector<int64_t> cur(om_ptr.begin(), om_ptr.end() - 1);
+        for (int64_t v = 0; v < n; ++v) {
+            const int32_t p = S.pos[(size_t)v], s = S.sn_of[(size_t)p];
+            const int32_t l = local_index(s, p);
+            omap[(size_t)cur[(size_t)s]++] = OEnt{(int32_t)v, (int16_t)l, (int16_t)l, 0, 0};
+        }
+        for (int64_t q = 0; q < n_pairs; ++q) {
+            const int32_t plo = S.pos[(size_t)pair_lo[q]], phi = S.pos[(size_t)pair_hi[q]];
+            const int32_t later = plo > phi ? plo : phi, earlier = plo > phi ? phi : plo;
+            const int32_t s = S.sn_of[(size_t)earlier];
+            const int32_t a = local_index(s, later), b = local_index(s, earlier);
+            if (a < 0 || b < 0) return DPG_ERR_NUMERIC;
+            // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
+            omap[(size_t)cur[(size_t)s]++] = OEnt{(int32_t)(n + q), (int16_t)a, (int16_t)b, plo > phi ? 0 : 1, 0};
+        }
     }
-    for (int64_t q = 0; q < n_pairs; ++q) {
-        const int32_t lo = pair_lo[q], hi = pair_hi[q];
-        const int32_t plo = S.pos[(size_t)lo], phi = S.pos[(size_t)hi];
-        const int32_t later = plo > phi ? plo : phi, earlier = plo > phi ? phi : plo;
-        const int32_t s = S.sn_of[(size_t)earlier];
-        const int32_t a = local_index(s, later), b = local_index(s, earlier);
-        if (a < 0 || b < 0) return DPG_ERR_NUMERIC;
-        // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
-        per[(size_t)s].push_back(OEnt{(int32_t)(n + q), (int16_t)a, (int16_t)b, plo > phi ? 0 : 1, 0});
-    }
-    for (auto& v : per)
-        std::sort(v.begin(), v.end(), [](const OEnt& x, const OEnt& y) { return x.b != y.b ? x.b < y.b : x.a < y.a; });
-    std::vector<OEnt> omap;
+    for (int32_t s = 0; s < S.ns; ++s)
+        std::sort(omap.begin() + om_ptr[(size_t)s], omap.begin() + om_ptr[(size_t)s + 1],
+                  [](const OEnt& x, const OEnt& y) { return x.b != y.b ? x.b < y.b : x.a < y.a; });
     std::vector<SnDev> sns((size_t)S.ns);
     int64_t acc_total = 0;
     for (int32_t s = 0; s < S.ns; ++s) {
@@ -1492,8 +1509,8 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
         d.front_off = S.front_off[(size_t)s];
         d.rows_off = S.sn_rows_ptr[(size_t)s];
         d.child_off = S.child_ptr[(size_t)s];
-        d.omap_off = (int64_t)omap.size();
-        d.omap_n = (int32_t)per[(size_t)s].size();
+        d.omap_off = om_ptr[(size_t)s];
+        d.omap_n = (int32_t)(om_ptr[(size_t)s + 1] - om_ptr[(size_t)s]);
         d.acc_off = acc_total;
         d.parent = S.sn_parent[(size_t)s];
         const int32_t m3 = 3 * (d.k + d.r);
@@ -1502,7 +1519,6 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
                   : std::min(kGmax, (3 * d.k + kFNB - 1) / kFNB + (3 * d.r + kFNB - 1) / kFNB);
         d.need = 0;
         acc_total += 3 * d.r;
-        omap.insert(omap.end(), per[(size_t)s].begin(), per[(size_t)s].end());
     }
     for (int32_t s = 0; s < S.ns; ++s)
         if (sns[(size_t)s].parent >= 0) sns[(size_t)sns[(size_t)s].parent].need += sns[(size_t)s].G;
@@ -1603,65 +1619,70 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
         }
     }
     c->fused = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_LEVELS") == nullptr;
-    c->lds_solve.assign((size_t)S.n_levels, 0);
+    // LDS of the DAG solves: the largest front
+    c->lds_solve_max = 0;
+    for (int32_t s = 0; s < S.ns; ++s) {
+        const int32_t m3 = 3 * (sns[(size_t)s].k + sns[(size_t)s].r);
+        c->lds_solve_max = std::max(c->lds_solve_max, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
+    }
+    if (c->lds_solve_max > 160 * 1024) return DPG_ERR_SIZE;
     std::vector<AsmTask> asm_t;
     std::vector<AsmChild> asm_c;
-    std::vector<size_t> lds_asm((size_t)S.n_levels, 0);
     std::vector<int2> panel_t;
     std::vector<int4> upd_t;
-    c->plan.assign((size_t)S.n_levels, CholDev::Level{});
-    for (int32_t l = 0; l < S.n_levels; ++l) {
-        size_t ms = 0;
-        int32_t maxk3 = 0;
-        CholDev::Level& L = c->plan[(size_t)l];
-        L.asm_off = (int32_t)asm_t.size();
-        for (int32_t q = S.level_ptr[(size_t)l]; q < S.level_ptr[(size_t)l + 1]; ++q) {
-            const int32_t s = S.level_list[(size_t)q];
-            const SnDev& d = sns[(size_t)s];
-            const int32_t m3 = 3 * (d.k + d.r);
-            ms = std::max(ms, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
-            lds_asm[(size_t)l] = std::max(lds_asm[(size_t)l], (size_t)kCT * m3 * sizeof(double));
-            maxk3 = std::max(maxk3, 3 * d.k);
-            build_tiles(s, kCT, asm_t, asm_c);
-        }
-        L.asm_cnt = (int32_t)asm_t.size() - L.asm_off;
-        c->n_launches += 1;
-        for (int32_t j0 = 0; j0 < maxk3; j0 += kNB) {
-            CholDev::Step st{(int32_t)panel_t.size(), 0, 1, 0, (int32_t)upd_t.size(), 0};
-            int32_t maxR = 0;
+    c->plan.clear();
+    if (!c->fused) {
+        // level-synchronous path: per level, assembly tiles, then panel + update steps
+        c->plan.assign((size_t)S.n_levels, CholDev::Level{});
+        for (int32_t l = 0; l < S.n_levels; ++l) {
+            int32_t maxk3 = 0;
+            CholDev::Level& L = c->plan[(size_t)l];
+            L.asm_off = (int32_t)asm_t.size();
+            L.lds_asm = 0;
             for (int32_t q = S.level_ptr[(size_t)l]; q < S.level_ptr[(size_t)l + 1]; ++q) {
                 const int32_t s = S.level_list[(size_t)q];
                 const SnDev& d = sns[(size_t)s];
-                const int32_t m3 = 3 * (d.k + d.r), k3 = 3 * d.k;
-                if (k3 <= j0) continue;
-                panel_t.push_back(make_int2(s, j0));
-                maxR = std::max(maxR, m3 - j0);
-                const int32_t base = j0 + std::min(kNB, k3 - j0), nt = (m3 - base + kUT - 1) / kUT;
-                for (int32_t ti = 0; ti < nt; ++ti)
-                    for (int32_t tl = 0; tl <= ti; ++tl) upd_t.push_back(make_int4(s, j0, base + kUT * ti, base + kUT * tl));
+                const int32_t m3 = 3 * (d.k + d.r);
+                L.lds_asm = std::max(L.lds_asm, (size_t)kCT * m3 * sizeof(double));
+                maxk3 = std::max(maxk3, 3 * d.k);
+                build_tiles(s, kCT, asm_t, asm_c);
             }
-            st.panel_cnt = (int32_t)panel_t.size() - st.panel_off;
-            st.upd_cnt = (int32_t)upd_t.size() - st.upd_off;
-            st.max_rows = maxR;
-            st.rpt = maxR <= kT ? 1 : maxR <= 2 * kT ? 2 : maxR <= 4 * kT ? 4 : 0;
-            if (st.rpt == 0) return DPG_ERR_SIZE;
-            L.steps.push_back(st);
-            c->n_launches += 1 + (st.upd_cnt > 0);
+            L.asm_cnt = (int32_t)asm_t.size() - L.asm_off;
+            c->n_launches += 1;
+            for (int32_t j0 = 0; j0 < maxk3; j0 += kNB) {
+                CholDev::Step st{(int32_t)panel_t.size(), 0, 1, 0, (int32_t)upd_t.size(), 0};
+                int32_t maxR = 0;
+                for (int32_t q = S.level_ptr[(size_t)l]; q < S.level_ptr[(size_t)l + 1]; ++q) {
+                    const int32_t s = S.level_list[(size_t)q];
+                    const SnDev& d = sns[(size_t)s];
+                    const int32_t m3 = 3 * (d.k + d.r), k3 = 3 * d.k;
+                    if (k3 <= j0) continue;
+                    panel_t.push_back(make_int2(s, j0));
+                    maxR = std::max(maxR, m3 - j0);
+                    const int32_t base = j0 + std::min(kNB, k3 - j0), nt = (m3 - base + kUT - 1) / kUT;
+                    for (int32_t ti = 0; ti < nt; ++ti)
+                        for (int32_t tl = 0; tl <= ti; ++tl) upd_t.push_back(make_int4(s, j0, base + kUT * ti, base + kUT * tl));
+                }
+                st.panel_cnt = (int32_t)panel_t.size() - st.panel_off;
+                st.upd_cnt = (int32_t)upd_t.size() - st.upd_off;
+                st.max_rows = maxR;
+                st.rpt = maxR <= kT ? 1 : maxR <= 2 * kT ? 2 : maxR <= 4 * kT ? 4 : 0;
+                if (st.rpt == 0) return DPG_ERR_SIZE;
+                L.steps.push_back(st);
+                c->n_launches += 1 + (st.upd_cnt > 0);
+            }
+            if (L.lds_asm > 160 * 1024) return DPG_ERR_SIZE;
         }
-        c->lds_solve[(size_t)l] = ms;
-        L.lds_asm = lds_asm[(size_t)l];
-        if (ms > 160 * 1024 || L.lds_asm > 160 * 1024) return DPG_ERR_SIZE;
     }
+    const double t_b1 = wall_ms();
     int rc = 0;
     rc |= dalloc_copy(&c->sns, &c->c_sns, sns);
     rc |= dalloc_copy(&c->omap, &c->c_omap, omap);
     rc |= dalloc_copy(&c->child_list, &c->c_child, S.child_list);
     rc |= dalloc_copy(&c->relmap, &c->c_relmap, S.relmap);
     rc |= dalloc_copy(&c->rows, &c->c_rows, S.sn_rows);
-    rc |= dalloc_copy(&c->level_list, &c->c_level, S.level_list);
     rc |= dalloc_copy(&c->perm, &c->c_perm, S.perm);
     rc |= dalloc_copy(&c->pos, &c->c_pos, S.pos);
-    rc |= dalloc_copy(&c->asm_tasks, &c->c_asm_t, asm_t);
     {
         // solves: the critical-path order (children first), and its reverse (parents first)
         std::vector<int32_t> bwd(fo.rbegin(), fo.rend());
@@ -1674,21 +1695,30 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
         //  pivot-tile hand-off flags [per large-front tile]]
         c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
         rc |= dreserve(&c->sync, &c->c_sync, c->sync_bytes / sizeof(int32_t));
-        c->lds_solve_max = 0;
-        for (size_t v : c->lds_solve) c->lds_solve_max = std::max(c->lds_solve_max, v);
     }
-    rc |= dalloc_copy(&c->asm_child, &c->c_asm_c, asm_c);
-    rc |= dalloc_copy(&c->panel_tasks, &c->c_panel, panel_t);
-    rc |= dalloc_copy(&c->upd_tasks, &c->c_upd, upd_t);
+    if (!c->fused) {
+        rc |= dalloc_copy(&c->asm_tasks, &c->c_asm_t, asm_t);
+        rc |= dalloc_copy(&c->asm_child, &c->c_asm_c, asm_c);
+        rc |= dalloc_copy(&c->panel_tasks, &c->c_panel, panel_t);
+        rc |= dalloc_copy(&c->upd_tasks, &c->c_upd, upd_t);
+    }
     rc |= dreserve(&c->fronts, &c->c_fronts, (size_t)S.front_off[(size_t)S.ns]);
     rc |= dreserve(&c->acc, &c->c_acc, (size_t)acc_total);
     rc |= dreserve(&c->ysol, &c->c_ysol, (size_t)(3 * n));
     rc |= dreserve(&c->xsol, &c->c_xsol, (size_t)(3 * n));
     rc |= dreserve(&c->status, &c->c_status, 1);
     if (!rc) rc |= hipMemset(c->status, 0, sizeof(int32_t)) != hipSuccess;
+    c->t_build[0] = t_b1 - t_b0;
+    c->t_build[1] = wall_ms() - t_b1;
     return rc ? DPG_ERR_HIP : DPG_OK;
 }
 }  // namespace
+
+void dpg_chol_build_times(void* h, double out[2]) {
+    const CholDev* c = reinterpret_cast<const CholDev*>(h);
+    out[0] = c ? c->t_build[0] : 0.0;
+    out[1] = c ? c->t_build[1] : 0.0;
+}
 
 extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);

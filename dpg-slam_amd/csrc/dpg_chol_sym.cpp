@@ -14,6 +14,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <functional>
+#include <queue>
 #include <vector>
 
 #include "dpg_chol.h"
@@ -38,11 +40,18 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
     pattern.assign((size_t)n, {});
     std::vector<int32_t> nb;
     nb.reserve(1024);
-    // degree buckets would be faster; n is a few thousand, a linear scan is fine (once per pattern)
+    // the uneliminated node of least degree, ties -> lowest index: a min-heap of (degree, node) with
+    // lazy deletion (an entry is current iff its degree is the node's degree now)
+    std::priority_queue<std::pair<int32_t, int32_t>, std::vector<std::pair<int32_t, int32_t>>,
+                        std::greater<std::pair<int32_t, int32_t>>> heap;
+    for (int64_t v = 0; v < n; ++v) heap.emplace(deg[(size_t)v], (int32_t)v);
     for (int64_t p = 0; p < n; ++p) {
-        int32_t v = -1, best = INT32_MAX;
-        for (int64_t u = 0; u < n; ++u)
-            if (!done[(size_t)u] && deg[(size_t)u] < best) { best = deg[(size_t)u]; v = (int32_t)u; }
+        int32_t v = -1;
+        while (!heap.empty()) {
+            const auto top = heap.top();
+            heap.pop();
+            if (!done[(size_t)top.second] && top.first == deg[(size_t)top.second]) { v = top.second; break; }
+        }
         done[(size_t)v] = 1;
         perm[(size_t)p] = v;
         nb.clear();
@@ -66,6 +75,7 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
             const uint64_t* bu = &bits[(size_t)(u * W)];
             int32_t d = 0;
             for (int64_t w = 0; w < W; ++w) d += __builtin_popcountll(bu[w]);
+            if (d != deg[(size_t)u]) heap.emplace(d, u);
             deg[(size_t)u] = d;
         }
         memset(&bits[(size_t)(v * W)], 0, sizeof(uint64_t) * (size_t)W);
@@ -111,16 +121,28 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
                                const dpg_chol_opts* opts, dpg_chol_sym* S) {
     if (n <= 0 || (int64_t)perm.size() != n || (int64_t)pat.size() != n) return -1;
-    std::vector<int32_t> pos((size_t)n);
-    for (int64_t p = 0; p < n; ++p) pos[(size_t)perm[(size_t)p]] = (int32_t)p;
-    std::vector<int32_t> parent((size_t)n, -1), nchild((size_t)n, 0);
+    std::vector<int64_t> cp((size_t)n + 1, 0);
+    for (int64_t p = 0; p < n; ++p) cp[(size_t)p + 1] = cp[(size_t)p] + (int64_t)pat[(size_t)p].size();
+    std::vector<int32_t> rows((size_t)cp[(size_t)n]);
+    for (int64_t p = 0; p < n; ++p) std::copy(pat[(size_t)p].begin(), pat[(size_t)p].end(), rows.begin() + cp[(size_t)p]);
+    return dpg_chol_sym_from_csr(n, perm.data(), cp.data(), rows.data(), opts, S);
+}
+
+int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow,
+                          const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    if (n <= 0) return -1;
+    auto psize = [&](int64_t p) { return cp[p + 1] - cp[p]; };
+    // scratch reused across calls (the incremental solver derives every update)
+    thread_local std::vector<int32_t> parent, nchild, sn_first, mark, rowbuf;
+    parent.assign((size_t)n, -1);
+    nchild.assign((size_t)n, 0);
     for (int64_t p = 0; p < n; ++p)
-        if (!pat[(size_t)p].empty()) { parent[(size_t)p] = pat[(size_t)p][0]; nchild[(size_t)parent[(size_t)p]]++; }
+        if (psize(p) > 0) { parent[(size_t)p] = prow[cp[p]]; nchild[(size_t)parent[(size_t)p]]++; }
     // ---- fundamental supernodes, then relaxed merging of chains
     // column p+1 joins p's supernode when p's only parent is p+1, p is p+1's only child and the
     // patterns nest (fundamental), or when the explicit zeros added stay within the budget.
-    std::vector<int32_t> sn_first;   // first column of each supernode
-    std::vector<int32_t> sn_of((size_t)n);
+    S->sn_of.resize((size_t)n);
+    sn_first.clear();
     const int32_t max_cols = opts && opts->max_supernode_cols > 0 ? opts->max_supernode_cols : 64;
     const double relax = opts ? opts->relax_fraction : 0.0;
     {
@@ -131,20 +153,20 @@ int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, cons
             if (p > 0 && s >= 0) {
                 const int64_t q = p - 1;
                 const bool chain = parent[(size_t)q] == (int32_t)p && nchild[(size_t)p] == 1;
-                const int64_t cq = (int64_t)pat[(size_t)q].size(), cp = (int64_t)pat[(size_t)p].size();
+                const int64_t cq = psize(q), cpp = psize(p);
                 const int64_t ncols = p - sn_first[(size_t)s] + 1;
                 if (chain && ncols <= max_cols) {
-                    if (cq == cp + 1) join = true;   // fundamental
+                    if (cq == cpp + 1) join = true;   // fundamental
                     else if (relax > 0.0) {
                         // every earlier column of the supernode would carry p's pattern: the rows
                         // of pat[p] missing from pat[q] \ {p} become explicit zeros in them
-                        const int64_t add = std::max<int64_t>(0, cp - (cq - 1)) * cols;
-                        if ((double)(zeros + add) <= relax * (double)((cols + 1) * (cp + 1))) { join = true; zeros += add; }
+                        const int64_t add = std::max<int64_t>(0, cpp - (cq - 1)) * cols;
+                        if ((double)(zeros + add) <= relax * (double)((cols + 1) * (cpp + 1))) { join = true; zeros += add; }
                     }
                 }
             }
             if (!join) { sn_first.push_back((int32_t)p); ++s; zeros = 0; cols = 0; }
-            sn_of[(size_t)p] = s;
+            S->sn_of[(size_t)p] = s;
             ++cols;
         }
     }
@@ -153,25 +175,27 @@ int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, cons
     // ---- supernode row sets: union of its columns' patterns beyond its last column
     S->n = n;
     S->ns = ns;
-    S->perm.assign(perm.begin(), perm.end());
-    S->pos.assign(pos.begin(), pos.end());
+    S->perm.assign(perm, perm + n);
+    S->pos.resize((size_t)n);
+    for (int64_t p = 0; p < n; ++p) S->pos[(size_t)perm[p]] = (int32_t)p;
     S->sn_c0.assign(sn_first.begin(), sn_first.end());
     S->sn_rows_ptr.assign((size_t)ns + 1, 0);
     S->sn_rows.clear();
     S->sn_parent.assign((size_t)ns, -1);
+    mark.assign((size_t)n, -1);
     for (int32_t s = 0; s < ns; ++s) {
         const int32_t c0 = sn_first[(size_t)s], c1 = sn_first[(size_t)s + 1];
-        std::vector<int32_t> rows;
+        rowbuf.clear();
         for (int32_t c = c0; c < c1; ++c)
-            for (int32_t r : pat[(size_t)c])
-                if (r >= c1) rows.push_back(r);
-        std::sort(rows.begin(), rows.end());
-        rows.erase(std::unique(rows.begin(), rows.end()), rows.end());
-        S->sn_rows.insert(S->sn_rows.end(), rows.begin(), rows.end());
+            for (int64_t t = cp[c]; t < cp[c + 1]; ++t) {
+                const int32_t r = prow[t];
+                if (r >= c1 && mark[(size_t)r] != s) { mark[(size_t)r] = s; rowbuf.push_back(r); }
+            }
+        if (c1 - c0 > 1) std::sort(rowbuf.begin(), rowbuf.end());   // one column: already sorted
+        S->sn_rows.insert(S->sn_rows.end(), rowbuf.begin(), rowbuf.end());
         S->sn_rows_ptr[(size_t)s + 1] = (int64_t)S->sn_rows.size();
-        if (!rows.empty()) S->sn_parent[(size_t)s] = sn_of[(size_t)rows[0]];
+        if (!rowbuf.empty()) S->sn_parent[(size_t)s] = S->sn_of[(size_t)rowbuf[0]];
     }
-    S->sn_of.assign(sn_of.begin(), sn_of.end());
     // ---- levels
     S->sn_level.assign((size_t)ns, 0);
     for (int32_t s = 0; s < ns; ++s) {   // children precede parents in elimination order
@@ -184,41 +208,42 @@ int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, cons
     S->level_ptr.assign((size_t)nl + 1, 0);
     for (int32_t s = 0; s < ns; ++s) S->level_ptr[(size_t)S->sn_level[(size_t)s] + 1]++;
     for (int32_t l = 0; l < nl; ++l) S->level_ptr[(size_t)l + 1] += S->level_ptr[(size_t)l];
-    S->level_list.assign((size_t)ns, 0);
+    S->level_list.resize((size_t)ns);
     {
-        std::vector<int32_t> cur(S->level_ptr.begin(), S->level_ptr.end() - 1);
-        for (int32_t s = 0; s < ns; ++s) S->level_list[(size_t)cur[(size_t)S->sn_level[(size_t)s]]++] = s;
+        rowbuf.assign(S->level_ptr.begin(), S->level_ptr.end() - 1);
+        for (int32_t s = 0; s < ns; ++s) S->level_list[(size_t)rowbuf[(size_t)S->sn_level[(size_t)s]]++] = s;
     }
     // ---- children lists and relative maps (child update rows -> parent front index)
     S->child_ptr.assign((size_t)ns + 1, 0);
     for (int32_t s = 0; s < ns; ++s)
         if (S->sn_parent[(size_t)s] >= 0) S->child_ptr[(size_t)S->sn_parent[(size_t)s] + 1]++;
     for (int32_t s = 0; s < ns; ++s) S->child_ptr[(size_t)s + 1] += S->child_ptr[(size_t)s];
-    S->child_list.assign((size_t)S->child_ptr[(size_t)ns], 0);
+    S->child_list.resize((size_t)S->child_ptr[(size_t)ns]);
     {
-        std::vector<int64_t> cur(S->child_ptr.begin(), S->child_ptr.end() - 1);
+        rowbuf.resize((size_t)ns);
+        for (int32_t s = 0; s < ns; ++s) rowbuf[(size_t)s] = (int32_t)S->child_ptr[(size_t)s];
         for (int32_t s = 0; s < ns; ++s)
-            if (S->sn_parent[(size_t)s] >= 0) S->child_list[(size_t)cur[(size_t)S->sn_parent[(size_t)s]]++] = s;
+            if (S->sn_parent[(size_t)s] >= 0) S->child_list[(size_t)rowbuf[(size_t)S->sn_parent[(size_t)s]]++] = s;
     }
-    S->relmap.assign(S->sn_rows.size(), 0);
-    for (int32_t s = 0; s < ns; ++s) {
-        const int32_t p = S->sn_parent[(size_t)s];
-        if (p < 0) continue;
+    // relmap: a parent's front row index by position (mark holds it while its children are mapped)
+    S->relmap.resize(S->sn_rows.size());
+    for (int32_t p = 0; p < ns; ++p) {
+        if (S->child_ptr[(size_t)p + 1] == S->child_ptr[(size_t)p]) continue;
         const int32_t pc0 = sn_first[(size_t)p], pk = sn_first[(size_t)p + 1] - pc0;
-        const int32_t* prow = S->sn_rows.data() + S->sn_rows_ptr[(size_t)p];
-        const int64_t pr = S->sn_rows_ptr[(size_t)p + 1] - S->sn_rows_ptr[(size_t)p];
-        for (int64_t t = S->sn_rows_ptr[(size_t)s]; t < S->sn_rows_ptr[(size_t)s + 1]; ++t) {
-            const int32_t row = S->sn_rows[(size_t)t];
-            int32_t li;
-            if (row < pc0 + pk) {
-                li = row - pc0;
-                if (li < 0) return -2;   // child rows must lie in the parent's front
-            } else {
-                const int32_t* it = std::lower_bound(prow, prow + pr, row);
-                if (it == prow + pr || *it != row) return -2;
-                li = pk + (int32_t)(it - prow);
+        for (int32_t c = 0; c < pk; ++c) mark[(size_t)(pc0 + c)] = c;
+        for (int64_t t = S->sn_rows_ptr[(size_t)p]; t < S->sn_rows_ptr[(size_t)p + 1]; ++t)
+            mark[(size_t)S->sn_rows[(size_t)t]] = pk + (int32_t)(t - S->sn_rows_ptr[(size_t)p]);
+        for (int64_t ci = S->child_ptr[(size_t)p]; ci < S->child_ptr[(size_t)p + 1]; ++ci) {
+            const int32_t s = S->child_list[(size_t)ci];
+            for (int64_t t = S->sn_rows_ptr[(size_t)s]; t < S->sn_rows_ptr[(size_t)s + 1]; ++t) {
+                const int32_t row = S->sn_rows[(size_t)t];
+                // child rows must lie in the parent's front (its columns or its rows)
+                const bool in = (row >= pc0 && row < pc0 + pk) ||
+                                std::binary_search(S->sn_rows.begin() + S->sn_rows_ptr[(size_t)p],
+                                                   S->sn_rows.begin() + S->sn_rows_ptr[(size_t)p + 1], row);
+                if (!in) return -2;
+                S->relmap[(size_t)t] = mark[(size_t)row];
             }
-            S->relmap[(size_t)t] = li;
         }
     }
     // ---- front offsets (doubles), stats
@@ -332,19 +357,24 @@ int64_t dpg_incsym_add_edge(dpg_chol_incsym* I, int32_t a, int32_t b) {
 }
 
 int dpg_incsym_derive(const dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S) {
-    const int64_t n = I->n;
-    std::vector<std::vector<int32_t>> pat((size_t)n);
+    const int64_t n = I->n, nw = (n + 63) / 64;
+    thread_local std::vector<int64_t> cp;
+    thread_local std::vector<int32_t> rows;
+    cp.resize((size_t)n + 1);
+    rows.clear();
+    rows.reserve((size_t)I->nnz);
+    cp[0] = 0;
     for (int64_t p = 0; p < n; ++p) {
         const uint64_t* row = &I->bits[(size_t)(p * I->words)];
-        auto& v = pat[(size_t)p];
-        for (int64_t w = (p + 1) / 64; w < I->words; ++w) {
+        for (int64_t w = (p + 1) / 64; w < nw; ++w) {
             uint64_t m = row[w];
             while (m) {
                 const int t = __builtin_ctzll(m);
                 m &= m - 1;
-                v.push_back((int32_t)(w * 64 + t));
+                rows.push_back((int32_t)(w * 64 + t));
             }
         }
+        cp[(size_t)p + 1] = (int64_t)rows.size();
     }
-    return dpg_chol_sym_from_patterns(n, I->perm, pat, opts, S);
+    return dpg_chol_sym_from_csr(n, I->perm.data(), cp.data(), rows.data(), opts, S);
 }

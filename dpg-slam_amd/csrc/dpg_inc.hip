@@ -133,6 +133,7 @@ struct dpg_inc {
     int32_t* cnt = nullptr;                    // relinearized variables of the last update
     size_t c_theta = 0, c_est = 0, c_maxd = 0;
     std::vector<dpg_factor> h_dev_factors;     // staging (Q1 scaling)
+    double prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // last update: incsym, derive, lists, chol host, chol upload
 };
 
 namespace {
@@ -197,7 +198,11 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
         return DPG_ERR_HIP;
     // the host vectors above must outlive the async copies
     if (hipStreamSynchronize(s) != hipSuccess) return DPG_ERR_HIP;
-    return dpg_chol_create_sym(&g.chol, n, q->plo.data(), q->phi.data(), P, &q->S);
+    const double t = now_ms();
+    const int rc2 = dpg_chol_create_sym(&g.chol, n, q->plo.data(), q->phi.data(), P, &q->S);
+    q->prof[3] = now_ms() - t;
+    if (!rc2) dpg_chol_build_times(g.chol, q->prof + 4);
+    return rc2;
 }
 
 int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
@@ -261,6 +266,14 @@ void dpg_inc_destroy(dpg_inc* q) {
 }
 
 int64_t dpg_inc_num_nodes(const dpg_inc* q) { return q ? q->V : -1; }
+
+// diagnostics: host-time breakdown (ms) of the last update's symbolic phase -- incremental
+// symbolic state, derived structures, contribution lists + factor upload, GPU solver structures
+int dpg_inc_last_profile(const dpg_inc* q, double* out, int n) {
+    if (!q || !out) return DPG_ERR_ARG;
+    for (int k = 0; k < n && k < 8; ++k) out[k] = q->prof[k];
+    return DPG_OK;
+}
 dpg_ctx* dpg_inc_ctx(dpg_inc* q) { return q ? q->ctx : nullptr; }
 
 int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_factor* factors, int64_t n_factors,
@@ -337,10 +350,15 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         q->nnz_at_order = q->I.nnz;
         q->reorders += 1;
     }
+    const double t1a = now_ms();
     if (dpg_incsym_derive(&q->I, &q->opts, &q->S))
         return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: symbolic derivation failed");
+    const double t1b = now_ms();
     if ((rc = inc_rebuild(q, s))) return set_err(rc, "dpg_inc_update: solver rebuild failed");
     const double t2 = now_ms();
+    q->prof[0] = t1a - t1;
+    q->prof[1] = t1b - t1a;
+    q->prof[2] = t2 - t1b - q->prof[3];
     dpg_inc_stats S;
     memset(&S, 0, sizeof(S));
     S.reordered = reordered ? 1 : 0;

@@ -134,19 +134,24 @@ typedef struct {
     int64_t v0, v1;
 } scan_job;
 
-static void scan_one(const scan_job* J, int64_t v) {
+/* segs: the segments that can be hit within range_max of (ox, oy) -- a segment farther away gives
+   a hit beyond range_max, which reads range_max like no hit at all, so the scan is unchanged */
+static void scan_one(const scan_job* J, int64_t v, int32_t* near) {
     rng_t r = {J->seed ^ (0xD1B54A32D192ED03ull * (uint64_t)(v + 1))};
     const double* gt = J->gt;
     const double c = cos(gt[3 * v + 2]), s = sin(gt[3 * v + 2]);
     const double ox = gt[3 * v] + c * J->lx - s * J->ly, oy = gt[3 * v + 1] + s * J->lx + c * J->ly;
+    int64_t nn = 0;
+    for (int64_t k = 0; k < J->ns; ++k)
+        if (seg_dist(ox, oy, J->segs + 4 * k) <= (double)J->rmax + 1e-3) near[nn++] = (int32_t)k;
     const double base = gt[3 * v + 2] + J->lth;
     const double inc = ((double)J->amax - (double)J->amin) / (double)(J->nb - 1);
     for (int32_t b = 0; b < J->nb; ++b) {
         const double a = base + (double)J->amin + inc * (double)b;
         const double dx = cos(a), dy = sin(a);
         double best = 1e30;
-        for (int64_t k = 0; k < J->ns; ++k) {
-            const float* g = J->segs + 4 * k;
+        for (int64_t q = 0; q < nn; ++q) {
+            const float* g = J->segs + 4 * (int64_t)near[q];
             const double ex = (double)g[2] - g[0], ey = (double)g[3] - g[1];
             const double den = dx * ey - dy * ex;
             if (fabs(den) < 1e-12) continue;
@@ -165,7 +170,10 @@ static void scan_one(const scan_job* J, int64_t v) {
 
 static void* scan_worker(void* arg) {
     const scan_job* J = (const scan_job*)arg;
-    for (int64_t v = J->v0; v < J->v1; ++v) scan_one(J, v);
+    int32_t* near = (int32_t*)malloc(sizeof(int32_t) * (size_t)(J->ns > 0 ? J->ns : 1));
+    if (!near) return NULL;
+    for (int64_t v = J->v0; v < J->v1; ++v) scan_one(J, v, near);
+    free(near);
     return NULL;
 }
 

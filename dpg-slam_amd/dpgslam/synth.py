@@ -218,7 +218,11 @@ def _box_segs(b) -> list:
 
 def make_dynamic(n_passes: int = 4, nodes_per_pass: int = 2500, n_beams: int = 5000, seed: int = 5,
                  world_size: float = 40.0, range_max: float = RANGE_MAX, n_boxes: int = 24,
-                 range_noise: float = 0.01, threads: int = 0) -> DynamicWorkload:
+                 range_noise: float = 0.01, threads: int = 0, fov_deg: float = 360.0,
+                 p_add: float | None = None, p_remove: float | None = None) -> DynamicWorkload:
+    """fov_deg: scan span centred on the laser's heading (360: ANGLE_MIN..ANGLE_MAX).  Box dynamics:
+    by default each later pass flips about a third of the boxes in or out; with p_add / p_remove an
+    absent box appears with probability p_add and a present one disappears with p_remove."""
     L = lib()
     segs = np.zeros((4096, 4), np.float32)
     ns = L.dpg_synth_world(seed, world_size, ptr(segs, C.c_float), len(segs))
@@ -233,11 +237,19 @@ def make_dynamic(n_passes: int = 4, nodes_per_pass: int = 2500, n_beams: int = 5
     present = np.zeros((n_passes, n_boxes), bool)
     present[0] = rng.random(n_boxes) < 0.5
     for p in range(1, n_passes):   # each later pass moves about a third of the boxes in or out
-        flip = rng.random(n_boxes) < 0.33
+        if p_add is None and p_remove is None:
+            flip = rng.random(n_boxes) < 0.33
+        else:
+            u = rng.random(n_boxes)
+            flip = np.where(present[p - 1], u < (p_remove or 0.0), u < (p_add or 0.0))
         present[p] = present[p - 1] ^ flip
     all_segs = np.ascontiguousarray(np.concatenate([static, np.asarray(sum((_box_segs(b) for b in boxes), []),
                                                                        np.float32)]), np.float32)
     threads = threads or min(16, os.cpu_count() or 1)
+    if fov_deg >= 360.0:
+        amin, amax = ANGLE_MIN, ANGLE_MAX
+    else:
+        amin, amax = -math.radians(fov_deg) / 2.0, math.radians(fov_deg) / 2.0
     gts, rs = [], []
     for p in range(n_passes):
         gt = np.zeros((nodes_per_pass, 3), np.float64)
@@ -247,12 +259,12 @@ def make_dynamic(n_passes: int = 4, nodes_per_pass: int = 2500, n_beams: int = 5
         world = np.ascontiguousarray(np.concatenate([static, np.asarray(bs, np.float32).reshape(-1, 4)]), np.float32)
         r = np.zeros((nodes_per_pass, n_beams), np.float32)
         _abi.check(L.dpg_synth_scans(ptr(gt, C.c_double), nodes_per_pass, ptr(world, C.c_float), len(world), n_beams,
-                                     ANGLE_MIN, ANGLE_MAX, range_max, LASER[0], LASER[1], LASER[2], range_noise,
+                                     amin, amax, range_max, LASER[0], LASER[1], LASER[2], range_noise,
                                      seed * 7919 + 17 * p + 1, threads, ptr(r, C.c_float)), "dpg_synth_scans")
         gts.append(gt)
         rs.append(r)
     V = n_passes * nodes_per_pass
-    geom = np.tile(np.array([ANGLE_MIN, ANGLE_MAX, range_max], np.float32), (V, 1))
+    geom = np.tile(np.array([amin, amax, range_max], np.float32), (V, 1))
     return DynamicWorkload(ranges=np.concatenate(rs), geom=geom, est=np.concatenate(gts).astype(np.float32),
                            pass_of=np.repeat(np.arange(n_passes, dtype=np.int32), nodes_per_pass),
                            pass_start=np.arange(n_passes + 1, dtype=np.int64) * nodes_per_pass,
