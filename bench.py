@@ -210,6 +210,324 @@ def main_incremental(args):
     print(json.dumps(line), flush=True)
 
 
+DPG_BUCKETS = ((0, 1), (1, 10), (10, 50), (50, 1 << 30))
+
+
+def main_dynamic(args):
+    """--workload dynamic: BASELINE config 5 ("10k-node graph with DPG node removal +
+    re-linearisation sweep") run through DpgSLAM (dpgslam/slam.py on the GPU backend): 4 passes x
+    2500 nodes of a patrol route (synth.make_patrol: 5000-beam 270-degree 30 m scans, noisy
+    odometry), ObserveOdometry + ObserveLaser per reading -> per node dpg_add_node (batched ICP of
+    the successive + loop-closure alignments, one incremental ISAM2-semantics update) and, from
+    pass 1 on, executeDPG (dpg_slam.cc:122-140,865-886); incrementPassNumber -> reoptimize sweep
+    at every pass boundary (:25-120), and one more sweep over all 10 000 nodes at the end.
+    Reported: nodes/s of the whole run, executeDPG calls/s split by submap-candidate count, the
+    sweep times, per-node latency, the map's active-node fraction per pass and the pose error
+    against ground truth.  CPU baseline: the oracle replays a fixed sample of the same executeDPG
+    calls from the GPU's state before each call (and must reproduce the GPU's counters and state
+    exactly), and times the ICP of a sample of the final sweep's edges + the final sweep's solve."""
+    import hashlib
+
+    from dpgslam import _abi, api, synth
+    from dpgslam.slam import DpgSLAM
+
+    t0 = time.time()
+    w = synth.make_patrol(n_passes=args.passes, steps=args.steps_per_pass)
+    log(f"generated config5 patrol workload: {w.n_passes} x {w.steps} readings in {time.time() - t0:.1f}s")
+    P, N = w.n_passes, w.steps
+    sample_k = sorted({0, 1, 2, 3, 50, 500, 1000, 1500, 2000, N - 1} & set(range(N)))
+    do_cpu = args.cpu_dpg_calls > 0
+    ctx = api.Context(0)
+    cp = _abi.default_change_params()
+    for kv in args.dpg_param:
+        k, v = kv.split("=")
+        setattr(cp, k, type(getattr(cp, k))(float(v)) if not isinstance(getattr(cp, k), int) else int(v))
+    slam = DpgSLAM(backend="gpu", ctx=ctx, change_params=cp)
+    orc, cpu_calls, mismatches = None, [], 0
+    if do_cpu:
+        from oracle import oracle as O
+    node_ms, add_icp_ms, add_upd_ms, dpg = [], [], [], []
+    sweeps, active_end, replay_s, pass_tot = [], [], 0.0, {}
+    amin, amax, rmax = (float(x) for x in w.geom[0])
+    t_run = time.perf_counter()
+    for p in range(P):
+        if p:
+            ts = time.perf_counter()
+            slam.incrementPassNumber()
+            sweeps.append({"before_pass": p, "nodes": len(slam.poses), "factors": int(slam.n_factors),
+                           "ms": (time.perf_counter() - ts) * 1e3})
+            log(f"pass {p}: sweep over {len(slam.poses)} nodes in {sweeps[-1]['ms']:.0f} ms")
+        for k in range(N):
+            o = w.odom[p, k]
+            rg = w.ranges[p * N + k]
+            V0 = len(slam.poses)
+            snap = None
+            if do_cpu and p >= 1 and k in sample_k and len(cpu_calls) < args.cpu_dpg_calls and slam._store is not None:
+                tr = time.perf_counter()
+                st_ = slam._dpg_store()
+                snap = st_.fetch()
+                replay_s += time.perf_counter() - tr
+            ts = time.perf_counter()
+            slam.ObserveOdometry(o[:2], o[2])
+            slam.ObserveLaser(rg, 0.0, rmax, amin, amax)
+            dt = (time.perf_counter() - ts) * 1e3
+            if len(slam.poses) == V0:
+                continue
+            node_ms.append(dt)
+            la = slam.be.last_add
+            add_icp_ms.append(la.ms_icp)
+            add_upd_ms.append(la.update.ms_total)
+            if p >= 1 and slam.last_dpg is not None:
+                d = slam.last_dpg
+                dpg.append((int(d.n_candidates), float(d.ms_total), int(d.n_submap_nodes)))
+                for key in ("n_removed", "n_added", "n_committed", "n_sectors_deactivated", "n_nodes_deactivated"):
+                    pass_tot.setdefault(p, {}).setdefault(key, 0)
+                    pass_tot[p][key] += int(getattr(d, key))
+            if snap is not None:
+                # replay this call on the oracle from the GPU's state before it
+                tr = time.perf_counter()
+                V1 = len(slam.poses)
+                if orc is None:
+                    orc = O.OracleDpgStore(np.stack(slam.ranges), np.asarray(slam.geom, np.float32), params=cp)
+                elif orc.V < V1:
+                    orc.append(np.stack(slam.ranges[orc.V:]), np.asarray(slam.geom[orc.V:], np.float32))
+                lab0, sec0, act0 = orc.fetch()   # node V1-1 (the new one) in its initial state
+                lab0[:len(snap[0])] = snap[0]
+                sec0[:len(snap[1])] = snap[1]
+                act0[:len(snap[2])] = snap[2]
+                orc.load(lab0, sec0, act0)
+                tc = time.perf_counter()
+                so = orc.execute_dpg(V1, len(slam.current_pass), slam.poses)
+                c_ms = (time.perf_counter() - tc) * 1e3
+                go = slam._store.fetch()
+                oo = orc.fetch()
+                same = so.counters() == slam.last_dpg.counters() and all(
+                    hashlib.sha1(a.tobytes()).digest() == hashlib.sha1(b.tobytes()).digest() for a, b in zip(go, oo))
+                mismatches += 0 if same else 1
+                cpu_calls.append((int(slam.last_dpg.n_candidates), c_ms, same))
+                replay_s += time.perf_counter() - tr
+            if len(node_ms) % 500 == 0:
+                log(f"pass {p} node {len(slam.poses)}: node {node_ms[-1]:.1f} ms, dpg {dpg[-1][1] if dpg else 0:.2f} ms "
+                    f"({dpg[-1][0] if dpg else 0} candidates)")
+        if p >= 1:
+            _, _, act = slam._store.fetch()
+            active_end.append({"pass": p, "active_fraction": float(act.mean()),
+                               "past_active_fraction": float(act[:int(np.sum(slam.node_pass < p))].mean()),
+                               **pass_tot.get(p, {})})
+    # the sweep at 10k nodes (incrementPassNumber after the last pass)
+    est_final = slam.poses.copy()
+    ts = time.perf_counter()
+    slam.reoptimize()
+    sweeps.append({"before_pass": P, "nodes": len(slam.poses), "factors": int(slam.n_factors),
+                   "ms": (time.perf_counter() - ts) * 1e3})
+    wall = time.perf_counter() - t_run - replay_s
+    V = len(slam.poses)
+    # pose error against ground truth (map frame = pass 0's start)
+    gtm = w.gt_map().reshape(-1, 3)
+    created = np.asarray(slam.node_pass)
+    err = None
+    if V == P * N:
+        e = slam.poses[:, :2].astype(np.float64) - gtm[:, :2]
+        err = {"rms_m": float(np.sqrt((e ** 2).sum(1).mean())), "max_m": float(np.sqrt((e ** 2).sum(1)).max())}
+        # what the change detection sees: each later-pass node against the nearest pass-0 node (by
+        # ground truth), relative pose estimated vs true
+        from scipy.spatial import cKDTree
+        n0 = int(np.sum(created == 0))
+        _, jn = cKDTree(gtm[:n0, :2]).query(gtm[n0:, :2])
+        rel_e = synth._relative(slam.poses[n0:].astype(np.float64), slam.poses[jn].astype(np.float64))
+        rel_t = synth._relative(gtm[n0:], gtm[jn])
+        dd = rel_e - rel_t
+        err["cross_pass_rel_rms_m"] = float(np.sqrt((dd[:, :2] ** 2).sum(1).mean()))
+        err["cross_pass_rel_rms_rad"] = float(np.sqrt((np.arctan2(np.sin(dd[:, 2]), np.cos(dd[:, 2])) ** 2).mean()))
+    dpg_a = np.asarray(dpg, np.float64).reshape(-1, 3)
+    buckets = []
+    for lo, hi in DPG_BUCKETS:
+        m = (dpg_a[:, 0] >= lo) & (dpg_a[:, 0] < hi)
+        if m.any():
+            ms = float(dpg_a[m, 1].mean())
+            bk = {"candidates": f"[{lo},{hi if hi < 1 << 30 else 'inf'})", "calls": int(m.sum()), "ms_per_call": ms,
+                  "calls_per_s": 1e3 / ms}
+            cm = [c for c in cpu_calls if lo <= c[0] < hi]
+            if cm:
+                bk["cpu_ms_per_call"] = float(np.mean([c[1] for c in cm]))
+                bk["cpu_calls"] = len(cm)
+            buckets.append(bk)
+    line = {
+        "metric": "config5 DpgSLAM run: nodes/s (per-node ICP + incremental solve + executeDPG, sweeps at pass "
+                  "boundaries); executeDPG calls/s by candidate count; sweep ms",
+        "value": V / wall, "unit": "nodes/s", "higher_is_better": True, "n_gpus": 1,
+        "config": {"workload": f"config5: {P} passes x {N} readings of a serpentine patrol route through a "
+                               f"16x16-room building (5000-beam 270-degree 30 m scans, 2 mm range noise, 64 movable "
+                               f"boxes), DpgSLAM defaults", "nodes": V},
+        "data": "synthetic (seeded ray-cast building, boxes added/removed between passes, noisy odometry)",
+        "wall_s": wall, "nodes_per_pass": [int(np.sum(created == q)) for q in range(P)],
+        "node_ms": {"p50": float(np.median(node_ms)), "p90": float(np.percentile(node_ms, 90)),
+                    "mean": float(np.mean(node_ms)), "icp_mean": float(np.mean(add_icp_ms)),
+                    "update_mean": float(np.mean(add_upd_ms))},
+        "dpg": {"calls": len(dpg_a), "ms_per_call": float(dpg_a[:, 1].mean()) if len(dpg_a) else None,
+                "calls_per_s": float(1e3 / dpg_a[:, 1].mean()) if len(dpg_a) else None,
+                "candidates_mean": float(dpg_a[:, 0].mean()) if len(dpg_a) else None,
+                "submap_nodes_mean": float(dpg_a[:, 2].mean()) if len(dpg_a) else None, "by_candidates": buckets},
+        "sweeps": sweeps, "active": active_end, "pose_error_vs_gt": err,
+    }
+    if do_cpu:
+        sp = api.Context  # noqa: F841 (keeps the import order explicit)
+        cb = {"value": float(1e3 / np.mean([c[1] for c in cpu_calls])) if cpu_calls else None,
+              "unit": "executeDPG calls/s", "cores": 1, "kind": "port",
+              "sample": f"oracle (C++ restatement, 1 thread) replaying {len(cpu_calls)} of the run's executeDPG calls "
+                        f"(readings {sample_k} of passes 1..{P - 1}) from the GPU's state before each call; "
+                        f"{len(cpu_calls) - mismatches} of {len(cpu_calls)} reproduce the GPU's counters and state "
+                        f"bit for bit",
+              "replay_bit_exact": mismatches == 0}
+        # the final sweep's ICP (a sample of its edges) and its solve on the oracle
+        lc = ctx.loop_closure_candidates(est_final, slam.node_pass, 5.0, 2.0)
+        rng = np.random.default_rng(0)
+        sel = lc[np.sort(rng.choice(len(lc), min(args.cpu_sample, len(lc)), replace=False))] if len(lc) else lc
+        pts, offs = slam._clouds()
+        p_icp = _abi.default_icp_params()
+        t, _ = _median_time(lambda: O.icp_batch(pts, offs, sel, est_final, p_icp, O.NN_GRID, 1), 3)
+        og = O.OracleIncGraph()
+        tg = time.perf_counter()
+        og.update(est_final.astype(np.float64), slam.factors)
+        cb["sweep_icp_edges_per_s"] = len(sel) / t
+        cb["sweep_solve_ms"] = (time.perf_counter() - tg) * 1e3
+        cb["sweep_sample"] = (f"oracle ICP (grid NN, 1 thread) on {len(sel)} random loop-closure edges of the final "
+                              f"sweep, median of 3; oracle solve of the final sweep's graph ({len(slam.factors)} factors)")
+        line["cpu_baseline"] = cb
+    print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def main_dpg(args):
+    """--workload dpg: executeDPG (dpg_slam.cc:865-886) at config-5 scale on a map that does not
+    collapse: 4 passes x 2500 nodes of a 64 m building (make_dynamic: 5000-beam 270-degree 30 m
+    noise-free scans, 48 movable boxes flipping between passes), every pass starting at the same
+    pose, node poses = ground truth, executeDPG after every node of passes 1..3 in order.  (With
+    estimated poses or range noise the reference's rules deactivate nearly every past node within
+    a pass -- see the dynamic workload and DESIGN.md; here 40-90 % stay active.)  Reported: calls/s
+    overall and split by submap-candidate count, per pass.  CPU baseline: after the timed run the
+    sequence is replayed on the GPU and, before a stratified sample of calls (spread over the
+    candidate buckets), the oracle takes over from the GPU's state, times the call and must
+    reproduce the GPU's counters and state bit for bit."""
+    import hashlib
+
+    from dpgslam import api, synth
+
+    t0 = time.time()
+    w = synth.make_dynamic(n_passes=args.passes, nodes_per_pass=args.steps_per_pass, world_size=64.0, fov_deg=270.0,
+                           n_boxes=48, range_noise=0.0)
+    log(f"generated the DPG workload: {w.V} nodes in {time.time() - t0:.1f}s")
+    ctx = api.Context(0)
+    calls = list(range(int(w.pass_start[1]), w.V))
+
+    def run(g, on_call=None):
+        out = []
+        for q, v in enumerate(calls):
+            p = int(w.pass_of[v])
+            if on_call is not None:
+                on_call(q, v, g)
+            st = g.execute_dpg(v + 1, int(v - w.pass_start[p] + 1), w.est[:v + 1])
+            out.append((int(st.n_candidates), float(st.ms_total), int(st.n_submap_nodes), p, st.counters()))
+            if q % 1000 == 999:
+                log(f"call {q + 1}/{len(calls)}: {st.ms_total:.2f} ms, {st.n_candidates} candidates")
+        return out
+
+    g = api.DpgStore(ctx, w.ranges, w.geom)
+    run(g)                       # warm-up pass over the whole sequence on a throw-away store
+    g.close()
+    g = api.DpgStore(ctx, w.ranges, w.geom)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    rec = run(g)
+    wall = time.perf_counter() - t1
+    _, _, act = g.fetch()
+    g.close()
+    cand = np.asarray([r[0] for r in rec])
+    ms = np.asarray([r[1] for r in rec])
+    passes = np.asarray([r[3] for r in rec])
+    buckets = []
+    for lo, hi in DPG_BUCKETS:
+        m = (cand >= lo) & (cand < hi)
+        if m.any():
+            buckets.append({"candidates": f"[{lo},{hi if hi < 1 << 30 else 'inf'})", "calls": int(m.sum()),
+                            "ms_per_call": float(ms[m].mean()), "calls_per_s": float(1e3 / ms[m].mean())})
+    per_pass = []
+    for p in range(1, args.passes):
+        m = passes == p
+        last = int(w.pass_start[p + 1]) if p + 1 < len(w.pass_start) else w.V
+        per_pass.append({"pass": p, "calls": int(m.sum()), "calls_per_s": float(1e3 / ms[m].mean()),
+                         "candidates_mean": float(cand[m].mean()), "calls_ge50": float((cand[m] >= 50).mean())})
+    line = {
+        "metric": "executeDPG calls/s at config-5 scale (10k-node 4-pass dynamic map), split by submap-candidate count",
+        "value": len(calls) / wall, "unit": "calls/s", "higher_is_better": True, "n_gpus": 1,
+        "ms_per_call": 1e3 * wall / len(calls), "calls": len(calls),
+        "config": {"workload": f"config5 DPG: {args.passes} passes x {args.steps_per_pass} nodes, 64 m building, "
+                               f"5000-beam 270-degree 30 m noise-free scans, 48 movable boxes, ground-truth poses, "
+                               f"executeDPG after every node of passes 1..{args.passes - 1}", "nodes": int(w.V)},
+        "data": "synthetic (seeded ray-cast building, boxes added/removed between passes)",
+        "by_candidates": buckets, "per_pass": per_pass,
+        "past_active_fraction_end": float(act[:int(w.pass_start[args.passes - 1])].mean()),
+    }
+    if args.cpu_dpg_calls > 0:
+        from oracle import oracle as O
+        rng = np.random.default_rng(1)
+        pick = set()
+        per_b = max(1, args.cpu_dpg_calls // len(DPG_BUCKETS))
+        for lo, hi in DPG_BUCKETS:
+            idx = np.nonzero((cand >= lo) & (cand < hi))[0]
+            if len(idx):
+                pick.update(int(i) for i in rng.choice(idx, min(per_b, len(idx)), replace=False))
+        orc = O.OracleDpgStore(w.ranges, w.geom)
+        res = []
+
+        def replay(q, v, gs):
+            if q not in pick:
+                return
+            snap = gs.fetch()
+            orc.load(*snap)
+            p = int(w.pass_of[v])
+            tc = time.perf_counter()
+            so = orc.execute_dpg(v + 1, int(v - w.pass_start[p] + 1), w.est[:v + 1])
+            c_ms = (time.perf_counter() - tc) * 1e3
+            res.append((q, int(so.n_candidates), c_ms, so.counters(), orc.fetch()))
+
+        g = api.DpgStore(ctx, w.ranges, w.geom)
+        posts = {}
+
+        def hook(q, v, gs):
+            if q - 1 in pick:   # the GPU's state after the picked call
+                posts[q - 1] = [hashlib.sha1(a.tobytes()).digest() for a in gs.fetch()]
+            replay(q, v, gs)
+
+        rec2 = run(g, hook)
+        last = len(calls) - 1
+        if last in pick:
+            posts[last] = [hashlib.sha1(a.tobytes()).digest() for a in g.fetch()]
+        g.close()
+        ok = 0
+        for q, nc, c_ms, cnt, st in res:
+            same = cnt == rec2[q][4] and [hashlib.sha1(a.tobytes()).digest() for a in st] == posts.get(q)
+            ok += int(same)
+        cb_b = []
+        for lo, hi in DPG_BUCKETS:
+            sel = [r for r in res if lo <= r[1] < hi]
+            if sel:
+                cb_b.append({"candidates": f"[{lo},{hi if hi < 1 << 30 else 'inf'})", "calls": len(sel),
+                             "cpu_ms_per_call": float(np.mean([r[2] for r in sel]))})
+        # the CPU rate of the whole sequence, weighting each bucket's mean by its share of the calls
+        tot = sum(b["calls"] for b in buckets)
+        cpu_ms = sum(b["calls"] / tot * next(c["cpu_ms_per_call"] for c in cb_b if c["candidates"] == b["candidates"])
+                     for b in buckets if any(c["candidates"] == b["candidates"] for c in cb_b))
+        line["cpu_baseline"] = {"value": 1e3 / cpu_ms if cpu_ms else None, "unit": "calls/s", "cores": 1, "kind": "port",
+                                "sample": f"oracle (C++ restatement, 1 thread) taking over from the GPU's state before "
+                                          f"{len(res)} calls stratified over the candidate buckets; bucket means "
+                                          f"weighted by the run's call mix; {ok} of {len(res)} reproduce the GPU's "
+                                          f"counters and state bit for bit",
+                                "by_candidates": cb_b, "replay_bit_exact": ok == len(res)}
+    print(json.dumps(line), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,15 +541,25 @@ def main():
                          "the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--icp-variant", default="angular", choices=["angular", "kdtree", "grid"],
                     help="nearest-neighbour machinery of the ICP kernel (results are identical)")
-    ap.add_argument("--workload", default="batch", choices=["batch", "incremental"],
+    ap.add_argument("--workload", default="batch", choices=["batch", "incremental", "dynamic", "dpg"],
                     help="batch: the headline step (all edges + GN); incremental: per-node latency of "
-                         "dpg_add_node_pairs at V = 5000 (1 GPU)")
+                         "dpg_add_node_pairs at V = 5000 (1 GPU); dynamic: config 5 through DpgSLAM (1 GPU); dpg: executeDPG at config-5 "
+                         "scale on a map that does not collapse (1 GPU)")
+    ap.add_argument("--passes", type=int, default=4)
+    ap.add_argument("--steps-per-pass", type=int, default=2500)
+    ap.add_argument("--cpu-dpg-calls", type=int, default=30, help="executeDPG calls replayed on the oracle")
+    ap.add_argument("--dpg-param", action="append", default=[],
+                    help="DpgParameters override, e.g. occ_grid_resolution=0.1 or num_sectors=8 (repeatable)")
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
     ap.add_argument("--inc-nodes", type=int, default=5000)
     ap.add_argument("--cpu-nodes", type=int, default=8, help="nodes in the incremental CPU-baseline sample")
     args = ap.parse_args()
     if args.workload == "incremental":
         return main_incremental(args)
+    if args.workload == "dynamic":
+        return main_dynamic(args)
+    if args.workload == "dpg":
+        return main_dpg(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -13,6 +13,7 @@ batched runIcp calls of reoptimize (dpg_slam.cc:85-106)  Context.upload_scans / 
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -143,9 +144,14 @@ class Context:
         self.device = device
         self.n_edges = 0
         self.V = 0
+        self._children = weakref.WeakSet()   # DpgStore / IncGraph objects living on this context
 
     def close(self):
+        """Destroys the context; the DPG stores and incremental graphs created on it are closed
+        first (their device state belongs to the context)."""
         if self.handle:
+            for ch in list(getattr(self, "_children", ())):
+                ch.close()
             lib().dpg_ctx_destroy(self.handle)
             self.handle = None
 
@@ -372,6 +378,7 @@ class DpgStore:
                                            ptr(g, C.c_float), C.byref(self.params))
         if not self.handle:
             raise _abi.DpgError("dpg_dpg_create failed: " + (lib().dpg_last_error() or b"").decode())
+        ctx._children.add(self)
 
     def close(self):
         if getattr(self, "handle", None):
@@ -455,6 +462,7 @@ class IncGraph:
         self.handle = lib().dpg_inc_create(ctx.handle, C.byref(p))
         if not self.handle:
             raise _abi.DpgError("dpg_inc_create failed: " + (lib().dpg_last_error() or b"").decode())
+        ctx._children.add(self)
 
     def close(self):
         if getattr(self, "handle", None):

@@ -46,14 +46,23 @@ class GpuBackend:
     def __init__(self, ctx: api.Context, inc_mode: str = "isam2"):
         self.ctx = ctx
         self.inc = api.IncGraph(ctx, mode=inc_mode)
+        self.stored = 0        # nodes in the context's scan store (dpg_add_node appends each node's cloud)
+        self.last_add = None   # AddNodeStats of the last node
 
     def add_node(self, cloud, passes, init_pose, extra, icp_params, reopt_params, non_successive):
         st = self.inc.add_node(cloud, passes, init_pose, extra, icp_params, reopt_params, non_successive)
+        self.stored += 1
+        self.last_add = st
         n_icp = (1 if len(passes) > 1 else 0) + int(st.n_loop_closures)
         return n_icp, self.inc.poses()
 
-    def icp_batch(self, pts, offsets, edges, est, p):
-        self.ctx.upload_scans(pts, offsets, p.downsample_icp_points_ratio)
+    def icp_batch(self, clouds, edges, est, p):
+        """clouds() -> (pts, offsets) of every node; the store already holds them when every node
+        came through add_node."""
+        if self.stored != len(est):
+            pts, offsets = clouds()
+            self.ctx.upload_scans(pts, offsets, p.downsample_icp_points_ratio)
+            self.stored = len(est)
         res, _ = self.ctx.icp_batch(edges, est, p, compute_cov=False)
         return res
 
@@ -70,8 +79,11 @@ class GpuBackend:
     def store(self, ranges, geom, offsets, params):
         return api.DpgStore(self.ctx, ranges, geom, offsets=offsets, params=params)
 
-    def get_map(self, pts, offsets, est, fraction, ratio):
-        self.ctx.upload_scans(pts, offsets, ratio)
+    def get_map(self, clouds, est, fraction, ratio):
+        if self.stored != len(est):
+            pts, offsets = clouds()
+            self.ctx.upload_scans(pts, offsets, ratio)
+            self.stored = len(est)
         return self.ctx.get_map(est, fraction)
 
 
@@ -110,8 +122,8 @@ class DpgSLAM:
         self.cum_dist = f32(0.0)
         self.prev_odom = np.zeros(3, f32)               # prev_odom_loc_, prev_odom_angle_
         self.odom_at_last_align = np.zeros(3, f32)      # odom_{loc,angle}_at_last_laser_align_
-        self.poses: list[np.ndarray] = []               # dpg_nodes_ estimated positions (float32)
-        self.node_pass: list[int] = []
+        self.poses = np.zeros((0, 3), f32)               # dpg_nodes_ estimated positions (float32)
+        self.node_pass = np.zeros(0, np.int32)
         self.ranges: list[np.ndarray] = []
         self.geom: list[tuple] = []
         self.clouds: list[np.ndarray] = []
@@ -121,6 +133,7 @@ class DpgSLAM:
         self.n_factors = 0                              # graph_->size()
         self._store = None
         self._store_V = 0
+        self.last_dpg = None                            # dpg_change_stats of the last executeDPG
 
     # ------------------------------------------------------------------ public API
     def ObserveOdometry(self, odom_loc, odom_angle):
@@ -138,7 +151,7 @@ class DpgSLAM:
         if not self._update_pose_graph(np.asarray(ranges, f32), f32(range_max), f32(angle_min), f32(angle_max)):
             return
         if self.pass_number >= 1:
-            self.executeDPG()
+            self.last_dpg = self.executeDPG()
 
     def incrementPassNumber(self):
         """dpg_slam.cc:25-33."""
@@ -150,8 +163,8 @@ class DpgSLAM:
 
     def GetPose(self):
         """dpg_slam.cc:528-553: the last node's estimate plus the odometry not yet in the graph."""
-        loc = self.poses[-1][:2] if self.poses else np.zeros(2, f32)
-        ang = self.poses[-1][2] if self.poses else f32(0)
+        loc = self.poses[-1][:2] if len(self.poses) else np.zeros(2, f32)
+        ang = self.poses[-1][2] if len(self.poses) else f32(0)
         un = self.prev_odom[:2] - self.odom_at_last_align[:2]
         dth = _angle_mod(self.prev_odom[2] - self.odom_at_last_align[2])   # AngleDiff
         disp = api.transform_point(np.array([un[0], un[1], 0], f32), np.array([0, 0, -self.odom_at_last_align[2]], f32))
@@ -160,19 +173,17 @@ class DpgSLAM:
 
     def GetMap(self):
         """dpg_slam.cc:555-575."""
-        if not self.poses:
+        if not len(self.poses):
             return np.zeros((0, 2), f32)
-        pts, offs = self._clouds()
-        return self.be.get_map(pts, offs, np.stack(self.poses), self.fraction,
-                               self.icp_params.downsample_icp_points_ratio)
+        return self.be.get_map(self._clouds, self.poses, self.fraction, self.icp_params.downsample_icp_points_ratio)
 
     def GetActiveAndDynamicMapPoints(self):
         """getActiveAndDynamicMapPoints (dpg_slam.cc:832-863) over the current node state."""
-        return self._dpg_store().active_dynamic_points(len(self.poses), np.stack(self.poses))
+        return self._dpg_store().active_dynamic_points(len(self.poses), self.poses)
 
     def executeDPG(self):
         """dpg_slam.cc:865-886 (dpg_execute_dpg on the node store)."""
-        return self._dpg_store().execute_dpg(len(self.poses), len(self.current_pass), np.stack(self.poses))
+        return self._dpg_store().execute_dpg(len(self.poses), len(self.current_pass), self.poses)
 
     def reoptimize(self):
         """dpg_slam.cc:35-120: a fresh graph -- per node the pass prior or the odometry Between, the
@@ -182,15 +193,14 @@ class DpgSLAM:
         V = len(self.poses)
         if V == 0:
             return
-        est = np.stack(self.poses)
-        passes = np.asarray(self.node_pass, np.int32)
+        est = self.poses.copy()
+        passes = self.node_pass
         lc = self.be.candidates(est, passes, float(self.within), float(self.across))
         succ = np.stack([np.arange(V - 1), np.arange(1, V)], 1).astype(np.int32)
         edges = np.concatenate([succ, np.asarray(lc, np.int32).reshape(-1, 2)], 0)
         res = None
         if len(edges):
-            pts, offs = self._clouds()
-            res = self.be.icp_batch(pts, offs, edges, est, self.icp_params)
+            res = self.be.icp_batch(self._clouds, edges, est, self.icp_params)
         F, cur = [], None
         for i in range(V):
             if i == 0 or passes[i] != cur:
@@ -198,14 +208,24 @@ class DpgSLAM:
                 cur = passes[i]
             elif self.odometry_constraints:
                 F.append(self._odometry_factor(self.odom_only[i - 1], self.odom_only[i], i - 1, i))
-        for k, (a, b) in enumerate(edges):
-            ok = res["converged"][k] != 0 and res["status"][k] == _abi.DPG_ICP_OK
-            if k < len(succ) or ok:
-                F.append(_icp_factor(res[k:k + 1], int(a), int(b), self.icp_params))
+        if len(edges):
+            # addObservationConstraint per aligned pair (dpg_icp_factor, vectorised): the successive
+            # pairs always, a loop closure when its alignment converged (dpg_slam.cc:85-104)
+            keep = np.ones(len(edges), bool)
+            keep[len(succ):] = (res["converged"][len(succ):] != 0) & (res["status"][len(succ):] == _abi.DPG_ICP_OK)
+            Fi = np.zeros(int(keep.sum()), FACTOR_DTYPE)
+            Fi["kind"] = _abi.DPG_FACTOR_BETWEEN
+            Fi["i"], Fi["j"] = edges[keep, 0], edges[keep, 1]
+            Fi["z"] = res["z"][keep].astype(np.float64)
+            p = self.icp_params
+            Fi["info"] = [1.0 / float(f32(p.laser_x_variance)), 1.0 / float(f32(p.laser_y_variance)),
+                          1.0 / float(f32(p.laser_theta_variance))]
+            F.append(Fi)
+        F = np.concatenate([np.asarray(f, FACTOR_DTYPE).reshape(-1) for f in F])
         self.factors = F
         self.n_factors = len(F)
-        X = self.be.rebuild_graph(est.astype(np.float64), np.concatenate(F))
-        self.poses = [np.asarray(x, f32) for x in X]
+        X = self.be.rebuild_graph(est.astype(np.float64), F)
+        self.poses = np.asarray(X, f32).reshape(-1, 3)
 
     # ------------------------------------------------------------------ internals
     def _odometry_factor(self, prev, cur, i, j):
@@ -221,8 +241,8 @@ class DpgSLAM:
     def _create_node(self, ranges, range_max, angle_min, angle_max, pose):
         """createNode (dpg_slam.cc:488-513): the base_link cloud of the scan, MAX_RANGE dropped."""
         cloud = api.scan_to_cloud(ranges, angle_min, angle_max, range_max, self.laser)
-        self.poses.append(np.asarray(pose, f32).copy())
-        self.node_pass.append(self.pass_number)
+        self.poses = np.concatenate([self.poses, np.asarray(pose, f32).reshape(1, 3)])
+        self.node_pass = np.append(self.node_pass, np.int32(self.pass_number))
         self.ranges.append(ranges.copy())
         self.geom.append((angle_min, angle_max, range_max))
         self.clouds.append(np.ascontiguousarray(cloud, f32))
@@ -266,11 +286,11 @@ class DpgSLAM:
         new node n with the preceding one and the preceding one with every earlier node within the
         distance rule (one batch), adds the factors and updates the graph."""
         extra = np.asarray(extra, FACTOR_DTYPE).reshape(-1)
-        n_icp, X = self.be.add_node(self.clouds[n], np.asarray(self.node_pass, np.int32), self.poses[n], extra,
+        n_icp, X = self.be.add_node(self.clouds[n], self.node_pass, self.poses[n], extra,
                                     self.icp_params, self._reopt_params(), aligned and self.non_successive)
         self.n_factors += len(extra) + n_icp
         self.current_pass.append(n)
-        self.poses = [np.asarray(x, f32) for x in X]
+        self.poses = np.asarray(X, f32).reshape(-1, 3)
 
     def _reopt_params(self):
         rp = _abi.default_reopt_params()

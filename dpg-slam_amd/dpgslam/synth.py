@@ -269,3 +269,124 @@ def make_dynamic(n_passes: int = 4, nodes_per_pass: int = 2500, n_beams: int = 5
                            pass_of=np.repeat(np.arange(n_passes, dtype=np.int32), nodes_per_pass),
                            pass_start=np.arange(n_passes + 1, dtype=np.int64) * nodes_per_pass,
                            boxes=boxes, present=present)
+
+
+# ------------------------------------------------------------------ config 5 (patrol passes)
+@dataclass
+class PatrolWorkload:
+    """BASELINE config 5 as a DpgSLAM run: a building of rooms x rooms rooms (2 m doors at the wall
+    centres), furniture and movable boxes kept off the room centre lines, and n_passes passes that
+    all start at the same pose and follow the same serpentine patrol route through every room
+    (dpg_slam's passes start where pass 0 started: createNewPassFirstNode puts each pass's first
+    node at the map origin).  Between passes movable boxes appear (p_add) or disappear (p_remove).
+    Per pass: ground truth, odometry readings (noisy increments integrated from (0, 0, 0)) and one
+    ray-cast scan per reading."""
+    segs: np.ndarray        # static world segments
+    boxes: np.ndarray       # [K, 4] movable boxes
+    present: np.ndarray     # [P, K] bool
+    gt: np.ndarray          # [P, N, 3] world frame (f64)
+    odom: np.ndarray        # [P, N, 3] odometry readings (f32)
+    ranges: np.ndarray      # [P * N, n_beams] f32
+    geom: np.ndarray        # [P * N, 3] angle_min, angle_max, range_max
+
+    @property
+    def n_passes(self) -> int:
+        return self.gt.shape[0]
+
+    @property
+    def steps(self) -> int:
+        return self.gt.shape[1]
+
+    def gt_map(self) -> np.ndarray:
+        """Ground truth in the map frame (pass 0's start pose), [P, N, 3]."""
+        return _relative(self.gt, self.gt[0, 0])
+
+
+def _patrol_world(rooms: int, cell: float, rng, n_movable: int, lane: float):
+    W = rooms * cell
+    segs = [[0, 0, W, 0], [W, 0, W, W], [W, W, 0, W], [0, W, 0, 0]]
+    for k in range(1, rooms):
+        c = k * cell
+        for m in range(rooms):
+            a0, mid, a1 = m * cell, m * cell + cell / 2.0, (m + 1) * cell
+            segs += [[c, a0, c, mid - 1.0], [c, mid + 1.0, c, a1], [a0, c, mid - 1.0, c], [mid + 1.0, c, a1, c]]
+
+    def off_lane_box(r, c, hmax):
+        cx, cy = (c + 0.5) * cell, (r + 0.5) * cell
+        qx, qy = rng.choice([-1.0, 1.0], 2)
+        h = rng.uniform(0.2, hmax, 2)
+        lo, hi = lane + h + 0.2, cell / 2.0 - h - 0.4
+        x = cx + qx * rng.uniform(lo[0], max(lo[0], hi[0]))
+        y = cy + qy * rng.uniform(lo[1], max(lo[1], hi[1]))
+        return [x - h[0], y - h[1], x + h[0], y + h[1]]
+
+    for r in range(rooms):
+        for c in range(rooms):
+            for _ in range(2):
+                segs += _box_segs(off_lane_box(r, c, 0.6))
+    cells = rng.choice(rooms * rooms, size=min(n_movable, rooms * rooms), replace=False)
+    boxes = np.asarray([off_lane_box(int(q) // rooms, int(q) % rooms, 0.5) for q in cells], np.float32).reshape(-1, 4)
+    return np.asarray(segs, np.float32), boxes
+
+
+def _serpentine(rooms: int, cell: float) -> np.ndarray:
+    pts = []
+    for r in range(rooms):
+        cols = range(rooms) if r % 2 == 0 else range(rooms - 1, -1, -1)
+        pts += [((c + 0.5) * cell, (r + 0.5) * cell) for c in cols]
+    return np.asarray(pts, np.float64)
+
+
+def make_patrol(n_passes: int = 4, steps: int = 2500, n_beams: int = 5000, rooms: int = 16, cell: float = 10.5,
+                step: float = 1.05, fov_deg: float = 270.0, range_max: float = RANGE_MAX, range_noise: float = 0.002,
+                n_movable: int = 64, p_add: float = 0.3, p_remove: float = 0.15, lateral: float = 0.35,
+                odom_noise: tuple = (0.01, 0.003), seed: int = 5, threads: int = 0) -> PatrolWorkload:
+    rng = np.random.default_rng(seed)
+    static, boxes = _patrol_world(rooms, cell, rng, n_movable, lane=1.5)
+    K = len(boxes)
+    present = np.zeros((n_passes, K), bool)
+    present[0] = rng.random(K) < 0.5
+    for p in range(1, n_passes):
+        u = rng.random(K)
+        present[p] = present[p - 1] ^ np.where(present[p - 1], u < p_remove, u < p_add)
+    # the route, sampled every `step` m of arc length
+    way = _serpentine(rooms, cell)
+    seg = np.diff(way, axis=0)
+    seg_len = np.linalg.norm(seg, axis=1)
+    cum = np.concatenate([[0.0], np.cumsum(seg_len)])
+    if cum[-1] < step * steps:
+        raise ValueError(f"route of {cum[-1]:.0f} m is shorter than {steps} steps of {step} m")
+    amin, amax = (ANGLE_MIN, ANGLE_MAX) if fov_deg >= 360.0 else (-math.radians(fov_deg) / 2, math.radians(fov_deg) / 2)
+    threads = threads or min(16, os.cpu_count() or 1)
+    gts, odoms, rs = [], [], []
+    for p in range(n_passes):
+        s = np.arange(steps) * step
+        k = np.minimum(np.searchsorted(cum, s, side="right") - 1, len(seg) - 1)
+        d = seg[k] / seg_len[k, None]
+        base = way[k] + d * (s - cum[k])[:, None]
+        ph = rng.uniform(0, 2 * np.pi, 2)
+        off = lateral * (0.6 * np.sin(2 * np.pi * s / 23.0 + ph[0]) + 0.4 * np.sin(2 * np.pi * s / 7.0 + ph[1]))
+        off[0] = 0.0   # every pass starts at the same pose
+        nrm = np.stack([-d[:, 1], d[:, 0]], 1)
+        xy = base + nrm * off[:, None]
+        th = np.arctan2(d[:, 1], d[:, 0]) + np.concatenate([[0.0], rng.normal(0, 0.02, steps - 1)])
+        gt = np.concatenate([xy, th[:, None]], 1)
+        od = np.zeros((steps, 3))
+        for v in range(1, steps):
+            inc = _relative(gt[v], gt[v - 1]) + np.array([rng.normal(0, odom_noise[0]), rng.normal(0, odom_noise[0]),
+                                                          rng.normal(0, odom_noise[1])])
+            od[v] = _compose(od[v - 1], inc)
+        bs = [q for b in range(K) if present[p, b] for q in _box_segs(boxes[b])]
+        world = np.ascontiguousarray(np.concatenate([static, np.asarray(bs, np.float32).reshape(-1, 4)]), np.float32)
+        r = np.zeros((steps, n_beams), np.float32)
+        gtc = np.ascontiguousarray(gt)
+        _abi.check(lib().dpg_synth_scans(ptr(gtc, C.c_double), steps, ptr(world, C.c_float), len(world), n_beams, amin,
+                                         amax, range_max, LASER[0], LASER[1], LASER[2], range_noise,
+                                         seed * 7919 + 17 * p + 1, threads, ptr(r, C.c_float)), "dpg_synth_scans")
+        gts.append(gt)
+        odoms.append(od.astype(np.float32))
+        rs.append(r)
+    V = n_passes * steps
+    geom = np.tile(np.array([amin, amax, range_max], np.float32), (V, 1))
+    return PatrolWorkload(segs=static, boxes=boxes, present=present, gt=np.stack(gts), odom=np.stack(odoms),
+                          ranges=np.concatenate(rs), geom=geom)

@@ -42,7 +42,8 @@ class OracleSlamBackend:
         self.g.update(np.asarray(init_pose, f32).astype(np.float64).reshape(1, 3), np.concatenate(F))
         return n_icp, self.g.poses()
 
-    def icp_batch(self, pts, offsets, edges, est, p):
+    def icp_batch(self, clouds, edges, est, p):
+        pts, offsets = clouds()
         return O.icp_batch(pts, offsets, edges, est, p, O.NN_GRID)[0]
 
     def candidates(self, est, passes, within, across):
@@ -56,5 +57,6 @@ class OracleSlamBackend:
     def store(self, ranges, geom, offsets, params):
         return O.OracleDpgStore(ranges, geom, offsets=offsets, params=params)
 
-    def get_map(self, pts, offsets, est, fraction, ratio):
+    def get_map(self, clouds, est, fraction, ratio):
+        pts, offsets = clouds()
         return O.get_map(pts, offsets, est, fraction)
