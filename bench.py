@@ -541,6 +541,8 @@ def main():
                          "the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--icp-variant", default="angular", choices=["angular", "kdtree", "grid"],
                     help="nearest-neighbour machinery of the ICP kernel (results are identical)")
+    ap.add_argument("--refactor-delta", type=float, default=None,
+                    help="dpg_gn_params.refactor_delta: chord steps (reuse the Cholesky factor) once max|delta| is below it")
     ap.add_argument("--workload", default="batch", choices=["batch", "incremental", "dynamic", "dpg"],
                     help="batch: the headline step (all edges + GN); incremental: per-node latency of "
                          "dpg_add_node_pairs at V = 5000 (1 GPU); dynamic: config 5 through DpgSLAM (1 GPU); dpg: executeDPG at config-5 "
@@ -586,6 +588,8 @@ def main():
     log(f"[rank {rank}] generated {args.config}: V={w.V} E={w.E} points={len(w.pts)} in {time.time() - t0:.1f}s")
     params = _abi.default_icp_params()
     gp = _abi.default_gn_params()
+    if args.refactor_delta is not None:
+        gp.refactor_delta = args.refactor_delta
 
     ctx = api.Context(gpu)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)

@@ -43,7 +43,11 @@
 // [8] search, [9] sums + fold, [10] arrival + fit + publish barrier, [11] move + barrier,
 // [12] wave-iterations, [45] queue phase (barrier, cooperative scans, barrier, finalize).
 // DPG_ICP_STATS also: [40] queued forward windows, [41] their candidates, [42] cooperative
-// reciprocal scans, [43] their candidates, [44] workgroup-iterations with a non-empty queue
+// reciprocal scans, [43] their candidates, [44] workgroup-iterations with a non-empty queue,
+// [46] float bits of max |moved - (F p + t)| over every moved source point (m, the incremental
+// move's accumulated float drift against the exact image of the static point under the current
+// float transform), [47] float bits of the max of that drift over the window margin the next
+// reciprocal test adds for it, 1e-4 + 5e-5 (k + 1) m (must stay below 1)
 #define DPG_ICP_DIAG 1
 __device__ unsigned long long g_icp_stats[48];
 #define ICP_STAT_ADD(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
@@ -839,6 +843,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
             sx[m] = (cf * x + nsf * y) + txf;
             sy[m] = (sf * x + cf * y) + tyf;
             if (i < N) put(m);
+#ifdef DPG_ICP_STATS
+            if (i < N) {   // drift of the moved point against F_{k+1} p, and the margin it gets
+                const float2 p0 = ds_pts[E.src_ds_off + i];
+                const double fx = ((double)L.bc->F[0] * p0.x + (double)L.bc->F[1] * p0.y) + (double)L.bc->F[2];
+                const double fy = ((double)L.bc->F[3] * p0.x + (double)L.bc->F[4] * p0.y) + (double)L.bc->F[5];
+                const double dv = sqrt(((double)sx[m] - fx) * ((double)sx[m] - fx) + ((double)sy[m] - fy) * ((double)sy[m] - fy));
+                const double ratio = dv / (1e-4 + 5e-5 * (double)(k + 2));
+                atomicMax(&g_icp_stats[46], (unsigned long long)__float_as_uint((float)dv));
+                atomicMax(&g_icp_stats[47], (unsigned long long)__float_as_uint((float)ratio));
+            }
+#endif
             const int sd = st_seed(st[m]);
             if (sd < -1) {   // the clearance shrinks by the distance the point just moved
                 const float dx = sx[m] - x, dy = sy[m] - y;

@@ -13,8 +13,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "dpg-slam_amd"))
 from dpgslam import _abi, api, synth  # noqa: E402
 
-w = synth.generate(sys.argv[1] if len(sys.argv) > 1 else "config4")
+import argparse  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("config", nargs="?", default="config4")
+ap.add_argument("--cap", action="store_true", help="transformation epsilon 0 and MSE threshold 0: every edge runs "
+                                                   "to the iteration cap")
+ap.add_argument("--edges", type=int, default=0, help="only the first N edges")
+a = ap.parse_args()
+w = synth.generate(a.config)
 p = _abi.default_icp_params()
+if a.cap:
+    p.icp_maximum_transformation_epsilon = 0.0
+    p.mse_threshold_absolute = 0.0
+if a.edges:
+    w.edges = w.edges[:a.edges]
 L = _abi.lib()
 L.dpg_icp_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 st = (C.c_ulonglong * 48)()
@@ -48,6 +61,10 @@ if s[0]:
     t = sum(s[o:o + 12])
     print(f"{name} wave trips by trips-per-slot bin (share of all {name} trips): " +
           " ".join(f"{b}:{s[o + k] / max(1, t):.1%}" for k, b in enumerate(bins)))
+if s[0]:
+  import struct
+  f = lambda u: struct.unpack("<f", struct.pack("<I", u & 0xffffffff))[0]   # noqa: E731
+  print(f"drift: max |moved - F p| {f(s[46]):.3e} m, max drift / window margin {f(s[47]):.4f}")
 tot = sum(s[8:12]) + s[45]
 if s[12]:
     names = ["search", "sums+fold", "arrive+fit+barrier", "move+barrier", "queue (barriers, scans)"]
