@@ -1,0 +1,200 @@
+// adapter_check.cpp -- exercises include/dpg_slam_adapter.hpp with stand-ins for the reference's
+// types (PCL cloud, Eigen matrices / vector, DpgNode, PoseGraphParameters): compiled and linked
+// against lib/libdpg.so by the CPU suite (tests/test_adapter.py), run on the GPU by the gpu suite.
+// Each adapter call is checked against the direct C-ABI call on the same inputs (bit for bit).
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <memory>
+#include <vector>
+
+#include "../include/dpg_slam_adapter.hpp"
+
+namespace {
+
+struct PointXYZ { float x, y, z; };
+struct Cloud {
+    std::vector<PointXYZ> points;
+    size_t size() const { return points.size(); }
+};
+using CloudPtr = std::shared_ptr<Cloud>;
+struct Vector2f {
+    float v[2];
+    Vector2f(float a = 0.f, float b = 0.f) : v{a, b} {}
+    float x() const { return v[0]; }
+    float y() const { return v[1]; }
+};
+struct Matrix4f {
+    float m[16];
+    float& operator()(int r, int c) { return m[4 * r + c]; }
+};
+struct MatrixXd {
+    std::vector<double> m;
+    int c = 0;
+    void resize(int r, int cc) { m.assign((size_t)(r * cc), 0.0); c = cc; }
+    double& operator()(int r, int cc) { return m[(size_t)(r * c + cc)]; }
+};
+struct Node {
+    CloudPtr cloud;
+    Vector2f loc;
+    float th = 0.f;
+    uint32_t pass = 0;
+    bool active = true;
+    CloudPtr getCachedPointCloudFromNode() const { return cloud; }
+    std::pair<Vector2f, float> getEstimatedPosition() const { return {loc, th}; }
+    void setPosition(const Vector2f& l, const float& t) { loc = l; th = t; }
+    uint32_t getPassNumber() const { return pass; }
+    void setInactive() { active = false; }
+};
+struct PGParams {   // parameters.h defaults
+    int icp_maximum_iterations_ = 500;
+    double icp_maximum_transformation_epsilon_ = 5e-9;
+    double icp_max_correspondence_distance_ = 0.6;
+    bool icp_use_reciprocal_correspondences_ = true;
+    int downsample_icp_points_ratio_ = 5;
+    float laser_x_variance_ = 0.5f, laser_y_variance_ = 0.5f, laser_theta_variance_ = 0.3f;
+    float maximum_node_dist_within_pass_scan_comparison_ = 5.f, maximum_node_dist_across_passes_scan_comparison_ = 2.f;
+    bool odometry_constraints_ = true;
+};
+
+// a 360-beam scan of a 10 x 6 m room from (x, y, th) (laser at the base_link origin here)
+std::vector<float> room_scan(double x, double y, double th, int n) {
+    std::vector<float> r((size_t)n);
+    for (int b = 0; b < n; ++b) {
+        const double a = th - M_PI + 2.0 * M_PI * b / (n - 1);
+        const double dx = cos(a), dy = sin(a);
+        double best = 30.0;
+        const double walls[4][3] = {{1, 0, 10}, {1, 0, 0}, {0, 1, 6}, {0, 1, 0}};   // x = 10, x = 0, y = 6, y = 0
+        for (auto& w : walls) {
+            const double d = w[0] * dx + w[1] * dy;
+            if (fabs(d) < 1e-12) continue;
+            const double t = (w[2] - (w[0] * x + w[1] * y)) / d;
+            if (t > 0 && t < best) best = t;
+        }
+        r[(size_t)b] = (float)best;
+    }
+    return r;
+}
+
+CloudPtr cloud_of(const std::vector<float>& r) {
+    std::vector<float> xy(2 * r.size());
+    const int64_t n = dpg_scan_to_cloud(r.data(), (int64_t)r.size(), (float)-M_PI, (float)M_PI, 30.f, 0.f, 0.f, 0.f,
+                                        xy.data());
+    auto c = std::make_shared<Cloud>();
+    for (int64_t i = 0; i < n; ++i) c->points.push_back({xy[2 * i], xy[2 * i + 1], 0.f});
+    return c;
+}
+
+int fails = 0;
+#define EXPECT(cond)                                                   \
+    do {                                                               \
+        if (!(cond)) { printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #cond); ++fails; } \
+    } while (0)
+
+}  // namespace
+
+int main() {
+    dpg_adapter::Context ctx(0);
+    PGParams pgp;
+    const double gt[4][3] = {{3.0, 3.0, 0.1}, {3.9, 3.1, 0.15}, {4.8, 3.0, 0.2}, {5.7, 2.9, 0.22}};
+    std::vector<Node> nodes(4);
+    std::vector<std::vector<float>> scans;
+    for (int k = 0; k < 4; ++k) {
+        scans.push_back(room_scan(gt[k][0], gt[k][1], gt[k][2], 360));
+        nodes[(size_t)k].cloud = cloud_of(scans.back());
+        nodes[(size_t)k].loc = Vector2f((float)(gt[k][0] - gt[0][0] + 0.03 * k), (float)(gt[k][1] - gt[0][1]));
+        nodes[(size_t)k].th = (float)(gt[k][2] - gt[0][2]);
+    }
+    // runIcp (dpg_slam.h:630) against dpg_run_icp
+    std::pair<std::pair<Vector2f, float>, MatrixXd> res;
+    const bool conv = dpg_adapter::runIcp(ctx.get(), pgp, nodes[0], nodes[1], res);
+    {
+        const auto s = dpg_adapter::xy_of(nodes[1].cloud), t = dpg_adapter::xy_of(nodes[0].cloud);
+        float p2[3], p1[3];
+        dpg_adapter::pose_of(nodes[1], p2);
+        dpg_adapter::pose_of(nodes[0], p1);
+        const dpg_icp_params ip = dpg_adapter::icp_params_from(pgp);
+        dpg_icp_result r;
+        double cov[9];
+        dpg_adapter::check(dpg_run_icp(ctx.get(), s.data(), (int64_t)s.size() / 2, t.data(), (int64_t)t.size() / 2, p2,
+                                       p1, &ip, &r, cov, nullptr), "dpg_run_icp");
+        EXPECT(conv == (r.converged && r.status == DPG_ICP_OK));
+        EXPECT(res.first.first.x() == r.z[0] && res.first.first.y() == r.z[1] && res.first.second == r.z[2]);
+        EXPECT(memcmp(res.second.m.data(), cov, sizeof(cov)) == 0);
+        printf("runIcp: converged %d z = (%.4f, %.4f, %.4f), %d iterations\n", (int)conv, r.z[0], r.z[1], r.z[2],
+               r.iterations);
+        // calculate_ICP_COV (cov_func_point_to_point.h:24) with the final transform
+        Matrix4f T{};
+        T(0, 0) = r.T[0]; T(0, 1) = r.T[1]; T(0, 3) = r.T[2];
+        T(1, 0) = r.T[3]; T(1, 1) = r.T[4]; T(1, 3) = r.T[5];
+        T(2, 2) = 1.f; T(3, 3) = 1.f;
+        MatrixXd C;
+        double hb[9], hb2[9], cov2[9];
+        dpg_adapter::calculate_ICP_COV(nodes[1].cloud, nodes[0].cloud, T, C, 0.5f, 0.5f, 0.3f, ctx.get(), hb);
+        dpg_adapter::check(icp_cov_calculate(ctx.get(), s.data(), (int64_t)s.size() / 2, t.data(), (int64_t)t.size() / 2,
+                                             T.m, 0.5f, 0.5f, 0.3f, cov2, hb2), "icp_cov_calculate");
+        EXPECT(memcmp(C.m.data(), cov2, sizeof(cov2)) == 0 && memcmp(hb, hb2, sizeof(hb)) == 0);
+    }
+    // optimizeGraph (dpg_slam.h:464): prior + odometry chain + the ICP factor
+    {
+        const double sig[3] = {0.2, 0.2, 0.15}, info[3] = {2.0, 2.0, 1.0 / 0.3f};
+        std::vector<dpg_factor> F{dpg_adapter::prior_factor(0, 0, 0, 0, sig)};
+        for (int k = 1; k < 4; ++k)
+            F.push_back(dpg_adapter::between_factor(k - 1, k, 0.9, 0.0, 0.03, info));
+        F.push_back(dpg_adapter::between_factor(0, 1, res.first.first.x(), res.first.first.y(), res.first.second, info));
+        std::vector<Node> a = nodes;
+        const dpg_gn_stats st = dpg_adapter::optimizeGraph(ctx.get(), a, F);
+        std::vector<double> X(12);
+        for (int k = 0; k < 4; ++k) { X[3 * k] = nodes[k].loc.x(); X[3 * k + 1] = nodes[k].loc.y(); X[3 * k + 2] = nodes[k].th; }
+        dpg_gn_params gp;
+        dpg_gn_params_default(&gp);
+        dpg_gn_stats st2;
+        dpg_adapter::check(dpg_optimize_graph(ctx.get(), X.data(), 4, F.data(), (int64_t)F.size(), &gp, &st2),
+                           "dpg_optimize_graph");
+        for (int k = 0; k < 4; ++k)
+            EXPECT(a[k].loc.x() == (float)X[3 * k] && a[k].loc.y() == (float)X[3 * k + 1] && a[k].th == (float)X[3 * k + 2]);
+        EXPECT(st.iterations == st2.iterations);
+        printf("optimizeGraph: %d iterations, error %.6g\n", st.iterations, st.final_error);
+    }
+    // incremental form: one add_node per node
+    {
+        dpg_adapter::IncGraph g(ctx.get());
+        std::vector<int32_t> passes;
+        const double sig[3] = {0.2, 0.2, 0.15}, info[3] = {2.0, 2.0, 1.0 / 0.3f};
+        for (int k = 0; k < 4; ++k) {
+            passes.push_back(0);
+            float ip[3];
+            dpg_adapter::pose_of(nodes[(size_t)k], ip);
+            std::vector<dpg_factor> extra{k == 0 ? dpg_adapter::prior_factor(0, 0, 0, 0, sig)
+                                                 : dpg_adapter::between_factor(k - 1, k, 0.9, 0.0, 0.03, info)};
+            const dpg_add_node_stats st = g.add_node(nodes[(size_t)k].cloud, passes, ip, extra, pgp, true);
+            EXPECT(st.update.n_nodes == k + 1);
+        }
+        std::vector<Node> b = nodes;
+        g.write_back(b);
+        EXPECT(g.size() == 4);
+        printf("IncGraph: node 3 at (%.4f, %.4f, %.4f)\n", b[3].loc.x(), b[3].loc.y(), b[3].th);
+    }
+    // executeDPG: the store grows scan by scan; a second pass sees the room with a wall moved
+    {
+        dpg_adapter::DpgStore store(ctx.get());
+        std::vector<Node> nd(2);
+        auto r0 = room_scan(5.0, 3.0, 0.0, 360);
+        auto r1 = r0;
+        for (int b = 0; b < 72; ++b) r1[(size_t)b] += 2.0f;
+        store.add_scan(r0, (float)-M_PI, (float)M_PI, 30.f);
+        store.add_scan(r1, (float)-M_PI, (float)M_PI, 30.f);
+        std::vector<Vector2f> s0, s1, s2, s3;
+        const dpg_change_stats st = store.executeDPG(nd, 1, s0, s1, s2, s3);
+        int64_t cnt[4];
+        const float est[6] = {0, 0, 0, 0, 0, 0};
+        dpg_active_dynamic_points(store.get(), 2, est, nullptr, 0, cnt);
+        EXPECT((int64_t)s0.size() == cnt[0] && (int64_t)s1.size() == cnt[1] && (int64_t)s2.size() == cnt[2] &&
+               (int64_t)s3.size() == cnt[3]);
+        printf("executeDPG: %lld candidates, %lld removed, lists %zu %zu %zu %zu\n", (long long)st.n_candidates,
+               (long long)st.n_removed, s0.size(), s1.size(), s2.size(), s3.size());
+    }
+    printf(fails ? "adapter check FAILED (%d)\n" : "adapter check ok\n", fails);
+    return fails ? 1 : 0;
+}
