@@ -718,7 +718,8 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
         }
     }
     std::vector<uint32_t> sect((size_t)V, (1u << p->num_sectors) - 1u), act((size_t)V, 1u);
-    auto bad = [&](const char* m) { dpg_set_error(DPG_ERR_HIP, m); delete d; return (dpg_dpg*)nullptr; };
+    // error paths free what was allocated so far (pinned mirrors, events, device buffers)
+    auto bad = [&](const char* m) { dpg_dpg_destroy(d); dpg_set_error(DPG_ERR_HIP, m); return (dpg_dpg*)nullptr; };
     if (hipSetDevice(d->device) != hipSuccess) return bad("hipSetDevice failed");
     if (d->d_off.reserve((size_t)(V + 1)) || d->d_plaser.reserve((size_t)d->B) || d->d_range.reserve((size_t)d->B) ||
         d->d_label.reserve((size_t)d->B) || d->d_sector.reserve((size_t)d->B) || d->d_geom.reserve((size_t)V) ||
@@ -757,6 +758,10 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
     std::vector<uint8_t> lab((size_t)nb_new), sec((size_t)nb_new);
     std::vector<float> gm((size_t)(4 * n_new));
     std::vector<int64_t> off(d->off);
+    // the new nodes' largest ranges and the beam maximum are committed to d only after every
+    // check, allocation and copy below succeeded (as off and V)
+    std::vector<float> rmax_new;
+    int32_t max_beams = d->max_beams;
     for (int64_t k = 0; k < n_new; ++k) {
         const int64_t nb = off_rel[k + 1] - off_rel[k];
         if (nb < 2 || nb > 65535) return dpg_set_error(DPG_ERR_SIZE, "beams per scan must be in [2, 65535]");
@@ -775,8 +780,8 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
             rm = std::max(rm, r);
         }
         off.push_back(off.back() + nb);
-        d->rmax_beam.push_back(rm);
-        d->max_beams = std::max<int32_t>(d->max_beams, (int32_t)nb);
+        rmax_new.push_back(rm);
+        max_beams = std::max<int32_t>(max_beams, (int32_t)nb);
     }
     // device arrays grow with their contents kept (amortised x1.5)
     auto grow = [&](auto& b, size_t used, size_t need) -> int {
@@ -812,12 +817,8 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
     (void)hipHostFree(d->h_act);
     d->h_frames = nf;
     d->h_act = na;
-    d->h_pose.resize((size_t)(3 * V1), NAN);
-    d->active_h.resize((size_t)V1, 1);
-    d->geom.insert(d->geom.end(), gm.begin(), gm.end());
-    d->off = off;
     std::vector<uint32_t> sect((size_t)n_new, (1u << d->p.num_sectors) - 1u), act((size_t)n_new, 1u);
-    DTRY(hipMemcpyAsync(d->d_off.p, d->off.data(), sizeof(int64_t) * (V1 + 1), hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_off.p, off.data(), sizeof(int64_t) * (V1 + 1), hipMemcpyHostToDevice, s));
     DTRY(hipMemcpyAsync(d->d_plaser.p + B0, pl.data(), sizeof(float2) * nb_new, hipMemcpyHostToDevice, s));
     DTRY(hipMemcpyAsync(d->d_range.p + B0, ranges, sizeof(float) * nb_new, hipMemcpyHostToDevice, s));
     DTRY(hipMemcpyAsync(d->d_label.p + B0, lab.data(), nb_new, hipMemcpyHostToDevice, s));
@@ -826,8 +827,14 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
     DTRY(hipMemcpyAsync(d->d_sect.p + V0, sect.data(), sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
     DTRY(hipMemcpyAsync(d->d_active.p + V0, act.data(), sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
     DTRY(hipStreamSynchronize(s));
+    d->h_pose.resize((size_t)(3 * V1), NAN);
+    d->active_h.resize((size_t)V1, 1);
+    d->geom.insert(d->geom.end(), gm.begin(), gm.end());
+    d->off = off;
     d->V = V1;
     d->B = (int64_t)B1;
+    d->rmax_beam.insert(d->rmax_beam.end(), rmax_new.begin(), rmax_new.end());
+    d->max_beams = max_beams;
     return DPG_OK;
 }
 

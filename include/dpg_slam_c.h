@@ -396,7 +396,12 @@ int dpg_add_node(dpg_inc* g, const float* cloud_xy, int64_t n_pts, const int32_t
  * transformed into the map frame once; unlabelled points count as STATIC; the uncovered-cell set
  * loses every cell the candidate covers; the bin ratio is a real division; the bin score uses the
  * pose-chain node whose grid is tested and its own scan's angle range; removed points are labelled
- * on their own node; a deactivated sector skips one removed point (continue, not break). */
+ * on their own node; a deactivated sector skips one removed point (continue, not break); the pose
+ * chain is placed at the nodes' CURRENT estimates (est_poses) everywhere -- the reference's
+ * current_pass_nodes_ holds by-value DpgNode copies made at creation (dpg_slam.cc:195,307,598,
+ * dpg_node.h:163) that optimizeGraph never updates, so its chain grids and proximity search sit at
+ * creation-time poses while its bin score (:793-800) and sector update (:893-898) use the
+ * optimised ones (DPG item 8). */
 enum { DPG_LABEL_STATIC = 0, DPG_LABEL_ADDED = 1, DPG_LABEL_REMOVED = 2, DPG_LABEL_NOT_YET_LABELED = 3,
        DPG_LABEL_MAX_RANGE = 4 };   /* PointLabel, dpg_measurement.h:21 */
 

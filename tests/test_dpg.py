@@ -249,6 +249,32 @@ def test_gpu_pose_updates_between_calls():
         sg = g.execute_dpg(v + 1, cur, est[:v + 1])
         assert sg.counters() == so.counters(), (v, sg.counters(), so.counters())
         _same_state(g, o)
+        if n % 3 == 2 or n == 25:   # the map lists after a pose change (inactive nodes' frames too)
+            _same_map_lists(g, o, v + 1, est[:v + 1])
+    # a node that went inactive while its pose changed, reactivated by dpg_dpg_load: its frame must
+    # follow the pose it has now
+    lab, sec, act = g.fetch()
+    dead = np.nonzero(act[:60] == 0)[0][:3]
+    if len(dead) < 3:   # make three nodes inactive if the sequence left fewer
+        dead = np.array([5, 6, 7])
+        act = act.copy()
+        act[dead] = 0
+        g.load(lab, sec, act)
+        o.load(lab, sec, act)
+    est[dead, :2] += np.float32(0.5)   # poses change while the nodes are inactive
+    _same_map_lists(g, o, 60, est[:60])   # their removed / added points move with them
+    act2, sec2 = act.copy(), sec.copy()
+    act2[dead] = 1
+    sec2[dead] = 0x1f
+    g.load(lab, sec2, act2)
+    o.load(lab, sec2, act2)
+    _same_map_lists(g, o, 60, est[:60])
+
+
+def _same_map_lists(g, o, n, est):
+    a, b = g.active_dynamic_points(n, est), o.active_dynamic_points(n, est)
+    for k in a:
+        assert np.array_equal(np.asarray(a[k]), np.asarray(b[k])), k
 
 
 def _append_sequence(store_factory, w):
