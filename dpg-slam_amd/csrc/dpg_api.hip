@@ -108,6 +108,7 @@ struct dpg_ctx {
     DevBuf<float> tree_pts;        // per-node index over the downsampled clouds (k-d tree or angle order)
     DevBuf<uint16_t> tree_idx;
     DevBuf<uint16_t> buckets;      // angle variant: [V][B+1] bucket starts
+    DevBuf<unsigned char> icp_scratch;   // angle variant, clouds above 4096 points: record slices
     std::vector<int64_t> full_off, ds_off;
     int64_t n_nodes = 0;
     int32_t ratio = 1;
@@ -172,7 +173,9 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
                  bool timed, int64_t tree_from = 0) {
     if (c->icp_variant != DPG_ICP_ANGULAR) tree_from = 0;   // the other variants rebuild everything
     const int32_t maxp = std::max(max_src, max_tgt);
-    if (maxp > 4096) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 4096", maxp);
+    if (maxp > 16384) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 16384", maxp);
+    if (maxp > 4096 && c->icp_variant != DPG_ICP_ANGULAR)
+        return fail(DPG_ERR_SIZE, "downsampled cloud of %d points: only the angular ICP variant takes more than 4096", maxp);
     int rc = 0;
     if (timed) HIP_TRY(hipEventRecord(c->ev[6], c->stream));
     if (c->icp_variant == DPG_ICP_KDTREE) {
@@ -185,10 +188,17 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     }
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (c->icp_variant == DPG_ICP_ANGULAR) {
-        kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 16);   // LDS record capacity
+        kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 16);   // record capacity
         kp.defer_cap = c->defer_cap;
+        // large clouds: a record slice per resident edge in global scratch, edges in chunks of <= 2048
+        const size_t per_edge = dpg_icp_ang_scratch_per_edge(kp.lds_tgt);
+        size_t sbytes = 0;
+        if (per_edge) {
+            sbytes = per_edge * (size_t)std::min<int64_t>(ne, 2048);
+            if (c->icp_scratch.reserve(sbytes)) return fail(DPG_ERR_HIP, "out of device memory for the ICP scratch");
+        }
         rc = dpg_launch_icp_ang(ds_dev, tree_pts, tree_idx, buckets, edges_dev, ne, &kp, maxp, res_dev, trace_dev,
-                                c->stream);
+                                per_edge ? c->icp_scratch.p : nullptr, sbytes, c->stream);
     } else if (c->icp_variant == DPG_ICP_KDTREE) {
         kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 64);
         rc = dpg_launch_icp_kd(ds_dev, tree_pts, tree_idx, edges_dev, ne, &kp, maxp, res_dev, trace_dev, c->stream);
@@ -262,7 +272,7 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
     c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release();
     c->s_off.release(); c->s_tree_pts.release(); c->s_tree_idx.release();
-    c->buckets.release(); c->s_buckets.release();
+    c->buckets.release(); c->s_buckets.release(); c->icp_scratch.release();
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->map_ev) if (e) (void)hipEventDestroy(e);
@@ -305,7 +315,7 @@ int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V
         dpg_downsample_cloud(pts + 2 * off[v], off[v + 1] - off[v], ratio, ds.data() + 2 * c->ds_off[(size_t)v]);
     int64_t mx = 0;
     for (int64_t v = 0; v < V; ++v) mx = std::max(mx, c->ds_off[(size_t)v + 1] - c->ds_off[(size_t)v]);
-    if (mx > 4096) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 4096)", (long long)mx);
+    if (mx > 16384) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 16384)", (long long)mx);
     if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(ds.size()) ||
         c->ds_off_dev.reserve((size_t)V + 1) || c->tree_pts.reserve(ds.size()) || c->tree_idx.reserve(ds.size() / 2) ||
         c->buckets.reserve((size_t)V * (size_t)(dpg_angle_buckets() + 1)))
@@ -342,7 +352,7 @@ int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k
         doff[(size_t)v + 1] = doff[(size_t)v] + (n + ratio - 1) / ratio;
         mx = std::max(mx, (n + ratio - 1) / ratio);
     }
-    if (mx > 4096) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 4096)", (long long)mx);
+    if (mx > 16384) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 16384)", (long long)mx);
     const int64_t nds = doff[(size_t)k] - D0;
     std::vector<float> ds((size_t)(2 * std::max<int64_t>(nds, 1)));
     for (int64_t v = 0; v < k; ++v)

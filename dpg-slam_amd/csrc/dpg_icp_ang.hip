@@ -27,6 +27,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "dpg_atan2f.h"
@@ -259,11 +260,17 @@ struct Lds {
     Bcast* bc;        // wave 0's fit, read by every wave
 };
 
-__host__ __device__ inline size_t ang_lds_layout(int cap, size_t* off /* [7] or null */) {
+// Record placement by cloud size (MODE): 0 -- target and source records in LDS (clouds up to 4096
+// points); 1 -- the source records in a global scratch slice of the edge, the target in LDS (up to
+// 8192); 2 -- both in global scratch (up to 16384).  The scratch slice of workgroup b is
+// [2 (cap + kU)] records at gscr + 2 (cap + kU) b: target, then source.
+constexpr int kModeMaxPts[3] = {4096, 8192, 16384};
+
+__host__ __device__ inline size_t ang_lds_layout(int cap, size_t* off /* [7] or null */, int mode = 0) {
     size_t o = 0, p[7];
     const size_t spos_q = 2 * (size_t)cap > sizeof(QItem) * kQCap ? 2 * (size_t)cap : sizeof(QItem) * kQCap;
-    p[0] = o; o = (o + 16 * (size_t)(cap + kU) + 15) & ~size_t(15);
-    p[1] = o; o = (o + 16 * (size_t)(cap + kU) + 15) & ~size_t(15);
+    p[0] = o; o = (o + (mode == 2 ? 0 : 16 * (size_t)(cap + kU)) + 15) & ~size_t(15);
+    p[1] = o; o = (o + (mode >= 1 ? 0 : 16 * (size_t)(cap + kU)) + 15) & ~size_t(15);
     p[2] = o; o = (o + spos_q + 15) & ~size_t(15);
     p[3] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
     p[4] = o; o = (o + 2 * (size_t)(kB + 1) + 15) & ~size_t(15);
@@ -274,12 +281,14 @@ __host__ __device__ inline size_t ang_lds_layout(int cap, size_t* off /* [7] or 
     return o;
 }
 
-__device__ Lds carve(unsigned char* base, int cap) {
+template <int MODE>
+__device__ Lds carve(unsigned char* base, int cap, Rec* gscr) {
     size_t p[7];
-    ang_lds_layout(cap, p);
+    ang_lds_layout(cap, p, MODE);
     Lds L;
-    L.tp = reinterpret_cast<Rec*>(base + p[0]);
-    L.scs = reinterpret_cast<Rec*>(base + p[1]);
+    Rec* g = gscr + (size_t)blockIdx.x * 2 * (size_t)(cap + kU);
+    L.tp = MODE == 2 ? g : reinterpret_cast<Rec*>(base + p[0]);
+    L.scs = MODE >= 1 ? g + (cap + kU) : reinterpret_cast<Rec*>(base + p[1]);
     L.spos = reinterpret_cast<uint16_t*>(base + p[2]);
     L.q = reinterpret_cast<QItem*>(base + p[2]);
     L.tb = reinterpret_cast<uint16_t*>(base + p[3]);
@@ -295,8 +304,15 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // kU consecutive records with four ds_read_b128 issued back to back and ONE wait (the compiler,
 // left alone, narrows an unused pad word to ds_read_b96 -- 8 LDS cycles instead of 4 -- or
 // serialises the loads behind per-load waits under the 64-VGPR budget)
+template <bool kLds>
 __device__ __forceinline__ void ld_recs(const Rec* p, uint4 (&r)[kU]) {
     static_assert(kU == 4 || kU == 8, "ld_recs issues four or eight loads");
+    if constexpr (!kLds) {   // records in global scratch (large clouds): plain 16-byte loads
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) r[u] = q[u];
+        return;
+    }
     const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(p);   // LDS byte offset
     if constexpr (kU == 4) {
         asm volatile(
@@ -434,14 +450,22 @@ __device__ __forceinline__ int st_seed(uint32_t st) { return (int)(int16_t)(uint
 __device__ __forceinline__ int st_sp(uint32_t st) { return (int)(st >> 16); }
 __device__ __forceinline__ uint32_t st_with_seed(uint32_t st, int seed) { return (st & 0xffff0000u) | (uint32_t)(uint16_t)(int16_t)seed; }
 
-template <int PPT>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE, DPG_ANG_WPE))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
+// waves per SIMD: 8 for clouds up to 1024 points (<= 64 VGPRs); wider forms hold more points per
+// lane in registers and are limited by LDS anyway (2 workgroups per CU at 2048 points, 1 above):
+// 4 (<= 128 VGPRs) at 4 points per lane, 2 (<= 256) beyond
+constexpr int ang_wpe(int ppt, int mode) { return mode == 0 && ppt <= 2 ? DPG_ANG_WPE : mode == 0 && ppt == 4 ? 4 : 2; }
+
+template <int PPT, int MODE>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT, MODE), ang_wpe(PPT, MODE)))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
                                                      const float2* __restrict__ idx_pts,
                                                      const uint16_t* __restrict__ idx_orig,
                                                      const uint16_t* __restrict__ buckets,
                                                      const dpg_icp_edge* __restrict__ edges,
                                                      dpg_icp_kparams kp, dpg_icp_result* __restrict__ results,
-                                                     int32_t* __restrict__ trace) {
+                                                     int32_t* __restrict__ trace, Rec* __restrict__ gscr) {
+    constexpr bool kTpL = MODE != 2, kScsL = MODE == 0;   // records in LDS?
+    // queue slots: PPT <= 4 packs them into okq / qhi (7 bits each), wider forms keep a byte per point
+    constexpr bool kWideQ = PPT >= 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const dpg_icp_edge E = edges[blockIdx.x];   // dispatch order (dpg_icp_batch_prepare)
@@ -455,7 +479,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
     if (t == 0) st_wmax = 0;
 #endif
     const int stepM = M > 0 ? kU % M : 0, stepN = N > 0 ? kU % N : 0;
-    Lds L = carve(smem, cap);
+    Lds L = carve<MODE>(smem, cap, gscr);
     // sorted target + the kU repeated records after it
     for (int i = t; i < M + kU && M > 0; i += kT) {
         const int p = i < M ? i : (i - M) % M;
@@ -552,14 +576,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
         const float drift = 1e-4f + 5e-5f * (float)(k + 1);
         // bit m: point t + 512 m has a (reciprocal) correspondence; bits 8 + 7 m ..: queue slot + 1
         uint32_t okq = 0;
-        static_assert(PPT <= 3 || sizeof(okq) == 4, "");
-        uint32_t qhi = 0;   // PPT > 3: slots of points 3.. (7 bits each)
+        static_assert(PPT <= 32, "one ok bit per point");
+        uint32_t qhi = 0;   // PPT == 4: the slot of point 3 (7 bits)
+        uint32_t qsl[kWideQ ? PPT / 4 : 1];   // PPT >= 8: slot + 1 of point m in byte m of qsl
+#pragma unroll
+        for (int q = 0; q < (kWideQ ? PPT / 4 : 1); ++q) qsl[q] = 0;
 #ifdef DPG_ICP_STATS
         unsigned wtrips = 0;
 #endif
         auto set_slot = [&](int m, int slot) {
-            if (m < 3) okq |= (uint32_t)(slot + 1) << (8 + 7 * m);
+            if constexpr (kWideQ) qsl[m >> 2] |= (uint32_t)(slot + 1) << (8 * (m & 3));
+            else if (m < 3) okq |= (uint32_t)(slot + 1) << (8 + 7 * m);
             else qhi |= (uint32_t)(slot + 1) << (7 * (m - 3));
+        };
+        auto get_slot = [&](int m) -> int {
+            if constexpr (kWideQ) return (int)((qsl[m >> 2] >> (8 * (m & 3))) & 0xffu) - 1;
+            else return (int)(m < 3 ? (okq >> (8 + 7 * m)) & 0x7fu : (qhi >> (7 * (m - 3))) & 0x7fu) - 1;
         };
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
@@ -596,7 +628,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
 #endif
                 for (int c = 0; __any(c < fc); c += kU) {   // exact (d, original index) argmin
                     uint4 r[kU];
-                    ld_recs(L.tp + s, r);
+                    ld_recs<kTpL>(L.tp + s, r);
 #pragma unroll
                     for (int u = 0; u < kU; ++u) {
                         const uint64_t kd = dkey(sqd(qx, qy, __uint_as_float(r[u].x), __uint_as_float(r[u].y)), r[u].z);
@@ -644,7 +676,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
 #endif
                 for (int c = 0; __any(ok & (c < rc)); c += kU) {
                     uint4 r[kU];
-                    ld_recs(L.scs + s, r);
+                    ld_recs<kScsL>(L.scs + s, r);
                     bool beat = false;
 #pragma unroll
                     for (int u = 0; u < kU; ++u) {
@@ -726,7 +758,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(DPG_ANG_WPE,
         // finalize the points whose windows were queued
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
-            const int slot = (int)(m < 3 ? (okq >> (8 + 7 * m)) & 0x7fu : (qhi >> (7 * (m - 3))) & 0x7fu) - 1;
+            const int slot = get_slot(m);
             if (slot >= 0) {
                 const uint4 it = *reinterpret_cast<const uint4*>(L.q + slot);
                 if ((it.y >> 31) == 0u)   // forward item: its best key -> match, next seed
@@ -926,7 +958,10 @@ extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
 }
 #endif
 
-extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) { return ang_lds_layout(cap, nullptr); }
+extern "C" size_t dpg_icp_ang_lds_bytes(int32_t cap) { return ang_lds_layout(cap, nullptr, cap <= 4096 ? 0 : cap <= 8192 ? 1 : 2); }
+extern "C" size_t dpg_icp_ang_scratch_per_edge(int32_t cap) {
+    return cap <= kModeMaxPts[0] ? 0 : 2 * (size_t)(cap + kU) * sizeof(Rec);
+}
 
 extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                                       int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
@@ -934,7 +969,7 @@ extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds
     if (n_nodes <= 0) return DPG_OK;
     int cap = 1;
     while (cap < max_points) cap <<= 1;
-    if (cap > 4096) return DPG_ERR_SIZE;
+    if (cap > kModeMaxPts[2]) return DPG_ERR_SIZE;
     hipLaunchKernelGGL(angle_index_kernel, dim3((unsigned)n_nodes), dim3(kTI), 8 * (size_t)cap,
                        reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(ds_pts_dev), ds_off_dev,
                        reinterpret_cast<float2*>(idx_pts_dev), idx_orig_dev, buckets_dev);
@@ -943,23 +978,39 @@ extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds
 
 extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_dev, const uint16_t* idx_orig_dev,
                                   const uint16_t* buckets_dev, const dpg_icp_edge* edges_dev, int64_t n_edges, const dpg_icp_kparams* kp,
-                                  int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* stream) {
+                                  int32_t max_points, dpg_icp_result* results_dev, int32_t* trace_dev, void* scratch,
+                                  size_t scratch_bytes, void* stream) {
     if (n_edges <= 0) return DPG_OK;
-    if (max_points > kp->lds_tgt || kp->lds_tgt > 4096) return DPG_ERR_SIZE;
-    const size_t lds = dpg_icp_ang_lds_bytes(kp->lds_tgt);
+    const int mode = max_points <= kModeMaxPts[0] ? 0 : max_points <= kModeMaxPts[1] ? 1 : 2;
+    if (max_points > kp->lds_tgt || max_points > kModeMaxPts[2] || kp->lds_tgt > kModeMaxPts[mode]) return DPG_ERR_SIZE;
+    const size_t lds = ang_lds_layout(kp->lds_tgt, nullptr, mode);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const dim3 grid((unsigned)n_edges), block(kT);
     const float2* ds = reinterpret_cast<const float2*>(ds_pts_dev);
     const float2* ip = reinterpret_cast<const float2*>(idx_pts_dev);
     const int ppt = (max_points + kT - 1) / kT;
-#define DPG_ANG_LAUNCH(P)                                                                                     \
-    hipLaunchKernelGGL(icp_ang_kernel<P>, grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, edges_dev, \
-                       *kp, results_dev, trace_dev)
-    if (ppt <= 1) DPG_ANG_LAUNCH(1);
-    else if (ppt <= 2) DPG_ANG_LAUNCH(2);
-    else if (ppt <= 4) DPG_ANG_LAUNCH(4);
-    else if (ppt <= 8) DPG_ANG_LAUNCH(8);
-    else return DPG_ERR_SIZE;
+    // the large-cloud forms run in chunks of edges that fit the scratch (one slice per workgroup)
+    const size_t per_edge = mode ? 2 * (size_t)(kp->lds_tgt + kU) * sizeof(Rec) : 0;
+    const int64_t chunk = mode ? (int64_t)(scratch && per_edge ? scratch_bytes / per_edge : 0) : n_edges;
+    if (chunk <= 0) return DPG_ERR_SIZE;
+    Rec* g = reinterpret_cast<Rec*>(scratch);
+    for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
+        const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
+        const dpg_icp_edge* ed = edges_dev + e0;
+#define DPG_ANG_LAUNCH(P, M)                                                                                     \
+        hipLaunchKernelGGL((icp_ang_kernel<P, M>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+                           results_dev, trace_dev, g)
+        if (mode == 0) {
+            if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
+            else if (ppt <= 2) DPG_ANG_LAUNCH(2, 0);
+            else if (ppt <= 4) DPG_ANG_LAUNCH(4, 0);
+            else DPG_ANG_LAUNCH(8, 0);
+        } else if (mode == 1) {
+            DPG_ANG_LAUNCH(16, 1);
+        } else {
+            DPG_ANG_LAUNCH(32, 2);
+        }
+        if (hipGetLastError() != hipSuccess) return DPG_ERR_HIP;
+    }
 #undef DPG_ANG_LAUNCH
-    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+    return DPG_OK;
 }

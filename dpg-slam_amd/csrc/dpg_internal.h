@@ -77,11 +77,14 @@ int dpg_launch_map_points(const float* pts_dev, const int64_t* off_dev, const fl
 int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                            int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
                            uint16_t* buckets_dev, void* stream);
+/* clouds of more than 4096 points: record slices in global scratch (scratch_bytes of it, used in
+   chunks of scratch_bytes / dpg_icp_ang_scratch_per_edge(cap) edges); up to 16384 points */
 int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_dev, const uint16_t* idx_orig_dev,
                        const uint16_t* buckets_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
                        const dpg_icp_kparams* kp, int32_t max_points, dpg_icp_result* results_dev,
-                       int32_t* trace_dev, void* stream);
+                       int32_t* trace_dev, void* scratch, size_t scratch_bytes, void* stream);
 size_t dpg_icp_ang_lds_bytes(int32_t cap);
+size_t dpg_icp_ang_scratch_per_edge(int32_t cap);
 
 /* Pose-graph system on device (defined in dpg_gn.hip). */
 typedef struct dpg_gn_dev {
