@@ -631,6 +631,86 @@ int icp_cov_calculate(dpg_ctx* c, const float* data, int64_t nd, const float* mo
     return DPG_OK;
 }
 
+// d2J_dX2 and d2J_dZdX cov_z d2J_dZdX^T from the 16 sums of cov6_kernel (+ the pair counts), then
+// cov6 = 0.01 inv(H) M inv(H) (Gauss-Jordan with partial pivoting, fp64, fixed order)
+static int cov6_from_sums(const double* sm, int64_t nh, int64_t nb, double cov6[36]) {
+    double H[36] = {0}, M[36] = {0};
+    enum { X = 0, Y = 1, Z = 2, A = 3, B = 4, C = 5 };
+    auto sym = [](double* m, int i, int j, double v) { m[6 * i + j] = v; m[6 * j + i] = v; };
+    sym(H, X, X, 2.0 * (double)nh); sym(H, Y, Y, 2.0 * (double)nh); sym(H, Z, Z, 2.0 * (double)nh);
+    sym(H, X, A, sm[0]); sym(H, Y, A, sm[1]); sym(H, A, A, sm[2]); sym(H, Z, B, sm[3]); sym(H, Z, C, sm[4]);
+    sym(H, B, B, sm[5]); sym(H, B, C, sm[6]); sym(H, C, C, sm[7]);
+    sym(M, X, X, 8.0 * (double)nb); sym(M, Y, Y, 8.0 * (double)nb); sym(M, Z, Z, 8.0 * (double)nb);
+    sym(M, X, A, sm[8]); sym(M, Y, A, sm[9]); sym(M, A, A, sm[10]); sym(M, Z, B, sm[11]); sym(M, Z, C, sm[12]);
+    sym(M, B, B, sm[13]); sym(M, B, C, sm[14]); sym(M, C, C, sm[15]);
+    double I[36] = {0};
+    for (int i = 0; i < 6; ++i) I[7 * i] = 1.0;
+    for (int c = 0; c < 6; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 6; ++r)
+            if (fabs(H[6 * r + c]) > fabs(H[6 * p + c])) p = r;
+        if (!(fabs(H[6 * p + c]) > 0.0)) return DPG_ERR_NUMERIC;
+        if (p != c)
+            for (int k = 0; k < 6; ++k) { std::swap(H[6 * p + k], H[6 * c + k]); std::swap(I[6 * p + k], I[6 * c + k]); }
+        const double d = H[6 * c + c];
+        for (int k = 0; k < 6; ++k) { H[6 * c + k] /= d; I[6 * c + k] /= d; }
+        for (int r = 0; r < 6; ++r) {
+            if (r == c) continue;
+            const double f = H[6 * r + c];
+            if (f == 0.0) continue;
+            for (int k = 0; k < 6; ++k) { H[6 * r + k] -= f * H[6 * c + k]; I[6 * r + k] -= f * I[6 * c + k]; }
+        }
+    }
+    double T1[36];
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < 6; ++k) acc += I[6 * i + k] * M[6 * k + j];
+            T1[6 * i + j] = acc;
+        }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < 6; ++k) acc += T1[6 * i + k] * I[6 * k + j];
+            cov6[6 * i + j] = 0.01 * acc;
+        }
+    return DPG_OK;
+}
+
+int icp_cov_sandwich(dpg_ctx* c, const float* data, int64_t nd, const float* model, int64_t nm, const float T[16],
+                     double cov6_out[36], double cov3_out[9]) {
+    if (!T || !data || !model || nd < 1 || nm < 1 || nd > INT32_MAX / 4 || nm > INT32_MAX / 4)
+        return fail(DPG_ERR_ARG, "icp_cov_sandwich: bad arguments");
+    if (!c) {
+        if (!g_default_ctx) g_default_ctx = dpg_ctx_create(0);
+        c = g_default_ctx;
+        if (!c) return DPG_ERR_HIP;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<float> buf((size_t)(2 * (nd + nm)) + 8);
+    memcpy(buf.data(), data, sizeof(float) * 2 * (size_t)nd);
+    memcpy(buf.data() + 2 * nd, model, sizeof(float) * 2 * (size_t)nm);
+    float* T6 = buf.data() + 2 * (nd + nm);   // rows (T00 T01 T03 / T10 T11 T13), as the ICP result keeps them
+    T6[0] = T[0]; T6[1] = T[1]; T6[2] = T[3]; T6[3] = T[4]; T6[4] = T[5]; T6[5] = T[7];
+    if (c->s_pts.reserve(buf.size()) || c->s_hess.reserve(16)) return fail(DPG_ERR_HIP, "out of device memory");
+    HIP_TRY(hipMemcpyAsync(c->s_pts.p, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice, c->stream));
+    int rc = dpg_launch_cov6(c->s_pts.p, (int32_t)nd, (int32_t)nm, c->s_pts.p + 2 * (nd + nm), c->s_hess.p, c->stream);
+    if (rc) return fail(rc, "covariance kernel launch failed");
+    double sm[16];
+    HIP_TRY(hipMemcpyAsync(sm, c->s_hess.p, sizeof(sm), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int64_t nh = std::min(nd, nm), nb = std::min<int64_t>(nh, 200);
+    double cov6[36];
+    if ((rc = cov6_from_sums(sm, nh, nb, cov6))) return fail(rc, "icp_cov_sandwich: d2J_dX2 is singular");
+    if (cov6_out) memcpy(cov6_out, cov6, sizeof(cov6));
+    if (cov3_out) {
+        const int ix[3] = {0, 1, 3};
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) cov3_out[3 * i + j] = cov6[6 * ix[i] + ix[j]];
+    }
+    return DPG_OK;
+}
+
 // ------------------------------------------------------------------ pose graph
 int dpg_gn_setup(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t b, int64_t e,
                  const dpg_gn_params* gp) {

@@ -381,6 +381,67 @@ __global__ __launch_bounds__(kThreads) void cov_block_kernel(const float2* __res
     }
 }
 
+// The 6x6 ICP covariance the reference computes and discards (cov :553-566, commented out): the
+// sums that d2J_dX2 (over s < n_h) and d2J_dZdX cov_z d2J_dZdX^T (over k < n_b) reduce to at
+// b = c = z = 0 (T20 = T21 = 0, T22 = 1), with a = atan2f(T10, T00), u = R(a) p, d = t - q,
+// w = d . (cos a, sin a), v = d . (sin a, -cos a) -- derived independently (tools/cov6_derive.py)
+// and checked against the reference's own expressions (tests/golden/cov6_expr.npz):
+//   d2J_dX2 per pair:   xx = yy = zz = 2, xa = -2 u_y, ya = 2 u_x, zb = -2 p_x, zc = 2 p_y,
+//                       aa = -2 u.d, bb = -2 p_x w, bc = 2 p_y w, cc = 2 p_y v (all others 0)
+//   B_k B_k^T per pair: xx = yy = zz = 8, xa = 4(-v cos a + w sin a - u_y),
+//                       ya = 4(-v sin a - w cos a + u_x), zb = 4(w - p_x), zc = 4(v + p_y),
+//                       aa = 4(v^2 + w^2 + |u|^2), bb = 4(w^2 + p_x^2), bc = 4(w v - p_x p_y),
+//                       cc = 4(v^2 + p_y^2)
+// out[0..7]: the d2J_dX2 sums xa ya aa zb zc bb bc cc; out[8..15] the same entries of sum B B^T.
+// One workgroup; fixed reduction order (strided per thread, wave shuffles, waves in order).
+__global__ __launch_bounds__(kThreads) void cov6_kernel(const float2* __restrict__ pts, int n_data, int n_model,
+                                                       const float* __restrict__ T6, double* __restrict__ out) {
+    __shared__ double red[kWaves][16];
+    const int t = threadIdx.x;
+    const double a = (double)dpg_atan2f(T6[3], T6[0]);   // yaw = atan2f(T10, T00) (cov :31)
+    const double x = T6[2], y = T6[5];
+    const double ca = cos(a), sa = sin(a);
+    const int nh = min(n_data, n_model), nb = min(nh, 200);
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.0;
+    for (int s = t; s < nh; s += kThreads) {
+        const float2 p = pts[s];
+        const float2 q = pts[n_data + s];
+        const double px = p.x, py = p.y, qx = q.x, qy = q.y;
+        const double ux = ca * px - sa * py, uy = sa * px + ca * py;
+        const double dx = x - qx, dy = y - qy;
+        const double w = dx * ca + dy * sa, v = dx * sa - dy * ca;
+        acc[0] += -2.0 * uy;
+        acc[1] += 2.0 * ux;
+        acc[2] += -2.0 * (ux * dx + uy * dy);
+        acc[3] += -2.0 * px;
+        acc[4] += 2.0 * py;
+        acc[5] += -2.0 * px * w;
+        acc[6] += 2.0 * py * w;
+        acc[7] += 2.0 * py * v;
+        if (s < nb) {
+            acc[8] += 4.0 * ((-v * ca + w * sa) - uy);
+            acc[9] += 4.0 * ((-v * sa - w * ca) + ux);
+            acc[10] += 4.0 * ((v * v + w * w) + (ux * ux + uy * uy));
+            acc[11] += 4.0 * (w - px);
+            acc[12] += 4.0 * (v + py);
+            acc[13] += 4.0 * (w * w + px * px);
+            acc[14] += 4.0 * (w * v - px * py);
+            acc[15] += 4.0 * (v * v + py * py);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) acc[q] += shfl_down_d(acc[q], off);
+    if ((t & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) red[t >> 6][q] = acc[q];
+    __syncthreads();
+    if (t < 16) out[t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+}
+
 }  // namespace
 
 extern "C" size_t dpg_icp_lds_bytes(int32_t lds_tgt, int32_t cells_max) {
@@ -428,5 +489,12 @@ extern "C" int dpg_launch_cov(const float* full_pts_dev, const dpg_icp_edge* edg
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(cov_block_kernel, dim3((unsigned)n_edges), dim3(kThreads), 0, s,
                        reinterpret_cast<const float2*>(full_pts_dev), edges_dev, results_dev, hess_dev);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_launch_cov6(const float* pts_dev, int32_t n_data, int32_t n_model, const float* T6_dev, double* out_dev,
+                               void* stream) {
+    hipLaunchKernelGGL(cov6_kernel, dim3(1), dim3(kThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const float2*>(pts_dev), n_data, n_model, T6_dev, out_dev);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }

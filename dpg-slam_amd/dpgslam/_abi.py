@@ -269,6 +269,7 @@ SIGNATURES = {
     "dpg_gn_last_solve_ms": (C.c_float, [P]),
     "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,
                                     C.c_float, F64P, F64P]),
+    "icp_cov_sandwich": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, F64P, F64P]),
     "dpg_reopt_params_default": (None, [C.POINTER(ReoptParams)]),
     "dpg_get_map": (C.c_int64, [P, F32P, C.c_int32, F32P, C.c_int64]),
     "dpg_get_map_kernel_ms": (C.c_float, [P]),

@@ -129,6 +129,17 @@ def calculate_ICP_COV(data_pi, model_qi, transform, laser_x_variance=0.5, laser_
     return cov.reshape(3, 3), (hess.reshape(3, 3) if hess is not None else None)
 
 
+def icp_cov_sandwich(data_pi, model_qi, transform, ctx: "Context | None" = None):
+    """The 6x6 ICP covariance the reference computes and discards (cov :553-566, optional):
+    (cov6 [6, 6] in x y z yaw pitch roll order, cov3 = its [x, y, yaw] block)."""
+    d, m = _f32(data_pi).reshape(-1, 2), _f32(model_qi).reshape(-1, 2)
+    T = _f32(transform).reshape(4, 4)
+    cov6, cov3 = np.zeros(36, np.float64), np.zeros(9, np.float64)
+    check(lib().icp_cov_sandwich(ctx.handle if ctx else None, ptr(d, C.c_float), len(d), ptr(m, C.c_float), len(m),
+                                 ptr(T, C.c_float), ptr(cov6, C.c_double), ptr(cov3, C.c_double)), "icp_cov_sandwich")
+    return cov6.reshape(6, 6), cov3.reshape(3, 3)
+
+
 def results_array(n: int) -> np.ndarray:
     return np.zeros(n, RESULT_DTYPE)
 

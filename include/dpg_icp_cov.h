@@ -36,6 +36,18 @@ int icp_cov_calculate(struct dpg_ctx* ctx, const float* data_xy, int64_t n_data,
                       float laser_x_variance, float laser_y_variance, float laser_theta_variance,
                       double cov_out[9], double hess_block_out[9]);
 
+/* The 6x6 ICP covariance the reference computes and then discards (cov_func_point_to_point.h:
+ * 553-566, commented out there; optional here, it is not what the graph uses): d2J_dX2 summed
+ * over every index pair s < min(n_data, n_model) (:45-283, SURVEY Q3 for the bound), d2J_dZdX over
+ * the first min(n_data, n_model, 200) pairs (:307-528), cov_z = 0.01 I (:553-554), and
+ *   cov6 = inv(d2J_dX2) d2J_dZdX cov_z d2J_dZdX^T inv(d2J_dX2)      (:560)
+ * in [x, y, z, yaw, pitch, roll] order (6x6 row-major), cov3 its [x, y, yaw] block (rows / columns
+ * 0, 1, 3, :563-566; 3x3 row-major; either output may be NULL).  Evaluated at the transform's
+ * planar angles (roll = pitch = 0, yaw = atan2f(T10, T00), z = T23 = 0): the sums on the GPU, the
+ * 6x6 inverse and products on the host in fp64.  DPG_ERR_NUMERIC when d2J_dX2 is singular. */
+int icp_cov_sandwich(struct dpg_ctx* ctx, const float* data_xy, int64_t n_data, const float* model_xy, int64_t n_model,
+                     const float transform[16], double cov6_out[36], double cov3_out[9]);
+
 #ifdef __cplusplus
 }
 #endif

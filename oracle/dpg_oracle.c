@@ -962,3 +962,108 @@ int oracle_symbolic_stats(int64_t n, const dpg_factor* f, int64_t nf, double out
     sym_free(&Y);
     return 0;
 }
+
+/* The commented-out 6x6 sandwich of calculate_ICP_COV (cov_func_point_to_point.h:553-566),
+ * restated literally: per index pair the full 6x6 d2J_dX2 block and the full 6x6 d2J_dZdX block
+ * (rows x y z a b c, columns pix piy piz qix qiy qiz -- the reference's layouts, :271-279 and
+ * :520-528), the Hessian summed over s < min(nd, nm), B_k B_k^T summed over k < min(nd, nm, 200)
+ * (:307), cov_z = 0.01 I, inverse by LU with partial pivoting, cov6 = inv(H) M inv(H) * 0.01.
+ * Entries at b = c = z = 0 (T20 = T21 = 0, T22 = 1, piz = qiz = 0); yaw = atan2f(T10, T00). */
+static void cov6_point(double ca, double sa, double x, double y, double px, double py, double qx, double qy,
+                       double H[36], double B[36]) {
+    const double ux = ca * px - sa * py, uy = sa * px + ca * py;
+    const double dx = x - qx, dy = y - qy;
+    const double w = dx * ca + dy * sa, v = dx * sa - dy * ca;
+    for (int k = 0; k < 36; ++k) { H[k] = 0.0; B[k] = 0.0; }
+    /* d2J_dX2 (symmetric) */
+    H[0] = 2.0; H[7] = 2.0; H[14] = 2.0;
+    H[3] = H[18] = -2.0 * uy;                 /* x a */
+    H[9] = H[19] = 2.0 * ux;                  /* y a */
+    H[16] = H[26] = -2.0 * px;                /* z b */
+    H[17] = H[32] = 2.0 * py;                 /* z c */
+    H[21] = -2.0 * (ux * dx + uy * dy);       /* a a */
+    H[28] = -2.0 * px * w;                    /* b b */
+    H[29] = H[34] = 2.0 * py * w;             /* b c */
+    H[35] = 2.0 * py * v;                     /* c c */
+    /* d2J_dZdX: row = X (x y z a b c), column = Z (pix piy piz qix qiy qiz) */
+    B[0] = 2.0 * ca;  B[1] = -2.0 * sa; B[3] = -2.0;
+    B[6] = 2.0 * sa;  B[7] = 2.0 * ca;  B[10] = -2.0;
+    B[14] = 2.0;      B[17] = -2.0;
+    B[18] = -2.0 * v; B[19] = -2.0 * w; B[21] = 2.0 * uy; B[22] = -2.0 * ux;
+    B[26] = 2.0 * w;  B[29] = 2.0 * px;
+    B[32] = 2.0 * v;  B[35] = -2.0 * py;
+}
+
+static int inv6(const double* A, double* Ai) {
+    double L[36];
+    int piv[6];
+    for (int k = 0; k < 36; ++k) L[k] = A[k];
+    for (int i = 0; i < 6; ++i) piv[i] = i;
+    for (int c = 0; c < 6; ++c) {   /* LU with partial pivoting */
+        int p = c;
+        for (int r = c + 1; r < 6; ++r)
+            if (fabs(L[6 * r + c]) > fabs(L[6 * p + c])) p = r;
+        if (!(fabs(L[6 * p + c]) > 0.0)) return -1;
+        if (p != c) {
+            for (int k = 0; k < 6; ++k) { double t = L[6 * p + k]; L[6 * p + k] = L[6 * c + k]; L[6 * c + k] = t; }
+            int t = piv[p]; piv[p] = piv[c]; piv[c] = t;
+        }
+        for (int r = c + 1; r < 6; ++r) {
+            L[6 * r + c] /= L[6 * c + c];
+            for (int k = c + 1; k < 6; ++k) L[6 * r + k] -= L[6 * r + c] * L[6 * c + k];
+        }
+    }
+    for (int j = 0; j < 6; ++j) {   /* column j of the inverse: solve L U x = P e_j */
+        double z[6];
+        for (int i = 0; i < 6; ++i) {
+            double s = piv[i] == j ? 1.0 : 0.0;
+            for (int k = 0; k < i; ++k) s -= L[6 * i + k] * z[k];
+            z[i] = s;
+        }
+        for (int i = 5; i >= 0; --i) {
+            double s = z[i];
+            for (int k = i + 1; k < 6; ++k) s -= L[6 * i + k] * z[k];
+            z[i] = s / L[6 * i + i];
+        }
+        for (int i = 0; i < 6; ++i) Ai[6 * i + j] = z[i];
+    }
+    return 0;
+}
+
+int oracle_icp_cov_sandwich(const float* data, int64_t nd, const float* model, int64_t nm, const float T6[6],
+                            double cov6[36], double cov3[9]) {
+    if (nd < 1 || nm < 1) return -1;
+    const double a = (double)atan2f(T6[3], T6[0]);   /* cov :31 yaw = atan2f(T10, T00) */
+    const double ca = cos(a), sa = sin(a), x = T6[2], y = T6[5];
+    const int64_t nh = nd < nm ? nd : nm, nb = nh < 200 ? nh : 200;
+    double H[36] = {0}, M[36] = {0}, Hs[36], Bk[36];
+    for (int64_t s = 0; s < nh; ++s) {
+        cov6_point(ca, sa, x, y, data[2 * s], data[2 * s + 1], model[2 * s], model[2 * s + 1], Hs, Bk);
+        for (int k = 0; k < 36; ++k) H[k] += Hs[k];
+        if (s < nb)
+            for (int i = 0; i < 6; ++i)
+                for (int j = 0; j < 6; ++j) {
+                    double acc = 0.0;
+                    for (int k = 0; k < 6; ++k) acc += Bk[6 * i + k] * Bk[6 * j + k];
+                    M[6 * i + j] += acc;
+                }
+    }
+    double Hi[36], T1[36];
+    if (inv6(H, Hi)) return -2;
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < 6; ++k) acc += Hi[6 * i + k] * M[6 * k + j];
+            T1[6 * i + j] = acc;
+        }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double acc = 0.0;
+            for (int k = 0; k < 6; ++k) acc += T1[6 * i + k] * Hi[6 * k + j];
+            cov6[6 * i + j] = 0.01 * acc;
+        }
+    static const int ix[3] = {0, 1, 3};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) cov3[3 * i + j] = cov6[6 * ix[i] + ix[j]];
+    return 0;
+}

@@ -60,6 +60,8 @@ double oracle_graph_error(const double* poses, const dpg_factor* f, int64_t nf);
 int oracle_optimize_graph(double* poses, int64_t n_nodes, const dpg_factor* f, int64_t nf,
                           const dpg_gn_params* gp, dpg_gn_stats* st);
 /* One linear solve H delta = -g at the given poses (for solver-level parity tests). */
+int oracle_icp_cov_sandwich(const float* data, int64_t nd, const float* model, int64_t nm, const float T6[6],
+                            double cov6[36], double cov3[9]);
 int oracle_gn_delta(const double* poses, int64_t n_nodes, const dpg_factor* f, int64_t nf,
                     double* delta, double* error);
 

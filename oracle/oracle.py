@@ -133,6 +133,19 @@ def icp_cov(data, model, T6, vx=0.5, vy=0.5, vth=0.3, literal=False):
     return cov.reshape(3, 3), hess.reshape(3, 3)
 
 
+def icp_cov_sandwich(data, model, T4):
+    """The commented-out 6x6 sandwich (cov :553-566): (cov6 [6, 6], cov3 [3, 3]); T4 row-major 4x4."""
+    d, m = _f32(data).reshape(-1, 2), _f32(model).reshape(-1, 2)
+    T = np.asarray(T4, np.float32).reshape(4, 4)
+    T6 = np.ascontiguousarray([T[0, 0], T[0, 1], T[0, 3], T[1, 0], T[1, 1], T[1, 3]], np.float32)
+    cov6, cov3 = np.zeros(36), np.zeros(9)
+    rc = lib().oracle_icp_cov_sandwich(_p(d, C.c_float), len(d), _p(m, C.c_float), len(m), _p(T6, C.c_float),
+                                       _p(cov6, C.c_double), _p(cov3, C.c_double))
+    if rc:
+        raise ValueError(f"oracle_icp_cov_sandwich failed ({rc})")
+    return cov6.reshape(6, 6), cov3.reshape(3, 3)
+
+
 def run_icp(src_full, tgt_full, pose_src, pose_tgt, params=None, nn=NN_GRID):
     from dpgslam import _abi
     p = params or _abi.default_icp_params()

@@ -9,6 +9,11 @@
                       seeded random inputs with b = c = 0 (T20 = T21 = 0, T22 = 1) and z = 0.
                       Needs /root/reference (read as text, evaluated as arithmetic); the inputs
                       and outputs are stored so the tests never read the reference.
+  cov6_expr.npz       the same for ALL 36 d2J_dX2 entries and all 36 d2J_dZdX entries of one
+                      point (:45-281, :311-528), in the reference's row/column layout, and the
+                      commented-out 6x6 sandwich (:553-566) over seeded clouds: d2J_dX2 summed
+                      over every index pair, d2J_dZdX over the first min(n, 200), cov_z = 0.01 I,
+                      bigger = inv(H) B cov_z B^T inv(H) and its [x, y, yaw] block (:563-566).
 
 Run from the repo root:  PYTHONPATH=.:dpg-slam_amd python tests/golden/make_golden.py
 """
@@ -71,6 +76,77 @@ def make_cov_expr():
     print("cov_expr.npz written")
 
 
+X_NAMES = ["x", "y", "z", "a", "b", "c"]
+Z_NAMES = ["pix", "piy", "piz", "qix", "qiy", "qiz"]
+
+
+def _h_name(i, j):
+    """The reference's variable in row i, column j of d2J_dX2_temp (:271-279)."""
+    if i == j:
+        return f"d2J_d{X_NAMES[i]}2"
+    return f"d2J_d{X_NAMES[j]}d{X_NAMES[i]}"
+
+
+def make_cov6():
+    if not os.path.exists(REF_COV):
+        print("reference not mounted; cov6_expr.npz kept as is")
+        return
+    src = open(REF_COV).read()
+    hx = {(i, j): _expr(src, _h_name(i, j)) for i in range(6) for j in range(6)}
+    bx = {(i, j): _expr(src, f"d2J_d{Z_NAMES[j]}_d{X_NAMES[i]}") for i in range(6) for j in range(6)}
+
+    def ev(e, env):
+        return np.asarray(eval(e, {"__builtins__": {}}, env), np.float64)   # arithmetic only
+
+    def blocks(pts_p, pts_q, a, x, y):
+        n = len(pts_p)
+        env = {"a": np.full(n, a), "x": np.full(n, x), "y": np.full(n, y), "b": np.zeros(n), "c": np.zeros(n),
+               "z": np.zeros(n), "pix": pts_p[:, 0], "piy": pts_p[:, 1], "piz": np.zeros(n), "qix": pts_q[:, 0],
+               "qiy": pts_q[:, 1], "qiz": np.zeros(n), "sin": np.sin, "cos": np.cos, "pow": np.power}
+        H = np.zeros((n, 6, 6))
+        B = np.zeros((n, 6, 6))
+        for (i, j), e in hx.items():
+            H[:, i, j] = ev(e, env)
+        for (i, j), e in bx.items():
+            B[:, i, j] = ev(e, env)
+        return H, B
+
+    rng = np.random.default_rng(20260315)
+    out = {}
+    # per point, 400 random inputs
+    n = 400
+    a = rng.uniform(-np.pi, np.pi, n)
+    x, y = rng.normal(0, 2, n), rng.normal(0, 2, n)
+    P, Q = rng.normal(0, 10, (n, 2)), rng.normal(0, 10, (n, 2))
+    Hs, Bs = np.zeros((n, 6, 6)), np.zeros((n, 6, 6))
+    for k in range(n):
+        h, bb = blocks(P[k:k + 1], Q[k:k + 1], a[k], x[k], y[k])
+        Hs[k], Bs[k] = h[0], bb[0]
+    out.update({"pt_a": a, "pt_x": x, "pt_y": y, "pt_p": P, "pt_q": Q, "pt_H": Hs, "pt_B": Bs})
+    # sandwiches: float clouds as calculate_ICP_COV receives them, a planar float transform
+    for c, (nd, nm) in enumerate([(300, 280), (150, 150), (1000, 1200)]):
+        p = rng.normal(0, 8, (nd, 2)).astype(np.float32)
+        q = (p[:nm] if nm <= nd else np.concatenate([p, rng.normal(0, 8, (nm - nd, 2)).astype(np.float32)]))
+        q = (q + rng.normal(0, 0.05, q.shape)).astype(np.float32)
+        th = np.float32(rng.uniform(-0.5, 0.5))
+        T = np.eye(4, dtype=np.float32)
+        T[0, 0], T[0, 1], T[1, 0], T[1, 1] = np.cos(th), -np.sin(th), np.sin(th), np.cos(th)
+        T[0, 3], T[1, 3] = np.float32(rng.normal(0, 0.3)), np.float32(rng.normal(0, 0.3))
+        yaw = float(np.arctan2(T[1, 0], T[0, 0]).astype(np.float32))   # atan2f; the oracle restates it exactly
+        nh, nb = min(nd, nm), min(nd, nm, 200)
+        h, _ = blocks(p[:nh].astype(np.float64), q[:nh].astype(np.float64), yaw, float(T[0, 3]), float(T[1, 3]))
+        _, bb = blocks(p[:nb].astype(np.float64), q[:nb].astype(np.float64), yaw, float(T[0, 3]), float(T[1, 3]))
+        H = h.sum(0)
+        Bm = np.concatenate(list(bb), axis=1)   # 6 x 6 nb, block k = point k
+        Hi = np.linalg.inv(H)
+        big = Hi @ Bm @ (0.01 * np.eye(6 * nb)) @ Bm.T @ Hi
+        out.update({f"s{c}_p": p, f"s{c}_q": q, f"s{c}_T": T, f"s{c}_yaw": np.float64(yaw), f"s{c}_H": H,
+                    f"s{c}_M": Bm @ Bm.T, f"s{c}_cov6": big, f"s{c}_cov3": big[np.ix_([0, 1, 3], [0, 1, 3])]})
+    np.savez_compressed(os.path.join(HERE, "cov6_expr.npz"), **out)
+    print("cov6_expr.npz written")
+
+
 if __name__ == "__main__":
     make_config1()
     make_cov_expr()
+    make_cov6()
