@@ -246,8 +246,10 @@ def main_dynamic(args):
     orc, cpu_calls, mismatches = None, [], 0
     if do_cpu:
         from oracle import oracle as O
-    node_ms, add_icp_ms, add_upd_ms, dpg = [], [], [], []
+    node_ms, add_icp_ms, add_upd_ms, dpg, add_split, prof = [], [], [], [], [], []
     sweeps, active_end, replay_s, pass_tot = [], [], 0.0, {}
+    import ctypes as C
+    L, pbuf = _abi.lib(), (C.c_double * 8)()
     amin, amax, rmax = (float(x) for x in w.geom[0])
     t_run = time.perf_counter()
     for p in range(P):
@@ -277,6 +279,10 @@ def main_dynamic(args):
             la = slam.be.last_add
             add_icp_ms.append(la.ms_icp)
             add_upd_ms.append(la.update.ms_total)
+            add_split.append((la.update.ms_symbolic, la.update.ms_numeric))
+            if p == P - 1:   # the last pass: where the symbolic host time goes
+                L.dpg_inc_last_profile(C.c_void_p(slam.be.inc.handle), pbuf, 8)
+                prof.append(list(pbuf)[:6])
             if p >= 1 and slam.last_dpg is not None:
                 d = slam.last_dpg
                 dpg.append((int(d.n_candidates), float(d.ms_total), int(d.n_submap_nodes)))
@@ -363,7 +369,12 @@ def main_dynamic(args):
         "wall_s": wall, "nodes_per_pass": [int(np.sum(created == q)) for q in range(P)],
         "node_ms": {"p50": float(np.median(node_ms)), "p90": float(np.percentile(node_ms, 90)),
                     "mean": float(np.mean(node_ms)), "icp_mean": float(np.mean(add_icp_ms)),
-                    "update_mean": float(np.mean(add_upd_ms))},
+                    "update_mean": float(np.mean(add_upd_ms)),
+                    "update_symbolic_mean": float(np.mean([a for a, _ in add_split])),
+                    "update_numeric_mean": float(np.mean([b for _, b in add_split])),
+                    "last_pass_symbolic_parts": dict(zip(("incsym", "derive", "lists_upload", "chol_build", "chol_host",
+                                                          "chol_upload"), np.round(np.mean(prof, 0), 4).tolist()))
+                    if prof else None},
         "dpg": {"calls": len(dpg_a), "ms_per_call": float(dpg_a[:, 1].mean()) if len(dpg_a) else None,
                 "calls_per_s": float(1e3 / dpg_a[:, 1].mean()) if len(dpg_a) else None,
                 "candidates_mean": float(dpg_a[:, 0].mean()) if len(dpg_a) else None,

@@ -54,8 +54,15 @@ struct dpg_chol_incsym {
     int64_t n = 0, words = 0;               // nodes, 64-bit words per pattern row (capacity)
     std::vector<int32_t> perm, pos;         // elimination order
     std::vector<uint64_t> bits;             // [n][words]: later positions in column p's pattern
+    int64_t swords = 0;                     // summary words per row: (words + 63) / 64
+    std::vector<uint64_t> summ;             // [n][swords]: bit w set when bits word w may be nonzero
     std::vector<int32_t> parent;            // elimination-tree parent position (-1: root)
     int64_t nnz = 0;                        // pattern entries (blocks below the diagonal)
+    // the same patterns in CSR form (column p: rows[cp[p] .. cp[p + 1]), sorted), as of the last
+    // derive, and the entries added since (merged in by the next derive)
+    std::vector<int64_t> cp;
+    std::vector<int32_t> rows, rows_tmp;
+    std::vector<std::pair<int32_t, int32_t>> added;
 };
 // a fresh minimum-degree order of the graph (pairs) -> state
 int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
@@ -64,14 +71,18 @@ void dpg_incsym_append(dpg_chol_incsym* I, int64_t k);
 // edge (a, b) of the graph (nodes); returns the number of pattern entries it added (fill)
 int64_t dpg_incsym_add_edge(dpg_chol_incsym* I, int32_t a, int32_t b);
 // the derived structures of the current state
-int dpg_incsym_derive(const dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S);
+int dpg_incsym_derive(dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S);
 
 
 // GPU solver structures (dpg_chol.hip) for a given symbolic analysis; *h is reused -- its device
-// buffers grow only when needed -- or created when NULL.  On error *h is destroyed and NULL.
+// buffers grow only when needed -- or created when NULL.  On error *h is destroyed and NULL.  The
+// analysis is moved into *h: *S is left holding *h's previous one (or nothing).
 int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                        const dpg_chol_sym* S);
+                        dpg_chol_sym* S);
 // host time (ms) of the last build of h: structures, uploads
 void dpg_chol_build_times(void* h, double out[2]);
+// the host half of a build alone (no device calls; tools/incsym_bench.cpp times it on the CPU)
+int dpg_chol_plan_host(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                       const dpg_chol_sym* S, double* ms);
 
 #endif

@@ -1347,13 +1347,6 @@ int dreserve(T** d, size_t* cap, size_t n) {
     *cap = nc;
     return DPG_OK;
 }
-template <typename T>
-int dalloc_copy(T** d, size_t* cap, const std::vector<T>& h) {
-    if (dreserve(d, cap, h.size())) return DPG_ERR_HIP;
-    if (!h.empty() && hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-        return DPG_ERR_HIP;
-    return DPG_OK;
-}
 
 struct CholDev {
     dpg_chol_sym sym;
@@ -1363,7 +1356,6 @@ struct CholDev {
     int32_t* child_list = nullptr;
     int32_t* relmap = nullptr;
     int32_t* rows = nullptr;
-    int32_t* level_list = nullptr;
     int32_t* perm = nullptr;
     int32_t* pos = nullptr;
     double* fronts = nullptr;
@@ -1397,10 +1389,12 @@ struct CholDev {
     size_t lds_fused = 0;
     bool fused_db = true;
     // capacities (elements) of the device buffers above, for rebuilds
-    size_t c_sns = 0, c_omap = 0, c_child = 0, c_relmap = 0, c_rows = 0, c_level = 0, c_perm = 0, c_pos = 0,
-           c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_asm_t = 0, c_asm_c = 0, c_panel = 0,
-           c_upd = 0, c_fwd = 0, c_fac = 0, c_ftasks = 0, c_fchild = 0, c_bwd = 0, c_sync = 0;
+    size_t c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_sync = 0;
     double t_build[2] = {0, 0};   // last chol_build: host structures, uploads (ms)
+    char* stage = nullptr;        // pinned staging buffer of the uploads
+    size_t c_stage = 0;
+    char* arena = nullptr;        // device: every structure array above (sns .. upd_tasks), one copy
+    size_t c_arena = 0;
 };
 
 }  // namespace
@@ -1408,11 +1402,11 @@ struct CholDev {
 extern "C" void dpg_chol_destroy(void* h) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!c) return;
-    void* ptrs[] = {c->sns, c->omap, c->child_list, c->relmap, c->rows, c->level_list, c->perm, c->pos,
-                    c->fronts, c->acc, c->ysol, c->xsol, c->status, c->asm_tasks, c->asm_child, c->panel_tasks, c->upd_tasks,
-                    c->order_fwd, c->order_bwd, c->sync, c->order_fac, c->ftasks, c->fchild};
+    // (the structure arrays live in c->arena)
+    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
+    if (c->stage) (void)hipHostFree(c->stage);
     delete c;
 }
 
@@ -1438,9 +1432,9 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
 
 // The same from a given symbolic analysis; *h is reused (its buffers grow when needed) or created.
 int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                        const dpg_chol_sym* S) {
+                        dpg_chol_sym* S) {
     CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
-    c->sym = *S;
+    std::swap(c->sym, *S);   // *S gets the previous analysis (its buffers are reused by the next derive)
     const int rc = chol_build(c, n, pair_lo, pair_hi, n_pairs);
     if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
     *h = c;
@@ -1454,52 +1448,155 @@ double wall_ms() {
     return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
 }
 
-int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
-    const double t_b0 = wall_ms();
+// host-side structures of one build (kept between builds: the incremental graph rebuilds per update)
+struct CholHost {
+    struct Blk { int32_t row, u, tr; };   // an upper block of H in its column's bucket
+    std::vector<int64_t> colptr;
+    std::vector<Blk> ent;
+    std::vector<int32_t> lidx, lstamp;
+    std::vector<int64_t> om_ptr, om_cur;
+    std::vector<OEnt> omap;
+    std::vector<SnDev> sns;
+    std::vector<FTask> ftasks;
+    std::vector<FChild> fchild;
+    std::vector<double> prio;
+    std::vector<std::pair<double, int32_t>> key;
+    std::vector<int32_t> fo, bwd, order_fac, cuts;
+    std::vector<AsmTask> asm_t;
+    std::vector<AsmChild> asm_c;
+    std::vector<int2> panel_t;
+    std::vector<int4> upd_t;
+    int64_t acc_total = 0;
+};
+
+#ifdef DPG_PLAN_TIMING
+double g_plan_t[8];
+#define PLAN_T(k) g_plan_t[k] += wall_ms()
+#else
+#define PLAN_T(k) do { } while (0)
+#endif
+
+// A child's update rows j = 0 .. 3r-1 land in parent front row 3 rm[j / 3] + j % 3, increasing in
+// j: the first j landing at or after parent row c.
+inline int32_t first_at_or_after(const int32_t* rm, int32_t r, int32_t c) {
+    int32_t lo = 0, hi = 3 * r;
+    while (lo < hi) {
+        const int32_t mid = (lo + hi) / 2;
+        if (3 * rm[mid / 3] + mid % 3 < c) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Host half of chol_build: every device structure, in H; the plan fields of c.
+int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, CholHost& H) {
     const dpg_chol_sym& S = c->sym;
     c->lds_fused = 0;
     c->n_launches = 0;
     c->n = n;
     c->nnzb_upper = n + n_pairs;
+    PLAN_T(0);
     // omap: every upper block of H -> (front, local block row, local block col, transpose), grouped
-    // by front (counting sort), each front's entries by (column, row)
-    auto local_index = [&](int32_t s, int32_t p) -> int32_t {
-        const int32_t c0 = S.sn_c0[(size_t)s], k = S.sn_c0[(size_t)s + 1] - c0;
-        if (p >= c0 && p < c0 + k) return p - c0;
-        const int32_t* b = S.sn_rows.data() + S.sn_rows_ptr[(size_t)s];
-        const int32_t* e = S.sn_rows.data() + S.sn_rows_ptr[(size_t)s + 1];
-        const int32_t* it = std::lower_bound(b, e, p);
-        if (it == e || *it != p) return -1;
-        return k + (int32_t)(it - b);
-    };
-    auto front_of_pair = [&](int64_t q) { return S.sn_of[(size_t)std::min(S.pos[(size_t)pair_lo[q]], S.pos[(size_t)pair_hi[q]])]; };
-    std::vector<int64_t> om_ptr((size_t)S.ns + 1, 0);
-    for (int64_t v = 0; v < n; ++v) om_ptr[(size_t)S.sn_of[(size_t)S.pos[(size_t)v]] + 1]++;
-    for (int64_t q = 0; q < n_pairs; ++q) om_ptr[(size_t)front_of_pair(q) + 1]++;
-    for (int32_t s = 0; s < S.ns; ++s) om_ptr[(size_t)s + 1] += om_ptr[(size_t)s];
-    std::vector<OEnt> omap((size_t)om_ptr[(size_t)S.ns]);
+    // by front, each front's entries by (column, row): the blocks are bucketed by column position
+    // (counting sort), each bucket sorted by row, and the fronts walked column by column
+    std::vector<int64_t>& colptr = H.colptr;
+    colptr.assign((size_t)n + 1, 0);
+    for (int64_t p = 0; p < n; ++p) colptr[(size_t)p + 1] = 1;   // the diagonal block
+    for (int64_t q = 0; q < n_pairs; ++q)
+        colptr[(size_t)std::min(S.pos[(size_t)pair_lo[q]], S.pos[(size_t)pair_hi[q]]) + 1]++;
+    for (int64_t p = 0; p < n; ++p) colptr[(size_t)p + 1] += colptr[(size_t)p];
+    std::vector<CholHost::Blk>& ent = H.ent;
+    ent.resize((size_t)colptr[(size_t)n]);
     {
-        std::vector<int64_t> cur(om_ptr.begin(), om_ptr.end() - 1);
-        for (int64_t v = 0; v < n; ++v) {
-            const int32_t p = S.pos[(size_t)v], s = S.sn_of[(size_t)p];
-            const int32_t l = local_index(s, p);
-            omap[(size_t)cur[(size_t)s]++] = OEnt{(int32_t)v, (int16_t)l, (int16_t)l, 0, 0};
-        }
+        std::vector<int64_t>& cur = H.om_cur;
+        cur.assign(colptr.begin(), colptr.end() - 1);
+        for (int64_t p = 0; p < n; ++p) ent[(size_t)cur[(size_t)p]++] = CholHost::Blk{(int32_t)p, S.perm[(size_t)p], 0};
         for (int64_t q = 0; q < n_pairs; ++q) {
             const int32_t plo = S.pos[(size_t)pair_lo[q]], phi = S.pos[(size_t)pair_hi[q]];
-            const int32_t later = plo > phi ? plo : phi, earlier = plo > phi ? phi : plo;
-            const int32_t s = S.sn_of[(size_t)earlier];
-            const int32_t a = local_index(s, later), b = local_index(s, earlier);
-            if (a < 0 || b < 0) return DPG_ERR_NUMERIC;
             // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
-            omap[(size_t)cur[(size_t)s]++] = OEnt{(int32_t)(n + q), (int16_t)a, (int16_t)b, plo > phi ? 0 : 1, 0};
+            ent[(size_t)cur[(size_t)std::min(plo, phi)]++] =
+                CholHost::Blk{std::max(plo, phi), (int32_t)(n + q), plo > phi ? 0 : 1};
+        }
+        for (int64_t p = 0; p < n; ++p) {   // insertion sort by row: buckets hold a few blocks
+            CholHost::Blk* b = ent.data() + colptr[(size_t)p];
+            const int64_t m = colptr[(size_t)p + 1] - colptr[(size_t)p];
+            for (int64_t i = 1; i < m; ++i) {
+                const CholHost::Blk x = b[i];
+                int64_t j = i - 1;
+                while (j >= 0 && b[j].row > x.row) { b[j + 1] = b[j]; --j; }
+                b[j + 1] = x;
+            }
         }
     }
-    for (int32_t s = 0; s < S.ns; ++s)
-        std::sort(omap.begin() + om_ptr[(size_t)s], omap.begin() + om_ptr[(size_t)s + 1],
-                  [](const OEnt& x, const OEnt& y) { return x.b != y.b ? x.b < y.b : x.a < y.a; });
-    std::vector<SnDev> sns((size_t)S.ns);
-    int64_t acc_total = 0;
+    PLAN_T(1);
+    std::vector<int64_t>& om_ptr = H.om_ptr;
+    om_ptr.assign((size_t)S.ns + 1, 0);
+    std::vector<OEnt>& omap = H.omap;
+    omap.resize(ent.size());
+    {
+        std::vector<int32_t>& lidx = H.lidx;
+        std::vector<int32_t>& lst = H.lstamp;
+        lidx.resize((size_t)n);
+        lst.assign((size_t)n, -1);
+        size_t o = 0;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const int32_t c0 = S.sn_c0[(size_t)s], c1 = S.sn_c0[(size_t)s + 1], k = c1 - c0;
+            for (int64_t t = S.sn_rows_ptr[(size_t)s]; t < S.sn_rows_ptr[(size_t)s + 1]; ++t) {
+                lidx[(size_t)S.sn_rows[(size_t)t]] = k + (int32_t)(t - S.sn_rows_ptr[(size_t)s]);
+                lst[(size_t)S.sn_rows[(size_t)t]] = s;
+            }
+            om_ptr[(size_t)s] = (int64_t)o;
+            for (int32_t cpos = c0; cpos < c1; ++cpos)
+                for (int64_t e = colptr[(size_t)cpos]; e < colptr[(size_t)cpos + 1]; ++e) {
+                    const CholHost::Blk& b = ent[(size_t)e];
+                    int32_t a;
+                    if (b.row < c1) a = b.row - c0;
+                    else if (lst[(size_t)b.row] == s) a = lidx[(size_t)b.row];
+                    else return DPG_ERR_NUMERIC;   // the block is outside its front: bad analysis
+                    omap[o++] = OEnt{b.u, (int16_t)a, (int16_t)(cpos - c0), b.tr, 0};
+                }
+        }
+        om_ptr[(size_t)S.ns] = (int64_t)o;
+    }
+#ifdef DPG_PLAN_VERIFY
+    {   // the straightforward construction (binary search per block, per-front sort) must agree
+        std::vector<OEnt> ref;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const int32_t c0 = S.sn_c0[(size_t)s], k = S.sn_c0[(size_t)s + 1] - c0;
+            auto li = [&](int32_t p) -> int32_t {
+                if (p >= c0 && p < c0 + k) return p - c0;
+                const int32_t* b = S.sn_rows.data() + S.sn_rows_ptr[(size_t)s];
+                const int32_t* e = S.sn_rows.data() + S.sn_rows_ptr[(size_t)s + 1];
+                const int32_t* it = std::lower_bound(b, e, p);
+                return (it == e || *it != p) ? -1 : k + (int32_t)(it - b);
+            };
+            const size_t r0 = ref.size();
+            for (int64_t v = 0; v < n; ++v)
+                if (S.sn_of[(size_t)S.pos[(size_t)v]] == s) {
+                    const int32_t l = li(S.pos[(size_t)v]);
+                    ref.push_back(OEnt{(int32_t)v, (int16_t)l, (int16_t)l, 0, 0});
+                }
+            for (int64_t q = 0; q < n_pairs; ++q) {
+                const int32_t plo = S.pos[(size_t)pair_lo[q]], phi = S.pos[(size_t)pair_hi[q]];
+                if (S.sn_of[(size_t)std::min(plo, phi)] != s) continue;
+                ref.push_back(OEnt{(int32_t)(n + q), (int16_t)li(std::max(plo, phi)), (int16_t)li(std::min(plo, phi)),
+                                   plo > phi ? 0 : 1, 0});
+            }
+            std::sort(ref.begin() + r0, ref.end(), [](const OEnt& x, const OEnt& y) { return x.b != y.b ? x.b < y.b : x.a < y.a; });
+            if ((int64_t)r0 != om_ptr[(size_t)s]) { fprintf(stderr, "omap ptr mismatch at front %d\n", s); abort(); }
+        }
+        for (size_t i = 0; i < ref.size(); ++i)
+            if (ref[i].u != omap[i].u || ref[i].a != omap[i].a || ref[i].b != omap[i].b || ref[i].tr != omap[i].tr) {
+                fprintf(stderr, "omap mismatch at %zu\n", i);
+                abort();
+            }
+    }
+#endif
+    PLAN_T(2);
+    std::vector<SnDev>& sns = H.sns;
+    sns.resize((size_t)S.ns);
+    int64_t& acc_total = H.acc_total;
+    acc_total = 0;
     for (int32_t s = 0; s < S.ns; ++s) {
         SnDev& d = sns[(size_t)s];
         d.c0 = S.sn_c0[(size_t)s];
@@ -1523,15 +1620,19 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
     for (int32_t s = 0; s < S.ns; ++s)
         if (sns[(size_t)s].parent >= 0) sns[(size_t)sns[(size_t)s].parent].need += sns[(size_t)s].G;
     // large fronts: per tile, the H blocks (omap range) and the children's column ranges
-    std::vector<FTask> ftasks;
-    std::vector<FChild> fchild;
+    PLAN_T(3);
+    std::vector<FTask>& ftasks = H.ftasks;
+    std::vector<FChild>& fchild = H.fchild;
+    ftasks.clear();
+    fchild.clear();
     for (int32_t s = 0; s < S.ns; ++s) {
         SnDev& d = sns[(size_t)s];
         d.ftask = (int32_t)ftasks.size();
         const int32_t k3 = 3 * d.k, m3 = 3 * (d.k + d.r);
         if (d.G == 1 && m3 <= kSmall && d.nchild <= kMaxCh) continue;
         const OEnt* ob = omap.data() + d.omap_off;
-        std::vector<int32_t> cuts;
+        std::vector<int32_t>& cuts = H.cuts;
+        cuts.clear();
         for (int32_t c = 0; c < k3; c += kFNB) cuts.push_back(c);
         for (int32_t c = k3; c < m3; c += kFNB) cuts.push_back(c);
         cuts.push_back(m3);
@@ -1546,11 +1647,9 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
                 const int32_t ch = S.child_list[(size_t)ci];
                 const SnDev& cd = sns[(size_t)ch];
                 const int32_t* rm = S.relmap.data() + cd.rows_off;
-                int32_t ja = 3 * cd.r, jb = 0;
-                for (int32_t j = 0; j < 3 * cd.r; ++j) {
-                    const int32_t pj = 3 * rm[j / 3] + j % 3;
-                    if (pj >= c0 && pj < c1) { ja = std::min(ja, j); jb = j + 1; }
-                }
+                if (cd.r == 0 || 3 * rm[cd.r - 1] + 2 < c0 || 3 * rm[0] >= c1) continue;   // misses the tile
+                const int32_t ja = first_at_or_after(rm, cd.r, c0);
+                const int32_t jb = first_at_or_after(rm, cd.r, c1);
                 if (jb > ja) fchild.push_back(FChild{ja, jb, cd.k, cd.r, cd.front_off, cd.rows_off});
             }
             ft.ch_cnt = (int32_t)fchild.size() - ft.ch_off;
@@ -1561,19 +1660,68 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
     // estimated time plus its parent's priority (the longest remaining path to the root), so
     // sorting by descending priority is topological (children first) and starts the long chains
     // before the bulk of the leaves
-    std::vector<double> prio((size_t)S.ns, 0.0);
+#ifdef DPG_PLAN_VERIFY
+    {   // the child column ranges by a linear scan must agree
+        size_t fi = 0;
+        for (int32_t s = 0; s < S.ns; ++s) {
+            const SnDev& d = sns[(size_t)s];
+            const int32_t k3 = 3 * d.k, m3 = 3 * (d.k + d.r);
+            if (d.G == 1 && m3 <= kSmall && d.nchild <= kMaxCh) continue;
+            std::vector<int32_t> cu;
+            for (int32_t c = 0; c < k3; c += kFNB) cu.push_back(c);
+            for (int32_t c = k3; c < m3; c += kFNB) cu.push_back(c);
+            cu.push_back(m3);
+            for (size_t t = 0; t + 1 < cu.size(); ++t)
+                for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
+                    const SnDev& cd = sns[(size_t)S.child_list[(size_t)ci]];
+                    const int32_t* rm = S.relmap.data() + cd.rows_off;
+                    int32_t ja = 3 * cd.r, jb = 0;
+                    for (int32_t j = 0; j < 3 * cd.r; ++j) {
+                        const int32_t pj = 3 * rm[j / 3] + j % 3;
+                        if (pj >= cu[t] && pj < cu[t + 1]) { ja = std::min(ja, j); jb = j + 1; }
+                    }
+                    if (jb > ja) {
+                        if (fi >= fchild.size() || fchild[fi].ja != ja || fchild[fi].jb != jb) {
+                            fprintf(stderr, "fchild mismatch at %zu\n", fi);
+                            abort();
+                        }
+                        ++fi;
+                    }
+                }
+        }
+        if (fi != fchild.size()) { fprintf(stderr, "fchild count mismatch\n"); abort(); }
+    }
+#endif
+    PLAN_T(4);
+    std::vector<double>& prio = H.prio;
+    prio.assign((size_t)S.ns, 0.0);
     for (int32_t s = S.ns - 1; s >= 0; --s) {
         const SnDev& d = sns[(size_t)s];
         const int32_t m3 = 3 * (d.k + d.r);
         const double est = d.G == 1 ? 4.0 + 0.05 * m3 : 10.0 + 20.0 * ((3 * d.k + kFNB - 1) / kFNB);
         prio[(size_t)s] = est + (d.parent >= 0 ? prio[(size_t)d.parent] : 0.0);
     }
-    std::vector<int32_t> fo(S.level_list.begin(), S.level_list.end());
-    std::stable_sort(fo.begin(), fo.end(), [&](int32_t a, int32_t b) { return prio[(size_t)a] > prio[(size_t)b]; });
-    std::vector<int32_t> order_fac;
+    // (descending priority, ties in level-list order)
+    std::vector<std::pair<double, int32_t>>& key = H.key;
+    key.resize((size_t)S.ns);
+    for (int32_t i = 0; i < S.ns; ++i) key[(size_t)i] = {-prio[(size_t)S.level_list[(size_t)i]], i};
+    std::sort(key.begin(), key.end());
+    std::vector<int32_t>& fo = H.fo;
+    fo.resize((size_t)S.ns);
+    for (int32_t i = 0; i < S.ns; ++i) fo[(size_t)i] = S.level_list[(size_t)key[(size_t)i].second];
+#ifdef DPG_PLAN_VERIFY
+    {
+        std::vector<int32_t> ref(S.level_list.begin(), S.level_list.end());
+        std::stable_sort(ref.begin(), ref.end(), [&](int32_t a, int32_t b) { return prio[(size_t)a] > prio[(size_t)b]; });
+        if (ref != fo) { fprintf(stderr, "front order mismatch\n"); abort(); }
+    }
+#endif
+    std::vector<int32_t>& order_fac = H.order_fac;
+    order_fac.clear();
     for (int32_t s : fo)
         for (int32_t m = 0; m < sns[(size_t)s].G; ++m) order_fac.push_back(s * 64 + m);
     c->n_tickets = (int64_t)order_fac.size();
+    PLAN_T(5);
     c->level_ptr = S.level_ptr;
     // assembly tiles of front s, `ct` columns each: the omap range and the children (with their
     // contiguous column range) that land in the tile
@@ -1592,12 +1740,8 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
             for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
                 const int32_t ch = S.child_list[(size_t)ci];
                 const SnDev& cd = sns[(size_t)ch];
-                const int32_t* rm = S.relmap.data() + cd.rows_off;
-                int32_t ja = 3 * cd.r, jb = 0;
-                for (int32_t j = 0; j < 3 * cd.r; ++j) {
-                    const int32_t pj = 3 * rm[j / 3] + j % 3;
-                    if (pj >= c0 && pj < c1) { ja = std::min(ja, j); jb = j + 1; }
-                }
+                const int32_t ja = first_at_or_after(S.relmap.data() + cd.rows_off, cd.r, c0);
+                const int32_t jb = first_at_or_after(S.relmap.data() + cd.rows_off, cd.r, c1);
                 if (jb > ja) cl.push_back(AsmChild{ch, ja, jb, 0});
             }
             t.ch_cnt = (int32_t)cl.size() - t.ch_off;
@@ -1626,10 +1770,14 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
         c->lds_solve_max = std::max(c->lds_solve_max, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
     }
     if (c->lds_solve_max > 160 * 1024) return DPG_ERR_SIZE;
-    std::vector<AsmTask> asm_t;
-    std::vector<AsmChild> asm_c;
-    std::vector<int2> panel_t;
-    std::vector<int4> upd_t;
+    std::vector<AsmTask>& asm_t = H.asm_t;
+    std::vector<AsmChild>& asm_c = H.asm_c;
+    std::vector<int2>& panel_t = H.panel_t;
+    std::vector<int4>& upd_t = H.upd_t;
+    asm_t.clear();
+    asm_c.clear();
+    panel_t.clear();
+    upd_t.clear();
     c->plan.clear();
     if (!c->fused) {
         // level-synchronous path: per level, assembly tiles, then panel + update steps
@@ -1674,45 +1822,113 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
             if (L.lds_asm > 160 * 1024) return DPG_ERR_SIZE;
         }
     }
-    const double t_b1 = wall_ms();
-    int rc = 0;
-    rc |= dalloc_copy(&c->sns, &c->c_sns, sns);
-    rc |= dalloc_copy(&c->omap, &c->c_omap, omap);
-    rc |= dalloc_copy(&c->child_list, &c->c_child, S.child_list);
-    rc |= dalloc_copy(&c->relmap, &c->c_relmap, S.relmap);
-    rc |= dalloc_copy(&c->rows, &c->c_rows, S.sn_rows);
-    rc |= dalloc_copy(&c->perm, &c->c_perm, S.perm);
-    rc |= dalloc_copy(&c->pos, &c->c_pos, S.pos);
-    {
-        // solves: the critical-path order (children first), and its reverse (parents first)
-        std::vector<int32_t> bwd(fo.rbegin(), fo.rend());
-        rc |= dalloc_copy(&c->order_fwd, &c->c_fwd, fo);
-        rc |= dalloc_copy(&c->order_fac, &c->c_fac, order_fac);
-        rc |= dalloc_copy(&c->ftasks, &c->c_ftasks, ftasks);
-        rc |= dalloc_copy(&c->fchild, &c->c_fchild, fchild);
-        rc |= dalloc_copy(&c->order_bwd, &c->c_bwd, bwd);
-        // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
-        //  pivot-tile hand-off flags [per large-front tile]]
-        c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
-        rc |= dreserve(&c->sync, &c->c_sync, c->sync_bytes / sizeof(int32_t));
-    }
+    // solves: the critical-path order (children first), and its reverse (parents first)
+    PLAN_T(6);
+    H.bwd.assign(fo.rbegin(), fo.rend());
+    // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
+    //  pivot-tile hand-off flags [per large-front tile]]
+    c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
+    PLAN_T(7);
+    return DPG_OK;
+}
+
+// The structure arrays are packed into one pinned staging buffer and go up in ONE asynchronous
+// copy into one device arena (the pointers of c point into it); one synchronisation at the end.
+int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
+    const dpg_chol_sym& S = c->sym;
+    auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+    struct Piece { void** d; const void* h; size_t bytes; };
+    Piece pieces[16];
+    int np = 0;
+    auto add = [&](auto** d, const auto& h) {
+        using T = typename std::remove_reference<decltype(h)>::type::value_type;
+        pieces[np++] = Piece{reinterpret_cast<void**>(d), h.data(), h.size() * sizeof(T)};
+    };
+    add(&c->sns, H.sns);
+    add(&c->omap, H.omap);
+    add(&c->child_list, S.child_list);
+    add(&c->relmap, S.relmap);
+    add(&c->rows, S.sn_rows);
+    add(&c->perm, S.perm);
+    add(&c->pos, S.pos);
+    add(&c->order_fwd, H.fo);
+    add(&c->order_fac, H.order_fac);
+    add(&c->ftasks, H.ftasks);
+    add(&c->fchild, H.fchild);
+    add(&c->order_bwd, H.bwd);
     if (!c->fused) {
-        rc |= dalloc_copy(&c->asm_tasks, &c->c_asm_t, asm_t);
-        rc |= dalloc_copy(&c->asm_child, &c->c_asm_c, asm_c);
-        rc |= dalloc_copy(&c->panel_tasks, &c->c_panel, panel_t);
-        rc |= dalloc_copy(&c->upd_tasks, &c->c_upd, upd_t);
+        add(&c->asm_tasks, H.asm_t);
+        add(&c->asm_child, H.asm_c);
+        add(&c->panel_tasks, H.panel_t);
+        add(&c->upd_tasks, H.upd_t);
     }
+    size_t total = 0;
+    for (int i = 0; i < np; ++i) total += al(std::max<size_t>(pieces[i].bytes, 1));
+    if (total > c->c_stage) {
+        if (c->stage) (void)hipHostFree(c->stage);
+        c->stage = nullptr;
+        const size_t want = std::max(total, c->c_stage + c->c_stage / 2);
+        c->c_stage = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->stage), want) != hipSuccess) return DPG_ERR_HIP;
+        c->c_stage = want;
+    }
+    if (total > c->c_arena) {
+        if (c->arena) (void)hipFree(c->arena);
+        c->arena = nullptr;
+        const size_t want = std::max(total, c->c_arena + c->c_arena / 2);
+        c->c_arena = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&c->arena), want) != hipSuccess) return DPG_ERR_HIP;
+        c->c_arena = want;
+    }
+    size_t off = 0;
+    for (int i = 0; i < np; ++i) {
+        if (pieces[i].bytes) memcpy(c->stage + off, pieces[i].h, pieces[i].bytes);
+        *pieces[i].d = c->arena + off;
+        off += al(std::max<size_t>(pieces[i].bytes, 1));
+    }
+    int rc = hipMemcpyAsync(c->arena, c->stage, total, hipMemcpyHostToDevice, nullptr) != hipSuccess;
+    rc |= dreserve(&c->sync, &c->c_sync, c->sync_bytes / sizeof(int32_t));
     rc |= dreserve(&c->fronts, &c->c_fronts, (size_t)S.front_off[(size_t)S.ns]);
-    rc |= dreserve(&c->acc, &c->c_acc, (size_t)acc_total);
+    rc |= dreserve(&c->acc, &c->c_acc, (size_t)H.acc_total);
     rc |= dreserve(&c->ysol, &c->c_ysol, (size_t)(3 * n));
     rc |= dreserve(&c->xsol, &c->c_xsol, (size_t)(3 * n));
     rc |= dreserve(&c->status, &c->c_status, 1);
-    if (!rc) rc |= hipMemset(c->status, 0, sizeof(int32_t)) != hipSuccess;
-    c->t_build[0] = t_b1 - t_b0;
-    c->t_build[1] = wall_ms() - t_b1;
+    if (!rc) rc |= hipMemsetAsync(c->status, 0, sizeof(int32_t), nullptr) != hipSuccess;
+    // the staging buffer is reused by the next build: wait for the copy (always, even after an error)
+    rc |= hipStreamSynchronize(nullptr) != hipSuccess;
     return rc ? DPG_ERR_HIP : DPG_OK;
 }
+
+int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
+    thread_local CholHost H;
+    const double t_b0 = wall_ms();
+    int rc = chol_plan(c, n, pair_lo, pair_hi, n_pairs, H);
+    if (rc) return rc;
+    const double t_b1 = wall_ms();
+    rc = chol_upload(c, n, H);
+    c->t_build[0] = t_b1 - t_b0;
+    c->t_build[1] = wall_ms() - t_b1;
+    return rc;
+}
 }  // namespace
+
+#ifdef DPG_PLAN_TIMING
+double dpg_plan_t_export[8];
+#endif
+// host half of a build alone (no device calls), for CPU timing of the incremental rebuild
+int dpg_chol_plan_host(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                       const dpg_chol_sym* S, double* ms) {
+    thread_local CholHost H;
+    thread_local CholDev c;
+    c.sym = *S;
+    const double t0 = wall_ms();
+    const int rc = chol_plan(&c, n, pair_lo, pair_hi, n_pairs, H);
+    if (ms) *ms = wall_ms() - t0;
+#ifdef DPG_PLAN_TIMING
+    for (int k = 0; k < 8; ++k) dpg_plan_t_export[k] = g_plan_t[k];
+#endif
+    return rc;
+}
 
 void dpg_chol_build_times(void* h, double out[2]) {
     const CholDev* c = reinterpret_cast<const CholDev*>(h);

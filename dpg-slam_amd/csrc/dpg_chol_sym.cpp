@@ -12,6 +12,7 @@
 //      -> front positions, child update matrix rows -> parent front rows
 #include <stdint.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <functional>
@@ -28,10 +29,15 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
                 std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pattern) {
     const int64_t W = (n + 63) / 64;
     std::vector<uint64_t> bits((size_t)(n * W), 0ull);
+    // [wlo, whi): a word range of each row holding all its set bits (pose-graph neighbourhoods are
+    // mostly local in node id, so the row operations below touch few words)
+    std::vector<int32_t> wlo((size_t)n, (int32_t)W), whi((size_t)n, 0);
     for (int64_t v = 0; v < n; ++v)
         for (int64_t q = aptr[v]; q < aptr[v + 1]; ++q) {
             const int32_t u = adj[(size_t)q];
             bits[(size_t)(v * W + u / 64)] |= 1ull << (u % 64);
+            wlo[(size_t)v] = std::min(wlo[(size_t)v], u / 64);
+            whi[(size_t)v] = std::max(whi[(size_t)v], u / 64 + 1);
         }
     std::vector<int32_t> deg((size_t)n);
     for (int64_t v = 0; v < n; ++v) deg[(size_t)v] = (int32_t)(aptr[v + 1] - aptr[v]);
@@ -55,8 +61,9 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
         done[(size_t)v] = 1;
         perm[(size_t)p] = v;
         nb.clear();
-        const uint64_t* bv = &bits[(size_t)(v * W)];
-        for (int64_t w = 0; w < W; ++w) {
+        uint64_t* bv = &bits[(size_t)(v * W)];
+        const int32_t vlo = wlo[(size_t)v], vhi = whi[(size_t)v];
+        for (int64_t w = vlo; w < vhi; ++w) {
             uint64_t b = bv[w];
             while (b) {
                 const int t = __builtin_ctzll(b);
@@ -67,18 +74,20 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
         pattern[(size_t)p] = nb;   // node ids; converted to positions after the ordering is known
         for (int32_t u : nb) {
             uint64_t* bu = &bits[(size_t)(u * W)];
-            for (int64_t w = 0; w < W; ++w) bu[w] |= bv[w];
+            for (int64_t w = vlo; w < vhi; ++w) bu[w] |= bv[w];
             bu[u / 64] &= ~(1ull << (u % 64));
             bu[v / 64] &= ~(1ull << (v % 64));
-        }
-        for (int32_t u : nb) {
-            const uint64_t* bu = &bits[(size_t)(u * W)];
+            int32_t lo = std::min(wlo[(size_t)u], vlo), hi = std::max(whi[(size_t)u], vhi);
+            while (lo < hi && bu[lo] == 0) ++lo;
+            while (hi > lo && bu[hi - 1] == 0) --hi;
+            wlo[(size_t)u] = lo;
+            whi[(size_t)u] = hi;
             int32_t d = 0;
-            for (int64_t w = 0; w < W; ++w) d += __builtin_popcountll(bu[w]);
+            for (int64_t w = lo; w < hi; ++w) d += __builtin_popcountll(bu[w]);
             if (d != deg[(size_t)u]) heap.emplace(d, u);
             deg[(size_t)u] = d;
         }
-        memset(&bits[(size_t)(v * W)], 0, sizeof(uint64_t) * (size_t)W);
+        for (int64_t w = vlo; w < vhi; ++w) bv[w] = 0;
     }
 }
 
@@ -128,12 +137,25 @@ int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, cons
     return dpg_chol_sym_from_csr(n, perm.data(), cp.data(), rows.data(), opts, S);
 }
 
+#ifdef DPG_PLAN_TIMING
+double dpg_csr_t[8];
+static double csr_now() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+#define CSR_T(k) dpg_csr_t[k] += csr_now()
+#else
+#define CSR_T(k) do { } while (0)
+#endif
+
 int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow,
                           const dpg_chol_opts* opts, dpg_chol_sym* S) {
     if (n <= 0) return -1;
+    CSR_T(0);
     auto psize = [&](int64_t p) { return cp[p + 1] - cp[p]; };
     // scratch reused across calls (the incremental solver derives every update)
-    thread_local std::vector<int32_t> parent, nchild, sn_first, mark, rowbuf;
+    thread_local std::vector<int32_t> parent, nchild, sn_first, mark, rowbuf, stamp, mergebuf;
     parent.assign((size_t)n, -1);
     nchild.assign((size_t)n, 0);
     for (int64_t p = 0; p < n; ++p)
@@ -172,6 +194,7 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
     }
     const int32_t ns = (int32_t)sn_first.size();
     sn_first.push_back((int32_t)n);
+    CSR_T(1);
     // ---- supernode row sets: union of its columns' patterns beyond its last column
     S->n = n;
     S->ns = ns;
@@ -185,17 +208,22 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
     mark.assign((size_t)n, -1);
     for (int32_t s = 0; s < ns; ++s) {
         const int32_t c0 = sn_first[(size_t)s], c1 = sn_first[(size_t)s + 1];
-        rowbuf.clear();
-        for (int32_t c = c0; c < c1; ++c)
-            for (int64_t t = cp[c]; t < cp[c + 1]; ++t) {
-                const int32_t r = prow[t];
-                if (r >= c1 && mark[(size_t)r] != s) { mark[(size_t)r] = s; rowbuf.push_back(r); }
-            }
-        if (c1 - c0 > 1) std::sort(rowbuf.begin(), rowbuf.end());   // one column: already sorted
+        // sorted union of the columns' rows >= c1, merged from the last column down (the last
+        // column's rows all qualify; in a fundamental supernode every merge adds nothing)
+        rowbuf.assign(prow + cp[c1 - 1], prow + cp[c1]);
+        for (int32_t c = c1 - 2; c >= c0; --c) {
+            const int32_t* b = std::lower_bound(prow + cp[c], prow + cp[c + 1], c1);
+            const int32_t* e = prow + cp[c + 1];
+            if (std::includes(rowbuf.begin(), rowbuf.end(), b, e)) continue;
+            mergebuf.resize(rowbuf.size() + (size_t)(e - b));
+            mergebuf.resize((size_t)(std::set_union(rowbuf.begin(), rowbuf.end(), b, e, mergebuf.begin()) - mergebuf.begin()));
+            rowbuf.swap(mergebuf);
+        }
         S->sn_rows.insert(S->sn_rows.end(), rowbuf.begin(), rowbuf.end());
         S->sn_rows_ptr[(size_t)s + 1] = (int64_t)S->sn_rows.size();
         if (!rowbuf.empty()) S->sn_parent[(size_t)s] = S->sn_of[(size_t)rowbuf[0]];
     }
+    CSR_T(2);
     // ---- levels
     S->sn_level.assign((size_t)ns, 0);
     for (int32_t s = 0; s < ns; ++s) {   // children precede parents in elimination order
@@ -213,6 +241,7 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
         rowbuf.assign(S->level_ptr.begin(), S->level_ptr.end() - 1);
         for (int32_t s = 0; s < ns; ++s) S->level_list[(size_t)rowbuf[(size_t)S->sn_level[(size_t)s]]++] = s;
     }
+    CSR_T(3);
     // ---- children lists and relative maps (child update rows -> parent front index)
     S->child_ptr.assign((size_t)ns + 1, 0);
     for (int32_t s = 0; s < ns; ++s)
@@ -225,27 +254,29 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
         for (int32_t s = 0; s < ns; ++s)
             if (S->sn_parent[(size_t)s] >= 0) S->child_list[(size_t)rowbuf[(size_t)S->sn_parent[(size_t)s]]++] = s;
     }
-    // relmap: a parent's front row index by position (mark holds it while its children are mapped)
+    // relmap: a parent's front row index by position (mark holds it while its children are mapped,
+    // stamp says which parent's front the position is in)
     S->relmap.resize(S->sn_rows.size());
+    stamp.assign((size_t)n, -1);
     for (int32_t p = 0; p < ns; ++p) {
         if (S->child_ptr[(size_t)p + 1] == S->child_ptr[(size_t)p]) continue;
         const int32_t pc0 = sn_first[(size_t)p], pk = sn_first[(size_t)p + 1] - pc0;
-        for (int32_t c = 0; c < pk; ++c) mark[(size_t)(pc0 + c)] = c;
-        for (int64_t t = S->sn_rows_ptr[(size_t)p]; t < S->sn_rows_ptr[(size_t)p + 1]; ++t)
+        for (int32_t c = 0; c < pk; ++c) { mark[(size_t)(pc0 + c)] = c; stamp[(size_t)(pc0 + c)] = p; }
+        for (int64_t t = S->sn_rows_ptr[(size_t)p]; t < S->sn_rows_ptr[(size_t)p + 1]; ++t) {
             mark[(size_t)S->sn_rows[(size_t)t]] = pk + (int32_t)(t - S->sn_rows_ptr[(size_t)p]);
+            stamp[(size_t)S->sn_rows[(size_t)t]] = p;
+        }
         for (int64_t ci = S->child_ptr[(size_t)p]; ci < S->child_ptr[(size_t)p + 1]; ++ci) {
             const int32_t s = S->child_list[(size_t)ci];
             for (int64_t t = S->sn_rows_ptr[(size_t)s]; t < S->sn_rows_ptr[(size_t)s + 1]; ++t) {
                 const int32_t row = S->sn_rows[(size_t)t];
                 // child rows must lie in the parent's front (its columns or its rows)
-                const bool in = (row >= pc0 && row < pc0 + pk) ||
-                                std::binary_search(S->sn_rows.begin() + S->sn_rows_ptr[(size_t)p],
-                                                   S->sn_rows.begin() + S->sn_rows_ptr[(size_t)p + 1], row);
-                if (!in) return -2;
+                if (stamp[(size_t)row] != p) return -2;
                 S->relmap[(size_t)t] = mark[(size_t)row];
             }
         }
     }
+    CSR_T(4);
     // ---- front offsets (doubles), stats
     S->front_off.assign((size_t)ns + 1, 0);
     double flops = 0.0;
@@ -261,6 +292,7 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
     }
     S->max_front = maxm;
     S->flops = flops;
+    CSR_T(5);
     return 0;
 }
 
@@ -271,15 +303,48 @@ void incsym_grow_words(dpg_chol_incsym* I, int64_t need_bits) {
     if (need_bits <= I->words * 64) return;
     int64_t w = std::max<int64_t>(64, I->words * 2);
     while (w * 64 < need_bits) w *= 2;
-    std::vector<uint64_t> nb((size_t)(I->n * w), 0ull);
-    for (int64_t p = 0; p < I->n; ++p)
+    const int64_t sw = (w + 63) / 64;
+    std::vector<uint64_t> nb((size_t)(I->n * w), 0ull), ns((size_t)(I->n * sw), 0ull);
+    for (int64_t p = 0; p < I->n; ++p) {
         memcpy(&nb[(size_t)(p * w)], &I->bits[(size_t)(p * I->words)], sizeof(uint64_t) * (size_t)I->words);
+        memcpy(&ns[(size_t)(p * sw)], &I->summ[(size_t)(p * I->swords)], sizeof(uint64_t) * (size_t)I->swords);
+    }
     I->bits.swap(nb);
+    I->summ.swap(ns);
     I->words = w;
+    I->swords = sw;
 }
 
 inline bool has(const dpg_chol_incsym* I, int64_t j, int64_t r) {
     return (I->bits[(size_t)(j * I->words + r / 64)] >> (r % 64)) & 1ull;
+}
+
+inline void set_bit(dpg_chol_incsym* I, int64_t j, int64_t r) {
+    const int64_t w = r / 64;
+    I->bits[(size_t)(j * I->words + w)] |= 1ull << (r % 64);
+    I->summ[(size_t)(j * I->swords + w / 64)] |= 1ull << (w % 64);
+}
+
+// the set positions > `after` of column j, in increasing order, through the summary words
+template <typename F>
+inline void for_rows_after(const dpg_chol_incsym* I, int64_t j, int64_t after, F&& f) {
+    const uint64_t* row = &I->bits[(size_t)(j * I->words)];
+    const uint64_t* sm = &I->summ[(size_t)(j * I->swords)];
+    const int64_t w0 = (after + 1) / 64;
+    for (int64_t sw = w0 / 64; sw < I->swords; ++sw) {
+        uint64_t s = sm[sw];
+        if (sw == w0 / 64) s &= ~0ull << (w0 % 64);
+        while (s) {
+            const int64_t w = sw * 64 + __builtin_ctzll(s);
+            s &= s - 1;
+            uint64_t m = row[w];
+            if (w == w0) m &= ~0ull << ((after + 1) % 64);
+            while (m) {
+                f(w * 64 + __builtin_ctzll(m));
+                m &= m - 1;
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -290,14 +355,21 @@ int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, cons
     if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
     I->n = n;
     I->words = std::max<int64_t>(64, (n + 63) / 64 * 2);
+    I->swords = (I->words + 63) / 64;
     I->perm = perm;
     I->pos.assign((size_t)n, 0);
     for (int64_t p = 0; p < n; ++p) I->pos[(size_t)perm[(size_t)p]] = (int32_t)p;
     I->bits.assign((size_t)(n * I->words), 0ull);
+    I->summ.assign((size_t)(n * I->swords), 0ull);
     I->parent.assign((size_t)n, -1);
     I->nnz = 0;
+    I->cp.assign((size_t)n + 1, 0);
+    I->rows.clear();
+    I->added.clear();
     for (int64_t p = 0; p < n; ++p) {
-        for (int32_t r : pat[(size_t)p]) I->bits[(size_t)(p * I->words + r / 64)] |= 1ull << (r % 64);
+        for (int32_t r : pat[(size_t)p]) set_bit(I, p, r);
+        I->rows.insert(I->rows.end(), pat[(size_t)p].begin(), pat[(size_t)p].end());
+        I->cp[(size_t)p + 1] = (int64_t)I->rows.size();
         if (!pat[(size_t)p].empty()) I->parent[(size_t)p] = pat[(size_t)p][0];
         I->nnz += (int64_t)pat[(size_t)p].size();
     }
@@ -314,6 +386,8 @@ void dpg_incsym_append(dpg_chol_incsym* I, int64_t k) {
     }
     I->n += k;
     I->bits.resize((size_t)(I->n * I->words), 0ull);
+    I->summ.resize((size_t)(I->n * I->swords), 0ull);
+    I->cp.resize((size_t)I->n + 1, I->cp.empty() ? 0 : I->cp.back());   // the new columns: empty
 }
 
 // Row r enters column j's pattern (j < r, positions) and everything the elimination implies: it
@@ -331,22 +405,14 @@ int64_t dpg_incsym_add_edge(dpg_chol_incsym* I, int32_t a, int32_t b) {
         work.pop_back();
         while (j >= 0 && j < r) {
             if (has(I, j, r)) break;
-            I->bits[(size_t)(j * I->words + r / 64)] |= 1ull << (r % 64);
+            set_bit(I, j, r);
+            I->added.emplace_back((int32_t)j, (int32_t)r);
             ++added;
             const int64_t p_old = I->parent[(size_t)j];
             if (p_old < 0 || r < p_old) {
                 I->parent[(size_t)j] = (int32_t)r;
                 // column r inherits column j's rows above r
-                const uint64_t* row = &I->bits[(size_t)(j * I->words)];
-                for (int64_t w = (r + 1) / 64; w < I->words; ++w) {
-                    uint64_t m = row[w];
-                    if (w == (r + 1) / 64) m &= ~0ull << ((r + 1) % 64);
-                    while (m) {
-                        const int t = __builtin_ctzll(m);
-                        m &= m - 1;
-                        work.emplace_back(r, w * 64 + t);
-                    }
-                }
+                for_rows_after(I, j, r, [&](int64_t t) { work.emplace_back(r, t); });
                 break;
             }
             j = p_old;
@@ -356,25 +422,38 @@ int64_t dpg_incsym_add_edge(dpg_chol_incsym* I, int32_t a, int32_t b) {
     return added;
 }
 
-int dpg_incsym_derive(const dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S) {
-    const int64_t n = I->n, nw = (n + 63) / 64;
-    thread_local std::vector<int64_t> cp;
-    thread_local std::vector<int32_t> rows;
-    cp.resize((size_t)n + 1);
-    rows.clear();
-    rows.reserve((size_t)I->nnz);
-    cp[0] = 0;
-    for (int64_t p = 0; p < n; ++p) {
-        const uint64_t* row = &I->bits[(size_t)(p * I->words)];
-        for (int64_t w = (p + 1) / 64; w < nw; ++w) {
-            uint64_t m = row[w];
-            while (m) {
-                const int t = __builtin_ctzll(m);
-                m &= m - 1;
-                rows.push_back((int32_t)(w * 64 + t));
+int dpg_incsym_derive(dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    const int64_t n = I->n;
+    if ((int64_t)I->cp.size() != n + 1) return -3;
+    if (!I->added.empty()) {
+        // merge the entries added since the last derive into the CSR patterns, in one pass
+        std::sort(I->added.begin(), I->added.end());
+        std::vector<int32_t>& out = I->rows_tmp;
+        out.resize(I->rows.size() + I->added.size());
+        size_t a = 0, o = 0;
+        int64_t prev = 0;
+        for (int64_t p = 0; p < n; ++p) {
+            const int64_t b = prev, e = I->cp[(size_t)p + 1];
+            prev = e;
+            I->cp[(size_t)p] = (int64_t)o;
+            if (a == I->added.size() || I->added[a].first != p) {
+                if (e > b) memcpy(out.data() + o, I->rows.data() + b, sizeof(int32_t) * (size_t)(e - b));
+                o += (size_t)(e - b);
+                continue;
             }
+            int64_t t = b;
+            while (a < I->added.size() && I->added[a].first == p) {
+                const int32_t r = I->added[a++].second;
+                while (t < e && I->rows[(size_t)t] < r) out[o++] = I->rows[(size_t)t++];
+                out[o++] = r;
+            }
+            while (t < e) out[o++] = I->rows[(size_t)t++];
         }
-        cp[(size_t)p + 1] = (int64_t)rows.size();
+        I->cp[(size_t)n] = (int64_t)o;
+        out.resize(o);
+        I->rows.swap(out);
+        I->added.clear();
     }
-    return dpg_chol_sym_from_csr(n, I->perm.data(), cp.data(), rows.data(), opts, S);
+    if (I->cp[(size_t)n] != I->nnz) return -3;
+    return dpg_chol_sym_from_csr(n, I->perm.data(), I->cp.data(), I->rows.data(), opts, S);
 }

@@ -29,6 +29,32 @@ def test_incremental_symbolic_matches_elimination(incsym_bin, n0, steps, seed):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_solver_plan_matches_straightforward_construction(tmp_path):
+    """The GPU solver's host plan (dpg_chol.hip chol_plan: H-block -> front map by column buckets,
+    child column ranges by binary search, critical-path front order) equals the straightforward
+    construction (per-block binary search + per-front sort, linear scans, stable sort) after every
+    update of a growing graph: tools/incsym_bench.cpp built with DPG_PLAN_VERIFY aborts on the first
+    difference.  Host code only (hipcc compiles it; no device call runs)."""
+    exe = str(tmp_path / "incsym_bench_v")
+    csrc = os.path.join(ROOT, "dpg-slam_amd", "csrc")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off",
+                    "-DDPG_PLAN_VERIFY", "-o", exe, os.path.join(ROOT, "tools", "incsym_bench.cpp"),
+                    os.path.join(csrc, "dpg_chol.hip"), os.path.join(csrc, "dpg_chol_sym.cpp")], check=True)
+    rng = np.random.default_rng(5)
+    V, buf = 700, [700]
+    for v in range(V):
+        e = [(v - 1, v)] if v else []
+        for _ in range(rng.integers(0, 4) if v > 20 else 0):
+            e.append((int(rng.integers(0, v - 10)), v))
+        e = sorted(set(e))
+        buf.append(len(e))
+        buf.extend(x for p in e for x in p)
+    path = str(tmp_path / "edges.bin")
+    np.asarray(buf, np.int32).tofile(path)
+    r = subprocess.run([exe, path, "50", "32", "1.5"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "V=700" in r.stdout, r.stdout + r.stderr
+
+
 def _per_node(F):
     """Factors grouped by the update that adds them: the one whose largest key is the new node."""
     key = np.maximum(F["i"], np.where(F["kind"] == _abi.DPG_FACTOR_BETWEEN, F["j"], -1))

@@ -66,6 +66,16 @@ int main(int argc, char** argv) {
             if (pref != I.parent[(size_t)j]) { printf("step %d: parent of %lld: %d vs %d\n", s, (long long)j, I.parent[(size_t)j], pref); return 1; }
         }
         if (nnz != I.nnz) { printf("step %d: nnz %lld vs %lld\n", s, (long long)I.nnz, (long long)nnz); return 1; }
+        if (s % 3 == 0) {   // the CSR patterns derive keeps up to date (merged every few steps)
+            dpg_chol_sym S;
+            dpg_chol_opts o{64, 0.3};
+            if (dpg_incsym_derive(&I, &o, &S)) { printf("step %d: derive failed\n", s); return 1; }
+            for (int64_t j = 0; j < n; ++j) {
+                const std::vector<int> csr(I.rows.begin() + I.cp[(size_t)j], I.rows.begin() + I.cp[(size_t)j + 1]);
+                const std::vector<int> want(ref[(size_t)j].begin(), ref[(size_t)j].end());
+                if (csr != want) { printf("step %d: CSR column %lld differs\n", s, (long long)j); return 1; }
+            }
+        }
     }
     dpg_chol_sym S;
     dpg_chol_opts o{64, 0.3};
