@@ -249,7 +249,7 @@ def main_dynamic(args):
     node_ms, add_icp_ms, add_upd_ms, dpg, add_split, prof = [], [], [], [], [], []
     sweeps, active_end, replay_s, pass_tot = [], [], 0.0, {}
     import ctypes as C
-    L, pbuf = _abi.lib(), (C.c_double * 8)()
+    L, pbuf = _abi.lib(), (C.c_double * 12)()
     amin, amax, rmax = (float(x) for x in w.geom[0])
     t_run = time.perf_counter()
     for p in range(P):
@@ -281,8 +281,8 @@ def main_dynamic(args):
             add_upd_ms.append(la.update.ms_total)
             add_split.append((la.update.ms_symbolic, la.update.ms_numeric))
             if p == P - 1:   # the last pass: where the symbolic host time goes
-                L.dpg_inc_last_profile(C.c_void_p(slam.be.inc.handle), pbuf, 8)
-                prof.append(list(pbuf)[:6])
+                L.dpg_inc_last_profile(C.c_void_p(slam.be.inc.handle), pbuf, 12)
+                prof.append(list(pbuf)[:11])
             if p >= 1 and slam.last_dpg is not None:
                 d = slam.last_dpg
                 dpg.append((int(d.n_candidates), float(d.ms_total), int(d.n_submap_nodes)))
@@ -320,6 +320,13 @@ def main_dynamic(args):
             active_end.append({"pass": p, "active_fraction": float(act.mean()),
                                "past_active_fraction": float(act[:int(np.sum(slam.node_pass < p))].mean()),
                                **pass_tot.get(p, {})})
+    if args.dump_pairs:   # the graph's node pairs in arrival order, for offline ordering studies
+        L.dpg_inc_pairs.restype = C.c_int64
+        hdl = C.c_void_p(slam.be.inc.handle)
+        npairs = L.dpg_inc_pairs(hdl, None, None, C.c_int64(0))
+        lo, hi = np.zeros(npairs, np.int32), np.zeros(npairs, np.int32)
+        L.dpg_inc_pairs(hdl, lo.ctypes.data_as(C.c_void_p), hi.ctypes.data_as(C.c_void_p), C.c_int64(npairs))
+        np.savez_compressed(args.dump_pairs, lo=lo, hi=hi)
     # the sweep at 10k nodes (incrementPassNumber after the last pass)
     est_final = slam.poses.copy()
     ts = time.perf_counter()
@@ -373,7 +380,11 @@ def main_dynamic(args):
                     "update_symbolic_mean": float(np.mean([a for a, _ in add_split])),
                     "update_numeric_mean": float(np.mean([b for _, b in add_split])),
                     "last_pass_symbolic_parts": dict(zip(("incsym", "derive", "lists_upload", "chol_build", "chol_host",
-                                                          "chol_upload"), np.round(np.mean(prof, 0), 4).tolist()))
+                                                          "chol_upload", "factor_mflop", "max_front_blocks",
+                                                          "fused_fraction", "supernodes", "levels"),
+                                                         np.round(np.mean(prof, 0), 4).tolist()))
+                    if prof else None,
+                    "end_factor": dict(zip(("mflop", "max_front_blocks", "fused", "supernodes", "levels"), prof[-1][6:11]))
                     if prof else None},
         "dpg": {"calls": len(dpg_a), "ms_per_call": float(dpg_a[:, 1].mean()) if len(dpg_a) else None,
                 "calls_per_s": float(1e3 / dpg_a[:, 1].mean()) if len(dpg_a) else None,
@@ -552,6 +563,7 @@ def main():
                          "the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--icp-variant", default="angular", choices=["angular", "kdtree", "grid"],
                     help="nearest-neighbour machinery of the ICP kernel (results are identical)")
+    ap.add_argument("--dump-pairs", default=None, help="dynamic: save the graph's node pairs (npz) after the run")
     ap.add_argument("--refactor-delta", type=float, default=None,
                     help="dpg_gn_params.refactor_delta: chord steps (reuse the Cholesky factor) once max|delta| is below it")
     ap.add_argument("--workload", default="batch", choices=["batch", "incremental", "dynamic", "dpg"],

@@ -41,6 +41,9 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
 // (in elimination positions, sorted), and everything derived from an order + patterns
 int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                    std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
+// nested dissection (BFS level separators; parts of <= leaf nodes by minimum degree): shallow trees
+int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
+                      std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
                                const dpg_chol_opts* opts, dpg_chol_sym* S);
 // the same from patterns in CSR form: column p's rows are prow[cp[p] .. cp[p + 1]) (sorted)
@@ -81,6 +84,8 @@ int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32
                         dpg_chol_sym* S);
 // host time (ms) of the last build of h: structures, uploads
 void dpg_chol_build_times(void* h, double out[2]);
+// 1 when h factors with the fused DAG kernel (every front fits its LDS budget), 0 on the level path
+int dpg_chol_fused(void* h);
 // the host half of a build alone (no device calls; tools/incsym_bench.cpp times it on the CPU)
 int dpg_chol_plan_host(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                        const dpg_chol_sym* S, double* ms);

@@ -1930,6 +1930,8 @@ int dpg_chol_plan_host(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi
     return rc;
 }
 
+int dpg_chol_fused(void* h) { return h && reinterpret_cast<const CholDev*>(h)->fused ? 1 : 0; }
+
 void dpg_chol_build_times(void* h, double out[2]) {
     const CholDev* c = reinterpret_cast<const CholDev*>(h);
     out[0] = c ? c->t_build[0] : 0.0;

@@ -133,7 +133,9 @@ struct dpg_inc {
     int32_t* cnt = nullptr;                    // relinearized variables of the last update
     size_t c_theta = 0, c_est = 0, c_maxd = 0;
     std::vector<dpg_factor> h_dev_factors;     // staging (Q1 scaling)
-    double prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}; // last update: incsym, derive, lists, chol host, chol upload
+    double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
+                                               // chol upload (ms); factor Mflop, largest front (blocks),
+                                               // fused DAG path (1) or level path (0), supernodes
 };
 
 namespace {
@@ -201,7 +203,16 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
     const double t = now_ms();
     const int rc2 = dpg_chol_create_sym(&g.chol, n, q->plo.data(), q->phi.data(), P, &q->S);
     q->prof[3] = now_ms() - t;
-    if (!rc2) dpg_chol_build_times(g.chol, q->prof + 4);
+    if (!rc2) {
+        dpg_chol_build_times(g.chol, q->prof + 4);
+        double st[6];
+        dpg_chol_stats(g.chol, st);
+        q->prof[6] = st[3] * 1e-6;
+        q->prof[7] = st[2];
+        q->prof[8] = dpg_chol_fused(g.chol);
+        q->prof[9] = st[0];
+        q->prof[10] = st[1];
+    }
     return rc2;
 }
 
@@ -271,10 +282,20 @@ int64_t dpg_inc_num_nodes(const dpg_inc* q) { return q ? q->V : -1; }
 // symbolic state, derived structures, contribution lists + factor upload, GPU solver structures
 int dpg_inc_last_profile(const dpg_inc* q, double* out, int n) {
     if (!q || !out) return DPG_ERR_ARG;
-    for (int k = 0; k < n && k < 8; ++k) out[k] = q->prof[k];
+    for (int k = 0; k < n && k < 12; ++k) out[k] = q->prof[k];
     return DPG_OK;
 }
 dpg_ctx* dpg_inc_ctx(dpg_inc* q) { return q ? q->ctx : nullptr; }
+
+// diagnostics: the graph's unique node pairs in arrival order (lo < hi); returns their number and
+// copies min(n, number) of them when lo / hi are given
+int64_t dpg_inc_pairs(const dpg_inc* q, int32_t* lo, int32_t* hi, int64_t n) {
+    if (!q) return -1;
+    const int64_t P = (int64_t)q->plo.size();
+    if (lo && hi)
+        for (int64_t k = 0; k < P && k < n; ++k) { lo[k] = q->plo[(size_t)k]; hi[k] = q->phi[(size_t)k]; }
+    return P;
+}
 
 int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_factor* factors, int64_t n_factors,
                    dpg_inc_stats* st) {

@@ -27,7 +27,7 @@ int main(int argc, char** argv) {
     const int tail = argc > 2 ? atoi(argv[2]) : 500;
     const int every = argc > 3 ? atoi(argv[3]) : 64;
     const double grow = argc > 4 ? atof(argv[4]) : 1.5;
-    double flops = 0, maxf = 0;
+    double flops = 0, maxf = 0, levels = 0, crit_sum = 0;
     FILE* f = fopen(argv[1], "rb");
     if (!f) return 2;
     std::vector<int32_t> buf;
@@ -112,6 +112,21 @@ int main(int argc, char** argv) {
             acc[2] += plan;
             flops += S.flops;
             maxf = std::max<double>(maxf, S.max_front);
+            levels += S.n_levels;
+            // the critical-path estimate the fused factorization schedules by (dpg_chol.hip chol_plan)
+            std::vector<double> cpe((size_t)S.ns, 0.0);
+            double crit = 0.0;
+            for (int32_t s = S.ns - 1; s >= 0; --s) {
+                const int32_t k = S.sn_c0[(size_t)s + 1] - S.sn_c0[(size_t)s];
+                const int32_t r = (int32_t)(S.sn_rows_ptr[(size_t)s + 1] - S.sn_rows_ptr[(size_t)s]);
+                const int32_t nch = (int32_t)(S.child_ptr[(size_t)s + 1] - S.child_ptr[(size_t)s]);
+                const int32_t m3 = 3 * (k + r);
+                const double est = (m3 <= 96 && nch <= 8) ? 4.0 + 0.05 * m3 : 10.0 + 20.0 * ((3 * k + 23) / 24);
+                const int32_t pa = S.sn_parent[(size_t)s];
+                cpe[(size_t)s] = est + (pa >= 0 ? cpe[(size_t)pa] : 0.0);
+                crit = std::max(crit, cpe[(size_t)s]);
+            }
+            crit_sum += crit;
             ++cnt;
         }
     }
@@ -119,7 +134,8 @@ int main(int argc, char** argv) {
            "plan %.3f total %.3f (derive's from_csr alone %.3f, reorder %.3f, of which the ordering %.3f)\n",
            V, plo.size(), (long long)I.nnz, S.ns, reorders, cnt, acc[0] / cnt, acc[1] / cnt, acc[2] / cnt,
            (acc[0] + acc[1] + acc[2]) / cnt, acc[3] / cnt, t_reset / cnt, t_order / cnt);
-    printf("mean factor Mflop %.1f, max front %.0f blocks\n", flops / cnt * 1e-6, maxf);
+    printf("mean factor Mflop %.1f, max front %.0f blocks, mean levels %.1f, mean critical-path estimate %.0f us\n",
+           flops / cnt * 1e-6, maxf, levels / cnt, crit_sum / cnt);
 #ifdef DPG_PLAN_TIMING
     printf("plan parts, mean ms over the tail:");
     for (int k = 1; k < 8; ++k)
