@@ -1269,34 +1269,20 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
                 __syncthreads();
                 if (tid == 0) __hip_atomic_store(trdy + tc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            // the last panel's update of an update tile is its final value: stored write-through for
+            // the parent (no republishing pass after the chain)
+            const bool fin = p == T.np - 1 && S.parent >= 0;
             for (int t = t_first; t < T.nt; t += t_step)
-                if (t > p && !(t == p + 1 && t < T.np) && !(mine && t == tc)) update_tile<false>(t, p, T, F, P);
+                if (t > p && !(t == p + 1 && t < T.np) && !(mine && t == tc)) {
+                    if (fin) update_tile<true>(t, p, T, F, P);
+                    else update_tile<false>(t, p, T, F, P);
+                }
             __syncthreads();
             if (has_b) rhs_panel(p, T, P, bv);
         }
     }
     if (bad && (tid & 63) == 0) atomicExch(status, 1);
-    // ---- out: own update tiles write-through for the parent; member 0: y and the pending updates
-    if (S.parent >= 0) {
-        for (int t = t_first; t < T.nt; t += t_step) {
-            if (t < T.np) continue;
-            const int cs = T.c0(t), n = (T.c1(t) - cs) * m3;
-            for (int e0 = 0; e0 < n; e0 += kFT * kPFL) {
-                double v[kPFL];
-                int a[kPFL];
-#pragma unroll
-                for (int q = 0; q < kPFL; ++q) {
-                    const int e = e0 + tid + kFT * q;
-                    const int col = cs + e / m3, row = e % m3;
-                    a[q] = (e < n && row >= col) ? col * m3 + row : -1;
-                    v[q] = a[q] >= 0 ? F[(uint32_t)a[q]] : 0.0;
-                }
-#pragma unroll
-                for (int q = 0; q < kPFL; ++q)
-                    if (a[q] >= 0) st_agent(F + (uint32_t)a[q], v[q]);
-            }
-        }
-    }
+    // ---- out: member 0 (or the right-hand side's owner): y and the pending updates
     if (has_b) {
         for (int t = tid; t < k3; t += kFT) ysol[3 * (int64_t)S.c0 + t] = bv[t];
         if (S.parent >= 0)
@@ -1698,7 +1684,9 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     for (int32_t s = S.ns - 1; s >= 0; --s) {
         const SnDev& d = sns[(size_t)s];
         const int32_t m3 = 3 * (d.k + d.r);
-        const double est = d.G == 1 ? 4.0 + 0.05 * m3 : 10.0 + 20.0 * ((3 * d.k + kFNB - 1) / kFNB);
+        // (us, fitted to tools/chol_bench_t's per-front log: a small front's time grows with its
+        // columns -- ~0.9 us each for the in-LDS factorization -- as well as its rows)
+        const double est = d.G == 1 ? 4.0 + 0.06 * m3 + 0.9 * (3 * d.k) : 10.0 + 20.0 * ((3 * d.k + kFNB - 1) / kFNB);
         prio[(size_t)s] = est + (d.parent >= 0 ? prio[(size_t)d.parent] : 0.0);
     }
     // (descending priority, ties in level-list order)
