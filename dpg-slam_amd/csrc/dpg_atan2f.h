@@ -10,6 +10,17 @@
 // polynomial's first coefficient is 0x3eaaaaab), evaluated with -ffp-contract=off; it is checked
 // against the host atan2f on 40 M random arguments by tools/atan2f_check.hip and through the DPG
 // parity tests.
+//
+// The algorithm restated here is fdlibm's (as carried by glibc's float port); its notice:
+//   Conversion to float by Ian Lance Taylor, Cygnus Support, ian@cygnus.com.
+//   ====================================================
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this
+//   software is freely granted, provided that this notice
+//   is preserved.
+//   ====================================================
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
