@@ -23,9 +23,11 @@ def incsym_bin(tmp_path_factory):
     return out
 
 
-@pytest.mark.parametrize("n0,steps,seed", [(200, 150, 1), (500, 200, 7), (64, 300, 3), (30, 120, 11)])
-def test_incremental_symbolic_matches_elimination(incsym_bin, n0, steps, seed):
-    r = subprocess.run([incsym_bin, str(n0), str(steps), str(seed)], capture_output=True, text=True)
+@pytest.mark.parametrize("n0,steps,seed,split", [(200, 150, 1, ""), (500, 200, 7, ""), (64, 300, 3, ""),
+                                                 (30, 120, 11, ""), (400, 120, 5, "split")])
+def test_incremental_symbolic_matches_elimination(incsym_bin, n0, steps, seed, split):
+    r = subprocess.run([incsym_bin, str(n0), str(steps), str(seed)] + ([split] if split else []), capture_output=True,
+                       text=True)
     assert r.returncode == 0, r.stdout + r.stderr
 
 

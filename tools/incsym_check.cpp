@@ -2,7 +2,7 @@
 // pose graph grown node by node (chain + loop closures to older nodes, some between two older
 // nodes), starting from a minimum-degree order of its first part; after every step the maintained
 // column patterns must equal a from-scratch symbolic elimination of the current graph in the
-// maintained order.  usage: incsym_check N0 STEPS SEED   (exit 0 = all equal)
+// maintained order.  usage: incsym_check N0 STEPS SEED [split]   (exit 0 = all equal)
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -32,10 +32,17 @@ static std::vector<std::set<int>> eliminate(int64_t n, const std::vector<int32_t
 int main(int argc, char** argv) {
     const int n0 = argc > 1 ? atoi(argv[1]) : 200, steps = argc > 2 ? atoi(argv[2]) : 100;
     std::mt19937 rng(argc > 3 ? atoi(argv[3]) : 1);
+    // "split": the initial graph is several components (chain breaks every 40 nodes, no closures
+    // across them) and some nodes are isolated -- the nested dissection's component handling
+    const bool split = argc > 4 && argv[4][0] == 's';
     std::vector<std::pair<int, int>> edges;
     for (int v = 1; v < n0; ++v) {
+        if (split && (v % 40 == 0 || v % 97 == 5)) continue;
         edges.emplace_back(v - 1, v);
-        if (v > 10 && rng() % 3 == 0) edges.emplace_back((int)(rng() % (v - 5)), v);
+        if (v > 10 && rng() % 3 == 0) {
+            const int j = (int)(rng() % (v - 5));
+            if (!split || j / 40 == v / 40) edges.emplace_back(j, v);
+        }
     }
     std::vector<int32_t> lo, hi;
     for (auto& e : edges) { lo.push_back(e.first); hi.push_back(e.second); }
