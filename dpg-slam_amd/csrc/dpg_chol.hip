@@ -419,17 +419,22 @@ __device__ __forceinline__ void sub_coldots(double* z, const double* A, int64_t 
     const int g = threadIdx.x >> 4, gl = threadIdx.x & 15;
     for (int j0 = 0; j0 < nj; j0 += kT / 16) {
         const int j = j0 + g;
-        double a0 = 0.0, a1 = 0.0;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         if (j < nj) {
             const double* Aj = A + (int64_t)j * lda;
             int t = gl;
-            for (; t + 16 < nt; t += 32) {
-                a0 = fma(Aj[t], x[t], a0);
-                a1 = fma(Aj[t + 16], x[t + 16], a1);
+            // 8 loads in flight per lane (the fronts come from L2/MALL: latency, not bandwidth)
+#pragma unroll 2
+            for (; t + 48 < nt; t += 64) {
+                const double v0 = Aj[t], v1 = Aj[t + 16], v2 = Aj[t + 32], v3 = Aj[t + 48];
+                a0 = fma(v0, x[t], a0);
+                a1 = fma(v1, x[t + 16], a1);
+                a2 = fma(v2, x[t + 32], a2);
+                a3 = fma(v3, x[t + 48], a3);
             }
-            if (t < nt) a0 = fma(Aj[t], x[t], a0);
+            for (; t < nt; t += 16) a0 = fma(Aj[t], x[t], a0);
         }
-        const double a = group16_sum(a0 + a1);
+        const double a = group16_sum((a0 + a1) + (a2 + a3));
         if (j < nj && gl == 0) z[j] -= a;
     }
 }
@@ -493,20 +498,26 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
         }
         __syncthreads();
         for (int i = jb + bw + tid; i < k3; i += kT) {
-            double a0 = 0.0, a1 = 0.0;
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
             int j = 0;
-            for (; j + 1 < bw; j += 2) {
-                a0 = fma(F[(jb + j) * m3 + i], y[jb + j], a0);
-                a1 = fma(F[(jb + j + 1) * m3 + i], y[jb + j + 1], a1);
+#pragma unroll 2
+            for (; j + 3 < bw; j += 4) {   // loads batched: the front comes from L2/MALL
+                const double v0 = F[(jb + j) * m3 + i], v1 = F[(jb + j + 1) * m3 + i];
+                const double v2 = F[(jb + j + 2) * m3 + i], v3 = F[(jb + j + 3) * m3 + i];
+                a0 = fma(v0, y[jb + j], a0);
+                a1 = fma(v1, y[jb + j + 1], a1);
+                a2 = fma(v2, y[jb + j + 2], a2);
+                a3 = fma(v3, y[jb + j + 3], a3);
             }
-            if (j < bw) a0 = fma(F[(jb + j) * m3 + i], y[jb + j], a0);
-            y[i] -= a0 + a1;
+            for (; j < bw; ++j) a0 = fma(F[(jb + j) * m3 + i], y[jb + j], a0);
+            y[i] -= (a0 + a1) + (a2 + a3);
         }
         __syncthreads();
     }
     for (int t = tid; t < r3; t += kT) {
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         int j = 0;
+#pragma unroll 2
         for (; j + 3 < k3; j += 4) {
             a0 = fma(F[j * m3 + k3 + t], y[j], a0);
             a1 = fma(F[(j + 1) * m3 + k3 + t], y[j + 1], a1);
