@@ -373,11 +373,20 @@ __device__ __forceinline__ double rdlane(double v, int l) {
 __device__ __forceinline__ int chain_len(int bw) { return bw <= 8 ? 8 : bw <= 16 ? 16 : bw <= 32 ? 32 : 64; }
 __device__ __forceinline__ void load_diag(double* D, double* rd, const double* F, int m3, int jb, int bw) {
     const int nb = chain_len(bw);
-    for (int e = threadIdx.x; e < nb * nb; e += kT) {
-        const int i = e % nb, j = e / nb;
-        const double v = (i < bw && j < bw && i >= j) ? F[(int64_t)(jb + j) * m3 + jb + i] : 0.0;
-        D[j * kSB + i] = i > j ? v : 0.0;
-        if (i == j) rd[j] = j < bw ? 1.0 / v : 0.0;
+    constexpr int kPer = kSB * kSB / kT;   // every load of the block in flight at once (8 per thread)
+    double v[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int e = threadIdx.x + kT * q, i = e % nb, j = e / nb;
+        v[q] = (e < nb * nb && i < bw && j < bw && i >= j) ? F[(int64_t)(jb + j) * m3 + jb + i] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int e = threadIdx.x + kT * q, i = e % nb, j = e / nb;
+        if (e < nb * nb) {
+            D[j * kSB + i] = i > j ? v[q] : 0.0;
+            if (i == j) rd[j] = j < bw ? 1.0 / v[q] : 0.0;
+        }
     }
 }
 
