@@ -746,6 +746,8 @@ int dpg_gn_set_poses(dpg_ctx* c, const double* poses) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->gn.have_factor = 0;            // a new linearization point: the next solve refactors
     c->gn.last_delta_inf = 1e300;
+    c->gn.prev_delta_inf = 1e300;
+    c->gn.last_was_chord = 0;
     c->gn.n_factorizations = 0;
     return DPG_OK;
 }

@@ -553,7 +553,12 @@ extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg
     g->last_pcg_iters = 0;
     g->last_used_chol = gp->linear_solver == DPG_SOLVER_CHOLESKY && g->chol;
     if (g->last_used_chol) {
-        const bool reuse = gp->reuse_factorization && g->have_factor && g->last_delta_inf < gp->refactor_delta;
+        // chord steps once the step is small -- while they keep contracting: a chord step that
+        // shrank the step by less than 10x (linear convergence gone slow, e.g. a sweep far from the
+        // optimum) hands back to a fresh factorization
+        const bool slow = g->last_was_chord && g->last_delta_inf > 0.1 * g->prev_delta_inf;
+        const bool reuse = gp->reuse_factorization && g->have_factor && g->last_delta_inf < gp->refactor_delta && !slow;
+        g->last_was_chord = reuse ? 1 : 0;
         const int rc = reuse ? dpg_chol_resolve(g->chol, hb, stream) : dpg_chol_solve(g->chol, hb, stream);
         if (rc) return rc;
         if (!reuse) {
@@ -584,6 +589,7 @@ extern "C" int dpg_gn_dev_fetch(dpg_gn_dev* g, const double* hb, void* stream, d
     out[0] = g->scal3_host[0];
     out[1] = g->scal3_host[1];
     out[2] = g->scal3_host[2];
+    g->prev_delta_inf = g->last_delta_inf;
     g->last_delta_inf = out[0];
     return DPG_OK;
 }

@@ -120,7 +120,7 @@ void dpg_gn_params_default(dpg_gn_params* p) {
     p->pcg_max_iterations = 20000;
     p->pcg_check_every = 16;
     p->reuse_factorization = 1;
-    p->refactor_delta = 1e-4;
+    p->refactor_delta = 1e-3;
 }
 
 /* R9: odometry BetweenFactor from two odom_only_estimates (dpg_slam.cc:56-75). */

@@ -413,6 +413,8 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         q->g.poses = q->est;
         q->g.have_factor = 0;
         q->g.last_delta_inf = 1e300;
+        q->g.prev_delta_inf = 1e300;
+        q->g.last_was_chord = 0;
         q->g.n_factorizations = 0;
         const dpg_gn_params& gp = q->P.gn;
         double sc[3] = {0, 0, 0};

@@ -121,7 +121,9 @@ typedef struct dpg_gn_dev {
     int32_t last_pcg_iters;
     int32_t last_used_chol;        /* the last solve ran the Cholesky (its status word is meaningful) */
     double last_delta_inf;         /* host: max |delta| of the last fetched retraction */
+    double prev_delta_inf;         /* host: the one before it */
     int32_t have_factor;           /* the Cholesky holds a factorization of this graph */
+    int32_t last_was_chord;        /* the last solve reused the factor */
     int32_t n_factorizations;      /* since dpg_gn_set_poses */
 } dpg_gn_dev;
 

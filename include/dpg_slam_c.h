@@ -100,7 +100,8 @@ typedef struct dpg_gn_params {
                                     with the previous Cholesky factor (a chord step: same fixed point
                                     g(X) = 0, H barely changes that close to it); 0: refactor every
                                     iteration (plain Gauss-Newton) */
-    double refactor_delta;       /* 1e-4 */
+    double refactor_delta;       /* 1e-3 (tools/refactor_sweep.sh: config 4 converges in 8 iterations
+                                    with 3 factorizations instead of 7 with 4, 2.4 % less per step) */
 } dpg_gn_params;
 
 #define DPG_SOLVER_CHOLESKY 0    /* supernodal multifrontal Cholesky on the GPU */
