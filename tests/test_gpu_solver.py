@@ -76,3 +76,27 @@ def test_async_gn_loop_matches_optimize_graph(ctx, workload):
     Xa = ctx.gn_get_poses(w.V)
     assert st["iterations"] == sc.iterations
     np.testing.assert_array_equal(Xa, Xc)
+
+
+@pytest.mark.parametrize("name", ["config3", "config4"])
+def test_orders_agree(ctx, workload, name):
+    """The nested-dissection order (default) and plain minimum degree (DPG_CHOL_ORDER=md) factor the
+    same system: the GN solutions agree to rounding, and against the oracle on config 3."""
+    from oracle import oracle as O
+    from dpgslam import _abi
+    w = workload(name)
+    p = _abi.default_icp_params()
+    ctx.upload_scans(w.pts, w.offsets, 5)
+    res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
+    F = w.factors_with_icp(res, p)
+    X0 = w.est.astype(np.float64)
+    Xn, sn = _optimize(ctx, X0, F)
+    os.environ["DPG_CHOL_ORDER"] = "md"   # read when the Cholesky is set up
+    try:
+        Xm, sm = _optimize(ctx, X0, F)
+    finally:
+        os.environ.pop("DPG_CHOL_ORDER", None)
+    assert np.abs(pose_diff(Xn, Xm)).max() < 1e-9
+    if name == "config3":
+        Xo, _ = O.optimize_graph(X0, F)
+        assert np.abs(pose_diff(Xn, Xo)).max() < 1e-6
