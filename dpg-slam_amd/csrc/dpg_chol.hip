@@ -393,24 +393,89 @@ __device__ __forceinline__ void load_diag(double* D, double* rd, const double* F
 // One wave solves the padded unit-scaled triangle by a readlane -> fma chain; lane = row, the
 // lane's scaled entries in registers (lanes >= N compute garbage nobody reads).
 // forward (L y = b):  yl_i -= L(i, j) / L(j, j) * yl_j, j ascending; y = yl / L_ii afterwards
+// rl: this lane's reciprocal of the block's diagonal (0 past bw), broadcast per column by readlane
+// (scalar operands: the 64-step chains fit two waves per SIMD)
 template <int N>
-__device__ __forceinline__ double fwd_chain(const double* D, const double* rd, double yl, int lane) {
+__device__ __forceinline__ double fwd_chain(const double* D, double rl, double yl, int lane) {
     double dr[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) dr[j] = D[j * kSB + lane] * rd[j];
+    for (int j = 0; j < N; ++j) dr[j] = D[j * kSB + lane] * rdlane(rl, j);
 #pragma unroll
     for (int j = 0; j < N; ++j) yl = fma(-dr[j], rdlane(yl, j), yl);
     return yl;
 }
 // backward (L^T x = z): zl_i -= L(j, i) / L(j, j) * zl_j, j descending; x = zl / L_ii afterwards
 template <int N>
-__device__ __forceinline__ double bwd_chain(const double* D, const double* rd, double zl, int lane) {
+__device__ __forceinline__ double bwd_chain(const double* D, double rl, double zl, int lane) {
     double dr[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) dr[j] = D[lane * kSB + j] * rd[j];
+    for (int j = 0; j < N; ++j) dr[j] = D[lane * kSB + j] * rdlane(rl, j);
 #pragma unroll
     for (int j = N - 1; j >= 0; --j) zl = fma(-dr[j], rdlane(zl, j), zl);
     return zl;
+}
+template <bool kFwd>
+__device__ __forceinline__ double run_chain(const double* D, double rl, double v, int lane, int bw) {
+    const int nb = chain_len(bw);
+    if constexpr (kFwd)
+        return nb == 8 ? fwd_chain<8>(D, rl, v, lane) : nb == 16 ? fwd_chain<16>(D, rl, v, lane)
+             : nb == 32 ? fwd_chain<32>(D, rl, v, lane) : fwd_chain<64>(D, rl, v, lane);
+    else
+        return nb == 8 ? bwd_chain<8>(D, rl, v, lane) : nb == 16 ? bwd_chain<16>(D, rl, v, lane)
+             : nb == 32 ? bwd_chain<32>(D, rl, v, lane) : bwd_chain<64>(D, rl, v, lane);
+}
+
+// Staging of a front's L in LDS while the solve waits for its children (forward) or its parent
+// (backward): every load the front's own arithmetic needs is issued before the wait, so after it
+// only the handed-off values (pending row updates / the ancestors' x) travel.  The region holds
+// R doubles (a launch parameter), beside the kSB x kSB diagonal-block buffer D:
+//   full:  the front's pivot columns, [k3][m3] column-major exactly as in HBM (ld m3), when
+//          m3 k3 <= R (its diagonal blocks are copied LDS -> D);
+//   else:  the first C columns of L21 (rows k3..m3, ld r3), C a multiple of 4 (the dot products
+//          keep their 4-accumulator order whichever memory a column comes from); the diagonal
+//          blocks come from HBM (the first one needed is loaded before the wait).
+struct Stage {
+    bool full;
+    int C;
+};
+__device__ __forceinline__ Stage stage_plan(int m3, int k3, int R) {
+    if ((int64_t)m3 * k3 <= (int64_t)R) return Stage{true, k3};
+    const int r3 = m3 - k3;
+    const int C = r3 > 0 ? min(k3, R / r3) & ~3 : 0;
+    return Stage{false, C};
+}
+// n doubles src -> dst, 8 loads in flight per thread
+__device__ __forceinline__ void stage_copy(double* dst, const double* src, int n) {
+    for (int e0 = 0; e0 < n; e0 += 8 * kT) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = e0 + threadIdx.x + kT * q;
+            v[q] = e < n ? src[e] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = e0 + threadIdx.x + kT * q;
+            if (e < n) dst[e] = v[q];
+        }
+    }
+}
+// the first C columns of L21 (rows k3..m3 of the front at F) -> dst [C][r3]
+__device__ __forceinline__ void stage_l21(double* dst, const double* F, int m3, int k3, int C) {
+    const int r3 = m3 - k3, n = C * r3;
+    for (int e0 = 0; e0 < n; e0 += 8 * kT) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = e0 + threadIdx.x + kT * q;
+            v[q] = e < n ? F[(int64_t)(e / r3) * m3 + k3 + e % r3] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int e = e0 + threadIdx.x + kT * q;
+            if (e < n) dst[e] = v[q];
+        }
+    }
 }
 
 // 16-lane groups: sum of a partial over the group (xor butterfly: every lane gets the total)
@@ -424,8 +489,44 @@ __device__ __forceinline__ double group16_sum(double a) {
 
 // z[j] -= sum_t A[j * lda + t] x[t] for j < nj, t < nt (A column-major, the dot runs down a
 // column: contiguous): 16 lanes per j, so a long dot is 1/16 of the serial chain.
+// Dots of at most 64 terms (a lane holds at most 4 of them: the triangular blocks' row panels,
+// short L21s) are straight-line: four columns per 16-lane group in flight at once (16 loads per
+// lane instead of one dependent round trip per column pass), the same fma order as the loop below.
 __device__ __forceinline__ void sub_coldots(double* z, const double* A, int64_t lda, const double* x, int nj, int nt) {
     const int g = threadIdx.x >> 4, gl = threadIdx.x & 15;
+    if (nt <= 64) {
+        constexpr int kU = 4;
+        for (int j0 = 0; j0 < nj; j0 += kU * (kT / 16)) {
+            double v[kU][4];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int j = j0 + u * (kT / 16) + g;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int t = gl + 16 * q;
+                    v[u][q] = (j < nj && t < nt) ? A[(int64_t)j * lda + t] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int j = j0 + u * (kT / 16) + g;
+                double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+                if (gl + 48 < nt) {   // the loop's one 4-wide trip
+                    a0 = fma(v[u][0], x[gl], a0);
+                    a1 = fma(v[u][1], x[gl + 16], a1);
+                    a2 = fma(v[u][2], x[gl + 32], a2);
+                    a3 = fma(v[u][3], x[gl + 48], a3);
+                } else {              // its tail
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        if (gl + 16 * q < nt) a0 = fma(v[u][q], x[gl + 16 * q], a0);
+                }
+                const double a = group16_sum((a0 + a1) + (a2 + a3));
+                if (j < nj && gl == 0) z[j] -= a;
+            }
+        }
+        return;
+    }
     for (int j0 = 0; j0 < nj; j0 += kT / 16) {
         const int j = j0 + g;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
@@ -448,32 +549,110 @@ __device__ __forceinline__ void sub_coldots(double* z, const double* A, int64_t 
     }
 }
 
-__global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict__ order, int32_t* sync,
+// The front's own arithmetic of the forward solve after its children's pending row updates are in:
+// diagonal blocks by one wave, the rows below each block, then the pending update L21 y for the
+// parent.  kFull: the front is staged in LDS at Rg (ld m3); else D holds the current diagonal block
+// (the first one prestaged) and L21s the first C columns of L21.
+template <bool kFull>
+__device__ __forceinline__ void fwd_front(const SnDev& S, const double* F, double* Rg, double* D, const double* L21s,
+                                          int C, double* rd, double* y, double* aR, double* acc) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
+    const double* A = kFull ? Rg : F;   // the front's columns, ld m3
+    for (int jb = 0; jb < k3; jb += kSB) {
+        const int bw = min(kSB, k3 - jb);
+        if (jb > 0) {   // the first block was loaded before the wait
+            if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
+            else load_diag(D, rd, F, m3, jb, bw);
+            __syncthreads();
+        }
+        if (wave == 0) {   // lane = row; y_j broadcast by v_readlane (uniform j)
+            double yl = lane < bw ? y[jb + lane] : 0.0;
+            const double rl = lane < bw ? rd[lane] : 0.0;
+            yl = run_chain<true>(D, rl, yl, lane, bw);
+            if (lane < bw) y[jb + lane] = yl * rl;
+        }
+        __syncthreads();
+        for (int i = jb + bw + tid; i < k3; i += kT) {
+            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+            int j = 0;
+#pragma unroll 2
+            for (; j + 3 < bw; j += 4) {   // loads batched: a front not staged comes from L2/MALL
+                const double v0 = A[(jb + j) * m3 + i], v1 = A[(jb + j + 1) * m3 + i];
+                const double v2 = A[(jb + j + 2) * m3 + i], v3 = A[(jb + j + 3) * m3 + i];
+                a0 = fma(v0, y[jb + j], a0);
+                a1 = fma(v1, y[jb + j + 1], a1);
+                a2 = fma(v2, y[jb + j + 2], a2);
+                a3 = fma(v3, y[jb + j + 3], a3);
+            }
+            for (; j < bw; ++j) a0 = fma(A[(jb + j) * m3 + i], y[jb + j], a0);
+            y[i] -= (a0 + a1) + (a2 + a3);
+        }
+        __syncthreads();
+    }
+    for (int t = tid; t < r3; t += kT) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int j = 0;
+        if constexpr (kFull) {
+#pragma unroll 2
+            for (; j + 3 < k3; j += 4) {
+                a0 = fma(Rg[j * m3 + k3 + t], y[j], a0);
+                a1 = fma(Rg[(j + 1) * m3 + k3 + t], y[j + 1], a1);
+                a2 = fma(Rg[(j + 2) * m3 + k3 + t], y[j + 2], a2);
+                a3 = fma(Rg[(j + 3) * m3 + k3 + t], y[j + 3], a3);
+            }
+            for (; j < k3; ++j) a0 = fma(Rg[j * m3 + k3 + t], y[j], a0);
+        } else {
+            for (; j < C; j += 4) {   // C is a multiple of 4: the same accumulator order as below
+                a0 = fma(L21s[j * r3 + t], y[j], a0);
+                a1 = fma(L21s[(j + 1) * r3 + t], y[j + 1], a1);
+                a2 = fma(L21s[(j + 2) * r3 + t], y[j + 2], a2);
+                a3 = fma(L21s[(j + 3) * r3 + t], y[j + 3], a3);
+            }
+#pragma unroll 2
+            for (; j + 3 < k3; j += 4) {
+                a0 = fma(F[j * m3 + k3 + t], y[j], a0);
+                a1 = fma(F[(j + 1) * m3 + k3 + t], y[j + 1], a1);
+                a2 = fma(F[(j + 2) * m3 + k3 + t], y[j + 2], a2);
+                a3 = fma(F[(j + 3) * m3 + k3 + t], y[j + 3], a3);
+            }
+            for (; j < k3; ++j) a0 = fma(F[j * m3 + k3 + t], y[j], a0);
+        }
+        st_agent(acc + S.acc_off + t, aR[t] + ((a0 + a1) + (a2 + a3)));
+    }
+}
+
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void chol_forward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                        int32_t* status, const SnDev* __restrict__ sns,
                                                        const int32_t* __restrict__ child_list,
                                                        const int32_t* __restrict__ relmap,
                                                        const double* __restrict__ fronts,
                                                        const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm,
-                                                       double* __restrict__ ysol, double* acc) {
+                                                       double* __restrict__ ysol, double* acc, int R) {
     extern __shared__ __attribute__((aligned(16))) double smem_fw[];
     double* sm = smem_fw + 2;   // smem_fw[0]: the claimed front (no static LDS)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_fw));
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     double* D = sm;                  // kSB x kSB diagonal block
-    double* rd = sm + kSB * kSB;     // kSB reciprocals of its diagonal
+    double* Rg = D + kSB * kSB;      // staging region, R doubles (Stage)
+    double* L21s = Rg;               // (not full) first C columns of L21
+    double* rd = Rg + R;             // kSB reciprocals of the diagonal block's diagonal
     double* y = rd + kSB;            // k3
     double* aR = y + k3;             // r3
-    // before the wait: the right-hand side and the first diagonal block (earlier launches)
+    const Stage P = stage_plan(m3, k3, R);
+    // before the wait: the right-hand side and the front's L (earlier launches)
     for (int t = tid; t < k3; t += kT) {
         const int node = perm[S.c0 + t / 3];
         y[t] = -g[3 * node + t % 3];
     }
     for (int t = tid; t < r3; t += kT) aR[t] = 0.0;
     load_diag(D, rd, F, m3, 0, min(kSB, k3));
+    if (P.full) stage_copy(Rg, F, m3 * k3);
+    else stage_l21(L21s, F, m3, k3, P.C);
     if (S.nchild > 0) {
         if (tid == 0) wait_geq_sc1(sync + 1 + s, S.nchild, status);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -491,51 +670,8 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
         }
         __syncthreads();
     }
-    for (int jb = 0; jb < k3; jb += kSB) {
-        const int bw = min(kSB, k3 - jb);
-        if (jb > 0) {
-            load_diag(D, rd, F, m3, jb, bw);
-            __syncthreads();
-        }
-        if (wave == 0) {   // lane = row; y_j broadcast by v_readlane (uniform j)
-            double yl = lane < bw ? y[jb + lane] : 0.0;
-            const double rl = lane < bw ? rd[lane] : 0.0;
-            const int nb = chain_len(bw);
-            yl = nb == 8 ? fwd_chain<8>(D, rd, yl, lane) : nb == 16 ? fwd_chain<16>(D, rd, yl, lane)
-               : nb == 32 ? fwd_chain<32>(D, rd, yl, lane) : fwd_chain<64>(D, rd, yl, lane);
-            if (lane < bw) y[jb + lane] = yl * rl;
-        }
-        __syncthreads();
-        for (int i = jb + bw + tid; i < k3; i += kT) {
-            double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-            int j = 0;
-#pragma unroll 2
-            for (; j + 3 < bw; j += 4) {   // loads batched: the front comes from L2/MALL
-                const double v0 = F[(jb + j) * m3 + i], v1 = F[(jb + j + 1) * m3 + i];
-                const double v2 = F[(jb + j + 2) * m3 + i], v3 = F[(jb + j + 3) * m3 + i];
-                a0 = fma(v0, y[jb + j], a0);
-                a1 = fma(v1, y[jb + j + 1], a1);
-                a2 = fma(v2, y[jb + j + 2], a2);
-                a3 = fma(v3, y[jb + j + 3], a3);
-            }
-            for (; j < bw; ++j) a0 = fma(F[(jb + j) * m3 + i], y[jb + j], a0);
-            y[i] -= (a0 + a1) + (a2 + a3);
-        }
-        __syncthreads();
-    }
-    for (int t = tid; t < r3; t += kT) {
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        int j = 0;
-#pragma unroll 2
-        for (; j + 3 < k3; j += 4) {
-            a0 = fma(F[j * m3 + k3 + t], y[j], a0);
-            a1 = fma(F[(j + 1) * m3 + k3 + t], y[j + 1], a1);
-            a2 = fma(F[(j + 2) * m3 + k3 + t], y[j + 2], a2);
-            a3 = fma(F[(j + 3) * m3 + k3 + t], y[j + 3], a3);
-        }
-        for (; j < k3; ++j) a0 = fma(F[j * m3 + k3 + t], y[j], a0);
-        st_agent(acc + S.acc_off + t, aR[t] + ((a0 + a1) + (a2 + a3)));
-    }
+    if (P.full) fwd_front<true>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc);
+    else fwd_front<false>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc);
     for (int t = tid; t < k3; t += kT) ysol[3 * (int64_t)S.c0 + t] = y[t];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -544,34 +680,70 @@ __global__ __launch_bounds__(kT) void chol_forward_dag(const int32_t* __restrict
 }
 
 // backward: L^T x = y.  A front waits for its parent (hence every ancestor), gathers x at its row
-// positions, solves, and publishes its own x.
+// positions, solves, and publishes its own x.  Its L is staged in LDS before the wait (Stage).
+template <bool kFull>
+__device__ __forceinline__ void bwd_front(int s, const SnDev& S, const double* F, double* Rg, double* D, const double* L21s,
+                                          int C, double* rd, double* z, const double* xr) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
+    if constexpr (kFull) {
+        sub_coldots(z, Rg + k3, m3, xr, k3, r3);   // z = y - L21^T x_r
+    } else {
+        sub_coldots(z, L21s, r3, xr, C, r3);
+        sub_coldots(z + C, F + (int64_t)C * m3 + k3, m3, xr, k3 - C, r3);
+    }
+    __syncthreads();
+    BW_MARK(s, 2);
+    const int nblk = (k3 + kSB - 1) / kSB;
+    for (int b = nblk - 1; b >= 0; --b) {
+        const int jb = b * kSB, bw = min(kSB, k3 - jb);
+        if (b != nblk - 1) {   // the last block was loaded before the wait
+            if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
+            else load_diag(D, rd, F, m3, jb, bw);
+            __syncthreads();
+        }
+        if (wave == 0) {   // lane = row; x_j broadcast by v_readlane (uniform j): ~3 dependent ops per step
+            double zl = lane < bw ? z[jb + lane] : 0.0;
+            const double rl = lane < bw ? rd[lane] : 0.0;
+            zl = run_chain<false>(D, rl, zl, lane, bw);
+            if (lane < bw) z[jb + lane] = zl * rl;
+        }
+        __syncthreads();
+        sub_coldots(z, (kFull ? Rg : F) + jb, m3, z + jb, jb, bw);
+        __syncthreads();
+    }
+}
 
-__global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                         int32_t* status, const SnDev* __restrict__ sns,
                                                         const int32_t* __restrict__ rows,
                                                         const double* __restrict__ fronts,
-                                                        const double* __restrict__ ysol, double* xsol) {
+                                                        const double* __restrict__ ysol, double* xsol, int R) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x;
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_b));
     const SnDev S = sns[s];
     BW_MARK(s, 0);
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
-    double* D = sm;
-    double* rd = sm + kSB * kSB;     // kSB reciprocals of the diagonal block's diagonal
+    double* D = sm;                  // kSB x kSB diagonal block
+    double* Rg = D + kSB * kSB;      // staging region, R doubles (Stage)
+    double* L21s = Rg;               // (not full) first C columns of L21
+    double* rd = Rg + R;             // kSB reciprocals of the diagonal block's diagonal
     double* z = rd + kSB;            // k3
     double* xr = z + k3;             // r3
     int32_t* rp = reinterpret_cast<int32_t*>(xr + r3);   // r3 / 3 row positions
-    // before the wait: y, the row positions, the last diagonal block (all from earlier launches)
+    const Stage P = stage_plan(m3, k3, R);
+    // before the wait: y, the row positions, the front's L (all from earlier launches)
     for (int j = tid; j < k3; j += kT) z[j] = ysol[3 * (int64_t)S.c0 + j];
     for (int t = tid; t < S.r; t += kT) rp[t] = rows[S.rows_off + t];
-    const int nblk = (k3 + kSB - 1) / kSB;
     {
-        const int jb = (nblk - 1) * kSB;
+        const int jb = ((k3 + kSB - 1) / kSB - 1) * kSB;
         load_diag(D, rd, F, m3, jb, k3 - jb);
     }
+    if (P.full) stage_copy(Rg, F, m3 * k3);
+    else stage_l21(L21s, F, m3, k3, P.C);
     if (S.parent >= 0) {
         if (tid == 0) wait_geq_sc1(sync + 1 + S.parent, 1, status);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -580,27 +752,8 @@ __global__ __launch_bounds__(kT) void chol_backward_dag(const int32_t* __restric
     BW_MARK(s, 1);
     for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
     __syncthreads();
-    sub_coldots(z, F + k3, m3, xr, k3, r3);   // z = y - L21^T x_r
-    __syncthreads();
-    BW_MARK(s, 2);
-    for (int b = nblk - 1; b >= 0; --b) {
-        const int jb = b * kSB, bw = min(kSB, k3 - jb);
-        if (b != nblk - 1) {
-            load_diag(D, rd, F, m3, jb, bw);
-            __syncthreads();
-        }
-        if (wave == 0) {   // lane = row; x_j broadcast by v_readlane (uniform j): ~3 dependent ops per step
-            double zl = lane < bw ? z[jb + lane] : 0.0;
-            const double rl = lane < bw ? rd[lane] : 0.0;
-            const int nb = chain_len(bw);
-            zl = nb == 8 ? bwd_chain<8>(D, rd, zl, lane) : nb == 16 ? bwd_chain<16>(D, rd, zl, lane)
-               : nb == 32 ? bwd_chain<32>(D, rd, zl, lane) : bwd_chain<64>(D, rd, zl, lane);
-            if (lane < bw) z[jb + lane] = zl * rl;
-        }
-        __syncthreads();
-        sub_coldots(z, F + jb, m3, z + jb, jb, bw);
-        __syncthreads();
-    }
+    if (P.full) bwd_front<true>(s, S, F, Rg, D, L21s, P.C, rd, z, xr);
+    else bwd_front<false>(s, S, F, Rg, D, L21s, P.C, rd, z, xr);
     BW_MARK(s, 3);
     for (int j = tid; j < k3; j += kT) st_agent(xsol + 3 * (int64_t)S.c0 + j, z[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1382,6 +1535,7 @@ struct CholDev {
     int32_t* sync = nullptr;           // [ticket_f, cnt_f[ns], ticket_b, done_b[ns]], zeroed per solve
     size_t sync_bytes = 0;
     size_t lds_solve_max = 0;
+    int32_t solve_stage = 0;   // R: LDS staging region of the solves, doubles (Stage)
     AsmTask* asm_tasks = nullptr;
     AsmChild* asm_child = nullptr;
     int2* panel_tasks = nullptr;
@@ -1465,7 +1619,7 @@ struct CholHost {
     std::vector<SnDev> sns;
     std::vector<FTask> ftasks;
     std::vector<FChild> fchild;
-    std::vector<double> prio;
+    std::vector<double> prio, hgt;
     std::vector<std::pair<double, int32_t>> key;
     std::vector<int32_t> fo, bwd, order_fac, cuts;
     std::vector<AsmTask> asm_t;
@@ -1772,11 +1926,23 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     }
     c->fused = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_LEVELS") == nullptr;
     // LDS of the DAG solves: the largest front
-    c->lds_solve_max = 0;
+    // the solves' LDS: diagonal block D + staging region R + reciprocals + right-hand side / gathered
+    // x + row positions.  Their VGPR budget (the 64-step chains) already holds them to two
+    // workgroups per CU, so R defaults to what fills 80 KB; DPG_SOLVE_STAGE overrides it (doubles,
+    // 0 = no staging)
+    size_t lds_rest = 0;
     for (int32_t s = 0; s < S.ns; ++s) {
         const int32_t m3 = 3 * (sns[(size_t)s].k + sns[(size_t)s].r);
-        c->lds_solve_max = std::max(c->lds_solve_max, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
+        lds_rest = std::max(lds_rest, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
     }
+    {
+        const char* env = getenv("DPG_SOLVE_STAGE");
+        const long room = (long)(80 * 1024) - (long)lds_rest;
+        const long want = env ? atol(env) : room / (long)sizeof(double);
+        const long cap = ((long)(160 * 1024) - (long)lds_rest) / (long)sizeof(double);
+        c->solve_stage = (int32_t)std::max<long>(0, std::min<long>(want, cap)) & ~1;
+    }
+    c->lds_solve_max = (size_t)c->solve_stage * sizeof(double) + lds_rest;
     if (c->lds_solve_max > 160 * 1024) return DPG_ERR_SIZE;
     std::vector<AsmTask>& asm_t = H.asm_t;
     std::vector<AsmChild>& asm_c = H.asm_c;
@@ -1830,9 +1996,27 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
             if (L.lds_asm > 160 * 1024) return DPG_ERR_SIZE;
         }
     }
-    // solves: the critical-path order (children first), and its reverse (parents first)
+    // solves: the forward solve runs in the factorization's critical-path order (children first);
+    // the backward solve by descending height -- the estimated time of the longest path from a
+    // front DOWN to a leaf, which exceeds every child's, so the order is topological (parents
+    // first) and the deepest chain is claimed first (the reverse of the forward order claimed the
+    // fronts near the root first, whatever hangs below them: a chain front could be claimed
+    // microseconds after its parent finished)
     PLAN_T(6);
-    H.bwd.assign(fo.rbegin(), fo.rend());
+    {
+        std::vector<double>& hgt = H.hgt;
+        hgt.assign((size_t)S.ns, 0.0);
+        for (int32_t s = 0; s < S.ns; ++s) {   // children precede parents in supernode order
+            const SnDev& d = sns[(size_t)s];
+            hgt[(size_t)s] += 2.0 + 0.01 * (3 * (d.k + d.r)) + 0.05 * (3 * d.k);   // us, tools/chol_bench_t
+            if (d.parent >= 0) hgt[(size_t)d.parent] = std::max(hgt[(size_t)d.parent], hgt[(size_t)s]);
+        }
+        key.resize((size_t)S.ns);
+        for (int32_t s = 0; s < S.ns; ++s) key[(size_t)s] = {-hgt[(size_t)s], s};
+        std::sort(key.begin(), key.end());
+        H.bwd.resize((size_t)S.ns);
+        for (int32_t i = 0; i < S.ns; ++i) H.bwd[(size_t)i] = key[(size_t)i].second;
+    }
     // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
     //  pivot-tile hand-off flags [per large-front tile]]
     c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
@@ -1959,7 +2143,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
                            c->perm, c->fronts,
                            c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol);
+                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol, c->solve_stage);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -1980,9 +2164,9 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     int32_t* sync_f = c->sync;
     int32_t* sync_b = c->sync + 1 + S.ns;
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->fronts, c->ysol, c->xsol);
+                       c->sns, c->rows, c->fronts, c->ysol, c->xsol, c->solve_stage);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -1994,9 +2178,9 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     const double* g = hb + 9 * c->nnzb_upper;
     if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol, c->solve_stage);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

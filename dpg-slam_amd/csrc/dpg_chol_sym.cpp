@@ -385,12 +385,17 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
     for (int64_t p = 0; p < n; ++p)
         if (psize(p) > 0) { parent[(size_t)p] = prow[cp[p]]; nchild[(size_t)parent[(size_t)p]]++; }
     // ---- fundamental supernodes, then relaxed merging of chains
-    // column p+1 joins p's supernode when p's only parent is p+1, p is p+1's only child and the
-    // patterns nest (fundamental), or when the explicit zeros added stay within the budget.
+    // column p+1 joins p's supernode when p's parent is p+1 and the patterns nest (fundamental),
+    // or when the explicit zeros added stay within the budget.
     S->sn_of.resize((size_t)n);
     sn_first.clear();
     const int32_t max_cols = opts && opts->max_supernode_cols > 0 ? opts->max_supernode_cols : 64;
     const double relax = opts ? opts->relax_fraction : 0.0;
+    // a column joins its child's supernode whatever its other children (they hang off the merged
+    // front, whose index set holds their rows): nested dissection's separators become one front
+    // each instead of a chain of fronts split at every subtree root attached to them.
+    // DPG_CHOL_MERGE_SINGLE=1 restores the single-child rule.
+    static const bool any_child = getenv("DPG_CHOL_MERGE_SINGLE") == nullptr;
     {
         int32_t s = -1;
         int64_t zeros = 0, cols = 0;
@@ -398,9 +403,12 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
             bool join = false;
             if (p > 0 && s >= 0) {
                 const int64_t q = p - 1;
-                const bool chain = parent[(size_t)q] == (int32_t)p && nchild[(size_t)p] == 1;
                 const int64_t cq = psize(q), cpp = psize(p);
                 const int64_t ncols = p - sn_first[(size_t)s] + 1;
+                // (a merge past another child keeps the front within 127 blocks: the fused
+                // factorization's two LDS panel buffers still fit)
+                const bool chain = parent[(size_t)q] == (int32_t)p &&
+                                   (nchild[(size_t)p] == 1 || (any_child && ncols + cpp <= 127));
                 if (chain && ncols <= max_cols) {
                     if (cq == cpp + 1) join = true;   // fundamental
                     else if (relax > 0.0) {
