@@ -85,7 +85,12 @@ struct SnDev {
     int32_t omap_n, parent;     // parent supernode, -1 at a root
     int32_t G, need;            // fused factorization: team size, sum of the children's team sizes
     int32_t ftask, pad;         // large fronts: first tile task
+    int32_t seg_off, seg_n;     // backward solve: the row segments by owning supernode (SolveSeg)
 };
+
+// A front's rows (ascending positions) fall into segments owned by its ancestors, the parent's
+// first: the backward solve takes each segment's x as soon as its owner has published it.
+struct SolveSeg { int32_t sn, t0, t1, pad; };   // rows [t0, t1) (blocks) owned by supernode sn
 
 struct OEnt {                   // one upper 3x3 block of H -> its front position
     int32_t u;                  // block index in the packed hb buffer
@@ -679,21 +684,29 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
         __hip_atomic_fetch_add(sync + 1 + S.parent, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// backward: L^T x = y.  A front waits for its parent (hence every ancestor), gathers x at its row
-// positions, solves, and publishes its own x.  Its L is staged in LDS before the wait (Stage).
+// backward: L^T x = y.  A front gathers x at its row positions and subtracts L21^T x_r from y,
+// segment by segment as the rows' owners publish (the highest ancestor's rows first, the parent's
+// last: after the parent's signal only its own rows remain), then solves its diagonal blocks and
+// publishes its own x.  Its L is staged in LDS before any wait (Stage).
+constexpr int kMaxSeg = 32;   // row segments held in LDS (a front with more waits for its parent, then takes every row)
+
+// z -= L21[rows r0..r1)^T x_r[r0..r1) (scalar rows of the L21 block)
 template <bool kFull>
-__device__ __forceinline__ void bwd_front(int s, const SnDev& S, const double* F, double* Rg, double* D, const double* L21s,
-                                          int C, double* rd, double* z, const double* xr) {
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
+__device__ __forceinline__ void bwd_z(const double* F, const double* Rg, const double* L21s, int C, int m3, int k3,
+                                      double* z, const double* xr, int r0, int r1) {
+    const int r3 = m3 - k3;
     if constexpr (kFull) {
-        sub_coldots(z, Rg + k3, m3, xr, k3, r3);   // z = y - L21^T x_r
+        sub_coldots(z, Rg + k3 + r0, m3, xr + r0, k3, r1 - r0);
     } else {
-        sub_coldots(z, L21s, r3, xr, C, r3);
-        sub_coldots(z + C, F + (int64_t)C * m3 + k3, m3, xr, k3 - C, r3);
+        sub_coldots(z, L21s + r0, r3, xr + r0, C, r1 - r0);
+        sub_coldots(z + C, F + (int64_t)C * m3 + k3 + r0, m3, xr + r0, k3 - C, r1 - r0);
     }
-    __syncthreads();
-    BW_MARK(s, 2);
+}
+
+template <bool kFull>
+__device__ __forceinline__ void bwd_diag(const double* F, const double* Rg, double* D, double* rd, int m3, int k3,
+                                         double* z) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nblk = (k3 + kSB - 1) / kSB;
     for (int b = nblk - 1; b >= 0; --b) {
         const int jb = b * kSB, bw = min(kSB, k3 - jb);
@@ -714,9 +727,43 @@ __device__ __forceinline__ void bwd_front(int s, const SnDev& S, const double* F
     }
 }
 
+template <bool kFull>
+__device__ __forceinline__ void bwd_front(int s, const SnDev& S, int nseg, const SolveSeg* sg, const int32_t* rp,
+                                          int32_t* sync, int32_t* status, double* xsol, const double* F, double* Rg,
+                                          double* D, const double* L21s, int C, double* rd, double* z, double* xr) {
+    const int tid = threadIdx.x;
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
+    if (nseg == 0) {   // the root (no rows), or too many segments: wait for the parent, take every row
+        if (S.parent >= 0) {
+            if (tid == 0) wait_geq_sc1(sync + 1 + S.parent, 1, status);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        BW_MARK(s, 1);
+        for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
+        __syncthreads();
+        bwd_z<kFull>(F, Rg, L21s, C, m3, k3, z, xr, 0, r3);
+    } else {
+        for (int q = nseg - 1; q >= 0; --q) {
+            const SolveSeg g = sg[q];
+            if (tid == 0) wait_geq_sc1(sync + 1 + g.sn, 1, status);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (q == 0) BW_MARK(s, 1);
+            for (int t = 3 * g.t0 + tid; t < 3 * g.t1; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
+            __syncthreads();
+            bwd_z<kFull>(F, Rg, L21s, C, m3, k3, z, xr, 3 * g.t0, 3 * g.t1);
+        }
+    }
+    __syncthreads();
+    BW_MARK(s, 2);
+    bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z);
+}
+
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
                                                         int32_t* status, const SnDev* __restrict__ sns,
                                                         const int32_t* __restrict__ rows,
+                                                        const SolveSeg* __restrict__ segs,
                                                         const double* __restrict__ fronts,
                                                         const double* __restrict__ ysol, double* xsol, int R) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
@@ -734,26 +781,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     double* z = rd + kSB;            // k3
     double* xr = z + k3;             // r3
     int32_t* rp = reinterpret_cast<int32_t*>(xr + r3);   // r3 / 3 row positions
+    SolveSeg* sg = reinterpret_cast<SolveSeg*>(xr + r3 + ((S.r + 3) / 4) * 2);   // [kMaxSeg], 16-B aligned
+    const int nseg = S.seg_n <= kMaxSeg ? S.seg_n : 0;
     const Stage P = stage_plan(m3, k3, R);
-    // before the wait: y, the row positions, the front's L (all from earlier launches)
+    // before any wait: y, the row positions, the segments, the front's L (all from earlier launches)
     for (int j = tid; j < k3; j += kT) z[j] = ysol[3 * (int64_t)S.c0 + j];
     for (int t = tid; t < S.r; t += kT) rp[t] = rows[S.rows_off + t];
+    for (int q = tid; q < nseg; q += kT) sg[q] = segs[S.seg_off + q];
     {
         const int jb = ((k3 + kSB - 1) / kSB - 1) * kSB;
         load_diag(D, rd, F, m3, jb, k3 - jb);
     }
     if (P.full) stage_copy(Rg, F, m3 * k3);
     else stage_l21(L21s, F, m3, k3, P.C);
-    if (S.parent >= 0) {
-        if (tid == 0) wait_geq_sc1(sync + 1 + S.parent, 1, status);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
     __syncthreads();
-    BW_MARK(s, 1);
-    for (int t = tid; t < r3; t += kT) xr[t] = ld_agent(xsol + 3 * (int64_t)rp[t / 3] + t % 3);
-    __syncthreads();
-    if (P.full) bwd_front<true>(s, S, F, Rg, D, L21s, P.C, rd, z, xr);
-    else bwd_front<false>(s, S, F, Rg, D, L21s, P.C, rd, z, xr);
+    if (P.full) bwd_front<true>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr);
+    else bwd_front<false>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr);
     BW_MARK(s, 3);
     for (int j = tid; j < k3; j += kT) st_agent(xsol + 3 * (int64_t)S.c0 + j, z[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1532,6 +1575,7 @@ struct CholDev {
     FChild* fchild = nullptr;
     int64_t n_tickets = 0;
     int32_t* order_bwd = nullptr;
+    SolveSeg* segs = nullptr;
     int32_t* sync = nullptr;           // [ticket_f, cnt_f[ns], ticket_b, done_b[ns]], zeroed per solve
     size_t sync_bytes = 0;
     size_t lds_solve_max = 0;
@@ -1620,6 +1664,7 @@ struct CholHost {
     std::vector<FTask> ftasks;
     std::vector<FChild> fchild;
     std::vector<double> prio, hgt;
+    std::vector<SolveSeg> segs;
     std::vector<std::pair<double, int32_t>> key;
     std::vector<int32_t> fo, bwd, order_fac, cuts;
     std::vector<AsmTask> asm_t;
@@ -1779,6 +1824,21 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     }
     for (int32_t s = 0; s < S.ns; ++s)
         if (sns[(size_t)s].parent >= 0) sns[(size_t)sns[(size_t)s].parent].need += sns[(size_t)s].G;
+    std::vector<SolveSeg>& segs = H.segs;
+    segs.clear();
+    for (int32_t s = 0; s < S.ns; ++s) {
+        SnDev& d = sns[(size_t)s];
+        d.seg_off = (int32_t)segs.size();
+        const int32_t* rw = S.sn_rows.data() + d.rows_off;
+        for (int32_t t = 0; t < d.r;) {
+            const int32_t a = S.sn_of[(size_t)rw[t]];
+            int32_t t1 = t + 1;
+            while (t1 < d.r && S.sn_of[(size_t)rw[t1]] == a) ++t1;
+            segs.push_back(SolveSeg{a, t, t1, 0});
+            t = t1;
+        }
+        d.seg_n = (int32_t)segs.size() - d.seg_off;
+    }
     // large fronts: per tile, the H blocks (omap range) and the children's column ranges
     PLAN_T(3);
     std::vector<FTask>& ftasks = H.ftasks;
@@ -1933,7 +1993,7 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     size_t lds_rest = 0;
     for (int32_t s = 0; s < S.ns; ++s) {
         const int32_t m3 = 3 * (sns[(size_t)s].k + sns[(size_t)s].r);
-        lds_rest = std::max(lds_rest, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 1) * sizeof(double));
+        lds_rest = std::max(lds_rest, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 2 + 2 * kMaxSeg) * sizeof(double));
     }
     {
         const char* env = getenv("DPG_SOLVE_STAGE");
@@ -2030,7 +2090,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     const dpg_chol_sym& S = c->sym;
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
     struct Piece { void** d; const void* h; size_t bytes; };
-    Piece pieces[16];
+    Piece pieces[20];
     int np = 0;
     auto add = [&](auto** d, const auto& h) {
         using T = typename std::remove_reference<decltype(h)>::type::value_type;
@@ -2048,6 +2108,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     add(&c->ftasks, H.ftasks);
     add(&c->fchild, H.fchild);
     add(&c->order_bwd, H.bwd);
+    add(&c->segs, H.segs);
     if (!c->fused) {
         add(&c->asm_tasks, H.asm_t);
         add(&c->asm_child, H.asm_c);
@@ -2143,7 +2204,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
                            c->perm, c->fronts,
                            c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol, c->solve_stage);
+                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -2166,7 +2227,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->fronts, c->ysol, c->xsol, c->solve_stage);
+                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2180,7 +2241,7 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->fronts, c->ysol, c->xsol, c->solve_stage);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
