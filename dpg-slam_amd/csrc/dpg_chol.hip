@@ -1048,69 +1048,62 @@ __device__ void factor_lds(int q, int s, const Tiles& T, double* P, double* scr,
     const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
     double* Lt = scr;
     double* rdg = Lt + kFNB * kFNB;
-    for (int e = tid; e < kFNB * kFNB; e += kFT) Lt[e] = 0.0;
+    int* flg = reinterpret_cast<int*>(rdg + 8 * (kFNB / 3));   // [kFNB / 3] step epochs (zeroed by the chain's start)
     PN_MARK(s, q, 5);
-    // POTRF of the top w x w block by all 8 waves: lane = row, wave v holds columns v, v + 8, v + 16
-    // in registers.  Per 3x3 step the three owning waves post their columns to LDS (double-
-    // buffered: one barrier per step), every wave factors the 3x3 block and computes its rows' x
-    // redundantly, and updates its own columns (the other rows' x by v_readlane).
+    // POTRF of the top w x w block, pipelined over the waves: wave v owns the 3x3 block column
+    // 3v..3v+2 (lane = row, its three columns in registers).  It applies each earlier step's
+    // update as soon as that step's columns are posted (L_top in LDS + an LDS epoch flag: a
+    // wave-to-wave hand-off, no workgroup barrier per step), then factors its own 3x3 block,
+    // posts its columns and raises its flag -- the chain per step is flag -> three fma ->
+    // chol3 -> post.  Same arithmetic and order as a step-by-step POTRF.
     {
-        const int i = lane;
-        double col[3];
+        const int i = lane, cv = 3 * wave, ep = q + 1;
+        if (cv < w) {   // wave-uniform
+            double col[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int c = wave + 8 * k;
-            col[k] = (c < w && i < w && i >= c) ? P[c * Rp + off + i] : 0.0;
-        }
-        double* cb = rdg + 8 * (kFNB / 3);   // [2][3][64]
-#pragma unroll 1
-        for (int c0 = 0, st = 0; c0 < w; c0 += 3, ++st) {
-            ST_MARK(s, q, st);
-            double* cbs = cb + (st & 1) * 192;
+            for (int r = 0; r < 3; ++r) {
+                const int c = cv + r;
+                col[r] = (i < w && i >= c) ? P[c * Rp + off + i] : 0.0;
+            }
+            for (int st = 0; st < wave; ++st) {
+                while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(flg + st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < ep)
+                    __builtin_amdgcn_s_sleep(0);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const int c0 = 3 * st;
+                const int ii = i < kFNB ? i : 0;
+                const double x0 = Lt[c0 * kFNB + ii], x1 = Lt[(c0 + 1) * kFNB + ii], x2 = Lt[(c0 + 2) * kFNB + ii];
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const int cj = c0 + j;
-                if ((cj & 7) == wave) {
-                    const int k = cj >> 3;
-                    cbs[j * 64 + i] = k == 0 ? col[0] : (k == 1 ? col[1] : col[2]);
+                for (int r = 0; r < 3; ++r) {
+                    const int c = cv + r;
+                    const double y0 = Lt[c0 * kFNB + c], y1 = Lt[(c0 + 1) * kFNB + c], y2 = Lt[(c0 + 2) * kFNB + c];
+                    const double v = fma(-x2, y2, fma(-x1, y1, fma(-x0, y0, col[r])));
+                    col[r] = (i >= c && i < w) ? v : col[r];
                 }
             }
-            __syncthreads();
-            // every LDS read of the step issues at once (the row's values are pinned here, so the
-            // compiler cannot sink their loads behind the 3x3 factorization)
-            double p0 = cbs[i], p1 = cbs[64 + i], p2 = cbs[128 + i];
-            const double d00 = cbs[c0], d10 = cbs[c0 + 1], d11 = cbs[64 + c0 + 1];
-            const double d20 = cbs[c0 + 2], d21 = cbs[64 + c0 + 2], d22 = cbs[128 + c0 + 2];
-            asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2));
+            ST_MARK(s, q, wave);
+            const double d00 = rdlane(col[0], cv), d10 = rdlane(col[0], cv + 1), d20 = rdlane(col[0], cv + 2);
+            const double d11 = rdlane(col[1], cv + 1), d21 = rdlane(col[1], cv + 2), d22 = rdlane(col[2], cv + 2);
             const Chol3 L = chol3(d00, d10, d11, d20, d21, d22, bad);
-            double x0 = p0 * L.m00;
-            double x1 = fma(p0, L.m10, p1 * L.m11);
-            double x2 = fma(p0, L.m20, fma(p1, L.m21, p2 * L.m22));
-            if (i == c0) { x0 = L.l00; x1 = 0.0; x2 = 0.0; }
-            else if (i == c0 + 1) { x0 = L.l10; x1 = L.l11; x2 = 0.0; }
-            else if (i == c0 + 2) { x0 = L.l20; x1 = L.l21; x2 = L.l22; }
-            if (i == 0 && wave == 0) {
-                double* mi = rdg + 2 * c0;   // 8 doubles per 3x3 block
+            double x0 = col[0] * L.m00;
+            double x1 = fma(col[0], L.m10, col[1] * L.m11);
+            double x2 = fma(col[0], L.m20, fma(col[1], L.m21, col[2] * L.m22));
+            if (i == cv) { x0 = L.l00; x1 = 0.0; x2 = 0.0; }
+            else if (i == cv + 1) { x0 = L.l10; x1 = L.l11; x2 = 0.0; }
+            else if (i == cv + 2) { x0 = L.l20; x1 = L.l21; x2 = L.l22; }
+            if (i < kFNB) {
+                Lt[cv * kFNB + i] = (i >= cv && i < w) ? x0 : 0.0;
+                Lt[(cv + 1) * kFNB + i] = (i >= cv + 1 && i < w) ? x1 : 0.0;
+                Lt[(cv + 2) * kFNB + i] = (i >= cv + 2 && i < w) ? x2 : 0.0;
+            }
+            if (i == 0) {
+                double* mi = rdg + 2 * cv;   // 8 doubles per 3x3 block
                 mi[0] = L.m00; mi[1] = L.m10; mi[2] = L.m11; mi[3] = L.m20; mi[4] = L.m21; mi[5] = L.m22;
             }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const int c = wave + 8 * k;
-                if (c < c0 || c >= w) continue;   // wave-uniform
-                if (c < c0 + 3) {                  // the step's own columns: final L values
-                    const double xv = c == c0 ? x0 : (c == c0 + 1 ? x1 : x2);
-                    col[k] = (i >= c && i < w) ? xv : 0.0;
-                } else {
-                    const double y0 = rdlane(x0, c), y1 = rdlane(x1, c), y2 = rdlane(x2, c);
-                    const double v = fma(-x2, y2, fma(-x1, y1, fma(-x0, y0, col[k])));
-                    col[k] = (i >= c && i < w) ? v : col[k];
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int c = wave + 8 * k;
-            if (c < w && i < w) Lt[c * kFNB + i] = col[k];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (i == 0) __hip_atomic_store(flg + wave, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (cv < kFNB) {   // a short last panel: this wave's columns are past w
+            for (int r = 0; r < 3; ++r)
+                if (i < kFNB) Lt[(cv + r) * kFNB + i] = 0.0;
         }
     }
     __syncthreads();
@@ -1430,6 +1423,7 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
     if (mem == 0) {
         // ---- the panel chain
         double* cur = PA;
+        if (tid < kFNB / 3) reinterpret_cast<int*>(scr + kFNB * kFNB + 8 * (kFNB / 3))[tid] = 0;   // POTRF step epochs
         load_panel<false>(0, T, F, cur);   // tile 0: assembled by this workgroup
         __syncthreads();
         factor_lds(0, s, T, cur, scr, bad);
