@@ -376,7 +376,10 @@ __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float
         start = 0;
         return n;
     }
-    const float half = kPaSlope * sn * __builtin_amdgcn_rsqf(1.0f - sn * sn) * 1.0001f + kPaMargin;
+    // 1 / sqrt(1 - x) is convex on x = sn^2 in [0, 0.49]: below its chord 1 + 0.8172 x (the value
+    // 1/sqrt(0.51) = 1.40028 at the end), so the half-angle bound needs no reciprocal square root
+    // (the window only widens: a superset, exact as above)
+    const float half = kPaSlope * sn * fmaf(sn * sn, 0.8172f, 1.0f) * 1.0001f + kPaMargin;
     const float pq = pseudo_angle(qx, qy);
     float lo = pq - half, hi = pq + half;
     if (lo < 0.0f) lo += kTwoPi;

@@ -31,7 +31,8 @@ def half_width(qx, qy, rad):
         sn = (rad * (F(1) / np.sqrt((qx * qx + qy * qy).astype(F))).astype(F) * F(1.0001) + F(1e-6)).astype(F)
     ok = sn < F(0.7)
     s2 = np.where(ok, sn, F(0))
-    half = (SLOPE * s2 * (F(1) / np.sqrt(F(1) - s2 * s2)).astype(F) * F(1.0001) + MARGIN).astype(F)
+    # the kernel's chord bound of 1/sqrt(1 - sn^2) (dpg_icp_ang.hip window())
+    half = (SLOPE * s2 * (s2 * s2 * F(0.8172) + F(1)).astype(F) * F(1.0001) + MARGIN).astype(F)
     return ok, half
 
 
