@@ -1618,6 +1618,9 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
     *out = nullptr;
     CholDev* c = new CholDev();
     dpg_chol_opts o{64, 0.3};
+    // supernode size / explicit-zero budget (A/B only: DPG_CHOL_MAXCOLS, DPG_CHOL_RELAX)
+    if (const char* e = getenv("DPG_CHOL_MAXCOLS")) o.max_supernode_cols = atoi(e);
+    if (const char* e = getenv("DPG_CHOL_RELAX")) o.relax_fraction = atof(e);
     if (dpg_chol_symbolic(n, pair_lo, pair_hi, n_pairs, &o, &c->sym)) {
         delete c;
         return DPG_ERR_NUMERIC;
