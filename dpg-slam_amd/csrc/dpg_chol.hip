@@ -765,7 +765,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                         const int32_t* __restrict__ rows,
                                                         const SolveSeg* __restrict__ segs,
                                                         const double* __restrict__ fronts,
-                                                        const double* __restrict__ ysol, double* xsol, int R) {
+                                                        const double* __restrict__ ysol, double* xsol, int R,
+                                                        int max_seg) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
@@ -782,7 +783,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     double* xr = z + k3;             // r3
     int32_t* rp = reinterpret_cast<int32_t*>(xr + r3);   // r3 / 3 row positions
     SolveSeg* sg = reinterpret_cast<SolveSeg*>(xr + r3 + ((S.r + 3) / 4) * 2);   // [kMaxSeg], 16-B aligned
-    const int nseg = S.seg_n <= kMaxSeg ? S.seg_n : 0;
+    const int nseg = S.seg_n <= max_seg ? S.seg_n : 0;   // max_seg <= kMaxSeg
     const Stage P = stage_plan(m3, k3, R);
     // before any wait: y, the row positions, the segments, the front's L (all from earlier launches)
     for (int j = tid; j < k3; j += kT) z[j] = ysol[3 * (int64_t)S.c0 + j];
@@ -1574,6 +1575,7 @@ struct CholDev {
     size_t sync_bytes = 0;
     size_t lds_solve_max = 0;
     int32_t solve_stage = 0;   // R: LDS staging region of the solves, doubles (Stage)
+    int32_t solve_maxseg = 0;  // backward: fronts with more row segments wait for the parent (<= kMaxSeg)
     AsmTask* asm_tasks = nullptr;
     AsmChild* asm_child = nullptr;
     int2* panel_tasks = nullptr;
@@ -1998,6 +2000,8 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         const long want = env ? atol(env) : room / (long)sizeof(double);
         const long cap = ((long)(160 * 1024) - (long)lds_rest) / (long)sizeof(double);
         c->solve_stage = (int32_t)std::max<long>(0, std::min<long>(want, cap)) & ~1;
+        const char* ms = getenv("DPG_SOLVE_MAXSEG");   // tests: 0 = every front takes the parent path
+        c->solve_maxseg = ms ? std::max(0, std::min(atoi(ms), kMaxSeg)) : kMaxSeg;
     }
     c->lds_solve_max = (size_t)c->solve_stage * sizeof(double) + lds_rest;
     if (c->lds_solve_max > 160 * 1024) return DPG_ERR_SIZE;
@@ -2201,7 +2205,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
                            c->perm, c->fronts,
                            c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage);
+                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -2224,7 +2228,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage);
+                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2238,7 +2242,7 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

@@ -100,3 +100,28 @@ def test_orders_agree(ctx, workload, name):
     if name == "config3":
         Xo, _ = O.optimize_graph(X0, F)
         assert np.abs(pose_diff(Xn, Xo)).max() < 1e-6
+
+
+@pytest.mark.parametrize("env", [{"DPG_SOLVE_STAGE": "0"}, {"DPG_SOLVE_STAGE": "15000"}, {"DPG_SOLVE_MAXSEG": "0"},
+                                 {"DPG_SOLVE_MAXSEG": "1"}, {"DPG_CHOL_MERGE_SINGLE": "1"}])
+def test_solve_paths_agree(ctx, workload, env):
+    """The triangular solves' code paths give the same GN solution on config 4 (chord steps and
+    fresh factorizations): no LDS staging, staging of whole fronts up to 15 000 doubles, the
+    backward solve with every front waiting for its parent (no row segments) or with segments only
+    where there is one, and the single-child supernode rule -- against the default build."""
+    from dpgslam import _abi
+    w = workload("config4")
+    p = _abi.default_icp_params()
+    ctx.upload_scans(w.pts, w.offsets, 5)
+    res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
+    F = w.factors_with_icp(res, p)
+    X0 = w.est.astype(np.float64)
+    Xd, sd = _optimize(ctx, X0, F)
+    os.environ.update(env)   # read when the Cholesky is set up
+    try:
+        Xe, se = _optimize(ctx, X0, F)
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    assert se.iterations == sd.iterations
+    assert np.abs(pose_diff(Xe, Xd)).max() < 1e-9
