@@ -395,7 +395,7 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
     // front, whose index set holds their rows): nested dissection's separators become one front
     // each instead of a chain of fronts split at every subtree root attached to them.
     // DPG_CHOL_MERGE_SINGLE=1 restores the single-child rule.
-    static const bool any_child = getenv("DPG_CHOL_MERGE_SINGLE") == nullptr;
+    const bool any_child = getenv("DPG_CHOL_MERGE_SINGLE") == nullptr;
     {
         int32_t s = -1;
         int64_t zeros = 0, cols = 0;
