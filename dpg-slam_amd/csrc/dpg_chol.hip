@@ -1663,6 +1663,7 @@ struct CholHost {
     std::vector<FTask> ftasks;
     std::vector<FChild> fchild;
     std::vector<double> prio, hgt;
+    std::vector<int32_t> hcnt;
     std::vector<SolveSeg> segs;
     std::vector<std::pair<double, int32_t>> key;
     std::vector<int32_t> fo, bwd, order_fac, cuts;
@@ -2072,11 +2073,18 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
             hgt[(size_t)s] += 2.0 + 0.01 * (3 * (d.k + d.r)) + 0.05 * (3 * d.k);   // us, tools/chol_bench_t
             if (d.parent >= 0) hgt[(size_t)d.parent] = std::max(hgt[(size_t)d.parent], hgt[(size_t)s]);
         }
-        key.resize((size_t)S.ns);
-        for (int32_t s = 0; s < S.ns; ++s) key[(size_t)s] = {-hgt[(size_t)s], s};
-        std::sort(key.begin(), key.end());
+        // counting sort by height in 0.25 us buckets, descending; inside a bucket by descending
+        // supernode index, so a parent (higher index, greater height) still precedes its children
+        std::vector<int32_t>& cnt = H.hcnt;
+        double hmax = 0.0;
+        for (int32_t s = 0; s < S.ns; ++s) hmax = std::max(hmax, hgt[(size_t)s]);
+        const int32_t nb = (int32_t)(hmax * 4.0) + 2;
+        cnt.assign((size_t)nb + 1, 0);
+        for (int32_t s = 0; s < S.ns; ++s) ++cnt[(size_t)(nb - 1 - (int32_t)(hgt[(size_t)s] * 4.0)) + 1];
+        for (int32_t b = 0; b < nb; ++b) cnt[(size_t)b + 1] += cnt[(size_t)b];
         H.bwd.resize((size_t)S.ns);
-        for (int32_t i = 0; i < S.ns; ++i) H.bwd[(size_t)i] = key[(size_t)i].second;
+        for (int32_t s = S.ns - 1; s >= 0; --s)
+            H.bwd[(size_t)cnt[(size_t)(nb - 1 - (int32_t)(hgt[(size_t)s] * 4.0))]++] = s;
     }
     // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
     //  pivot-tile hand-off flags [per large-front tile]]
