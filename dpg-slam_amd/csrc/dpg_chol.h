@@ -82,6 +82,11 @@ int dpg_incsym_derive(dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sy
 // analysis is moved into *h: *S is left holding *h's previous one (or nothing).
 int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                         dpg_chol_sym* S);
+// the same in two halves: the plan (host only, no device call) and its upload (the same thread,
+// no other build in between); on error *h is destroyed and NULL
+int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                             dpg_chol_sym* S);
+int dpg_chol_create_sym_upload(void** h);
 // host time (ms) of the last build of h: structures, uploads
 void dpg_chol_build_times(void* h, double out[2]);
 // 1 when h factors with the fused DAG kernel (every front fits its LDS budget), 0 on the level path

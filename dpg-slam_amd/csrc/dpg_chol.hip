@@ -2161,18 +2161,48 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     return rc ? DPG_ERR_HIP : DPG_OK;
 }
 
-int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
+// the host structures of the build in progress on this thread (a plan and its upload may be split:
+// dpg_chol_create_sym_plan / _upload)
+CholHost& build_host() {
     thread_local CholHost H;
+    return H;
+}
+int chol_build_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
     const double t_b0 = wall_ms();
-    int rc = chol_plan(c, n, pair_lo, pair_hi, n_pairs, H);
-    if (rc) return rc;
+    const int rc = chol_plan(c, n, pair_lo, pair_hi, n_pairs, build_host());
+    c->t_build[0] = wall_ms() - t_b0;
+    return rc;
+}
+int chol_build_upload(CholDev* c) {
     const double t_b1 = wall_ms();
-    rc = chol_upload(c, n, H);
-    c->t_build[0] = t_b1 - t_b0;
+    const int rc = chol_upload(c, c->n, build_host());
     c->t_build[1] = wall_ms() - t_b1;
     return rc;
 }
+int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
+    const int rc = chol_build_plan(c, n, pair_lo, pair_hi, n_pairs);
+    return rc ? rc : chol_build_upload(c);
+}
 }  // namespace
+
+// dpg_chol_create_sym in two halves: the plan (host only: no device call, so it may run while the
+// caller's stream still works) and the upload of what it planned (same thread, nothing between)
+int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                             dpg_chol_sym* S) {
+    CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
+    std::swap(c->sym, *S);
+    const int rc = chol_build_plan(c, n, pair_lo, pair_hi, n_pairs);
+    if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
+    *h = c;
+    return DPG_OK;
+}
+int dpg_chol_create_sym_upload(void** h) {
+    CholDev* c = reinterpret_cast<CholDev*>(*h);
+    if (!c) return DPG_ERR_STATE;
+    const int rc = chol_build_upload(c);
+    if (rc) { dpg_chol_destroy(c); *h = nullptr; }
+    return rc;
+}
 
 #ifdef DPG_PLAN_TIMING
 double dpg_plan_t_export[8];

@@ -133,6 +133,10 @@ struct dpg_inc {
     int32_t* cnt = nullptr;                    // relinearized variables of the last update
     size_t c_theta = 0, c_est = 0, c_maxd = 0;
     std::vector<dpg_factor> h_dev_factors;     // staging (Q1 scaling)
+    bool prepared = false;                     // inc_prepare ran for the coming update (its pairs are in)
+    int64_t prep_new = 0;                      // ... for this many new nodes
+    bool prep_reordered = false;
+    double prep_ms[3] = {};                    // its incsym, derive, chol plan times
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
                                                // chol upload (ms); factor Mflop, largest front (blocks),
                                                // fused DAG path (1) or level path (0), supernodes
@@ -201,8 +205,8 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
     // the host vectors above must outlive the async copies
     if (hipStreamSynchronize(s) != hipSuccess) return DPG_ERR_HIP;
     const double t = now_ms();
-    const int rc2 = dpg_chol_create_sym(&g.chol, n, q->plo.data(), q->phi.data(), P, &q->S);
-    q->prof[3] = now_ms() - t;
+    const int rc2 = dpg_chol_create_sym_upload(&g.chol);   // planned by inc_prepare
+    q->prof[3] = now_ms() - t + q->prep_ms[2];
     if (!rc2) {
         dpg_chol_build_times(g.chol, q->prof + 4);
         double st[6];
@@ -297,6 +301,62 @@ int64_t dpg_inc_pairs(const dpg_inc* q, int32_t* lo, int32_t* hi, int64_t n) {
     return P;
 }
 
+// The structural half of the next update (host only, no device call): n_new nodes join, the node
+// pairs (a_k, b_k) enter the pattern (a superset of the coming Between factors' pairs is fine: a
+// pair without factors is an explicit zero block), the symbolic analysis is extended or redone and
+// the Cholesky planned.  dpg_add_node_pairs runs it while the GPU aligns the node's edges; the
+// next dpg_inc_update (for the same n_new) uploads the plan and solves.
+int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs) {
+    if (!q || n_new < 0 || n_pairs < 0 || (n_pairs > 0 && !pairs)) return set_err(DPG_ERR_ARG, "dpg_inc_prepare: bad arguments");
+    const int64_t V1 = q->V + n_new;
+    for (int64_t e = 0; e < n_pairs; ++e)
+        if (pairs[2 * e] < 0 || pairs[2 * e + 1] < 0 || pairs[2 * e] >= V1 || pairs[2 * e + 1] >= V1 ||
+            pairs[2 * e] == pairs[2 * e + 1])
+            return set_err(DPG_ERR_ARG, "dpg_inc_prepare: a pair references a missing node");
+    if (V1 == 0) return set_err(DPG_ERR_STATE, "dpg_inc_prepare: empty graph");
+    const double t1 = now_ms();
+    if (q->I.n > 0) dpg_incsym_append(&q->I, n_new);
+    std::vector<std::pair<int32_t, int32_t>> new_pairs;
+    for (int64_t e = 0; e < n_pairs; ++e) {
+        const int32_t lo = std::min(pairs[2 * e], pairs[2 * e + 1]), hi = std::max(pairs[2 * e], pairs[2 * e + 1]);
+        if (q->pair_id.find(pkey(lo, hi)) == q->pair_id.end()) {
+            q->pair_id.emplace(pkey(lo, hi), (int32_t)q->plo.size());
+            q->plo.push_back(lo);
+            q->phi.push_back(hi);
+            new_pairs.emplace_back(lo, hi);
+        }
+    }
+    // ordering: extended, or fresh every reorder_every nodes / after 1.5x fill growth
+    bool reordered = false;
+    const double expect = q->V_at_order > 0 ? (double)q->nnz_at_order * (double)V1 / (double)q->V_at_order : 0.0;
+    if (q->I.n == 0 || V1 - q->V_at_order >= q->P.reorder_every) {
+        reordered = true;
+    } else {
+        for (auto& pr : new_pairs) dpg_incsym_add_edge(&q->I, pr.first, pr.second);
+        if ((double)q->I.nnz > 1.5 * expect + 64.0) reordered = true;
+    }
+    if (reordered) {
+        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size()))
+            return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic analysis failed");
+        q->V_at_order = V1;
+        q->nnz_at_order = q->I.nnz;
+        q->reorders += 1;
+    }
+    const double t1a = now_ms();
+    if (dpg_incsym_derive(&q->I, &q->opts, &q->S))
+        return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic derivation failed");
+    const double t1b = now_ms();
+    const int rc = dpg_chol_create_sym_plan(&q->g.chol, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size(), &q->S);
+    if (rc) return set_err(rc, "dpg_inc_prepare: Cholesky plan failed");
+    q->prep_ms[0] = t1a - t1;
+    q->prep_ms[1] = t1b - t1a;
+    q->prep_ms[2] = now_ms() - t1b;
+    q->prep_reordered = reordered;
+    q->prep_new = n_new;
+    q->prepared = true;
+    return DPG_OK;
+}
+
 int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_factor* factors, int64_t n_factors,
                    dpg_inc_stats* st) {
     if (!q || n_new < 0 || n_factors < 0 || (n_new > 0 && !init) || (n_factors > 0 && !factors))
@@ -328,58 +388,41 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
             hipMemsetAsync(q->maxd + V0, 0, sizeof(double) * (size_t)n_new, s) != hipSuccess)
             return set_err(DPG_ERR_HIP, "dpg_inc_update: upload failed");
     }
-    // graph + symbolic state
+    // graph + symbolic state: the pairs of this update's Between factors are in the pattern already
+    // when dpg_add_node_pairs prepared it while its alignments ran, else prepare them now
+    if (!q->prepared) {
+        std::vector<int32_t> pr;
+        pr.reserve((size_t)(2 * n_factors));
+        for (int64_t k = 0; k < n_factors; ++k)
+            if (factors[k].kind == DPG_FACTOR_BETWEEN) { pr.push_back(factors[k].i); pr.push_back(factors[k].j); }
+        if ((rc = dpg_inc_prepare(q, n_new, pr.data(), (int64_t)pr.size() / 2))) return rc;
+    } else if (q->prep_new != n_new) {
+        q->prepared = false;
+        return set_err(DPG_ERR_STATE, "dpg_inc_update: prepared for another number of new nodes");
+    }
+    q->prepared = false;
     const bool relin = q->P.mode == DPG_INC_ISAM2 && (q->updates % q->P.relinearize_skip) == 0 && V0 > 0;
     q->updates += 1;
     q->V = V1;
-    if (q->I.n > 0) dpg_incsym_append(&q->I, n_new);
-    std::vector<std::pair<int32_t, int32_t>> new_pairs;
     for (int64_t k = 0; k < n_factors; ++k) {
         const dpg_factor& f = factors[k];
         int32_t pid = -1;
         if (f.kind == DPG_FACTOR_BETWEEN) {
-            const int32_t lo = std::min(f.i, f.j), hi = std::max(f.i, f.j);
-            auto it = q->pair_id.find(pkey(lo, hi));
-            if (it == q->pair_id.end()) {
-                pid = (int32_t)q->plo.size();
-                q->pair_id.emplace(pkey(lo, hi), pid);
-                q->plo.push_back(lo);
-                q->phi.push_back(hi);
-                new_pairs.emplace_back(lo, hi);
-            } else {
-                pid = it->second;
-            }
+            auto it = q->pair_id.find(pkey(std::min(f.i, f.j), std::max(f.i, f.j)));
+            if (it == q->pair_id.end()) return set_err(DPG_ERR_STATE, "dpg_inc_update: a factor's pair was not prepared");
+            pid = it->second;
         }
         q->F.push_back(f);
         q->f_created.push_back((int32_t)q->updates);
         q->f_pair.push_back(pid);
     }
-    const double t1 = now_ms();
-    // ordering: extended, or fresh every reorder_every nodes / after 1.5x fill growth
-    bool reordered = false;
-    const double expect = q->V_at_order > 0 ? (double)q->nnz_at_order * (double)V1 / (double)q->V_at_order : 0.0;
-    if (q->I.n == 0 || V1 - q->V_at_order >= q->P.reorder_every) {
-        reordered = true;
-    } else {
-        for (auto& pr : new_pairs) dpg_incsym_add_edge(&q->I, pr.first, pr.second);
-        if ((double)q->I.nnz > 1.5 * expect + 64.0) reordered = true;
-    }
-    if (reordered) {
-        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size()))
-            return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: symbolic analysis failed");
-        q->V_at_order = V1;
-        q->nnz_at_order = q->I.nnz;
-        q->reorders += 1;
-    }
-    const double t1a = now_ms();
-    if (dpg_incsym_derive(&q->I, &q->opts, &q->S))
-        return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: symbolic derivation failed");
+    const bool reordered = q->prep_reordered;
     const double t1b = now_ms();
     if ((rc = inc_rebuild(q, s))) return set_err(rc, "dpg_inc_update: solver rebuild failed");
     const double t2 = now_ms();
-    q->prof[0] = t1a - t1;
-    q->prof[1] = t1b - t1a;
-    q->prof[2] = t2 - t1b - q->prof[3];
+    q->prof[0] = q->prep_ms[0];
+    q->prof[1] = q->prep_ms[1];
+    q->prof[2] = t2 - t1b - (q->prof[3] - q->prep_ms[2]);
     dpg_inc_stats S;
     memset(&S, 0, sizeof(S));
     S.reordered = reordered ? 1 : 0;
@@ -441,7 +484,7 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     S.n_factors = (int64_t)q->F.size();
     S.nnz_l = q->I.nnz;
     S.ms_total = t3 - t0;
-    S.ms_symbolic = t2 - t1;
+    S.ms_symbolic = t2 - t1b + q->prep_ms[0] + q->prep_ms[1] + q->prep_ms[2];
     S.ms_numeric = t3 - t2;
     if (st) *st = S;
     return DPG_OK;
