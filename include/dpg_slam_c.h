@@ -371,7 +371,10 @@ typedef struct dpg_add_node_stats {
  * joins the scan store; ONE batched ICP aligns the successive pair (V-1, V) when `successive` and
  * every pair in pairs[n_pairs][2] = {node_1 (target), node_2 (source)}, keys <= V; the successive
  * factor always joins the graph, the other pairs' factors when converged (dpg_slam.cc:263-267,
- * 295-301), after the caller's `extra` factors, in one dpg_inc_update (initial pose init_pose). */
+ * 295-301), after the caller's `extra` factors, in one dpg_inc_update (initial pose init_pose).
+ * The update's symbolic work runs on the host while the GPU aligns, with every pair in the pattern:
+ * a pair whose alignment does not converge stays an explicit zero block of H (no factor; the
+ * solution is unchanged, the update's nnz statistics count it). */
 int dpg_add_node_pairs(dpg_inc* g, const float* cloud_xy, int64_t n_pts, const float init_pose[3],
                        const dpg_factor* extra, int64_t n_extra, const int32_t* pairs, int64_t n_pairs,
                        int32_t successive, const dpg_icp_params* icp_params, dpg_add_node_stats* stats);
