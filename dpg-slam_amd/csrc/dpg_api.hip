@@ -378,6 +378,15 @@ int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k
     return DPG_OK;
 }
 
+// the scan store back to its first V nodes (dpg_add_node_pairs' rollback); the device arrays keep
+// their capacity, the entries past V are overwritten by the next append
+static void scans_truncate(dpg_ctx* c, int64_t V) {
+    if (!c || V < 0 || V >= c->n_nodes) return;
+    c->full_off.resize((size_t)V + 1);
+    c->ds_off.resize((size_t)V + 1);
+    c->n_nodes = V;
+}
+
 int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
     if (!c || (!edges && ne > 0) || !poses) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
     if (c->n_nodes <= 0) return fail(DPG_ERR_STATE, "no scans uploaded");
@@ -681,6 +690,11 @@ int icp_cov_sandwich(dpg_ctx* c, const float* data, int64_t nd, const float* mod
                      double cov6_out[36], double cov3_out[9]) {
     if (!T || !data || !model || nd < 1 || nm < 1 || nd > INT32_MAX / 4 || nm > INT32_MAX / 4)
         return fail(DPG_ERR_ARG, "icp_cov_sandwich: bad arguments");
+    // the closed forms hold at the planar operating point z = pitch = roll = 0 (the reference reads
+    // z, roll, pitch from T's third row, cov_func_point_to_point.h:26-31): a non-planar T is refused
+    // rather than silently evaluated at the wrong point
+    if (T[2] != 0.f || T[6] != 0.f || T[8] != 0.f || T[9] != 0.f || T[10] != 1.f || T[11] != 0.f)
+        return fail(DPG_ERR_ARG, "icp_cov_sandwich: T is not planar (needs T20 = T21 = T02 = T12 = T23 = 0, T22 = 1)");
     if (!c) {
         if (!g_default_ctx) g_default_ctx = dpg_ctx_create(0);
         c = g_default_ctx;
@@ -990,37 +1004,29 @@ int64_t dpg_get_map(dpg_ctx* c, const float* est, int32_t fraction, float* out, 
 
 float dpg_get_map_kernel_ms(dpg_ctx* c) { return c ? c->map_ms : -1.f; }
 
-int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, const float* odom,
-                   const dpg_icp_params* ip, const dpg_gn_params* gp, const dpg_reopt_params* rp, double* poses_out,
-                   dpg_reopt_stats* st) {
-    if (!c || V <= 0 || !pass || !est || !odom || !poses_out) return fail(DPG_ERR_ARG, "bad arguments");
-    if (c->n_nodes != V) return fail(DPG_ERR_STATE, "scans of %lld nodes uploaded, sweep over %lld",
-                                     (long long)c->n_nodes, (long long)V);
-    dpg_icp_params I;
-    if (ip) I = *ip;
-    else dpg_icp_params_default(&I);
-    dpg_gn_params P;
-    if (gp) P = *gp;
-    else dpg_gn_params_default(&P);
-    dpg_reopt_params R;
-    if (rp) R = *rp;
-    else dpg_reopt_params_default(&R);
-    dpg_reopt_stats S;
-    memset(&S, 0, sizeof(S));
+// The sweep of DpgSLAM::reoptimize up to the alignments (dpg_slam.cc:35-107): candidates, the ICP
+// edge list (successive, then candidates), the factor list (per node a pass prior or the odometry
+// Between, then one Between slot per ICP edge, first at first_icp) and ONE batched ICP launched on
+// the context's stream (not waited for).
+static int reopt_sweep(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, const float* odom,
+                       const dpg_icp_params& I, const dpg_reopt_params& R, std::vector<int32_t>& edges,
+                       std::vector<dpg_factor>& F, int64_t& first_icp, int64_t& n_succ, dpg_reopt_stats& S,
+                       double& t1) {
     const double t0 = now_ms();
     // 1. loop-closure candidates (dpg_slam.cc:91-98)
     std::vector<int32_t> lc;
     const int64_t K = lc_candidates(c, V, pass, est, R.max_node_dist_within_pass, R.max_node_dist_across_passes, lc);
     if (K < 0) return (int)K;
-    const double t1 = now_ms();
+    t1 = now_ms();
     // 2. ICP edges: successive (i-1, i), then the candidates (j, i) -- {node_1 target, node_2 source}
-    const int64_t n_succ = V - 1, E = n_succ + K;
-    std::vector<int32_t> edges((size_t)(2 * E));
+    n_succ = V - 1;
+    const int64_t E = n_succ + K;
+    edges.assign((size_t)(2 * E), 0);
     for (int64_t i = 1; i < V; ++i) { edges[(size_t)(2 * (i - 1))] = (int32_t)(i - 1); edges[(size_t)(2 * (i - 1) + 1)] = (int32_t)i; }
     if (K > 0) memcpy(edges.data() + 2 * n_succ, lc.data(), sizeof(int32_t) * 2 * (size_t)K);
     // 3. factors: per node a prior (new pass) or the odometry Between (dpg_slam.cc:40-79), then one
     //    slot per ICP edge (measurements filled on device after the batch)
-    std::vector<dpg_factor> F;
+    F.clear();
     F.reserve((size_t)(V + E));
     int32_t cur_pass = -1;
     for (int64_t i = 0; i < V; ++i) {
@@ -1044,7 +1050,7 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
             F.push_back(f);
         }
     }
-    const int64_t first_icp = (int64_t)F.size();
+    first_icp = (int64_t)F.size();
     for (int64_t e = 0; e < E; ++e) {
         dpg_factor f;
         memset(&f, 0, sizeof(f));
@@ -1056,7 +1062,36 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
     // 4. one batched ICP of every edge from the estimated poses (runIcp, dpg_slam.cc:362-446)
     int rc = dpg_icp_batch_prepare(c, edges.data(), E, est, &I);
     if (!rc) rc = dpg_icp_batch_run(c, 0, 0);
+    S.n_candidates = K;
+    S.n_icp_edges = E;
+    S.ms_candidates = t1 - t0;
+    return rc;
+}
+
+int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est, const float* odom,
+                   const dpg_icp_params* ip, const dpg_gn_params* gp, const dpg_reopt_params* rp, double* poses_out,
+                   dpg_reopt_stats* st) {
+    if (!c || V <= 0 || !pass || !est || !odom || !poses_out) return fail(DPG_ERR_ARG, "bad arguments");
+    if (c->n_nodes != V) return fail(DPG_ERR_STATE, "scans of %lld nodes uploaded, sweep over %lld",
+                                     (long long)c->n_nodes, (long long)V);
+    dpg_icp_params I;
+    if (ip) I = *ip;
+    else dpg_icp_params_default(&I);
+    dpg_gn_params P;
+    if (gp) P = *gp;
+    else dpg_gn_params_default(&P);
+    dpg_reopt_params R;
+    if (rp) R = *rp;
+    else dpg_reopt_params_default(&R);
+    dpg_reopt_stats S;
+    memset(&S, 0, sizeof(S));
+    std::vector<int32_t> edges;
+    std::vector<dpg_factor> F;
+    int64_t first_icp = 0, n_succ = 0;
+    double t1 = 0.0;
+    int rc = reopt_sweep(c, V, pass, est, odom, I, R, edges, F, first_icp, n_succ, S, t1);
     if (rc) return rc;
+    const int64_t E = S.n_icp_edges;
     if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(DPG_ERR_HIP, "ICP batch failed");
     const double t2 = now_ms();
     // 5. batch Gauss-Newton from the estimated poses (optimizeGraph, dpg_slam.cc:111-119, 316-329)
@@ -1073,11 +1108,63 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
     if ((rc = gn_loop(c, P, poses_out, t2, now_ms(), &S.gn))) return rc;
     const double t3 = now_ms();
     S.n_factors = (int64_t)F.size();
-    S.n_icp_edges = E;
-    S.n_candidates = K;
-    S.ms_candidates = t1 - t0;
     S.ms_icp = t2 - t1;
     S.ms_gn = t3 - t2;
+    if (st) *st = S;
+    return DPG_OK;
+}
+
+int dpg_reoptimize_inc(dpg_inc* g, int64_t V, const int32_t* pass, const float* est, const float* odom,
+                       const dpg_icp_params* ip, const dpg_reopt_params* rp, double* poses_out, dpg_reopt_stats* st) {
+    if (!g || V <= 0 || !pass || !est || !odom || !poses_out) return fail(DPG_ERR_ARG, "dpg_reoptimize_inc: bad arguments");
+    dpg_ctx* c = dpg_inc_ctx(g);
+    if (c->n_nodes != V) return fail(DPG_ERR_STATE, "scans of %lld nodes uploaded, sweep over %lld",
+                                     (long long)c->n_nodes, (long long)V);
+    dpg_icp_params I;
+    if (ip) I = *ip;
+    else dpg_icp_params_default(&I);
+    dpg_reopt_params R;
+    if (rp) R = *rp;
+    else dpg_reopt_params_default(&R);
+    dpg_reopt_stats S;
+    memset(&S, 0, sizeof(S));
+    std::vector<int32_t> edges;
+    std::vector<dpg_factor> F;
+    int64_t first_icp = 0, n_succ = 0;
+    double t1 = 0.0;
+    int rc = reopt_sweep(c, V, pass, est, odom, I, R, edges, F, first_icp, n_succ, S, t1);
+    if (rc) return rc;
+    const int64_t E = S.n_icp_edges;
+    std::vector<dpg_icp_result> res((size_t)std::max<int64_t>(E, 1));
+    if (E > 0 && (rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+    const double t2 = now_ms();
+    // addObservationConstraint per aligned pair: the successive pairs always, a loop closure when
+    // its alignment converged (dpg_slam.cc:85-104); the slots of dropped closures go away
+    F.resize((size_t)first_icp);
+    for (int64_t e = 0; e < E; ++e) {
+        const dpg_icp_result& r = res[(size_t)e];
+        if (r.status == DPG_ICP_INTERNAL)
+            return fail(DPG_ERR_INTERNAL, "dpg_reoptimize_inc: alignment %lld failed its internal check", (long long)e);
+        if (e < n_succ || (r.converged && r.status == DPG_ICP_OK)) {
+            dpg_factor f;
+            dpg_icp_factor(&r, edges[(size_t)(2 * e)], edges[(size_t)(2 * e + 1)], &I, &f);
+            F.push_back(f);
+            if (e >= n_succ) ++S.n_loop_closures;
+        }
+    }
+    // the new ISAM2 + graph_ and its one update from the current estimates (dpg_slam.cc:36-39,111-119)
+    std::vector<double> X0((size_t)(3 * V));
+    for (int64_t v = 0; v < 3 * V; ++v) X0[(size_t)v] = (double)est[v];
+    if ((rc = dpg_inc_reset(g))) return rc;
+    dpg_inc_stats is;
+    if ((rc = dpg_inc_update(g, V, X0.data(), F.data(), (int64_t)F.size(), &is))) return rc;
+    if ((rc = dpg_inc_get_poses(g, poses_out, V))) return rc;
+    const double t3 = now_ms();
+    S.n_factors = (int64_t)F.size();
+    S.ms_icp = t2 - t1;
+    S.ms_gn = t3 - t2;
+    S.gn.iterations = is.gn_iterations;
+    S.gn.final_error = is.error;
     if (st) *st = S;
     return DPG_OK;
 }
@@ -1100,11 +1187,24 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
     for (int64_t e = 0; e < n_pairs; ++e)
         if (pairs[2 * e] < 0 || pairs[2 * e + 1] < 0 || pairs[2 * e] > V || pairs[2 * e + 1] > V || pairs[2 * e] == pairs[2 * e + 1])
             return fail(DPG_ERR_ARG, "dpg_add_node_pairs: pair %lld references a missing node", (long long)e);
-    // createNode: the node's cloud joins the store (node id V)
+    // createNode: the node's cloud joins the store (node id V).  Any failure after this point
+    // takes the node out of the store again (and undoes a prepared update), so the store and the
+    // graph keep the same node count and the next dpg_add_node can proceed.
     const int64_t offs[2] = {0, n_pts};
     const float dummy[2] = {0.f, 0.f};
     int rc = dpg_scans_append(c, n_pts > 0 ? cloud : dummy, offs, 1, I.downsample_icp_points_ratio);
     if (rc) return rc;
+    struct Undo {
+        dpg_ctx* c;
+        dpg_inc* g;
+        int64_t V;
+        bool armed = true;
+        ~Undo() {
+            if (!armed) return;
+            dpg_inc_abort_prepare(g);
+            scans_truncate(c, V);
+        }
+    } undo{c, g, V};
     // estimates as float (dpg_nodes_ positions), the new node's initial pose last
     std::vector<double> est((size_t)(3 * std::max<int64_t>(V, 1)));
     if (V > 0 && (rc = dpg_inc_get_poses(g, est.data(), V))) return rc;
@@ -1133,6 +1233,9 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
         if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
         S.ms_icp = now_ms() - t0;
         S.n_icp_edges = E;
+        for (int64_t e = 0; e < E; ++e)   // a failed kernel self-check is an error, never a factor
+            if (res[(size_t)e].status == DPG_ICP_INTERNAL)
+                return fail(DPG_ERR_INTERNAL, "dpg_add_node_pairs: alignment %lld failed its internal check", (long long)e);
         for (int64_t e = 0; e < E; ++e) {
             const dpg_icp_result& r = res[(size_t)e];
             const bool ok = r.converged && r.status == DPG_ICP_OK;
@@ -1149,7 +1252,8 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
         if (rc) return fail(rc, "angle index build failed");
     }
     const double init[3] = {(double)init_pose[0], (double)init_pose[1], (double)init_pose[2]};
-    if ((rc = dpg_inc_update(g, 1, init, F.data(), (int64_t)F.size(), &S.update))) return rc;
+    if ((rc = dpg_inc_update(g, 1, init, F.data(), (int64_t)F.size(), &S.update))) return rc;   // rolled back itself
+    undo.armed = false;
     if (st) *st = S;
     return DPG_OK;
 }

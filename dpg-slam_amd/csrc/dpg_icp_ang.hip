@@ -26,6 +26,7 @@
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -361,6 +362,27 @@ __device__ __forceinline__ float sqd(float ax, float ay, float bx, float by) {
     return d.x + d.y;
 }
 
+// one candidate record r against (qx, qy): the 64-bit order word (bits(d) << 32 | key) with d
+// computed straight into the record's pad register (the hi half of the word: no register move),
+// d = (qx - rx)^2 + (qy - ry)^2 in float as sqd (packed subtract / multiply, one add)
+__device__ __forceinline__ uint64_t cand_key(const uint4& r, float qx, float qy) {
+    f2v d = (f2v){qx, qy} - (f2v){__uint_as_float(r.x), __uint_as_float(r.y)};
+    d = d * d;
+    uint32_t w = r.w;
+    asm volatile("v_add_f32 %0, %1, %2" : "+v"(w) : "v"(d.x), "v"(d.y));
+    return ((uint64_t)w << 32) | r.z;
+}
+
+// hardware square root (<= 1 ulp): only ever used for window radii and clearances that carry a
+// relative margin of >= 1e-5, so the windows stay supersets (exact) without the correctly
+// rounded sequence
+__device__ __forceinline__ float hw_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+template <int VAR>
+__device__ __forceinline__ float bsqrt(float x) {
+    if constexpr (VAR >= 1) return hw_sqrt(x);
+    else return sqrtf(x);
+}
+
 // (s + step) mod n for s in [0, n), step = kU mod n < n: one add and an unsigned min
 __device__ __forceinline__ int advance(int s, int step, int n) {
     const uint32_t a = (uint32_t)(s + step);
@@ -419,6 +441,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 // match (its distance bounds the radius), -1 means no knowledge (search r + kClear, probing the
 // target at q's own bearing first).  Returns the initial best key and sets the radius.  Used by
 // the owner lane and by the cooperative scan with identical arithmetic.
+template <int VAR>
 __device__ __forceinline__ uint64_t forward_init(const Lds& L, int M, int sd, float qx, float qy, float r2f, float rmax,
                                                  float rext, float r2ext, float& rad) {
     uint64_t best = dkey(r2f, 0xffffffffu);   // "none": every candidate with d <= r beats it
@@ -433,7 +456,7 @@ __device__ __forceinline__ uint64_t forward_init(const Lds& L, int M, int sd, fl
             const float d = sqd(qx, qy, r.x, r.y);
             if (d <= r2ext) {
                 best = dkey(d, r.key);
-                rad = sqrtf(d) * 1.0001f + 1e-6f;
+                rad = bsqrt<VAR>(d) * 1.0001f + 1e-6f;
             }
         }
     } else {
@@ -441,7 +464,7 @@ __device__ __forceinline__ uint64_t forward_init(const Lds& L, int M, int sd, fl
         const float d = sqd(qx, qy, r.x, r.y);
         if (d <= r2f) {
             best = dkey(d, r.key);
-            rad = sqrtf(d) * 1.0001f + 1e-6f;
+            rad = bsqrt<VAR>(d) * 1.0001f + 1e-6f;
         }
     }
     return best;
@@ -458,7 +481,7 @@ __device__ __forceinline__ uint32_t st_with_seed(uint32_t st, int seed) { return
 // 4 (<= 128 VGPRs) at 4 points per lane, 2 (<= 256) beyond
 constexpr int ang_wpe(int ppt, int mode) { return mode == 0 && ppt <= 2 ? DPG_ANG_WPE : mode == 0 && ppt == 4 ? 4 : 2; }
 
-template <int PPT, int MODE>
+template <int PPT, int MODE, int VAR>
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT, MODE), ang_wpe(PPT, MODE)))) void icp_ang_kernel(const float2* __restrict__ ds_pts,
                                                      const float2* __restrict__ idx_pts,
                                                      const uint16_t* __restrict__ idx_orig,
@@ -564,7 +587,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         const int bp = (bkey == 0xffffffffu || bd > r2f) ? -1 : (int)(bkey & 0xffffu);   // R4: d > r^2 rejected
         int nsd = bp;
         if (bp < 0 && ext) {   // nothing within r: the nearest target is >= min(sqrt(bd), rext) away
-            const float clr = fminf(sqrtf(bd), rext) * 0.99999f - rmax_hi;
+            const float clr = fminf(bsqrt<VAR>(bd), rext) * 0.99999f - rmax_hi;
             const int q = clr > 0.f ? (int)(clr * 1e4f) : 0;   // units of 1e-4 m, rounded down
             nsd = -1 - q;
         }
@@ -607,7 +630,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             // ---- forward 1-NN (target index), seeded radius ----
             const bool search = live && sd >= -1;   // < -1: clearance, provably no target within r
             float rad;
-            uint64_t best = forward_init(L, M, search ? sd : 0, qx, qy, r2f, rmax, rext, r2ext, rad);
+            uint64_t best = forward_init<VAR>(L, M, search ? sd : 0, qx, qy, r2f, rmax, rext, r2ext, rad);
             bool pend;   // this point's forward window went to the queue
             {
                 int s = 0;
@@ -634,7 +657,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     ld_recs<kTpL>(L.tp + s, r);
 #pragma unroll
                     for (int u = 0; u < kU; ++u) {
-                        const uint64_t kd = dkey(sqd(qx, qy, __uint_as_float(r[u].x), __uint_as_float(r[u].y)), r[u].z);
+                        uint64_t kd;
+                        if constexpr (VAR >= 1) kd = cand_key(r[u], qx, qy);
+                        else kd = dkey(sqd(qx, qy, __uint_as_float(r[u].x), __uint_as_float(r[u].y)), r[u].z);
                         best = kd < best ? kd : best;
                     }
                     s = advance(s, stepM, M);
@@ -654,7 +679,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     // t_j in the source node frame; float error ~1e-6 m, far inside the window margin
                     const float ux = tj.x - ftx, uy = tj.y - fty;
                     const float px = i00 * ux + i01 * uy, py = i10 * ux + i11 * uy;
-                    rc = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
+                    rc = window(L.sb, N, px, py, bsqrt<VAR>(bd) * 1.0001f + drift, s);
                 }
                 const int slot = queue_push(ok && rc > dcap, &L.bc->qtail);
                 if (slot >= 0) {
@@ -677,6 +702,21 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     wtrips += trips;
                 }
 #endif
+                if constexpr (VAR >= 1) {
+                    // the wave's still-reciprocal lanes as a mask: the beat tests are ballots
+                    // folded by scalar ors, the loop condition one scalar and
+                    uint64_t okm = __ballot(ok);
+                    for (int c = 0; (okm & __ballot(c < rc)) != 0; c += kU) {
+                        uint4 r[kU];
+                        ld_recs<kScsL>(L.scs + s, r);
+                        uint64_t beat = 0;
+#pragma unroll
+                        for (int u = 0; u < kU; ++u) beat |= __ballot(cand_key(r[u], tj.x, tj.y) < mine);
+                        okm &= ~beat;
+                        s = advance(s, stepN, N);
+                    }
+                    ok = ok && ((okm >> lane) & 1u);
+                } else {
                 for (int c = 0; __any(ok & (c < rc)); c += kU) {
                     uint4 r[kU];
                     ld_recs<kScsL>(L.scs + s, r);
@@ -688,6 +728,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     }
                     ok = ok & !beat;
                     s = advance(s, stepN, N);
+                }
                 }
             }
 #ifdef DPG_ICP_STATS
@@ -711,7 +752,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 uint64_t best = 0;
                 if ((w1 & 1u) == 0u) {   // forward argmin over the window, then the reciprocal test
                     float rad;
-                    const uint64_t b0 = forward_init(L, M, (int)(w1 >> 1) - 1, qx, qy, r2f, rmax, rext, r2ext, rad);
+                    const uint64_t b0 = forward_init<VAR>(L, M, (int)(w1 >> 1) - 1, qx, qy, r2f, rmax, rext, r2ext, rad);
                     const int fc = window(L.tb, M, qx, qy, rad, s);
                     best = lane == 0 ? b0 : ~0ull;
                     for (int c = lane; c < fc; c += 64) {
@@ -737,7 +778,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     const float bd = sqd(qx, qy, tjx, tjy);   // the same float the forward search kept
                     const float ux = tjx - ftx, uy = tjy - fty;
                     const float px = i00 * ux + i01 * uy, py = i10 * ux + i11 * uy;
-                    cnt = window(L.sb, N, px, py, sqrtf(bd) * 1.0001f + drift, s);
+                    cnt = window(L.sb, N, px, py, bsqrt<VAR>(bd) * 1.0001f + drift, s);
                     const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)ps);
                     bool beat = false;
                     for (int c = lane; c < cnt; c += 64) {
@@ -892,7 +933,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             const int sd = st_seed(st[m]);
             if (sd < -1) {   // the clearance shrinks by the distance the point just moved
                 const float dx = sx[m] - x, dy = sy[m] - y;
-                const float mv = sqrtf(dx * dx + dy * dy) * 1.0001f + 1e-6f;
+                const float mv = bsqrt<VAR>(dx * dx + dy * dy) * 1.0001f + 1e-6f;
                 const int q = (-1 - sd) - (int)ceilf(mv * 1e4f);
                 st[m] = st_with_seed(st[m], q > 0 ? -1 - q : -1);
             }
@@ -996,11 +1037,15 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     const int64_t chunk = mode ? (int64_t)(scratch && per_edge ? scratch_bytes / per_edge : 0) : n_edges;
     if (chunk <= 0) return DPG_ERR_SIZE;
     Rec* g = reinterpret_cast<Rec*>(scratch);
+    const char* ve = getenv("DPG_ICP_VARIANT");   // A/B of kernel variants (tools/icp_ab.py)
+    const int var = ve ? atoi(ve) : 1;
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
-        hipLaunchKernelGGL((icp_ang_kernel<P, M>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+        if (var == 0) hipLaunchKernelGGL((icp_ang_kernel<P, M, 0>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+                           results_dev, trace_dev, g);                                                               \
+        else hipLaunchKernelGGL((icp_ang_kernel<P, M, 1>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);

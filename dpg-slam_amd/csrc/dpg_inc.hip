@@ -15,8 +15,9 @@
 //   DPG_INC_ISAM2 (default) -- GTSAM ISAM2 with its default parameters: a
 //     linearization point theta per variable, relinearized (theta_k <- theta_k (+) delta_k) only
 //     for variables whose max |delta_k| >= relinearize_threshold (0.1), and only on updates whose
-//     count before the update is a multiple of relinearize_skip (10) -- GTSAM 4.0's
-//     UpdateImpl::relinarizationNeeded; every update re-linearizes every factor at theta, solves
+//     count, this update included, is a multiple of relinearize_skip (10): updates 10, 20, 30 --
+//     GTSAM 4.0's ISAM2::update increments update_count_ first and then asks
+//     UpdateImpl::relinarizationNeeded(update_count_) (update_count % relinearizeSkip == 0); every update re-linearizes every factor at theta, solves
 //     H(theta) delta = -g(theta) by Cholesky and returns the estimate theta (+) delta, one
 //     Gauss-Newton step from a lagging linearization point.  Deviation, documented: the solve is
 //     exact (ISAM2's back-substitution stops at the wildfire threshold 0.001).
@@ -130,11 +131,18 @@ struct dpg_inc {
     double* theta = nullptr;                   // [V][3] linearization points (g.poses aliases it)
     double* est = nullptr;                     // [V][3] current estimate
     double* maxd = nullptr;                    // [V] max |delta_v| of the last update
+    double* est_nxt = nullptr;                 // ISAM2 mode: the update's estimate and max |delta| are
+    double* maxd_nxt = nullptr;                // written here and swapped in once the solve succeeded
+    size_t c_est_nxt = 0, c_maxd_nxt = 0;
     int32_t* cnt = nullptr;                    // relinearized variables of the last update
     size_t c_theta = 0, c_est = 0, c_maxd = 0;
     std::vector<dpg_factor> h_dev_factors;     // staging (Q1 scaling)
     bool prepared = false;                     // inc_prepare ran for the coming update (its pairs are in)
     int64_t prep_new = 0;                      // ... for this many new nodes
+    int64_t prep_pairs0 = 0;                   // number of unique pairs before that prepare (rollback)
+    double* theta_bak = nullptr;               // [V][3] theta before a relinearization (rollback)
+    double* est_bak = nullptr;                 // [V][3] estimate before a batch update (rollback)
+    size_t c_theta_bak = 0, c_est_bak = 0;
     bool prep_reordered = false;
     double prep_ms[3] = {};                    // its incsym, derive, chol plan times
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
@@ -264,6 +272,25 @@ int dpg_inc_reset(dpg_inc* q) {
     q->phi.clear();
     q->I = dpg_chol_incsym();
     q->V_at_order = q->nnz_at_order = 0;
+    q->prepared = false;
+    q->prep_new = 0;
+    q->prep_pairs0 = 0;
+    return DPG_OK;
+}
+
+// Undo the structural half of an update that will not happen (its alignments failed, or its
+// numeric update failed): the pairs it added leave the pattern and the symbolic state is dropped,
+// so the next prepare orders the graph afresh from the pairs that remain.
+int dpg_inc_abort_prepare(dpg_inc* q) {
+    if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_abort_prepare: NULL");
+    if (!q->prepared) return DPG_OK;
+    for (size_t k = (size_t)q->prep_pairs0; k < q->plo.size(); ++k) q->pair_id.erase(pkey(q->plo[k], q->phi[k]));
+    q->plo.resize((size_t)q->prep_pairs0);
+    q->phi.resize((size_t)q->prep_pairs0);
+    q->I = dpg_chol_incsym();
+    q->V_at_order = q->nnz_at_order = 0;
+    q->prepared = false;
+    q->prep_new = 0;
     return DPG_OK;
 }
 
@@ -272,7 +299,7 @@ void dpg_inc_destroy(dpg_inc* q) {
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
     (void)hipStreamSynchronize(s);
     void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.contrib, q->g.partials, q->g.scal3,
-                    q->theta, q->est, q->maxd, q->cnt};
+                    q->theta, q->est, q->maxd, q->cnt, q->est_nxt, q->maxd_nxt, q->theta_bak, q->est_bak};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (q->g.scal3_host) (void)hipHostFree(q->g.scal3_host);
@@ -314,7 +341,9 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
             pairs[2 * e] == pairs[2 * e + 1])
             return set_err(DPG_ERR_ARG, "dpg_inc_prepare: a pair references a missing node");
     if (V1 == 0) return set_err(DPG_ERR_STATE, "dpg_inc_prepare: empty graph");
+    if (q->prepared) return set_err(DPG_ERR_STATE, "dpg_inc_prepare: an update is already prepared");
     const double t1 = now_ms();
+    q->prep_pairs0 = (int64_t)q->plo.size();
     if (q->I.n > 0) dpg_incsym_append(&q->I, n_new);
     std::vector<std::pair<int32_t, int32_t>> new_pairs;
     for (int64_t e = 0; e < n_pairs; ++e) {
@@ -336,18 +365,28 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
         if ((double)q->I.nnz > 1.5 * expect + 64.0) reordered = true;
     }
     if (reordered) {
-        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size()))
+        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size())) {
+            q->prepared = true;
+            dpg_inc_abort_prepare(q);
             return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic analysis failed");
+        }
         q->V_at_order = V1;
         q->nnz_at_order = q->I.nnz;
         q->reorders += 1;
     }
     const double t1a = now_ms();
-    if (dpg_incsym_derive(&q->I, &q->opts, &q->S))
+    if (dpg_incsym_derive(&q->I, &q->opts, &q->S)) {
+        q->prepared = true;
+        dpg_inc_abort_prepare(q);
         return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic derivation failed");
+    }
     const double t1b = now_ms();
     const int rc = dpg_chol_create_sym_plan(&q->g.chol, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size(), &q->S);
-    if (rc) return set_err(rc, "dpg_inc_prepare: Cholesky plan failed");
+    if (rc) {
+        q->prepared = true;
+        dpg_inc_abort_prepare(q);
+        return set_err(rc, "dpg_inc_prepare: Cholesky plan failed");
+    }
     q->prep_ms[0] = t1a - t1;
     q->prep_ms[1] = t1b - t1a;
     q->prep_ms[2] = now_ms() - t1b;
@@ -397,28 +436,50 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
             if (factors[k].kind == DPG_FACTOR_BETWEEN) { pr.push_back(factors[k].i); pr.push_back(factors[k].j); }
         if ((rc = dpg_inc_prepare(q, n_new, pr.data(), (int64_t)pr.size() / 2))) return rc;
     } else if (q->prep_new != n_new) {
-        q->prepared = false;
+        dpg_inc_abort_prepare(q);
         return set_err(DPG_ERR_STATE, "dpg_inc_update: prepared for another number of new nodes");
     }
+    // ISAM2::update counts the update first, then relinearizes when the count is a multiple of
+    // relinearizeSkip (updates 10, 20, ...)
+    const bool relin = q->P.mode == DPG_INC_ISAM2 && ((q->updates + 1) % q->P.relinearize_skip) == 0 && V0 > 0;
+    // every pair of this update's Between factors must be in the prepared pattern
+    for (int64_t k = 0; k < n_factors; ++k)
+        if (factors[k].kind == DPG_FACTOR_BETWEEN &&
+            q->pair_id.find(pkey(std::min(factors[k].i, factors[k].j), std::max(factors[k].i, factors[k].j))) ==
+                q->pair_id.end()) {
+            dpg_inc_abort_prepare(q);
+            return set_err(DPG_ERR_STATE, "dpg_inc_update: a factor's pair was not prepared");
+        }
+    // from here the update commits; any failure below rolls the graph back to its state before the
+    // call (factors, node count, update count, the pairs this update added, theta and the estimate)
+    const int64_t nF0 = (int64_t)q->F.size(), upd0 = q->updates;
     q->prepared = false;
-    const bool relin = q->P.mode == DPG_INC_ISAM2 && (q->updates % q->P.relinearize_skip) == 0 && V0 > 0;
     q->updates += 1;
     q->V = V1;
     for (int64_t k = 0; k < n_factors; ++k) {
         const dpg_factor& f = factors[k];
-        int32_t pid = -1;
-        if (f.kind == DPG_FACTOR_BETWEEN) {
-            auto it = q->pair_id.find(pkey(std::min(f.i, f.j), std::max(f.i, f.j)));
-            if (it == q->pair_id.end()) return set_err(DPG_ERR_STATE, "dpg_inc_update: a factor's pair was not prepared");
-            pid = it->second;
-        }
+        const int32_t pid = f.kind == DPG_FACTOR_BETWEEN ? q->pair_id[pkey(std::min(f.i, f.j), std::max(f.i, f.j))] : -1;
         q->F.push_back(f);
         q->f_created.push_back((int32_t)q->updates);
         q->f_pair.push_back(pid);
     }
+    bool theta_saved = false, est_saved = false;
+    auto rollback = [&](int code, const char* msg) -> int {
+        (void)hipStreamSynchronize(s);
+        q->F.resize((size_t)nF0);
+        q->f_created.resize((size_t)nF0);
+        q->f_pair.resize((size_t)nF0);
+        q->V = V0;
+        q->updates = upd0;
+        q->prepared = true;   // the pairs this update added leave the pattern
+        dpg_inc_abort_prepare(q);
+        if (theta_saved) (void)hipMemcpy(q->theta, q->theta_bak, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice);
+        if (est_saved) (void)hipMemcpy(q->est, q->est_bak, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice);
+        return set_err(code, msg);
+    };
     const bool reordered = q->prep_reordered;
     const double t1b = now_ms();
-    if ((rc = inc_rebuild(q, s))) return set_err(rc, "dpg_inc_update: solver rebuild failed");
+    if ((rc = inc_rebuild(q, s))) return rollback(rc, "dpg_inc_update: solver rebuild failed");
     const double t2 = now_ms();
     q->prof[0] = q->prep_ms[0];
     q->prof[1] = q->prep_ms[1];
@@ -429,21 +490,33 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     if (q->P.mode == DPG_INC_ISAM2) {
         // 1. relinearize the variables whose delta passed the threshold (before the new factors)
         if (relin) {
-            if (hipMemsetAsync(q->cnt, 0, sizeof(int32_t), s) != hipSuccess) return set_err(DPG_ERR_HIP, "memset");
+            if (dgrow(&q->theta_bak, &q->c_theta_bak, (size_t)(3 * V0), s, 0) ||
+                hipMemcpyAsync(q->theta_bak, q->theta, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice, s) !=
+                    hipSuccess)
+                return rollback(DPG_ERR_HIP, "dpg_inc_update: theta snapshot failed");
+            theta_saved = true;
+            if (hipMemsetAsync(q->cnt, 0, sizeof(int32_t), s) != hipSuccess) return rollback(DPG_ERR_HIP, "memset");
             hipLaunchKernelGGL(inc_relin_kernel, dim3(nblk(V0)), dim3(kThreads), 0, s, q->theta, q->est, q->maxd, V0,
                                q->P.relinearize_threshold, q->cnt);
         }
-        // 2. linearize everything at theta, factor, solve, estimate = theta (+) delta
+        // 2. linearize everything at theta, factor, solve, estimate = theta (+) delta (into the
+        //    spare buffers: the current estimate stays intact until the solve is known good)
+        if (dgrow(&q->est_nxt, &q->c_est_nxt, (size_t)(3 * V1), s, 0) || dgrow(&q->maxd_nxt, &q->c_maxd_nxt, (size_t)V1, s, 0))
+            return rollback(DPG_ERR_HIP, "dpg_inc_update: out of device memory");
         q->g.poses = q->theta;
-        if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return set_err(rc, "assembly failed");
-        if ((rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s))) return set_err(rc, "Cholesky launch failed");
-        if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return set_err(DPG_ERR_HIP, "memset");
+        if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return rollback(rc, "assembly failed");
+        if ((rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s))) return rollback(rc, "Cholesky launch failed");
+        if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return rollback(DPG_ERR_HIP, "memset");
         hipLaunchKernelGGL(inc_estimate_kernel, dim3(nblk(V1)), dim3(kThreads), 0, s, q->theta, dpg_chol_x_dev(q->g.chol),
-                           dpg_chol_pos_dev(q->g.chol), V1, q->est, q->maxd, q->g.scal3);
+                           dpg_chol_pos_dev(q->g.chol), V1, q->est_nxt, q->maxd_nxt, q->g.scal3);
         double sc[3];
         q->g.last_used_chol = 1;
-        if ((rc = dpg_gn_dev_fetch(&q->g, q->g.hb_own, s, sc))) return set_err(rc, "fetch failed");
-        if (sc[2] != 0.0) return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed (H not positive definite)");
+        if ((rc = dpg_gn_dev_fetch(&q->g, q->g.hb_own, s, sc))) return rollback(rc, "fetch failed");
+        if (sc[2] != 0.0) return rollback(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed (H not positive definite)");
+        std::swap(q->est, q->est_nxt);
+        std::swap(q->c_est, q->c_est_nxt);
+        std::swap(q->maxd, q->maxd_nxt);
+        std::swap(q->c_maxd, q->c_maxd_nxt);
         int32_t nrel = 0;
         if (relin && hipMemcpy(&nrel, q->cnt, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
             return set_err(DPG_ERR_HIP, "read-back failed");
@@ -462,12 +535,18 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         const dpg_gn_params& gp = q->P.gn;
         double sc[3] = {0, 0, 0};
         int it = 0;
-        if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return set_err(rc, "assembly failed");
+        if (V0 > 0) {
+            if (dgrow(&q->est_bak, &q->c_est_bak, (size_t)(3 * V0), s, 0) ||
+                hipMemcpyAsync(q->est_bak, q->est, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice, s) != hipSuccess)
+                return rollback(DPG_ERR_HIP, "dpg_inc_update: estimate snapshot failed");
+            est_saved = true;
+        }
+        if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return rollback(rc, "assembly failed");
         for (; it < gp.max_iterations;) {
             if ((rc = dpg_gn_dev_solve_async(&q->g, q->g.hb_own, &gp, s)) ||
                 (rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s)) || (rc = dpg_gn_dev_fetch(&q->g, q->g.hb_own, s, sc)))
-                return set_err(rc, "Gauss-Newton step failed");
-            if (sc[2] != 0.0) return set_err(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed");
+                return rollback(rc, "Gauss-Newton step failed");
+            if (sc[2] != 0.0) return rollback(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed");
             ++it;
             if (sc[0] < gp.delta_tol) break;
         }

@@ -284,6 +284,8 @@ SIGNATURES = {
     "dpg_active_dynamic_points": (C.c_int64, [P, C.c_int64, F32P, F32P, C.c_int64, I64P]),
     "dpg_reoptimize": (C.c_int, [P, C.c_int64, I32P, F32P, F32P, C.POINTER(IcpParams), C.POINTER(GnParams),
                                  C.POINTER(ReoptParams), F64P, C.POINTER(ReoptStats)]),
+    "dpg_reoptimize_inc": (C.c_int, [P, C.c_int64, I32P, F32P, F32P, C.POINTER(IcpParams), C.POINTER(ReoptParams),
+                                     F64P, C.POINTER(ReoptStats)]),
     "dpg_inc_params_default": (None, [C.POINTER(IncParams)]),
     "dpg_inc_create": (P, [P, C.POINTER(IncParams)]),
     "dpg_inc_destroy": (None, [P]),

@@ -526,6 +526,20 @@ class IncGraph:
                                  C.byref(st)), "dpg_add_node")
         return st
 
+    def reoptimize(self, passes, est, odom, icp_params=None, reopt_params=None):
+        """dpg_reoptimize_inc: the reoptimize sweep on the graph's context (every node's cloud is in
+        its scan store), then this graph rebuilt from the sweep's factors by one update from est
+        (dpg_slam.cc:35-120).  Returns (poses [V,3] f64, ReoptStats)."""
+        e, o = _f32(est).reshape(-1, 3), _f32(odom).reshape(-1, 3)
+        ps = np.ascontiguousarray(passes, np.int32)
+        X = np.zeros((len(e), 3), np.float64)
+        st = _abi.ReoptStats()
+        check(lib().dpg_reoptimize_inc(self.handle, len(e), ptr(ps, C.c_int32), ptr(e, C.c_float), ptr(o, C.c_float),
+                                       C.byref(icp_params or _abi.default_icp_params()),
+                                       C.byref(reopt_params or _abi.default_reopt_params()), ptr(X, C.c_double),
+                                       C.byref(st)), "dpg_reoptimize_inc")
+        return X, st
+
     def add_node_pairs(self, cloud, init_pose, pairs, extra=None, successive=True, icp_params=None) -> "_abi.AddNodeStats":
         """dpg_add_node_pairs: as add_node, with the loop-closure alignments given (pairs [k, 2] =
         (node_1 target, node_2 source), keys <= the new node's id)."""

@@ -44,7 +44,9 @@ int icp_cov_calculate(struct dpg_ctx* ctx, const float* data_xy, int64_t n_data,
  * in [x, y, z, yaw, pitch, roll] order (6x6 row-major), cov3 its [x, y, yaw] block (rows / columns
  * 0, 1, 3, :563-566; 3x3 row-major; either output may be NULL).  Evaluated at the transform's
  * planar angles (roll = pitch = 0, yaw = atan2f(T10, T00), z = T23 = 0): the sums on the GPU, the
- * 6x6 inverse and products on the host in fp64.  DPG_ERR_NUMERIC when d2J_dX2 is singular. */
+ * 6x6 inverse and products on the host in fp64.  DPG_ERR_NUMERIC when d2J_dX2 is singular;
+ * DPG_ERR_ARG when T is not planar (T02, T12, T20, T21, T23 != 0 or T22 != 1: the closed forms
+ * hold only at z = pitch = roll = 0, where every ICP result of this library lies). */
 int icp_cov_sandwich(struct dpg_ctx* ctx, const float* data_xy, int64_t n_data, const float* model_xy, int64_t n_model,
                      const float transform[16], double cov6_out[36], double cov3_out[9]);
 

@@ -208,6 +208,35 @@ class IncGraph {
               "dpg_add_node");
         return st;
     }
+    /* DpgSLAM::reoptimize (dpg_slam.cc:35-120) on this graph: the sweep over the clouds already in
+       the context's store (one per add_node), then the graph rebuilt from the sweep's factors --
+       the reference's new ISAM2 + graph_ -- so later add_node calls build on it; the nodes receive
+       the new estimates.  odom_only: odom_only_estimates_ (std::pair<Vector2f, float> per node). */
+    template <class NodeVec, class OdomVec, class PGParams>
+    dpg_reopt_stats reoptimize(NodeVec& nodes, const OdomVec& odom_only, const PGParams& pgp) {
+        const size_t V = nodes.size();
+        std::vector<float> est(3 * V), odom(3 * V);
+        std::vector<int32_t> pass(V);
+        for (size_t i = 0; i < V; ++i) {
+            pose_of(nodes[i], &est[3 * i]);
+            odom[3 * i] = odom_only[i].first.x();
+            odom[3 * i + 1] = odom_only[i].first.y();
+            odom[3 * i + 2] = odom_only[i].second;
+            pass[i] = (int32_t)nodes[i].getPassNumber();
+        }
+        const dpg_icp_params ip = icp_params_from(pgp);
+        dpg_reopt_params rp;
+        dpg_reopt_params_default(&rp);
+        rp.max_node_dist_within_pass = pgp.maximum_node_dist_within_pass_scan_comparison_;
+        rp.max_node_dist_across_passes = pgp.maximum_node_dist_across_passes_scan_comparison_;
+        rp.odometry_constraints = pgp.odometry_constraints_ ? 1 : 0;
+        std::vector<double> X(3 * V);
+        dpg_reopt_stats st;
+        check(dpg_reoptimize_inc(g_, (int64_t)V, pass.data(), est.data(), odom.data(), &ip, &rp, X.data(), &st),
+              "dpg_reoptimize_inc");
+        write_back(nodes);
+        return st;
+    }
     /* the current estimates -> the nodes (setPosition) */
     template <class NodeVec>
     void write_back(NodeVec& nodes) const {

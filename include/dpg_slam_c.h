@@ -31,6 +31,7 @@ extern "C" {
 #define DPG_ERR_STATE (-3)
 #define DPG_ERR_SIZE (-4)
 #define DPG_ERR_NUMERIC (-5)
+#define DPG_ERR_INTERNAL (-6) /* a kernel failed its own consistency check (DPG_ICP_INTERNAL) */
 
 /* Fixed reduction geometry of the ICP rigid fit (part of the algorithm's definition so that
  * CPU oracle and GPU agree bit for bit): lane l accumulates source points l, l+512, ... in
@@ -305,6 +306,20 @@ float dpg_get_map_kernel_ms(dpg_ctx* ctx);   /* device time of the last dpg_get_
 int dpg_reoptimize(dpg_ctx* ctx, int64_t n_nodes, const int32_t* pass_numbers, const float* est_poses,
                    const float* odom_only, const dpg_icp_params* icp_params, const dpg_gn_params* gn_params,
                    const dpg_reopt_params* params, double* poses_out, dpg_reopt_stats* stats);
+
+/* DpgSLAM::reoptimize for a live incremental graph g (dpg_slam.cc:35-120): the sweep of
+ * dpg_reoptimize (candidates, ONE batched ICP, the factors in the reference's order: pass prior or
+ * odometry per node, every successive alignment, the converged loop closures) on g's context, then g
+ * is rebuilt from exactly those factors -- dpg_inc_reset + ONE dpg_inc_update of all V nodes from
+ * est_poses: the reference's new ISAM2 + new graph_ and its one update (:36-39, :111-119), under g's
+ * own update semantics (DPG_INC_ISAM2: one step; DPG_INC_BATCH: to convergence).  Later
+ * dpg_add_node calls then build on the swept graph, as the reference's per-node updates do after
+ * reoptimize.  The context's scan store must hold the V nodes (it does after V dpg_add_node).
+ * poses_out[V][3] = g's estimate; stats.gn carries the update's iterations and error. */
+struct dpg_inc;
+int dpg_reoptimize_inc(struct dpg_inc* g, int64_t n_nodes, const int32_t* pass_numbers, const float* est_poses,
+                       const float* odom_only, const dpg_icp_params* icp_params, const dpg_reopt_params* params,
+                       double* poses_out, dpg_reopt_stats* stats);
 
 /* ---- incremental per-node solve (updatePoseGraphObsConstraints -> optimizeGraph -> isam_->update,
  *      dpg_slam.cc:255-329, ISAM2 built at :22 with default parameters) ----

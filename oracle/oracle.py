@@ -393,9 +393,10 @@ def retract(X, d):
 class OracleIncGraph:
     """CPU restatement of the incremental per-node solve (dpg_inc.hip; optimizeGraph per node,
     dpg_slam.cc:255-329, isam_->update at :320 with ISAM2's defaults):
-      isam2 -- linearization points theta; on updates whose count before the update is a multiple
-               of relinearize_skip, variables with max |delta| >= relinearize_threshold take
-               theta (+) delta; then every factor is linearized at theta, H delta = -g is solved
+      isam2 -- linearization points theta; on updates whose count (this update included) is a
+               multiple of relinearize_skip -- updates 10, 20, ...: GTSAM 4.0's ISAM2::update
+               increments update_count_ before relinarizationNeeded(update_count_) -- variables
+               with max |delta| >= relinearize_threshold take theta (+) delta; then every factor is linearized at theta, H delta = -g is solved
                (block-sparse Cholesky, oracle_gn_delta) and the estimate is theta (+) delta;
       batch -- Gauss-Newton to convergence from the current estimates (oracle_optimize_graph).
     duplicate_factors reproduces SURVEY Q1 (information x number of updates a factor has been in)."""
@@ -426,7 +427,7 @@ class OracleIncGraph:
     def update(self, init, factors):
         init = np.asarray(init, np.float64).reshape(-1, 3)
         V0 = self.V
-        relin = self.mode == "isam2" and self.updates % self.skip == 0 and V0 > 0
+        relin = self.mode == "isam2" and (self.updates + 1) % self.skip == 0 and V0 > 0
         self.updates += 1
         if relin:
             sel = self.maxd >= self.thr

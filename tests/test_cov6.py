@@ -91,3 +91,16 @@ def test_gpu_sandwich_config1(ctx, workload):
     assert np.abs(cov6 - o6).max() <= 1e-8 * np.abs(o6).max()
     # its Hessian's [x, y, yaw] block is the diagnostic block calculate_ICP_COV already returns
     assert np.all(np.isfinite(cov6)) and np.all(np.diag(cov3) > 0)
+
+
+@pytest.mark.gpu
+def test_gpu_sandwich_rejects_non_planar_T(ctx):
+    """The closed forms hold at z = pitch = roll = 0; a T with a third row / column that is not
+    planar is refused (DPG_ERR_ARG) instead of being evaluated at the wrong operating point."""
+    from dpgslam import _abi, api
+    p, q, T = G["s0_p"], G["s0_q"], np.asarray(G["s0_T"], np.float32).reshape(4, 4)
+    for (r, c, v) in [(2, 3, 0.1), (2, 0, 0.01), (0, 2, 0.01), (2, 2, 0.99)]:
+        Tb = T.copy()
+        Tb[r, c] = v
+        with pytest.raises(_abi.DpgError):
+            api.icp_cov_sandwich(p, q, Tb, ctx=ctx)

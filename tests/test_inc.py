@@ -131,3 +131,65 @@ def test_gpu_incremental_matches_oracle(ctx, mode, dup):
     assert worst < 1e-6, worst
     assert reorders < len(X0) / 8   # the order is extended, not recomputed
     g.close()
+
+
+def test_oracle_isam2_first_relinearization_is_update_10():
+    """ISAM2::update counts the update before relinarizationNeeded(update_count_) (GTSAM 4.0), so
+    with relinearizeSkip 10 the linearization points first move on the 10th update, then the 20th
+    -- never on updates 1-9 or 11-19 (threshold 0: every variable with a nonzero delta moves)."""
+    X0, F, _ = gtsam_test_graph()
+    key = _per_node(F)
+    g = O.OracleIncGraph(mode="isam2", relinearize_threshold=0.0)
+    moved = []
+    for u in range(1, 26):
+        before = g.theta.copy()
+        if u <= len(X0):
+            g.update(X0[u - 1:u], F[key == u - 1])
+        else:
+            g.update(np.zeros((0, 3)), F[:0])
+        n0 = len(before)
+        if n0 and not np.array_equal(g.theta[:n0], before):
+            moved.append(u)
+    assert moved == [10, 20], moved
+
+
+@pytest.mark.gpu
+def test_gpu_failed_update_rolls_back(ctx):
+    """A numeric failure (a node with no factor: H singular) leaves the device graph as it was --
+    node count, factors, pattern, estimate -- and the next updates proceed and still match the
+    oracle (the failure used to leave the graph one node ahead of itself)."""
+    from dpgslam import api
+    X0, F = _sequence("config3", 120)
+    key = _per_node(F)
+    g = api.IncGraph(ctx, mode="isam2", reorder_every=16)
+    o = O.OracleIncGraph(mode="isam2")
+    for v in range(len(X0)):
+        if v in (30, 77):   # the injected failure: the node arrives without its factors
+            before = g.poses()
+            with pytest.raises(_abi.DpgError):
+                g.update(X0[v:v + 1], F[:0])
+            assert g.V == v and np.array_equal(g.poses(), before)
+        g.update(X0[v:v + 1], F[key == v])
+        o.update(X0[v:v + 1], F[key == v])
+    assert np.abs(pose_diff(g.poses(), o.poses())).max() < 1e-6
+    g.close()
+
+
+@pytest.mark.gpu
+def test_gpu_add_node_failure_keeps_store_and_graph_in_step(ctx):
+    """dpg_add_node_pairs with no factor for the new node fails in the update; the scan store drops
+    the node again (store and graph keep the same count) and the next dpg_add_node succeeds."""
+    from dpgslam import api
+    w = synth.generate("config2")
+    p = _abi.default_icp_params()
+    g = api.IncGraph(ctx, mode="isam2")
+    prior = np.zeros(1, _abi.FACTOR_DTYPE)
+    prior["kind"], prior["i"], prior["info"] = _abi.DPG_FACTOR_PRIOR, 0, 1.0 / np.array([0.04, 0.04, 0.0225])
+    g.add_node(w.cloud(0), np.zeros(1, np.int32), w.est[0], extra=prior, icp_params=p)
+    g.add_node(w.cloud(1), np.zeros(2, np.int32), w.est[1], icp_params=p)
+    with pytest.raises(_abi.DpgError):   # no successive alignment, no pairs, no factor: singular
+        g.add_node_pairs(w.cloud(2), w.est[2], np.zeros((0, 2), np.int32), successive=False, icp_params=p)
+    assert g.V == 2
+    st = g.add_node(w.cloud(2), np.zeros(3, np.int32), w.est[2], icp_params=p)
+    assert g.V == 3 and st.n_icp_edges >= 1
+    g.close()

@@ -97,3 +97,29 @@ def test_get_map_bit_exact(ctx, workload):
         g = ctx.get_map(w.est, frac)
         o = O.get_map(w.pts, w.offsets, w.est, frac)
         assert g.shape == o.shape and g.tobytes() == o.tobytes()
+
+
+@pytest.mark.gpu
+def test_reoptimize_inc_rebuilds_the_live_graph(ctx, workload):
+    """dpg_reoptimize_inc: the sweep on a live incremental graph rebuilds it from the sweep's
+    factors (the reference's new ISAM2 + graph_, dpg_slam.cc:36-39,111-119).  In batch mode its
+    single update runs GN to convergence, so the poses equal the oracle's sweep to 1e-6; the graph
+    then keeps growing by dpg_add_node on top of the swept graph."""
+    from dpgslam import api
+    from oracle import oracle as O
+    w = workload("config2")
+    V = 60
+    pts, offs = w.pts[:w.offsets[V]], w.offsets[:V + 1]
+    passes = _passes(V, 30)
+    ctx.upload_scans(pts, offs, 5)
+    g = api.IncGraph(ctx, mode="batch")
+    X, st = g.reoptimize(passes, w.est[:V], w.odom[:V])
+    Xo, edges, res, so = O.reoptimize(pts, offs, passes, w.est[:V], w.odom[:V])
+    assert g.V == V and st.n_icp_edges == len(edges) and st.n_loop_closures > 0
+    err = np.abs(np.concatenate([X[:, :2] - Xo[:, :2], angle_wrap(X[:, 2:] - Xo[:, 2:])], 1)).max()
+    assert err < 1e-6, err
+    np.testing.assert_array_equal(g.poses(), X)
+    p2 = np.append(passes, np.int32(1))
+    s2 = g.add_node(w.cloud(V), p2, w.est[V])
+    assert g.V == V + 1 and s2.n_icp_edges >= 1
+    g.close()

@@ -175,6 +175,48 @@ int main() {
         g.write_back(b);
         EXPECT(g.size() == 4);
         printf("IncGraph: node 3 at (%.4f, %.4f, %.4f)\n", b[3].loc.x(), b[3].loc.y(), b[3].th);
+        // reoptimize on the live graph (the graph is rebuilt from the sweep's factors), against the
+        // direct C call on a second graph built the same way; then the graph keeps growing
+        std::vector<std::pair<Vector2f, float>> odom;
+        for (int k = 0; k < 4; ++k) odom.emplace_back(Vector2f(0.9f * (float)k, 0.0f), 0.03f * (float)k);
+        dpg_adapter::IncGraph g2(ctx.get());
+        for (int k = 0; k < 4; ++k) {
+            float ip[3];
+            dpg_adapter::pose_of(nodes[(size_t)k], ip);
+            std::vector<dpg_factor> extra{k == 0 ? dpg_adapter::prior_factor(0, 0, 0, 0, sig)
+                                                 : dpg_adapter::between_factor(k - 1, k, 0.9, 0.0, 0.03, info)};
+            std::vector<int32_t> ps(passes.begin(), passes.begin() + k + 1);
+            g2.add_node(nodes[(size_t)k].cloud, ps, ip, extra, pgp, true);
+        }
+        std::vector<float> est(12), od(12);
+        std::vector<int32_t> pass4(4, 0);
+        for (int k = 0; k < 4; ++k) {
+            dpg_adapter::pose_of(b[(size_t)k], &est[3 * (size_t)k]);
+            od[3 * (size_t)k] = odom[(size_t)k].first.x();
+            od[3 * (size_t)k + 1] = odom[(size_t)k].first.y();
+            od[3 * (size_t)k + 2] = odom[(size_t)k].second;
+        }
+        const dpg_reopt_stats rs = g.reoptimize(b, odom, pgp);
+        const dpg_icp_params ipar = dpg_adapter::icp_params_from(pgp);
+        dpg_reopt_params rp;
+        dpg_reopt_params_default(&rp);
+        rp.max_node_dist_within_pass = pgp.maximum_node_dist_within_pass_scan_comparison_;
+        rp.max_node_dist_across_passes = pgp.maximum_node_dist_across_passes_scan_comparison_;
+        rp.odometry_constraints = pgp.odometry_constraints_ ? 1 : 0;
+        std::vector<double> X2(12);
+        dpg_reopt_stats rs2;
+        dpg_adapter::check(dpg_reoptimize_inc(g2.get(), 4, pass4.data(), est.data(), od.data(), &ipar, &rp, X2.data(), &rs2),
+                           "dpg_reoptimize_inc");
+        for (int k = 0; k < 4; ++k)
+            EXPECT(b[k].loc.x() == (float)X2[3 * k] && b[k].loc.y() == (float)X2[3 * k + 1] && b[k].th == (float)X2[3 * k + 2]);
+        EXPECT(rs.n_factors == rs2.n_factors && rs.n_icp_edges == rs2.n_icp_edges && g.size() == 4);
+        passes.push_back(0);
+        float ip4[3] = {b[3].loc.x() + 0.9f, b[3].loc.y(), b[3].th};
+        std::vector<dpg_factor> ex4{dpg_adapter::between_factor(3, 4, 0.9, 0.0, 0.0, info)};
+        const dpg_add_node_stats st5 = g.add_node(nodes[3].cloud, passes, ip4, ex4, pgp, true);
+        EXPECT(st5.update.n_nodes == 5 && g.size() == 5);
+        printf("IncGraph::reoptimize: %lld factors, %lld ICP edges; then node 5 added\n", (long long)rs.n_factors,
+               (long long)rs.n_icp_edges);
     }
     // executeDPG: the store grows scan by scan; a second pass sees the room with a wall moved
     {
