@@ -563,6 +563,8 @@ def main():
                          "the multi-rank path on fewer GPUs than ranks)")
     ap.add_argument("--icp-variant", default="angular", choices=["angular", "kdtree", "grid"],
                     help="nearest-neighbour machinery of the ICP kernel (results are identical)")
+    ap.add_argument("--shard", default="interleave", choices=["interleave", "contiguous"],
+                    help="N > 1: ICP edge shares (dpgslam.dist.plan)")
     ap.add_argument("--dump-pairs", default=None, help="dynamic: save the graph's node pairs (npz) after the run")
     ap.add_argument("--refactor-delta", type=float, default=None,
                     help="dpg_gn_params.refactor_delta: chord steps (reuse the Cholesky factor) once max|delta| is below it")
@@ -620,11 +622,12 @@ def main():
     ctx.upload_scans(w.pts, w.offsets, params.downsample_icp_points_ratio)
     n_src = np.diff(w.offsets)[w.edges[:, 1]]
     n_tgt = np.diff(w.offsets)[w.edges[:, 0]]
-    pl = D.plan(rank, world, w.E, w.n_successive, w.icp_factor_first, edge_cost=n_src * n_tgt)
+    pl = D.plan(rank, world, w.E, w.n_successive, w.icp_factor_first, edge_cost=n_src * n_tgt,
+                strategy=args.shard)
     e0, e1 = pl.edge_range
-    my_edges = w.edges[e0:e1]
+    my_edges = pl.edges(w.edges)
     ctx.icp_prepare(my_edges, w.est, params)
-    F = w.factors_placeholder()
+    F = pl.factors(w.factors_placeholder(), w.icp_factor_first)
     hb_size = ctx.gn_setup(w.V, F, pl.factor_range, gp)
     backend = D.DeviceBackend(ctx, hb_size, hb_size - 2, dev)
     allreduce = (lambda hb: dist.all_reduce(hb)) if world > 1 else (lambda hb: None)

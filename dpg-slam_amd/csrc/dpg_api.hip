@@ -19,6 +19,8 @@
 #include <string.h>
 #include <time.h>
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cmath>
 #include <string>
@@ -138,7 +140,21 @@ struct dpg_ctx {
     bool gn_ready = false;
     dpg_gn_params gp{};
     float asm_ms = 0.f, solve_ms = 0.f;
+    // multi-GPU form (dpg_ctx_create_multi): this context drives device 0 of the set, `peers` are
+    // full single-device contexts of the others; one RCCL communicator per device
+    // (ncclCommInitAll, one process); `shard[k]` = the caller's edge indices staged on device k
+    std::vector<dpg_ctx*> peers;
+    std::vector<ncclComm_t> comms;
+    std::vector<std::vector<int64_t>> shard;
 };
+
+namespace {
+inline int n_dev(const dpg_ctx* c) { return 1 + (int)c->peers.size(); }
+inline dpg_ctx* dev_ctx(dpg_ctx* c, int k) { return k == 0 ? c : c->peers[(size_t)k - 1]; }
+// made by dpg_ctx_create_multi (even for one GPU: its calls then take the sharded paths, RCCL
+// all-reduce included, with one rank)
+inline bool is_multi(const dpg_ctx* c) { return !c->comms.empty(); }
+}  // namespace
 
 namespace {
 
@@ -264,8 +280,56 @@ dpg_ctx* dpg_ctx_create(int device) {
     return c;
 }
 
+dpg_ctx* dpg_ctx_create_multi(int32_t n_gpus, const int32_t* devices) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        fail(DPG_ERR_HIP, "no HIP device available");
+        return nullptr;
+    }
+    if (n_gpus < 1 || n_gpus > n) {
+        fail(DPG_ERR_ARG, "dpg_ctx_create_multi: %d GPUs asked, %d present", n_gpus, n);
+        return nullptr;
+    }
+    std::vector<int> dl((size_t)n_gpus);
+    for (int k = 0; k < n_gpus; ++k) {
+        dl[(size_t)k] = devices ? devices[k] : k;
+        for (int j = 0; j < k; ++j)
+            if (dl[(size_t)j] == dl[(size_t)k]) {
+                fail(DPG_ERR_ARG, "dpg_ctx_create_multi: device %d listed twice", dl[(size_t)k]);
+                return nullptr;
+            }
+    }
+    dpg_ctx* c = dpg_ctx_create(dl[0]);
+    if (!c) return nullptr;
+    for (int k = 1; k < n_gpus; ++k) {
+        dpg_ctx* q = dpg_ctx_create(dl[(size_t)k]);
+        if (!q) {
+            dpg_ctx_destroy(c);
+            return nullptr;
+        }
+        c->peers.push_back(q);
+    }
+    c->comms.assign((size_t)n_gpus, nullptr);
+    const ncclResult_t r = ncclCommInitAll(c->comms.data(), n_gpus, dl.data());
+    if (r != ncclSuccess) {
+        c->comms.clear();
+        dpg_ctx_destroy(c);
+        fail(DPG_ERR_HIP, "ncclCommInitAll over %d devices failed: %s", n_gpus, ncclGetErrorString(r));
+        return nullptr;
+    }
+    return c;
+}
+
+int32_t dpg_ctx_num_gpus(dpg_ctx* c) { return c ? n_dev(c) : -1; }
+int dpg_ctx_is_multi(dpg_ctx* c) { return c && is_multi(c) ? 1 : 0; }
+
 void dpg_ctx_destroy(dpg_ctx* c) {
     if (!c) return;
+    for (dpg_ctx* q : c->peers) dpg_ctx_destroy(q);
+    c->peers.clear();
+    for (ncclComm_t m : c->comms)
+        if (m) (void)ncclCommDestroy(m);
+    c->comms.clear();
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     c->full.release(); c->ds.release(); c->edges.release(); c->res.release(); c->hess.release();
@@ -292,12 +356,39 @@ int dpg_ctx_set_stream(dpg_ctx* c, void* s) {
 
 int dpg_ctx_synchronize(dpg_ctx* c) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < n_dev(c); ++k) {
+        HIP_TRY(hipSetDevice(dev_ctx(c, k)->device));
+        HIP_TRY(hipStreamSynchronize(dev_ctx(c, k)->stream));
+    }
+    HIP_TRY(hipSetDevice(c->device));
     return DPG_OK;
 }
 
 // ------------------------------------------------------------------ ICP, batched
+static int scans_upload_1(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V, int32_t ratio);
+static int scans_append_1(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k, int32_t ratio);
+
+// every device of a multi-GPU context holds every scan (5000 x 1000 points: 40 MB of downsampled
+// clouds per device), so any edge can be aligned on any device
 int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V, int32_t ratio) {
+    if (!c) return fail(DPG_ERR_ARG, "dpg_scans_upload: bad arguments");
+    for (int k = 0; k < n_dev(c); ++k) {
+        const int rc = scans_upload_1(dev_ctx(c, k), pts, off, V, ratio);
+        if (rc) return rc;
+    }
+    return hipSetDevice(c->device) == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k, int32_t ratio) {
+    if (!c) return fail(DPG_ERR_ARG, "dpg_scans_append: bad arguments");
+    for (int d = 0; d < n_dev(c); ++d) {
+        const int rc = scans_append_1(dev_ctx(c, d), pts, off, k, ratio);
+        if (rc) return rc;
+    }
+    return hipSetDevice(c->device) == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+static int scans_upload_1(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V, int32_t ratio) {
     if (!c || !pts || !off || V <= 0) return fail(DPG_ERR_ARG, "dpg_scans_upload: bad arguments");
     if (ratio < 1) ratio = 1;
     HIP_TRY(hipSetDevice(c->device));
@@ -331,10 +422,10 @@ int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V
     return DPG_OK;
 }
 
-int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k, int32_t ratio) {
+static int scans_append_1(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k, int32_t ratio) {
     if (!c || !pts || !off || k <= 0) return fail(DPG_ERR_ARG, "dpg_scans_append: bad arguments");
     if (ratio < 1) ratio = 1;
-    if (c->n_nodes == 0) return dpg_scans_upload(c, pts, off, k, ratio);
+    if (c->n_nodes == 0) return scans_upload_1(c, pts, off, k, ratio);
     if (ratio != c->ratio) return fail(DPG_ERR_STATE, "scans were uploaded with downsample ratio %d", c->ratio);
     HIP_TRY(hipSetDevice(c->device));
     const int64_t V0 = c->n_nodes, V1 = V0 + k;
@@ -381,14 +472,18 @@ int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k
 // the scan store back to its first V nodes (dpg_add_node_pairs' rollback); the device arrays keep
 // their capacity, the entries past V are overwritten by the next append
 static void scans_truncate(dpg_ctx* c, int64_t V) {
-    if (!c || V < 0 || V >= c->n_nodes) return;
-    c->full_off.resize((size_t)V + 1);
-    c->ds_off.resize((size_t)V + 1);
-    c->n_nodes = V;
+    if (!c) return;
+    for (int k = 0; k < n_dev(c); ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        if (V < 0 || V >= q->n_nodes) continue;
+        q->full_off.resize((size_t)V + 1);
+        q->ds_off.resize((size_t)V + 1);
+        q->n_nodes = V;
+    }
 }
 
-int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
-    if (!c || (!edges && ne > 0) || !poses) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
+static int batch_prepare_1(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
+    if (!c || (!edges && ne > 0) || !poses || !p) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
     if (c->n_nodes <= 0) return fail(DPG_ERR_STATE, "no scans uploaded");
     if (p->downsample_icp_points_ratio != c->ratio && !(p->downsample_icp_points_ratio < 1 && c->ratio == 1))
         return fail(DPG_ERR_STATE, "scans were uploaded with downsample ratio %d", c->ratio);
@@ -450,7 +545,7 @@ int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const fl
     return DPG_OK;
 }
 
-int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
+static int batch_run_1(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
     HIP_TRY(hipSetDevice(c->device));
     dpg_icp_kparams kp = c->kp;
@@ -470,6 +565,50 @@ int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
                         compute_cov ? c->hess.p : nullptr, tr, true);
 }
 
+// Multi-GPU form: device k aligns the edges e with e mod n == k (the caller's lists come grouped --
+// successive pairs, then loop closures nearest first -- so every device gets the same mix of
+// classes, whose alignments differ in length and in correspondences per iteration), in the
+// caller's order; results are gathered back into the caller's order by dpg_icp_batch_fetch.
+int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
+    if (!c) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
+    const int n = n_dev(c);
+    if (!is_multi(c)) return batch_prepare_1(c, edges, ne, poses, p);
+    if ((!edges && ne > 0) || ne < 0) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
+    c->shard.assign((size_t)n, {});
+    std::vector<int32_t> sub;
+    for (int k = 0; k < n; ++k) {
+        auto& ids = c->shard[(size_t)k];
+        sub.clear();
+        for (int64_t e = k; e < ne; e += n) {
+            ids.push_back(e);
+            sub.push_back(edges[2 * e]);
+            sub.push_back(edges[2 * e + 1]);
+        }
+        const int rc = batch_prepare_1(dev_ctx(c, k), sub.empty() ? nullptr : sub.data(), (int64_t)ids.size(), poses, p);
+        if (rc) return rc;
+    }
+    c->n_edges = ne;   // the whole batch, as the caller sees it (device 0 staged c->shard[0])
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
+int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    if (!is_multi(c)) return batch_run_1(c, compute_cov, trace_iters);
+    if (trace_iters > 0) return fail(DPG_ERR_STATE, "the correspondence trace is a single-device diagnostic");
+    const int64_t ne = c->n_edges;
+    for (int k = 0; k < n_dev(c); ++k) {   // launches only: the devices run concurrently
+        dpg_ctx* q = dev_ctx(c, k);
+        q->n_edges = (int64_t)c->shard[(size_t)k].size();
+        const int rc = batch_run_1(q, compute_cov, 0);
+        if (rc) return rc;
+    }
+    c->n_edges = ne;
+    c->have_cov = compute_cov != 0;
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
 // the staged batch, building only the indexes of nodes [tree_from, n_nodes) (nodes appended since
 // the last run: the others' indexes are still in place)
 static int icp_batch_run_from(dpg_ctx* c, int64_t tree_from) {
@@ -484,13 +623,13 @@ static int icp_batch_run_from(dpg_ctx* c, int64_t tree_from) {
 int dpg_ctx_set_icp_variant(dpg_ctx* c, int32_t variant) {
     if (!c || (variant != DPG_ICP_ANGULAR && variant != DPG_ICP_KDTREE && variant != DPG_ICP_GRID))
         return fail(DPG_ERR_ARG, "bad ICP variant");
-    c->icp_variant = variant;
+    for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->icp_variant = variant;
     return DPG_OK;
 }
 
 int dpg_ctx_set_icp_defer_cap(dpg_ctx* c, int32_t cap) {
     if (!c || cap < 0) return fail(DPG_ERR_ARG, "bad defer cap");
-    c->defer_cap = cap;
+    for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->defer_cap = cap;
     return DPG_OK;
 }
 
@@ -501,7 +640,36 @@ float dpg_kdtree_build_ms(dpg_ctx* c) {
     return ms;
 }
 
+static int batch_fetch_1(dpg_ctx* c, dpg_icp_result* results, double* hess);
+
 int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    const int n = n_dev(c);
+    if (!is_multi(c)) return batch_fetch_1(c, results, hess);
+    if (hess && !c->have_cov) return fail(DPG_ERR_STATE, "last batch ran without compute_cov");
+    const int64_t ne = c->n_edges;
+    std::vector<dpg_icp_result> r;
+    std::vector<double> h;
+    for (int k = 0; k < n; ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        const auto& ids = c->shard[(size_t)k];
+        r.resize(std::max<size_t>(ids.size(), 1));
+        if (hess) h.resize(9 * std::max<size_t>(ids.size(), 1));
+        q->n_edges = (int64_t)ids.size();
+        const int rc = batch_fetch_1(q, results ? r.data() : nullptr, hess ? h.data() : nullptr);
+        c->n_edges = ne;
+        if (rc) return rc;
+        for (size_t j = 0; j < ids.size(); ++j) {
+            if (results) results[ids[j]] = r[j];
+            if (hess) memcpy(hess + 9 * ids[j], h.data() + 9 * j, 9 * sizeof(double));
+        }
+    }
+    c->n_edges = ne;
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
+static int batch_fetch_1(dpg_ctx* c, dpg_icp_result* results, double* hess) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
     HIP_TRY(hipSetDevice(c->device));
     if (results && c->n_edges > 0)
@@ -518,6 +686,7 @@ int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
 
 int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t* max_src_out) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    if (is_multi(c)) return fail(DPG_ERR_STATE, "the correspondence trace is a single-device diagnostic");
     if (max_src_out) *max_src_out = std::max(c->max_src, 1);
     if (!trace) return DPG_OK;
     if (c->trace_iters <= 0) return fail(DPG_ERR_STATE, "last batch ran without a trace");
@@ -527,21 +696,43 @@ int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t* max_src_out) 
     return DPG_OK;
 }
 
-float dpg_icp_batch_kernel_ms(dpg_ctx* c) {
-    float ms = -1.f;
-    if (!c || hipEventSynchronize(c->ev[1]) != hipSuccess) return -1.f;
-    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) != hipSuccess) return -1.f;
-    return ms;
+// event pair (a, b) of the last batch: the slowest device of a multi-GPU context
+static float batch_ms(dpg_ctx* c, int a, int b) {
+    float worst = -1.f;
+    for (int k = 0; k < (c ? n_dev(c) : 0); ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        float ms = -1.f;
+        if (hipSetDevice(q->device) != hipSuccess || hipEventSynchronize(q->ev[b]) != hipSuccess ||
+            hipEventElapsedTime(&ms, q->ev[a], q->ev[b]) != hipSuccess)
+            return -1.f;
+        worst = std::max(worst, ms);
+    }
+    if (c) (void)hipSetDevice(c->device);
+    return worst;
 }
 
-float dpg_cov_batch_kernel_ms(dpg_ctx* c) {
-    float ms = -1.f;
-    if (!c || hipEventSynchronize(c->ev[2]) != hipSuccess) return -1.f;
-    if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) != hipSuccess) return -1.f;
-    return ms;
-}
+float dpg_icp_batch_kernel_ms(dpg_ctx* c) { return batch_ms(c, 0, 1); }
+
+float dpg_cov_batch_kernel_ms(dpg_ctx* c) { return batch_ms(c, 1, 2); }
+
+static double batch_bytes_1(dpg_ctx* c);
 
 double dpg_icp_batch_algorithmic_bytes(dpg_ctx* c) {
+    if (!c) return 0.0;
+    if (!is_multi(c)) return batch_bytes_1(c);
+    const int64_t ne = c->n_edges;
+    double b = 0.0;
+    for (int k = 0; k < n_dev(c); ++k) {
+        dev_ctx(c, k)->n_edges = (int64_t)c->shard[(size_t)k].size();
+        (void)hipSetDevice(dev_ctx(c, k)->device);
+        b += batch_bytes_1(dev_ctx(c, k));
+    }
+    c->n_edges = ne;
+    (void)hipSetDevice(c->device);
+    return b;
+}
+
+static double batch_bytes_1(dpg_ctx* c) {
     if (!c || c->n_edges <= 0) return 0.0;
     std::vector<dpg_icp_result> r((size_t)c->n_edges);
     if (hipMemcpy(r.data(), c->res.p, sizeof(dpg_icp_result) * r.size(), hipMemcpyDeviceToHost) != hipSuccess) return -1.0;
@@ -744,6 +935,8 @@ int dpg_gn_setup(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t
 int dpg_gn_take_icp_measurements(dpg_ctx* c, int64_t first, int64_t count, int64_t n_always,
                                  const dpg_icp_params* p) {
     if (!c || !c->gn_ready || !p) return fail(DPG_ERR_STATE, "graph not set up");
+    if (is_multi(c))
+        return fail(DPG_ERR_STATE, "the step API is per device: a multi-GPU context solves through dpg_optimize_graph / dpg_reoptimize");
     if (count > c->n_edges) return fail(DPG_ERR_ARG, "only %lld ICP results available", (long long)c->n_edges);
     int rc = dpg_gn_dev_icp_to_factors(&c->gn, c->res.p, first, count, n_always, 1.0 / (double)p->laser_x_variance,
                                        1.0 / (double)p->laser_y_variance, 1.0 / (double)p->laser_theta_variance,
@@ -879,12 +1072,107 @@ static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0,
     return DPG_OK;
 }
 
+// ONE all-reduce(sum, fp64) of every device's packed [H upper | g | chi2] buffer, in place, on the
+// devices' own streams (one thread drives every device: grouped)
+static int allreduce_hb(dpg_ctx* c) {
+    const size_t count = (size_t)dpg_gn_dev_hb_size(&c->gn);
+    if (ncclGroupStart() != ncclSuccess) return fail(DPG_ERR_HIP, "ncclGroupStart failed");
+    for (int k = 0; k < n_dev(c); ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        const ncclResult_t r = ncclAllReduce(q->gn.hb_own, q->gn.hb_own, count, ncclDouble, ncclSum, c->comms[(size_t)k],
+                                             q->stream);
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return fail(DPG_ERR_HIP, "ncclAllReduce failed: %s", ncclGetErrorString(r));
+        }
+    }
+    if (ncclGroupEnd() != ncclSuccess) return fail(DPG_ERR_HIP, "ncclGroupEnd failed");
+    return DPG_OK;
+}
+
+// The Gauss-Newton loop of a multi-GPU context: every device holds the whole factor list and
+// linearizes its contiguous shard of it; per iteration each device enqueues solve + retract +
+// re-linearization, then ONE all-reduce of the packed system, then one read of device 0's
+// scalars.  The devices factor and solve the identical reduced system, so their poses stay
+// bitwise equal without a broadcast.
+static int gn_loop_multi(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0, double t1, dpg_gn_stats* st) {
+    dpg_gn_stats S;
+    memset(&S, 0, sizeof(S));
+    const int n = n_dev(c);
+    int rc;
+    for (int k = 0; k < n; ++k)
+        if ((rc = hipSetDevice(dev_ctx(c, k)->device) != hipSuccess ? DPG_ERR_HIP : 0) ||
+            (rc = dpg_gn_assemble(dev_ctx(c, k), nullptr)))
+            return rc ? rc : fail(DPG_ERR_HIP, "hipSetDevice failed");
+    if ((rc = allreduce_hb(c))) return rc;
+    HIP_TRY(hipSetDevice(c->device));
+    if ((rc = read_error(c, &S.initial_error))) return rc;
+    double cur = S.initial_error, nw = cur, dinf = 0.0;
+    int it = 0;
+    if (!(cur <= 0.0) && P.max_iterations > 0) {
+        for (;;) {
+            for (int k = 0; k < n; ++k) {
+                dpg_ctx* q = dev_ctx(c, k);
+                HIP_TRY(hipSetDevice(q->device));
+                if ((rc = dpg_gn_solve_retract_async(q, nullptr)) || (rc = dpg_gn_assemble(q, nullptr))) return rc;
+            }
+            if ((rc = allreduce_hb(c))) return rc;
+            double sc[3];
+            HIP_TRY(hipSetDevice(c->device));
+            if ((rc = dpg_gn_fetch(c, nullptr, sc))) return rc;
+            if (sc[2] != 0.0) return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)sc[2]);
+            S.pcg_iterations += c->gn.last_pcg_iters;
+            ++it;
+            dinf = sc[0];
+            nw = sc[1];
+            if (it >= P.max_iterations) break;
+            if (P.use_error_criteria) {
+                if (check_conv(&P, cur, nw) || !std::isfinite(cur)) break;
+            } else if (dinf < P.delta_tol) {
+                break;
+            }
+            cur = nw;
+        }
+    }
+    if ((rc = dpg_ctx_synchronize(c)) || (rc = dpg_gn_get_poses(c, poses))) return rc;
+    const double t2 = now_ms();
+    S.iterations = it;
+    S.final_error = nw;
+    S.last_delta_inf = dinf;
+    S.ms_total = t2 - t0;
+    S.ms_per_iteration = it ? (t2 - t1) / it : 0.0;
+    if (st) *st = S;
+    return DPG_OK;
+}
+
+// every device of a multi-GPU context: the whole graph, linearizing factors [b_k, e_k) (equal
+// counts, contiguous), the same initial poses
+static int gn_setup_multi(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params& P,
+                          const double* poses) {
+    const int n = n_dev(c);
+    for (int k = 0; k < n; ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        const int64_t b = nf * k / n, e = nf * (k + 1) / n;
+        int rc = dpg_gn_setup(q, V, F, nf, b, e, &P);
+        if (!rc) rc = dpg_gn_set_poses(q, poses);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
 int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params* gp,
                        dpg_gn_stats* st) {
     const double t0 = now_ms();
     dpg_gn_params P;
     if (gp) P = *gp;
     else dpg_gn_params_default(&P);
+    if (c && is_multi(c)) {
+        if (!F || !poses || V <= 0 || nf < 0) return fail(DPG_ERR_ARG, "dpg_optimize_graph: bad arguments");
+        int rc = gn_setup_multi(c, V, F, nf, P, poses);
+        if (rc) return rc;
+        return gn_loop_multi(c, P, poses, t0, now_ms(), st);
+    }
     int rc = dpg_gn_setup(c, V, F, nf, 0, nf, &P);
     if (rc) return rc;
     if ((rc = dpg_gn_set_poses(c, poses))) return rc;
@@ -1092,6 +1380,33 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
     int rc = reopt_sweep(c, V, pass, est, odom, I, R, edges, F, first_icp, n_succ, S, t1);
     if (rc) return rc;
     const int64_t E = S.n_icp_edges;
+    if (is_multi(c)) {   // the alignments ran sharded: their measurements enter the factor slots on the host
+        std::vector<dpg_icp_result> res((size_t)std::max<int64_t>(E, 1));
+        if (E > 0 && (rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+        const double t2 = now_ms();
+        const double ix = 1.0 / (double)I.laser_x_variance, iy = 1.0 / (double)I.laser_y_variance,
+                     ith = 1.0 / (double)I.laser_theta_variance;
+        for (int64_t e = 0; e < E; ++e) {   // icp_to_factor_kernel's expressions (dpg_gn.hip)
+            const dpg_icp_result& r = res[(size_t)e];
+            dpg_factor& f = F[(size_t)(first_icp + e)];
+            const bool keep = e < n_succ || (r.converged && r.status == DPG_ICP_OK);
+            f.z[0] = r.z[0];
+            f.z[1] = r.z[1];
+            f.z[2] = r.z[2];
+            f.info[0] = keep ? ix : 0.0;
+            f.info[1] = keep ? iy : 0.0;
+            f.info[2] = keep ? ith : 0.0;
+            if (e >= n_succ && keep) ++S.n_loop_closures;
+        }
+        for (int64_t v = 0; v < 3 * V; ++v) poses_out[v] = (double)est[v];
+        if ((rc = gn_setup_multi(c, V, F.data(), (int64_t)F.size(), P, poses_out))) return rc;
+        if ((rc = gn_loop_multi(c, P, poses_out, t2, now_ms(), &S.gn))) return rc;
+        S.n_factors = (int64_t)F.size();
+        S.ms_icp = t2 - t1;
+        S.ms_gn = now_ms() - t2;
+        if (st) *st = S;
+        return DPG_OK;
+    }
     if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(DPG_ERR_HIP, "ICP batch failed");
     const double t2 = now_ms();
     // 5. batch Gauss-Newton from the estimated poses (optimizeGraph, dpg_slam.cc:111-119, 316-329)

@@ -250,6 +250,10 @@ dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
         set_err(DPG_ERR_ARG, "dpg_inc_create: ctx is NULL");
         return nullptr;
     }
+    if (dpg_ctx_num_gpus(ctx) != 1 || dpg_ctx_is_multi(ctx)) {
+        set_err(DPG_ERR_ARG, "dpg_inc_create: the incremental graph needs a single-device context (dpg_ctx_create)");
+        return nullptr;
+    }
     dpg_inc* q = new dpg_inc();
     q->ctx = ctx;
     if (p) q->P = *p;

@@ -20,6 +20,7 @@ dpg_ctx* dpg_inc_ctx(dpg_inc* g);   /* the context an incremental graph runs on 
  * its Between factors), so that it can run while the GPU aligns the node's edges (dpg_inc.hip) */
 int dpg_inc_prepare(dpg_inc* g, int64_t n_new, const int32_t* pairs, int64_t n_pairs);
 int dpg_inc_abort_prepare(dpg_inc* g);
+int dpg_ctx_is_multi(dpg_ctx* c);
 void* dpg_ctx_stream_of(dpg_ctx* c);
 int dpg_ctx_device_of(dpg_ctx* c);
 
@@ -52,6 +53,9 @@ typedef struct dpg_icp_kparams {
     int32_t trace_stride;
     int32_t defer_cap;  /* angular kernel: windows of more candidates go to the workgroup's
                            cooperative queue (0: never) */
+    int32_t prio_age;   /* angular kernel: wave priority rises by one every prio_age iterations
+                           of an alignment (s_setprio 1..3; 0: off) -- long alignments win issue
+                           slots, so the launch's tail of long edges shortens */
 } dpg_icp_kparams;
 
 /* Launchers (defined in dpg_icp.hip).  Return 0 or a negative DPG_ERR_*. */

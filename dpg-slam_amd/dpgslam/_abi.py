@@ -220,6 +220,8 @@ SIGNATURES = {
     "dpg_icp_params_default": (None, [C.POINTER(IcpParams)]),
     "dpg_gn_params_default": (None, [C.POINTER(GnParams)]),
     "dpg_ctx_create": (P, [C.c_int]),
+    "dpg_ctx_create_multi": (P, [C.c_int32, I32P]),
+    "dpg_ctx_num_gpus": (C.c_int32, [P]),
     "dpg_ctx_destroy": (None, [P]),
     "dpg_ctx_set_stream": (C.c_int, [P, P]),
     "dpg_ctx_synchronize": (C.c_int, [P]),

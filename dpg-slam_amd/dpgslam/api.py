@@ -148,11 +148,18 @@ def results_array(n: int) -> np.ndarray:
 class Context:
     """One dpg_ctx (one GPU, one HIP stream).  Creating it without a usable GPU raises."""
 
-    def __init__(self, device: int = 0):
-        self.handle = lib().dpg_ctx_create(device)
+    def __init__(self, device: int = 0, n_gpus: int | None = None):
+        """n_gpus: a multi-GPU context over devices device .. device + n_gpus - 1
+        (dpg_ctx_create_multi: one process, RCCL between the devices); None: one device."""
+        if n_gpus is None:
+            self.handle = lib().dpg_ctx_create(device)
+        else:
+            devs = np.arange(device, device + int(n_gpus), dtype=np.int32)
+            self.handle = lib().dpg_ctx_create_multi(int(n_gpus), ptr(devs, C.c_int32))
         if not self.handle:
             raise _abi.DpgError("dpg_ctx_create failed: " + (lib().dpg_last_error() or b"").decode())
         self.device = device
+        self.n_gpus = int(lib().dpg_ctx_num_gpus(self.handle))
         self.n_edges = 0
         self.V = 0
         self._children = weakref.WeakSet()   # DpgStore / IncGraph objects living on this context

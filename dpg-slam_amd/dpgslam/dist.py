@@ -1,13 +1,17 @@
 """Edge-sharded multi-GPU driver: one process per GPU, torch.distributed (RCCL over xGMI on the
 "nccl" backend) for the single collective of the path.
 
-  ICP:  edges are independent -> rank r aligns its contiguous, cost-balanced edge range; no
-        collective (every rank holds all scans).
+  ICP:  edges are independent -> rank r aligns its share of the edges; no collective (every rank
+        holds all scans).  The shares interleave the edge classes (edge_order): rank r takes the
+        successive pairs r, r + N, ... and the loop closures r, r + N, ... -- successive pairs
+        overlap more (more correspondences per iteration) and iterate longer, so the contiguous
+        cost-balanced ranges of round 2 left them all to ranks 0-1.  The edge list and the ICP
+        factor slots are permuted once so that every share stays one contiguous range.
   GN:   every rank holds the whole factor list (the sparsity pattern is global) but linearizes
         only its shard: rank 0 the prior + odometry factors and its ICP edges, rank r > 0 its ICP
         edges.  Per GN iteration ONE all-reduce(sum, fp64) of the packed [H upper | g | chi2]
-        buffer, then every rank runs the identical deterministic PCG + retraction (replicated
-        solve), so poses stay bitwise consistent without a broadcast.
+        buffer, then every rank runs the identical supernodal Cholesky solve + retraction
+        (replicated), so poses stay bitwise consistent without a broadcast.
 
 The GN loop is written against a small backend protocol so the orchestration can be exercised on
 CPU with the gloo backend (tests/test_dist_cpu.py); the GPU backend is `DeviceBackend`.
@@ -33,22 +37,55 @@ def shard_ranges(n: int, world: int, weights: np.ndarray | None = None) -> list[
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
 
 
+def edge_order(world: int, n_edges: int, n_successive: int) -> tuple[np.ndarray, list[tuple[int, int]], list[int]]:
+    """The interleaved shares: rank r gets successive pairs [r::world] then loop closures
+    [r::world] (each in the caller's order: successive first, as they always become factors).
+    Returns (perm, ranges, n_successive per rank): perm lists the edges rank 0's share first, and
+    rank r's share is perm[ranges[r][0]:ranges[r][1]].  world 1: the identity."""
+    succ, lc = np.arange(n_successive), np.arange(n_successive, n_edges)
+    if world <= 1:
+        return np.arange(n_edges), [(0, n_edges)], [n_successive]
+    parts = [np.concatenate([succ[r::world], lc[r::world]]) for r in range(world)]
+    cuts = np.concatenate([[0], np.cumsum([len(q) for q in parts])]).astype(int)
+    return (np.concatenate(parts).astype(np.int64), [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)],
+            [len(succ[r::world]) for r in range(world)])
+
+
 @dataclass
 class ShardPlan:
     rank: int
     world: int
-    edge_range: tuple[int, int]      # ICP edges of this rank
-    factor_range: tuple[int, int]    # factors this rank linearizes
-    n_always_local: int              # successive edges among this rank's edges
+    edge_range: tuple[int, int]      # ICP edges of this rank: positions in `perm`
+    factor_range: tuple[int, int]    # factors this rank linearizes (in the permuted factor list)
+    n_always_local: int              # successive edges among this rank's edges (its first ones)
+    perm: np.ndarray = None          # edge permutation (identity for world 1 / contiguous plans)
+
+    def edges(self, edges: np.ndarray) -> np.ndarray:
+        """This rank's edges, in dispatch order."""
+        return edges[self.perm[self.edge_range[0]:self.edge_range[1]]]
+
+    def factors(self, F: np.ndarray, icp_factor_first: int) -> np.ndarray:
+        """The factor list with its ICP slots in permuted edge order (what every rank holds)."""
+        G = F.copy()
+        G[icp_factor_first:icp_factor_first + len(self.perm)] = F[icp_factor_first + self.perm]
+        return G
 
 
 def plan(rank: int, world: int, n_edges: int, n_successive: int, icp_factor_first: int,
-         edge_cost: np.ndarray | None = None) -> ShardPlan:
-    er = shard_ranges(n_edges, world, edge_cost)[rank]
+         edge_cost: np.ndarray | None = None, strategy: str = "interleave") -> ShardPlan:
+    """strategy "interleave" (default): edge_order's class-interleaved shares; "contiguous": round
+    2's cost-balanced contiguous ranges of the caller's order (edge_cost weights)."""
+    if strategy == "interleave":
+        perm, ranges, n_succ = edge_order(world, n_edges, n_successive)
+        er = ranges[rank]
+        n_alw = n_succ[rank]
+    else:
+        perm = np.arange(n_edges)
+        er = shard_ranges(n_edges, world, edge_cost)[rank]
+        n_alw = int(np.clip(n_successive - er[0], 0, er[1] - er[0]))
     fb = 0 if rank == 0 else icp_factor_first + er[0]
     fe = icp_factor_first + er[1]
-    n_alw = int(np.clip(n_successive - er[0], 0, er[1] - er[0]))
-    return ShardPlan(rank, world, er, (fb, fe), n_alw)
+    return ShardPlan(rank, world, er, (fb, fe), n_alw, perm)
 
 
 def check_convergence(rel_tol: float, abs_tol: float, cur: float, new: float) -> bool:

@@ -128,7 +128,29 @@ void dpg_gn_params_default(dpg_gn_params* p);
 /* device = HIP device ordinal; returns NULL (and sets dpg_last_error) when no GPU is usable. */
 dpg_ctx* dpg_ctx_create(int device);
 void dpg_ctx_destroy(dpg_ctx* ctx);
-/* Run all work of this context on an external hipStream_t (e.g. torch's current stream). */
+/* Multi-GPU context (SURVEY 8b "dpg_ctx_create(int n_gpus)", 8e): ONE host process drives n_gpus
+ * devices (devices[k], or 0 .. n_gpus-1 when devices is NULL), one stream per device and one RCCL
+ * communicator per device (ncclCommInitAll over xGMI).  The same entry points then run sharded,
+ * so a single-threaded host -- the reference's ROS node (dpg_slam_main.cc:284-331) -- uses N GPUs
+ * through the unchanged call sites:
+ *   dpg_scans_upload / dpg_scans_append   every device holds every scan;
+ *   dpg_icp_batch_prepare / _run / _fetch edge e is aligned on device e mod n_gpus, all devices
+ *                                         concurrently; results (and covariance blocks) come back
+ *                                         in the caller's order; _kernel_ms is the slowest device;
+ *   dpg_optimize_graph, dpg_reoptimize    every device holds the factor list and linearizes a
+ *                                         contiguous 1/n of it; per Gauss-Newton iteration ONE
+ *                                         ncclAllReduce(sum, fp64) of the packed [H upper | g |
+ *                                         chi2]; every device factors and solves the identical
+ *                                         system (poses bitwise equal on all devices).
+ * dpg_run_icp, icp_cov_calculate / icp_cov_sandwich, dpg_get_map and dpg_loop_closure_candidates
+ * run on the first device.  The per-device step API (dpg_gn_take_icp_measurements ...), the trace
+ * and the incremental graph (dpg_inc_create: per-node updates are latency-bound, one GPU) need a
+ * single-device context.  n_gpus = 1 gives a context whose calls take the sharded paths with one
+ * rank (RCCL included): its results equal dpg_ctx_create's byte for byte. */
+dpg_ctx* dpg_ctx_create_multi(int32_t n_gpus, const int32_t* devices);
+int32_t dpg_ctx_num_gpus(dpg_ctx* ctx);   /* 1 for dpg_ctx_create */
+/* Run all work of this context on an external hipStream_t (e.g. torch's current stream); on a
+ * multi-GPU context it applies to the first device only. */
 int dpg_ctx_set_stream(dpg_ctx* ctx, void* hip_stream);
 int dpg_ctx_synchronize(dpg_ctx* ctx);
 

@@ -79,7 +79,7 @@ def _worker(rank, world, port, X0, F, nb_first, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     n_icp = len(F) - nb_first
     pl = D.plan(rank, world, n_icp, n_successive=0, icp_factor_first=nb_first)
-    be = DenseBackend(X0, F, pl.factor_range)
+    be = DenseBackend(X0, pl.factors(F, nb_first), pl.factor_range)
     gp = _abi.default_gn_params()
     st = D.gn_loop(be, lambda hb: dist.all_reduce(hb), gp)
     out[rank] = (be.X.copy(), st["iterations"], pl.factor_range)
@@ -139,6 +139,33 @@ def test_shard_ranges_tile_and_balance():
     rs = shard_ranges(1000, 2, cost)
     assert abs(cost[rs[0][0]:rs[0][1]].sum() - cost[rs[1][0]:rs[1][1]].sum()) <= 10.0
     # ICP factor ownership: successive edges stay "always kept" wherever they land
-    p0, p1 = plan(0, 2, 20000, 4999, 5000), plan(1, 2, 20000, 4999, 5000)
-    assert p0.factor_range[0] == 0 and p0.factor_range[1] == p1.factor_range[0] and p1.factor_range[1] == 25000
-    assert p0.n_always_local + p1.n_always_local == 4999
+    for strategy in ("contiguous", "interleave"):
+        p0, p1 = plan(0, 2, 20000, 4999, 5000, strategy=strategy), plan(1, 2, 20000, 4999, 5000, strategy=strategy)
+        assert p0.factor_range[0] == 0 and p0.factor_range[1] == p1.factor_range[0] and p1.factor_range[1] == 25000
+        assert p0.n_always_local + p1.n_always_local == 4999
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_interleaved_shares(world):
+    """dist.edge_order: a permutation; every rank's share is one contiguous range of it, its
+    successive pairs first (the always-kept factors), each class spread evenly over the ranks; the
+    permuted factor list keeps every base factor and moves each ICP slot with its edge."""
+    from dpgslam.dist import plan
+    E, ns, first = 20000, 4999, 5000
+    plans = [plan(r, world, E, ns, first) for r in range(world)]
+    perm = plans[0].perm
+    assert np.array_equal(np.sort(perm), np.arange(E))
+    assert plans[0].edge_range[0] == 0 and plans[-1].edge_range[1] == E
+    for r, pl in enumerate(plans):
+        a, b = pl.edge_range
+        share = perm[a:b]
+        k = pl.n_always_local
+        assert np.all(share[:k] < ns) and np.all(share[k:] >= ns)
+        assert np.array_equal(share[:k], np.arange(r, ns, world))
+        assert np.array_equal(share[k:], np.arange(ns + r, E, world))
+        if r + 1 < world:
+            assert pl.edge_range[1] == plans[r + 1].edge_range[0]
+    F = np.zeros(first + E, [("i", np.int32), ("j", np.int32)])
+    F["i"], F["j"] = np.arange(first + E), -1
+    G = plans[0].factors(F, first)
+    assert np.array_equal(G["i"][:first], np.arange(first)) and np.array_equal(G["i"][first:], first + perm)

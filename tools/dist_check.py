@@ -34,10 +34,11 @@ def main():
     ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
     n_src = np.diff(w.offsets)[w.edges[:, 1]]
     n_tgt = np.diff(w.offsets)[w.edges[:, 0]]
-    pl = D.plan(rank, world, w.E, w.n_successive, w.icp_factor_first, edge_cost=n_src * n_tgt)
+    pl = D.plan(rank, world, w.E, w.n_successive, w.icp_factor_first, edge_cost=n_src * n_tgt,
+                strategy=os.environ.get("DIST_SHARD", "interleave"))
     e0, e1 = pl.edge_range
-    ctx.icp_prepare(w.edges[e0:e1], w.est, p)
-    F = w.factors_placeholder()
+    ctx.icp_prepare(pl.edges(w.edges), w.est, p)
+    F = pl.factors(w.factors_placeholder(), w.icp_factor_first)
     hb_size = ctx.gn_setup(w.V, F, pl.factor_range, gp)
     be = D.DeviceBackend(ctx, hb_size, hb_size - 2, dev)
     ctx.icp_run(compute_cov=False)
@@ -51,10 +52,9 @@ def main():
     dist.all_gather_object(parts, (e0, e1, res.tobytes(), X.tobytes()))
     if rank == 0:
         ref_res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
-        ref_b = ref_res.tobytes()
-        rsz = ref_res.itemsize
         for a, b, rb, xb in parts:
-            assert rb == ref_b[a * rsz:b * rsz], f"ICP results of edges [{a}, {b}) differ from one batch"
+            mine = ref_res[pl.perm[a:b]].tobytes()   # the same edges of one batch over all
+            assert rb == mine, f"ICP results of shard [{a}, {b}) differ from one batch"
             assert xb == parts[0][3], "ranks disagree on the poses"
         Xr, st_r = ctx.optimize_graph(w.est.astype(np.float64), w.factors_with_icp(ref_res, p))
         d = float(np.abs(X - Xr).max())

@@ -22,8 +22,10 @@ with api.Context(0) as ctx:
     ctx.icp_prepare(w.edges, w.est, p)
     ref = None
     for r in range(rounds + 1):
-        for v in variants:
-            os.environ["DPG_ICP_VARIANT"] = v
+        for v in variants:   # "V" or "V:pA" (variant V, wave priority aging every A iterations)
+            var, _, age = v.partition(":p")
+            os.environ["DPG_ICP_VARIANT"] = var
+            os.environ["DPG_ICP_PRIO_AGE"] = age or "0"
             ctx.icp_run(compute_cov=False)
             ctx.synchronize()
             k = ctx.icp_kernel_ms()
