@@ -430,6 +430,132 @@ __device__ __forceinline__ double run_chain(const double* D, double rl, double v
              : nb == 32 ? bwd_chain<32>(D, rl, v, lane) : bwd_chain<64>(D, rl, v, lane);
 }
 
+// ---- inverted diagonal blocks (once per factorization) ----
+// The solves' diagonal blocks were triangular substitutions: a chain of up to 64 dependent steps
+// (readlane -> fp64 fma) on one wave, ~1 us per block, on the critical path of every forward and
+// backward solve -- and a Gauss-Newton step runs the solves 13 times per factorization... once.
+// chol_inv_diag inverts every 64-column diagonal block after the factorization (one wave per
+// block: lane c computes column c of inv(B) by column-oriented forward substitution, the block's
+// entries read as wave-uniform scalar loads, 64 accumulators in registers); the solves then apply
+// inv(B) (forward) or inv(B)^T (backward) as a mat-vec: independent products, 4 partial sums.
+// Layout: dinv[(3 c0 + jb + col) * kSB + row] = inv(B)[row][col] for row, col < bw, B = the front's
+// diagonal block at (jb, jb) (bw = min(kSB, k3 - jb)); one kSB-double column per pivot column.
+constexpr int kDL = kSB + 1;   // leading dimension of D in the inverse path (transposed stores conflict-free)
+
+// 8 consecutive doubles of LDS (16-B aligned, OFF bytes past base) into registers: four
+// ds_read_b128 and one wait as inline asm with immediate offsets; `dep` is a fake operand that
+// orders the loads after the arithmetic producing it.  (Left to itself the compiler issued all
+// 2016 loads of a block up front and spilled 4000 registers.)
+template <int OFF>
+__device__ __forceinline__ void lds_ld8(uint32_t base, double (&v)[8], double& dep) {
+    uint4 r0, r1, r2, r3;
+    asm volatile(
+        "ds_read_b128 %0, %5 offset:%6\n\t"
+        "ds_read_b128 %1, %5 offset:%7\n\t"
+        "ds_read_b128 %2, %5 offset:%8\n\t"
+        "ds_read_b128 %3, %5 offset:%9\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3), "+v"(dep)
+        : "v"(base), "i"(OFF), "i"(OFF + 16), "i"(OFF + 32), "i"(OFF + 48)
+        : "memory");
+    v[0] = __hiloint2double((int)r0.y, (int)r0.x); v[1] = __hiloint2double((int)r0.w, (int)r0.z);
+    v[2] = __hiloint2double((int)r1.y, (int)r1.x); v[3] = __hiloint2double((int)r1.w, (int)r1.z);
+    v[4] = __hiloint2double((int)r2.y, (int)r2.x); v[5] = __hiloint2double((int)r2.w, (int)r2.z);
+    v[6] = __hiloint2double((int)r3.y, (int)r3.x); v[7] = __hiloint2double((int)r3.w, (int)r3.z);
+}
+
+// inv(B) by column-oriented forward substitution, B (column-major kSB x kSB, identity past bw) in
+// LDS, lane c = column c of the inverse in registers (acc): x_J = acc_J / B_JJ, then
+// acc_i -= B_iJ x_J below it, 8 rows per LDS round (entries read as broadcasts: every lane the
+// same address).  Template recursion keeps every offset an immediate.
+template <int J, int Q>
+struct InvRows {
+    static __device__ __forceinline__ void run(uint32_t base, double (&acc)[kSB], double xj) {
+        if constexpr (Q < kSB / 8) {
+            double v[8];
+            // issued once the rows two rounds up have taken this column: two rounds in flight
+            lds_ld8<(J * kSB + 8 * Q) * 8>(base, v, acc[Q >= (J >> 3) + 3 ? 8 * (Q - 2) + 7 : J]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[8 * Q + u] = fma(-v[u], xj, acc[8 * Q + u]);
+            InvRows<J, Q + 1>::run(base, acc, xj);
+        }
+    }
+};
+template <int J>
+struct InvCol {
+    static __device__ __forceinline__ void run(uint32_t base, double (&acc)[kSB]) {
+        if constexpr (J < kSB) {
+            double v[8];
+            lds_ld8<(J * kSB + (J & ~7)) * 8>(base, v, acc[J > 0 ? J - 1 : 0]);   // after x_{J-1}
+            const double xj = acc[J] / v[J & 7];
+            acc[J] = xj;
+#pragma unroll
+            for (int u = (J & 7) + 1; u < 8; ++u) acc[(J & ~7) + u] = fma(-v[u], xj, acc[(J & ~7) + u]);
+            InvRows<J, (J >> 3) + 1>::run(base, acc, xj);
+            InvCol<J + 1>::run(base, acc);
+        }
+    }
+};
+
+// one wave per diagonal block; every block padded to 64 columns (one code path)
+__global__ __launch_bounds__(64) void chol_inv_diag(const int2* __restrict__ blocks, const SnDev* __restrict__ sns,
+                                                    const double* __restrict__ fronts, double* __restrict__ dinv) {
+    __shared__ __attribute__((aligned(16))) double B[kSB * kSB];
+    const int2 b = blocks[blockIdx.x];   // (front, jb)
+    const SnDev S = sns[b.x];
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, jb = b.y, bw = min(kSB, k3 - jb);
+    const int lane = threadIdx.x;
+    const double* F = fronts + S.front_off;
+    for (int j = 0; j < kSB; ++j)   // lane = row: column j of the block, padded with the identity
+        B[j * kSB + lane] = (j < bw && lane < bw) ? (lane >= j ? F[(int64_t)(jb + j) * m3 + jb + lane] : 0.0)
+                                                  : (lane == j ? 1.0 : 0.0);
+    __syncthreads();
+    double acc[kSB];
+#pragma unroll
+    for (int i = 0; i < kSB; ++i) acc[i] = i == lane ? 1.0 : 0.0;
+    InvCol<0>::run((uint32_t)reinterpret_cast<uintptr_t>(B), acc);
+    double* out = dinv + (3 * (int64_t)S.c0 + jb) * kSB;
+    if (lane < bw)
+#pragma unroll
+        for (int i = 0; i < kSB; ++i)
+            if (i < bw) out[(int64_t)lane * kSB + i] = acc[i];
+}
+
+// the inverted block at (jb, jb) into D (ld kDL), zero past bw: as stored (forward: D(i, j) =
+// inv(B)[i][j] at D[j kDL + i]) or transposed (backward: D[j kDL + i] = inv(B)[j][i])
+template <bool kT_>
+__device__ __forceinline__ void load_dinv(double* D, const double* dinv_front, int jb, int bw) {
+    const double* src = dinv_front + (int64_t)jb * kSB;
+    constexpr int kPer = kSB * kSB / kT;
+    double v[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int e = threadIdx.x + kT * q, r = e % kSB, cc = e / kSB;   // src[cc * kSB + r] = inv(B)[r][cc]
+        v[q] = (r < bw && cc < bw) ? src[e] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+        const int e = threadIdx.x + kT * q, r = e % kSB, cc = e / kSB;
+        if constexpr (kT_) D[r * kDL + cc] = v[q];
+        else D[cc * kDL + r] = v[q];
+    }
+}
+
+// one wave: v[jb + lane] <- sum_j D[j kDL + lane] v[jb + j], lane < bw (reads before the write)
+__device__ __forceinline__ void apply_dinv(const double* D, double* v, int jb, int bw, int lane) {
+    const int nb = chain_len(bw);
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (int j = 0; j < nb; j += 4) {
+        const double v0 = j < bw ? v[jb + j] : 0.0, v1 = j + 1 < bw ? v[jb + j + 1] : 0.0;
+        const double v2 = j + 2 < bw ? v[jb + j + 2] : 0.0, v3 = j + 3 < bw ? v[jb + j + 3] : 0.0;
+        a0 = fma(D[j * kDL + lane], v0, a0);
+        a1 = fma(D[(j + 1) * kDL + lane], v1, a1);
+        a2 = fma(D[(j + 2) * kDL + lane], v2, a2);
+        a3 = fma(D[(j + 3) * kDL + lane], v3, a3);
+    }
+    if (lane < bw) v[jb + lane] = (a0 + a1) + (a2 + a3);
+}
+
 // Staging of a front's L in LDS while the solve waits for its children (forward) or its parent
 // (backward): every load the front's own arithmetic needs is issued before the wait, so after it
 // only the handed-off values (pending row updates / the ancestors' x) travel.  The region holds
@@ -560,22 +686,27 @@ __device__ __forceinline__ void sub_coldots(double* z, const double* A, int64_t 
 // (the first one prestaged) and L21s the first C columns of L21.
 template <bool kFull>
 __device__ __forceinline__ void fwd_front(const SnDev& S, const double* F, double* Rg, double* D, const double* L21s,
-                                          int C, double* rd, double* y, double* aR, double* acc) {
+                                          int C, double* rd, double* y, double* aR, double* acc, const double* dinv_f) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* A = kFull ? Rg : F;   // the front's columns, ld m3
     for (int jb = 0; jb < k3; jb += kSB) {
         const int bw = min(kSB, k3 - jb);
         if (jb > 0) {   // the first block was loaded before the wait
-            if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
+            if (dinv_f) load_dinv<false>(D, dinv_f, jb, bw);
+            else if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
             else load_diag(D, rd, F, m3, jb, bw);
             __syncthreads();
         }
-        if (wave == 0) {   // lane = row; y_j broadcast by v_readlane (uniform j)
-            double yl = lane < bw ? y[jb + lane] : 0.0;
-            const double rl = lane < bw ? rd[lane] : 0.0;
-            yl = run_chain<true>(D, rl, yl, lane, bw);
-            if (lane < bw) y[jb + lane] = yl * rl;
+        if (wave == 0) {
+            if (dinv_f) {   // y_blk <- inv(B) y_blk
+                apply_dinv(D, y, jb, bw, lane);
+            } else {        // lane = row; y_j broadcast by v_readlane (uniform j)
+                double yl = lane < bw ? y[jb + lane] : 0.0;
+                const double rl = lane < bw ? rd[lane] : 0.0;
+                yl = run_chain<true>(D, rl, yl, lane, bw);
+                if (lane < bw) y[jb + lane] = yl * rl;
+            }
         }
         __syncthreads();
         for (int i = jb + bw + tid; i < k3; i += kT) {
@@ -634,7 +765,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                        const double* __restrict__ fronts,
                                                        const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm,
-                                                       double* __restrict__ ysol, double* acc, int R) {
+                                                       double* __restrict__ ysol, double* acc, int R,
+                                                       const double* __restrict__ dinv) {
     extern __shared__ __attribute__((aligned(16))) double smem_fw[];
     double* sm = smem_fw + 2;   // smem_fw[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
@@ -642,8 +774,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
-    double* D = sm;                  // kSB x kSB diagonal block
-    double* Rg = D + kSB * kSB;      // staging region, R doubles (Stage)
+    const double* dinv_f = dinv ? dinv + 3 * (int64_t)S.c0 * kSB : nullptr;   // inverted diagonal blocks
+    double* D = sm;                  // kSB x kDL diagonal block
+    double* Rg = D + kSB * kDL;      // staging region, R doubles (Stage)
     double* L21s = Rg;               // (not full) first C columns of L21
     double* rd = Rg + R;             // kSB reciprocals of the diagonal block's diagonal
     double* y = rd + kSB;            // k3
@@ -655,7 +788,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
         y[t] = -g[3 * node + t % 3];
     }
     for (int t = tid; t < r3; t += kT) aR[t] = 0.0;
-    load_diag(D, rd, F, m3, 0, min(kSB, k3));
+    if (dinv_f) load_dinv<false>(D, dinv_f, 0, min(kSB, k3));
+    else load_diag(D, rd, F, m3, 0, min(kSB, k3));
     if (P.full) stage_copy(Rg, F, m3 * k3);
     else stage_l21(L21s, F, m3, k3, P.C);
     if (S.nchild > 0) {
@@ -675,8 +809,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
         }
         __syncthreads();
     }
-    if (P.full) fwd_front<true>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc);
-    else fwd_front<false>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc);
+    if (P.full) fwd_front<true>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc, dinv_f);
+    else fwd_front<false>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc, dinv_f);
     for (int t = tid; t < k3; t += kT) ysol[3 * (int64_t)S.c0 + t] = y[t];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -705,21 +839,26 @@ __device__ __forceinline__ void bwd_z(const double* F, const double* Rg, const d
 
 template <bool kFull>
 __device__ __forceinline__ void bwd_diag(const double* F, const double* Rg, double* D, double* rd, int m3, int k3,
-                                         double* z) {
+                                         double* z, const double* dinv_f) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nblk = (k3 + kSB - 1) / kSB;
     for (int b = nblk - 1; b >= 0; --b) {
         const int jb = b * kSB, bw = min(kSB, k3 - jb);
         if (b != nblk - 1) {   // the last block was loaded before the wait
-            if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
+            if (dinv_f) load_dinv<true>(D, dinv_f, jb, bw);
+            else if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
             else load_diag(D, rd, F, m3, jb, bw);
             __syncthreads();
         }
-        if (wave == 0) {   // lane = row; x_j broadcast by v_readlane (uniform j): ~3 dependent ops per step
-            double zl = lane < bw ? z[jb + lane] : 0.0;
-            const double rl = lane < bw ? rd[lane] : 0.0;
-            zl = run_chain<false>(D, rl, zl, lane, bw);
-            if (lane < bw) z[jb + lane] = zl * rl;
+        if (wave == 0) {
+            if (dinv_f) {   // z_blk <- inv(B)^T z_blk
+                apply_dinv(D, z, jb, bw, lane);
+            } else {        // lane = row; x_j broadcast by v_readlane (uniform j): ~3 dependent ops per step
+                double zl = lane < bw ? z[jb + lane] : 0.0;
+                const double rl = lane < bw ? rd[lane] : 0.0;
+                zl = run_chain<false>(D, rl, zl, lane, bw);
+                if (lane < bw) z[jb + lane] = zl * rl;
+            }
         }
         __syncthreads();
         sub_coldots(z, (kFull ? Rg : F) + jb, m3, z + jb, jb, bw);
@@ -730,7 +869,8 @@ __device__ __forceinline__ void bwd_diag(const double* F, const double* Rg, doub
 template <bool kFull>
 __device__ __forceinline__ void bwd_front(int s, const SnDev& S, int nseg, const SolveSeg* sg, const int32_t* rp,
                                           int32_t* sync, int32_t* status, double* xsol, const double* F, double* Rg,
-                                          double* D, const double* L21s, int C, double* rd, double* z, double* xr) {
+                                          double* D, const double* L21s, int C, double* rd, double* z, double* xr,
+                                          const double* dinv_f) {
     const int tid = threadIdx.x;
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     if (nseg == 0) {   // the root (no rows), or too many segments: wait for the parent, take every row
@@ -757,7 +897,7 @@ __device__ __forceinline__ void bwd_front(int s, const SnDev& S, int nseg, const
     }
     __syncthreads();
     BW_MARK(s, 2);
-    bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z);
+    bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z, dinv_f);
 }
 
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
@@ -766,7 +906,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                         const SolveSeg* __restrict__ segs,
                                                         const double* __restrict__ fronts,
                                                         const double* __restrict__ ysol, double* xsol, int R,
-                                                        int max_seg) {
+                                                        int max_seg, const double* __restrict__ dinv) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
@@ -775,8 +915,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     BW_MARK(s, 0);
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
-    double* D = sm;                  // kSB x kSB diagonal block
-    double* Rg = D + kSB * kSB;      // staging region, R doubles (Stage)
+    const double* dinv_f = dinv ? dinv + 3 * (int64_t)S.c0 * kSB : nullptr;   // inverted diagonal blocks
+    double* D = sm;                  // kSB x kDL diagonal block
+    double* Rg = D + kSB * kDL;      // staging region, R doubles (Stage)
     double* L21s = Rg;               // (not full) first C columns of L21
     double* rd = Rg + R;             // kSB reciprocals of the diagonal block's diagonal
     double* z = rd + kSB;            // k3
@@ -791,13 +932,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     for (int q = tid; q < nseg; q += kT) sg[q] = segs[S.seg_off + q];
     {
         const int jb = ((k3 + kSB - 1) / kSB - 1) * kSB;
-        load_diag(D, rd, F, m3, jb, k3 - jb);
+        if (dinv_f) load_dinv<true>(D, dinv_f, jb, k3 - jb);
+        else load_diag(D, rd, F, m3, jb, k3 - jb);
     }
     if (P.full) stage_copy(Rg, F, m3 * k3);
     else stage_l21(L21s, F, m3, k3, P.C);
     __syncthreads();
-    if (P.full) bwd_front<true>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr);
-    else bwd_front<false>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr);
+    if (P.full) bwd_front<true>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f);
+    else bwd_front<false>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f);
     BW_MARK(s, 3);
     for (int j = tid; j < k3; j += kT) st_agent(xsol + 3 * (int64_t)S.c0 + j, z[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1560,6 +1702,10 @@ struct CholDev {
     double* ysol = nullptr;
     double* xsol = nullptr;
     int32_t* status = nullptr;
+    double* dinv = nullptr;            // inverted diagonal blocks of the solves ([3n][kSB])
+    int2* dblocks = nullptr;           // (front, jb) of every diagonal block
+    int64_t n_dblocks = 0;
+    bool use_dinv = false;             // DPG_SOLVE_DINV=1: inverted diagonal blocks (measured slower)
     std::vector<int32_t> level_ptr;
     std::vector<size_t> lds_solve;   // per level
     int64_t nnzb_upper = 0;
@@ -1589,7 +1735,7 @@ struct CholDev {
     size_t lds_fused = 0;
     bool fused_db = true;
     // capacities (elements) of the device buffers above, for rebuilds
-    size_t c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_sync = 0;
+    size_t c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_sync = 0, c_dinv = 0;
     double t_build[2] = {0, 0};   // last chol_build: host structures, uploads (ms)
     char* stage = nullptr;        // pinned staging buffer of the uploads
     size_t c_stage = 0;
@@ -1603,7 +1749,7 @@ extern "C" void dpg_chol_destroy(void* h) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!c) return;
     // (the structure arrays live in c->arena)
-    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync};
+    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync, c->dinv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stage) (void)hipHostFree(c->stage);
@@ -1671,6 +1817,7 @@ struct CholHost {
     std::vector<AsmChild> asm_c;
     std::vector<int2> panel_t;
     std::vector<int4> upd_t;
+    std::vector<int2> dblocks;
     int64_t acc_total = 0;
 };
 
@@ -1993,7 +2140,7 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     size_t lds_rest = 0;
     for (int32_t s = 0; s < S.ns; ++s) {
         const int32_t m3 = 3 * (sns[(size_t)s].k + sns[(size_t)s].r);
-        lds_rest = std::max(lds_rest, (size_t)(kSB * kSB + kSB + m3 + 2 + m3 / 6 + 2 + 2 * kMaxSeg) * sizeof(double));
+        lds_rest = std::max(lds_rest, (size_t)(kSB * kDL + kSB + m3 + 2 + m3 / 6 + 2 + 2 * kMaxSeg) * sizeof(double));
     }
     {
         const char* env = getenv("DPG_SOLVE_STAGE");
@@ -2089,6 +2236,14 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     // [ticket | children-done counters [ns] | panel flags [ns] | backward: ticket | done [ns] |
     //  pivot-tile hand-off flags [per large-front tile]]
     c->sync_bytes = ((size_t)(2 + 3 * S.ns + ftasks.size()) * sizeof(int32_t) + 15) & ~size_t(15);
+    H.dblocks.clear();
+    for (int32_t s = 0; s < S.ns; ++s)
+        for (int32_t jb = 0; jb < 3 * sns[(size_t)s].k; jb += kSB) H.dblocks.push_back(make_int2(s, jb));
+    c->n_dblocks = (int64_t)H.dblocks.size();
+    // measured (tools/r3_gn_job.sh, profiles/r03): the inversion launch (~55 us at config 4) costs
+    // more than the chains it removes from the solves (re-solve 0.250 -> 0.241 ms), so the chains
+    // stay the default; DPG_SOLVE_DINV=1 selects the inverted blocks
+    c->use_dinv = getenv("DPG_SOLVE_DINV") != nullptr;
     PLAN_T(7);
     return DPG_OK;
 }
@@ -2099,7 +2254,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     const dpg_chol_sym& S = c->sym;
     auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
     struct Piece { void** d; const void* h; size_t bytes; };
-    Piece pieces[20];
+    Piece pieces[24];
     int np = 0;
     auto add = [&](auto** d, const auto& h) {
         using T = typename std::remove_reference<decltype(h)>::type::value_type;
@@ -2118,6 +2273,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     add(&c->fchild, H.fchild);
     add(&c->order_bwd, H.bwd);
     add(&c->segs, H.segs);
+    add(&c->dblocks, H.dblocks);
     if (!c->fused) {
         add(&c->asm_tasks, H.asm_t);
         add(&c->asm_child, H.asm_c);
@@ -2155,6 +2311,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     rc |= dreserve(&c->ysol, &c->c_ysol, (size_t)(3 * n));
     rc |= dreserve(&c->xsol, &c->c_xsol, (size_t)(3 * n));
     rc |= dreserve(&c->status, &c->c_status, 1);
+    rc |= dreserve(&c->dinv, &c->c_dinv, (size_t)(3 * n) * kSB);
     if (!rc) rc |= hipMemsetAsync(c->status, 0, sizeof(int32_t), nullptr) != hipSuccess;
     // the staging buffer is reused by the next build: wait for the copy (always, even after an error)
     rc |= hipStreamSynchronize(nullptr) != hipSuccess;
@@ -2242,8 +2399,11 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
                            c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
                            c->perm, c->fronts,
                            c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0);
+        if (c->use_dinv && c->n_dblocks > 0)
+            hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg);
+                           c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg,
+                           c->use_dinv ? c->dinv : nullptr);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -2263,10 +2423,13 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
     int32_t* sync_f = c->sync;
     int32_t* sync_b = c->sync + 1 + S.ns;
+    if (c->use_dinv && c->n_dblocks > 0)
+        hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
+    const double* di = c->use_dinv ? c->dinv : nullptr;
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg);
+                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2277,10 +2440,11 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     const dpg_chol_sym& S = c->sym;
     const double* g = hb + 9 * c->nnzb_upper;
     if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
+    const double* di = c->use_dinv ? c->dinv : nullptr;   // inverted by the factorization's dpg_chol_solve
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

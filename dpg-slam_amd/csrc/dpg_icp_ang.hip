@@ -475,6 +475,11 @@ __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ float rdlane(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
+__device__ __forceinline__ double rdlane(double x, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ uint64_t rdlane(uint64_t x, int l) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
     return ((uint64_t)hi << 32) | lo;
@@ -648,11 +653,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     };
     for (;;) {
         ICP_STAMP(c0);
-        if (kp.prio_age > 0 && k > 0) {   // aging: an alignment that keeps iterating gains issue priority
-            if (k == kp.prio_age) __builtin_amdgcn_s_setprio(1);
-            else if (k == 2 * kp.prio_age) __builtin_amdgcn_s_setprio(2);
-            else if (k == 3 * kp.prio_age) __builtin_amdgcn_s_setprio(3);
-        }
         const float i00 = uni((float)L.bc->inv[0]), i01 = uni((float)L.bc->inv[1]);
         const float i10 = uni((float)L.bc->inv[2]), i11 = uni((float)L.bc->inv[3]);
         const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     }
                     s = advance(s, stepM, M);
                 };
-                if constexpr (VAR >= 2 && kTpL) {
+                if constexpr (VAR == 2 && kTpL) {
                     int c = 0;
                     for (; c < kU * kMinTrips && __any(c < fc); c += kU) ftrip();
                     if (__any(c < fc)) {
@@ -802,7 +802,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                         s = advance(s, stepN, N);
                     };
                     int c = 0;
-                    if constexpr (VAR >= 2 && kScsL) {
+                    if constexpr (VAR == 2 && kScsL) {
                         for (; c < kU * kMinTrips && (okm & __ballot(c < rc)) != 0; c += kU) rtrip();
                         const uint64_t act = okm & __ballot(c < rc);
                         if (act) {
@@ -963,8 +963,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         }
         if (__builtin_amdgcn_readlane(last, 0)) {
             double S[kSums];
+            if constexpr (VAR == 3) {   // lane q combines sum q (the same fixed tree), then broadcast
+                const double sq = lane < kSums ? dpg_tree::combine(L.wpart, kSums + 2, lane) : 0.0;
 #pragma unroll
-            for (int q = 0; q < kSums; ++q) S[q] = uni(dpg_tree::combine(L.wpart, kSums + 2, q));
+                for (int q = 0; q < kSums; ++q) S[q] = rdlane(sq, q);
+            } else {
+#pragma unroll
+                for (int q = 0; q < kSums; ++q) S[q] = uni(dpg_tree::combine(L.wpart, kSums + 2, q));
+            }
             Bcast B = *L.bc;
             float F[6];
 #pragma unroll
@@ -976,6 +982,54 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             B.iter = k + 1;
             if (B.cnt < kp.min_corr) {
                 B.code = 2;   // stop, "Not enough correspondences found" (transform unchanged)
+            } else if constexpr (VAR == 3) {
+                // the same IEEE operations as below, the seven independent divisions by the count
+                // (and S1 / S0) in ONE vector division across lanes 0-6, then the two by |(a, b)|
+                // in another: two division latencies on the fit's path instead of nine
+                const double n = S[0];
+                double num = 0.0, den = 1.0;
+                switch (lane) {
+                    case 0: num = S[2] * S[4] + S[3] * S[5]; den = n; break;
+                    case 1: num = S[2] * S[5] - S[3] * S[4]; den = n; break;
+                    case 2: num = S[2]; den = n; break;
+                    case 3: num = S[3]; den = n; break;
+                    case 4: num = S[4]; den = n; break;
+                    case 5: num = S[5]; den = n; break;
+                    case 6: num = S[1]; den = S[0]; break;
+                    default: break;
+                }
+                const double qv = num / den;
+                const double a = S[6] - rdlane(qv, 0), b = S[7] - rdlane(qv, 1);
+                const double mpx = rdlane(qv, 2), mpy = rdlane(qv, 3), mqx = rdlane(qv, 4), mqy = rdlane(qv, 5);
+                const double mse = rdlane(qv, 6);
+                const double hh = sqrt(a * a + b * b);
+                double c = 1.0, sn = 0.0;
+                if (hh > 0.0) {
+                    const double cs = (lane == 0 ? a : b) / hh;
+                    c = rdlane(cs, 0);
+                    sn = rdlane(cs, 1);
+                }
+                const double txd = mqx - (c * mpx - sn * mpy);
+                const double tyd = mqy - (sn * mpx + c * mpy);
+                const float cf = (float)c, sf = (float)sn, txf = (float)txd, tyf = (float)tyd;
+                const float nsf = -sf;
+                B.r[0] = cf; B.r[1] = sf; B.r[2] = txf; B.r[3] = tyf;
+                float Nf[6];
+                Nf[0] = cf * F[0] + nsf * F[3];
+                Nf[1] = cf * F[1] + nsf * F[4];
+                Nf[2] = (cf * F[2] + nsf * F[5]) + txf;
+                Nf[3] = sf * F[0] + cf * F[3];
+                Nf[4] = sf * F[1] + cf * F[4];
+                Nf[5] = (sf * F[2] + cf * F[5]) + tyf;
+#pragma unroll
+                for (int q = 0; q < 6; ++q) B.F[q] = Nf[q];
+                B.mse = mse;
+                const float tr = ((cf + cf) + 1.0f) - 1.0f;
+                const double cos_angle = 0.5 * (double)tr;
+                const double tsq = (double)(txf * txf + tyf * tyf);
+                B.code = (k + 1 >= kp.max_iter || (cos_angle >= kp.rot_thr && tsq <= kp.eps) ||
+                          fabs(mse - prev_mse) < kp.mse_abs) ? 1 : 0;
+                B.prev_mse = mse;
             } else {
                 const double n = S[0];
                 double a, b;
@@ -1059,10 +1113,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             float Fn[6];
 #pragma unroll
             for (int q = 0; q < 6; ++q) Fn[q] = uni(L.bc->F[q]);
-            inverse2(Fn, inv);
-            if (lane == 0)
+            if constexpr (VAR == 3) {   // inverse2's four divisions by the determinant, lanes 0-3
+                const double det = (double)Fn[0] * (double)Fn[4] - (double)Fn[1] * (double)Fn[3];
+                const double num = lane == 0 ? (double)Fn[4] : lane == 1 ? -(double)Fn[1] : lane == 2 ? -(double)Fn[3] : (double)Fn[0];
+                const double q = num / det;
+                if (lane < 4) L.bc->inv[lane] = q;
+            } else {
+                inverse2(Fn, inv);
+                if (lane == 0)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) L.bc->inv[q] = inv[q];
+                    for (int q = 0; q < 4; ++q) L.bc->inv[q] = inv[q];
+            }
         }
         __syncthreads();   // moved source complete before the next reciprocal tests
 #ifdef DPG_ICP_TIMING
@@ -1152,9 +1213,6 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     Rec* g = reinterpret_cast<Rec*>(scratch);
     const char* ve = getenv("DPG_ICP_VARIANT");   // A/B of kernel variants (tools/icp_var_ab.py)
     const int var = ve ? atoi(ve) : 1;
-    dpg_icp_kparams kpl = *kp;
-    if (const char* pa = getenv("DPG_ICP_PRIO_AGE")) kpl.prio_age = atoi(pa);
-    kp = &kpl;
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
@@ -1163,7 +1221,9 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
                            results_dev, trace_dev, g);                                                               \
         else if (var == 1) hipLaunchKernelGGL((icp_ang_kernel<P, M, 1>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g);                                                               \
-        else hipLaunchKernelGGL((icp_ang_kernel<P, M, 2>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+        else if (var == 2) hipLaunchKernelGGL((icp_ang_kernel<P, M, 2>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+                           results_dev, trace_dev, g);                                                               \
+        else hipLaunchKernelGGL((icp_ang_kernel<P, M, 3>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);

@@ -53,9 +53,6 @@ typedef struct dpg_icp_kparams {
     int32_t trace_stride;
     int32_t defer_cap;  /* angular kernel: windows of more candidates go to the workgroup's
                            cooperative queue (0: never) */
-    int32_t prio_age;   /* angular kernel: wave priority rises by one every prio_age iterations
-                           of an alignment (s_setprio 1..3; 0: off) -- long alignments win issue
-                           slots, so the launch's tail of long edges shortens */
 } dpg_icp_kparams;
 
 /* Launchers (defined in dpg_icp.hip).  Return 0 or a negative DPG_ERR_*. */

@@ -176,12 +176,13 @@ def test_gpu_failed_update_rolls_back(ctx):
 
 
 @pytest.mark.gpu
-def test_gpu_add_node_failure_keeps_store_and_graph_in_step(ctx):
+def test_gpu_add_node_failure_keeps_store_and_graph_in_step():
     """dpg_add_node_pairs with no factor for the new node fails in the update; the scan store drops
     the node again (store and graph keep the same count) and the next dpg_add_node succeeds."""
     from dpgslam import api
     w = synth.generate("config2")
     p = _abi.default_icp_params()
+    ctx = api.Context(0)   # a fresh scan store
     g = api.IncGraph(ctx, mode="isam2")
     prior = np.zeros(1, _abi.FACTOR_DTYPE)
     prior["kind"], prior["i"], prior["info"] = _abi.DPG_FACTOR_PRIOR, 0, 1.0 / np.array([0.04, 0.04, 0.0225])
@@ -193,3 +194,4 @@ def test_gpu_add_node_failure_keeps_store_and_graph_in_step(ctx):
     st = g.add_node(w.cloud(2), np.zeros(3, np.int32), w.est[2], icp_params=p)
     assert g.V == 3 and st.n_icp_edges >= 1
     g.close()
+    ctx.close()
