@@ -176,12 +176,6 @@ __device__ __forceinline__ Rec ld_rec(const Rec* p) {
     return Rec{__uint_as_float(v.x), __uint_as_float(v.y), v.z, v.w};
 }
 
-__device__ __forceinline__ uint4 ld_u4(const Rec* p) {
-    uint4 v = *reinterpret_cast<const uint4*>(p);
-    asm volatile("" : "+v"(v.w));
-    return v;
-}
-
 __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
     return ((uint64_t)__float_as_uint(d) << 32) | key;
 }
@@ -443,56 +437,11 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
     return v;
 }
 
-// Wave reductions by DPP (row shifts, then the row broadcasts 15 / 31): the result is lane 63's,
-// read back as a wave-uniform value.  Lanes shifted in from outside a row take the identity.
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint32_t dpp32(uint32_t v, uint32_t ident) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)ident, (int)v, CTRL, ROWS, 0xF, false);
-}
-template <int CTRL, int ROWS>
-__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
-    const uint32_t lo = dpp32<CTRL, ROWS>((uint32_t)v, 0xffffffffu), hi = dpp32<CTRL, ROWS>((uint32_t)(v >> 32), 0xffffffffu);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t wave_min_u64_dpp(uint64_t v) {
-    uint64_t o;
-    o = dpp64<0x111, 0xF>(v); v = o < v ? o : v;   // row_shr:1
-    o = dpp64<0x112, 0xF>(v); v = o < v ? o : v;   // row_shr:2
-    o = dpp64<0x114, 0xF>(v); v = o < v ? o : v;   // row_shr:4
-    o = dpp64<0x118, 0xF>(v); v = o < v ? o : v;   // row_shr:8: lane 15 of each row holds its row
-    o = dpp64<0x142, 0xA>(v); v = o < v ? o : v;   // row_bcast:15
-    o = dpp64<0x143, 0xC>(v); v = o < v ? o : v;   // row_bcast:31: lane 63 holds the wave
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, 63), hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), 63);
-    return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
-    v = max(v, dpp32<0x111, 0xF>(v, 0u));
-    v = max(v, dpp32<0x112, 0xF>(v, 0u));
-    v = max(v, dpp32<0x114, 0xF>(v, 0u));
-    v = max(v, dpp32<0x118, 0xF>(v, 0u));
-    v = max(v, dpp32<0x142, 0xA>(v, 0u));
-    v = max(v, dpp32<0x143, 0xC>(v, 0u));
-    return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ float rdlane(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
 __device__ __forceinline__ double rdlane(double x, int l) {
     const uint64_t b = (uint64_t)__double_as_longlong(x);
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__device__ __forceinline__ uint64_t rdlane(uint64_t x, int l) {
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, l), hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-// Straggler policy of variant 2 (per point slot and search direction): every lane runs kMinTrips
-// in-lane trips; if windows remain, the wave either keeps running in-lane trips (all 64 lanes pay
-// each trip of the longest remaining window, R trips) or takes the A remaining windows one at a
-// time with all 64 lanes (64 candidates per step): it keeps going in-lane while
-// R * trip cost <= A * cooperative cost (VALU instructions, measured from the ISA).
-constexpr int kMinTrips = 1;
-constexpr int kFwdTrip = 28, kFwdCoop = 64;   // in-lane forward trip / one cooperative forward window
-constexpr int kRecTrip = 20, kRecCoop = 26;   // the same for reciprocal windows
 
 // The forward search's starting point for a point at q (R4 seeding): seed >= 0 is the last
 // match (its distance bounds the radius), -1 means no knowledge (search r + kClear, probing the
@@ -721,35 +670,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     }
                     s = advance(s, stepM, M);
                 };
-                if constexpr (VAR == 2 && kTpL) {
-                    int c = 0;
-                    for (; c < kU * kMinTrips && __any(c < fc); c += kU) ftrip();
-                    if (__any(c < fc)) {
-                        const uint64_t act = __ballot(c < fc);
-                        const uint32_t R = wave_max_u32_dpp(c < fc ? (uint32_t)(fc - c + kU - 1) / kU : 0u);
-                        if ((int)R * kFwdTrip <= __popcll(act) * kFwdCoop) {
-                            for (; __any(c < fc); c += kU) ftrip();
-                        } else {   // the stragglers one at a time, 64 candidates per step
-                            for (uint64_t rem = act; rem; rem &= rem - 1) {
-                                const int l = __builtin_ctzll(rem);
-                                const float lx = rdlane(qx, l), ly = rdlane(qy, l);
-                                const int ls = __builtin_amdgcn_readlane(s, l);
-                                const int ln = __builtin_amdgcn_readlane(fc, l) - c;
-                                uint64_t b = ~0ull;
-                                for (int k = lane; k < ln + 63 - (ln + 63) % 64; k += 64) {
-                                    const int pk = ls + (k < ln ? k : 0);
-                                    const int p = pk >= M ? pk - M : pk;
-                                    const uint64_t kd = cand_key(ld_u4(L.tp + p), lx, ly);
-                                    b = kd < b ? kd : b;
-                                }
-                                b = wave_min_u64_dpp(b);
-                                if (lane == l) best = b < best ? b : best;
-                            }
-                        }
-                    }
-                } else {
-                    for (int c = 0; __any(c < fc); c += kU) ftrip();   // exact (d, original index) argmin
-                }
+                for (int c = 0; __any(c < fc); c += kU) ftrip();   // exact (d, original index) argmin
+
             }
             int bp = -1;
             if (search && !pend) bp = forward_done(m, best, sd == -1);
@@ -802,31 +724,6 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                         s = advance(s, stepN, N);
                     };
                     int c = 0;
-                    if constexpr (VAR == 2 && kScsL) {
-                        for (; c < kU * kMinTrips && (okm & __ballot(c < rc)) != 0; c += kU) rtrip();
-                        const uint64_t act = okm & __ballot(c < rc);
-                        if (act) {
-                            const bool mineact = ((act >> lane) & 1u) != 0;
-                            const uint32_t R = wave_max_u32_dpp(mineact ? (uint32_t)(rc - c + kU - 1) / kU : 0u);
-                            if ((int)R * kRecTrip > __popcll(act) * kRecCoop) {
-                                for (uint64_t rem = act; rem; rem &= rem - 1) {   // stragglers, 64 per step
-                                    const int l = __builtin_ctzll(rem);
-                                    const float lx = rdlane(tj.x, l), ly = rdlane(tj.y, l);
-                                    const uint64_t lm = rdlane(mine, l);
-                                    const int ls = __builtin_amdgcn_readlane(s, l);
-                                    const int ln = __builtin_amdgcn_readlane(rc, l) - c;
-                                    bool beat = false;
-                                    for (int k = lane; k < ln + 63 - (ln + 63) % 64; k += 64) {
-                                        const int pk = ls + (k < ln ? k : 0);
-                                        const int p = pk >= N ? pk - N : pk;
-                                        beat = beat | (cand_key(ld_u4(L.scs + p), lx, ly) < lm);
-                                    }
-                                    if (__ballot(beat)) okm &= ~(1ull << l);
-                                }
-                                c = 0x3fffffff;   // every window done
-                            }
-                        }
-                    }
                     for (; (okm & __ballot(c < rc)) != 0; c += kU) rtrip();
                     ok = ok && ((okm >> lane) & 1u);
                 } else {
@@ -963,7 +860,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         }
         if (__builtin_amdgcn_readlane(last, 0)) {
             double S[kSums];
-            if constexpr (VAR == 3) {   // lane q combines sum q (the same fixed tree), then broadcast
+            if constexpr (VAR >= 1) {   // lane q combines sum q (the same fixed tree), then broadcast
                 const double sq = lane < kSums ? dpg_tree::combine(L.wpart, kSums + 2, lane) : 0.0;
 #pragma unroll
                 for (int q = 0; q < kSums; ++q) S[q] = rdlane(sq, q);
@@ -982,7 +879,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             B.iter = k + 1;
             if (B.cnt < kp.min_corr) {
                 B.code = 2;   // stop, "Not enough correspondences found" (transform unchanged)
-            } else if constexpr (VAR == 3) {
+            } else if constexpr (VAR >= 1) {
                 // the same IEEE operations as below, the seven independent divisions by the count
                 // (and S1 / S0) in ONE vector division across lanes 0-6, then the two by |(a, b)|
                 // in another: two division latencies on the fit's path instead of nine
@@ -1113,7 +1010,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             float Fn[6];
 #pragma unroll
             for (int q = 0; q < 6; ++q) Fn[q] = uni(L.bc->F[q]);
-            if constexpr (VAR == 3) {   // inverse2's four divisions by the determinant, lanes 0-3
+            if constexpr (VAR >= 1) {   // inverse2's four divisions by the determinant, lanes 0-3
                 const double det = (double)Fn[0] * (double)Fn[4] - (double)Fn[1] * (double)Fn[3];
                 const double num = lane == 0 ? (double)Fn[4] : lane == 1 ? -(double)Fn[1] : lane == 2 ? -(double)Fn[3] : (double)Fn[0];
                 const double q = num / det;
@@ -1216,14 +1113,14 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
+// variant 1 (default): hardware square roots in the window bounds, the candidate distance
+// computed into the record's pad register, reciprocal beats as ballots, the fit's divisions as
+// lane-parallel vector divisions; variant 0: round 2's form of the same arithmetic (A/B reference,
+// DPG_ICP_VARIANT=0).  Both give byte-identical results.
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
         if (var == 0) hipLaunchKernelGGL((icp_ang_kernel<P, M, 0>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g);                                                               \
-        else if (var == 1) hipLaunchKernelGGL((icp_ang_kernel<P, M, 1>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
-                           results_dev, trace_dev, g);                                                               \
-        else if (var == 2) hipLaunchKernelGGL((icp_ang_kernel<P, M, 2>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
-                           results_dev, trace_dev, g);                                                               \
-        else hipLaunchKernelGGL((icp_ang_kernel<P, M, 3>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+        else hipLaunchKernelGGL((icp_ang_kernel<P, M, 1>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
