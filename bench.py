@@ -47,6 +47,22 @@ def pmc_traffic(kernel: str):
     return None, None, {}
 
 
+def kernel_src_sha256() -> str:
+    """Content hash of the ICP kernel's sources (the kernel file and the headers it includes): the
+    PMC record is stamped with the hash of the sources it profiled (tools/pmc_job.sh), so a stale
+    record is visible in the bench line."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("dpg_icp_ang.hip", "dpg_icp_tree.h", "dpg_internal.h", "dpg_atan2f.h"):
+        h.update(open(os.path.join(ROOT, "dpg-slam_amd", "csrc", f), "rb").read())
+    return h.hexdigest()
+
+
+def pmc_record() -> dict:
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    return json.load(open(path)) if os.path.exists(path) else {}
+
+
 def host_cpus() -> dict:
     """Core count of this host: the CPUs this process may run on, and lscpu's view of the machine."""
     info = {"affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()}
@@ -388,6 +404,11 @@ def main_dynamic(args):
                     if prof else None},
         "dpg": {"calls": len(dpg_a), "ms_per_call": float(dpg_a[:, 1].mean()) if len(dpg_a) else None,
                 "calls_per_s": float(1e3 / dpg_a[:, 1].mean()) if len(dpg_a) else None,
+                # the reference's sector rule collapses the past map on this route: most calls
+                # see an empty submap, so the rate over the calls with >= 1 candidate stands beside it
+                "calls_ge1_candidate": int((dpg_a[:, 0] >= 1).sum()) if len(dpg_a) else 0,
+                "calls_per_s_ge1_candidate": float(1e3 / dpg_a[dpg_a[:, 0] >= 1, 1].mean())
+                if len(dpg_a) and (dpg_a[:, 0] >= 1).any() else None,
                 "candidates_mean": float(dpg_a[:, 0].mean()) if len(dpg_a) else None,
                 "submap_nodes_mean": float(dpg_a[:, 2].mean()) if len(dpg_a) else None, "by_candidates": buckets},
         "sweeps": sweeps, "active": active_end, "pose_error_vs_gt": err,
@@ -693,16 +714,43 @@ def main():
                "gn_sample": f"oracle batch GN (block-sparse Cholesky, 1 thread) on the full {args.config} graph, "
                             f"{gnb['gn_iterations']} iterations, median of 5 runs ({gnb['s']:.2f} s per solve)",
                "host": cores}
-        # the same ICP sample over edges with OpenMP, at most 16 threads (the box's share)
-        nt = max(1, min(16, cores.get("affinity") or 1))
+        # the same ICP sample over edges with OpenMP on the lease's CPU share: the GPU
+        # box exposes every host CPU in the affinity mask (256) but one GPU's lease is 16 of them
+        # (OMP_NUM_THREADS=16 there; the pool's rules cap worker pools at the share)
+        share = int(os.environ.get("OMP_NUM_THREADS") or 0) or 16
+        nt = max(1, min(share, cores.get("affinity") or 1))
         if nt > 1:
             cm = cpu_baseline(w, params, args.cpu_sample, threads=nt)
             cpu["multithread"] = {"value": cm["icp_edges_per_s"], "unit": "edges/s", "cores": nt,
+                                  "share_rule": f"the GPU lease's CPU share: {nt} threads (OMP_NUM_THREADS on the "
+                                                f"box) of the {cores.get('affinity')} CPUs in the affinity mask",
                                   "sample": f"same sample, OpenMP over edges, median of 5 runs ({cm['icp_s']:.2f} s per run)"}
 
     traffic, traffic_src, sq = pmc_traffic(KERNEL_NAME[args.icp_variant])
     if world > 1:   # the PMC pass measured the whole 1-GPU launch; a rank's launch holds only its shard
         traffic, traffic_src, sq = None, None, {}
+    # the PMC record's provenance, and the kernel against the limiters the counters name: VALU issue
+    # (wave64 VALU = 2 cycles on a SIMD-32, 1024 SIMDs at 2.4 GHz) and the LDS array (one access
+    # cycle per CU per clock, SQ_LDS_IDX_ACTIVE), per launch from the PMC record over this run's
+    # kernel time
+    rec = pmc_record()
+    src_now = kernel_src_sha256()
+    pmc_meta = {"record": traffic_src, "src_sha256": rec.get("src_sha256"), "git_sha": rec.get("git_sha"),
+                "matches_running_kernel": rec.get("src_sha256") == src_now}
+    counts = next((v for k, v in rec.get("counts", {}).items() if k.split("<")[0] == KERNEL_NAME[args.icp_variant]), {})
+    limiters = []
+    if counts and world == 1:
+        t = k_ms * 1e-3
+        if counts.get("SQ_INSTS_VALU"):
+            a = counts["SQ_INSTS_VALU"] / t
+            limiters.append({"bound": "valu_issue", "achieved": a, "peak": 1024 * 2.4e9 / 2, "unit": "wave-instr/s",
+                             "frac": a / (1024 * 2.4e9 / 2)})
+        if counts.get("SQ_LDS_IDX_ACTIVE"):
+            a = counts["SQ_LDS_IDX_ACTIVE"] / t
+            limiters.append({"bound": "lds_array", "achieved": a, "peak": 256 * 2.4e9, "unit": "LDS cycles/s",
+                             "frac": a / (256 * 2.4e9),
+                             "bank_conflict_cycles_per_lds_instr": counts.get("SQ_LDS_BANK_CONFLICT", 0.0) /
+                             max(1.0, counts.get("SQ_INSTS_LDS", 0.0))})
     if rank == 0:
         line = {
             "metric": "ICP edges/sec + ms/GN-iter on 5k-node/20k-edge synthetic graph, 1->8 GPU",
@@ -740,7 +788,8 @@ def main():
                          "bytes_per_launch": algo_bytes,
                          "limiter": "VALU issue + LDS latency with per-iteration workgroup barriers, not HBM: "
                                     "the clouds stay in LDS for all iterations (traffic << algorithmic bytes)",
-                         **({"sq": sq} if sq else {})},
+                         **({"sq": sq} if sq else {}), "pmc": pmc_meta, "kernel_src_sha256": src_now},
+            "roofline_limiters": limiters,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -123,3 +123,38 @@ def test_reoptimize_inc_rebuilds_the_live_graph(ctx, workload):
     s2 = g.add_node(w.cloud(V), p2, w.est[V])
     assert g.V == V + 1 and s2.n_icp_edges >= 1
     g.close()
+
+
+@pytest.mark.gpu
+def test_reoptimize_pass_boundary_patrol_at_size(ctx):
+    """One pass-boundary sweep at size: the patrol workload of config 5 (5000-beam,
+    270-degree, 30 m scans of a serpentine route; bench.py --workload dynamic), 2 x 1300 readings as
+    nodes -- 2600 nodes over two passes, every node's cloud uploaded, the estimates = ground truth
+    perturbed by odometry-scale noise.  Against the oracle's restatement (its ICP over 16 threads):
+    the loop-closure candidate set and the ICP results of every edge bit for bit, the poses < 1e-6."""
+    from dpgslam import _abi, api, synth
+    from oracle import oracle as O
+    w = synth.make_patrol(n_passes=2, steps=1300)
+    V = 2 * w.steps
+    amin, amax, rmax = (float(x) for x in w.geom[0])
+    pts, offs = api.scans_to_clouds(w.ranges, amin, amax, rmax)
+    gtm = w.gt_map().reshape(-1, 3)
+    rng = np.random.default_rng(11)
+    est = (gtm + rng.normal(0.0, [0.05, 0.05, 0.01], gtm.shape)).astype(np.float32)
+    passes = np.repeat(np.arange(2, dtype=np.int32), w.steps)
+    odom = w.odom.reshape(-1, 3)
+    p = _abi.default_icp_params()
+    ctx.upload_scans(pts, offs, p.downsample_icp_points_ratio)
+    cand_g = ctx.loop_closure_candidates(est, passes)
+    cand_o = O.loop_closure_candidates(est, passes)
+    np.testing.assert_array_equal(cand_g, cand_o)
+    assert len(cand_o) > 2 * V   # within-pass neighbours along the route and the second pass's revisits
+    X, st = ctx.reoptimize(passes, est, odom)
+    Xo, edges, res_o, so = O.reoptimize(pts, offs, passes, est, odom, threads=16)
+    assert st.n_icp_edges == len(edges) and st.n_candidates == len(cand_o)
+    res_g, _ = ctx.icp_batch(edges, est, p, compute_cov=False)   # the sweep's batch, fetched whole
+    assert res_g.tobytes() == res_o.tobytes(), "ICP results differ from the oracle's"
+    conv = (res_o["converged"][V - 1:] != 0) & (res_o["status"][V - 1:] == 0)
+    assert st.n_loop_closures == int(conv.sum())
+    err = np.abs(np.concatenate([X[:, :2] - Xo[:, :2], angle_wrap(X[:, 2:] - Xo[:, 2:])], 1)).max()
+    assert err < 1e-6, err

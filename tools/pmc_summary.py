@@ -72,6 +72,12 @@ lines += ["", "SQ fractions (see tools/pmc_summary.py for the definitions):", ""
 lines += [f"* `{k}`: " + ", ".join(f"{a} {b:.3g}" for a, b in fr.items()) for k, fr in fracs.items() if fr]
 open(out_md, "w").write("\n".join(lines) + "\n")
 if out_json:
-    json.dump({"source": os.path.basename(os.path.normpath(d)), "traffic_bytes_per_launch": traffic,
-               "sq_fractions": fracs}, open(out_json, "w"), indent=1)
+    counts = {k: {c: mean(k, c) for (kk, c) in acc if kk == k} for k in kernels}
+    meta = {}
+    for name in ("src.sha256", "git.sha"):   # written by tools/pmc_job.sh beside the passes
+        f = os.path.join(d, name)
+        if os.path.exists(f):
+            meta["src_sha256" if name == "src.sha256" else "git_sha"] = open(f).read().split()[0]
+    json.dump({"source": os.path.basename(os.path.normpath(d)), **meta, "traffic_bytes_per_launch": traffic,
+               "sq_fractions": fracs, "counts": counts}, open(out_json, "w"), indent=1)
 print("\n".join(l for l in lines if l.startswith("* `icp") or l.startswith("* `chol")))
