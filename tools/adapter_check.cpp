@@ -179,7 +179,8 @@ int main() {
         // direct C call on a second graph built the same way; then the graph keeps growing
         std::vector<std::pair<Vector2f, float>> odom;
         for (int k = 0; k < 4; ++k) odom.emplace_back(Vector2f(0.9f * (float)k, 0.0f), 0.03f * (float)k);
-        dpg_adapter::IncGraph g2(ctx.get());
+        dpg_adapter::Context ctx2(0);   // its own scan store
+        dpg_adapter::IncGraph g2(ctx2.get());
         for (int k = 0; k < 4; ++k) {
             float ip[3];
             dpg_adapter::pose_of(nodes[(size_t)k], ip);
