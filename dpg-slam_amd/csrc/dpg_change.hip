@@ -70,6 +70,8 @@ struct DS {                      // device view of the node store + per-call scr
     const int32_t* chain;        // chain node ids
     const int32_t* slot;         // [chain]: bit-plane slot of chain node k (bits 2 slot, 2 slot + 1)
     const int32_t* rast;         // chain indices whose grid is (re)rasterised this call
+    const float4* cframe;        // [2 chain]: frames of the chain nodes at their CHAIN poses (grids)
+    int32_t chain_sep;           // 1: some chain pose differs from that node's estimate
     uint32_t chain_bits;         // planes of the current chain nodes
     uint32_t keep_mask;          // planes kept from the previous call (window reused)
     int32_t rebuild;             // 1: window (re)built, every plane starts empty
@@ -113,6 +115,14 @@ __device__ __forceinline__ bool cell_of(const DS& d, float x, float y, int64_t* 
 __device__ __forceinline__ float2 map_point(const DS& d, int64_t v, int64_t b) {
     const float4 f = d.frame[2 * v];
     const float2 p = d.plaser[b];
+    const float ns = -f.w;
+    const float rx = f.z * p.x + ns * p.y;
+    const float ry = f.w * p.x + f.z * p.y;
+    return make_float2(f.x + rx, f.y + ry);
+}
+
+// the same with the frame given (a chain node's grid pose)
+__device__ __forceinline__ float2 map_point_at(const float4 f, float2 p) {
     const float ns = -f.w;
     const float rx = f.z * p.x + ns * p.y;
     const float ry = f.w * p.x + f.z * p.y;
@@ -206,8 +216,9 @@ __global__ __launch_bounds__(kRB) void raster_kernel(DS d) {
     const uint32_t obit = MODE == 0 ? 1u << (2 * sl + 1) : kSubOcc;
     unsigned long long oob = 0, ns = 0;
     if (live) {
-        const float4 f = d.frame[2 * v];
-        const float2 m = map_point(d, v, b);
+        // a chain node's grid sits at its chain pose (current_pass_nodes_, dpg_slam.cc:591-620)
+        const float4 f = MODE == 0 ? d.cframe[2 * kc] : d.frame[2 * v];
+        const float2 m = MODE == 0 ? map_point_at(f, d.plaser[b]) : map_point(d, v, b);
         int64_t c;
         if (lane == 0 && d.label[b] != DPG_LABEL_MAX_RANGE) {      // occupied end point (:993-997)
             if (cell_of(d, m.x, m.y, &c)) mark_cell<MODE>(d, hset, c, true, k, chain_mask, fbit, obit);
@@ -340,13 +351,14 @@ __global__ __launch_bounds__(kT) void added_kernel(DS d) {
     const int64_t b = b0 + i;
     uint8_t is_added = 0;
     if (included(d, v, b) && d.label[b] != DPG_LABEL_MAX_RANGE) {
-        const float2 m = map_point(d, v, b);
+        // the cell from the chain grid's pose; the bin score from the node's estimate (:786-800)
+        const float2 m = map_point_at(d.cframe[2 * k], d.plaser[b]);
         int64_t c;
         if (cell_of(d, m.x, m.y, &c)) {
             const uint32_t w = d.grid[c];
             if ((w & kSubFree) && !(w & kSubOcc)) {
                 is_added = 1;
-                score_bin(d, k, m);
+                score_bin(d, k, d.chain_sep ? map_point(d, v, b) : m);
             }
         }
     }
@@ -566,7 +578,7 @@ struct dpg_dpg {
     std::vector<float> h_pose;        // [V][3] pose bits the cached frames were computed from (NaN: none)
     float* h_frames = nullptr;        // [V][8] cached node frames, pinned (see upload_frames)
     // pinned staging of the per-call inputs/outputs: one H2D copy of [chain 16 | slot 16 | rast 16 |
-    // candidates], one D2H of the node activity and the commit flags
+    // chain frames 128 | candidates], one D2H of the node activity and the commit flags
     int32_t* h_stage = nullptr;
     int64_t stage_cap = 0;
     uint32_t* h_act = nullptr;
@@ -601,6 +613,8 @@ struct dpg_dpg {
 
 namespace {
 
+constexpr int64_t kStageCand = 48 + 128;   // int32 offset of the candidates in the staging block
+
 DS make_ds(dpg_dpg* d) {
     DS s;
     memset(&s, 0, sizeof(s));
@@ -608,7 +622,8 @@ DS make_ds(dpg_dpg* d) {
     s.sector = d->d_sector.p; s.geom = d->d_geom.p; s.sect = d->d_sect.p; s.active = d->d_active.p;
     s.frame = d->d_frame.p; s.grid = d->d_grid.p; s.first = d->d_first.p; s.chain = d->d_stage.p;
     s.slot = d->d_stage.p ? d->d_stage.p + 16 : nullptr; s.rast = d->d_stage.p ? d->d_stage.p + 32 : nullptr;
-    s.cand = d->d_stage.p ? d->d_stage.p + 48 : nullptr; s.cand_cnt = d->d_cand_cnt.p; s.acc = d->d_acc.p; s.bins = d->d_bins.p;
+    s.cframe = d->d_stage.p ? reinterpret_cast<const float4*>(d->d_stage.p + 48) : nullptr;
+    s.cand = d->d_stage.p ? d->d_stage.p + kStageCand : nullptr; s.cand_cnt = d->d_cand_cnt.p; s.acc = d->d_acc.p; s.bins = d->d_bins.p;
     s.inrange = d->d_inrange.p; s.commit = d->d_commit.p; s.added = d->d_added.p; s.rmask = d->d_rmask.p;
     s.removed_xy = d->d_removed.p; s.ctl = d->d_ctl.p;
     s.res = d->p.occ_grid_resolution; s.inv_res = 1.0 / d->p.occ_grid_resolution; s.max_beams = d->max_beams; s.num_sectors = d->p.num_sectors;
@@ -852,6 +867,11 @@ void dpg_dpg_destroy(dpg_dpg* d) {
 }
 
 int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dpg_change_stats* st) {
+    return dpg_execute_dpg_chain(d, V, cur_len, est, nullptr, st);
+}
+
+int dpg_execute_dpg_chain(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, const float* chain_poses,
+                          dpg_change_stats* st) {
     if (!d || !est || V <= 0 || V > d->V || cur_len < 0 || cur_len > V) return dpg_set_error(DPG_ERR_ARG, "bad arguments");
     const double t0 = now_ms();
     dpg_change_stats local;
@@ -865,12 +885,16 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     st->n_chain = chain_n;
     std::vector<int32_t> chain;
     for (int64_t k = 0; k < chain_n; ++k) chain.push_back((int32_t)(V - chain_n + k));
+    // the pose of chain node k for its grid and the proximity search: the caller's chain pose
+    // (current_pass_nodes_, dpg_slam.cc:591-620,646-668) or the node's estimate
+    auto cpose = [&](int64_t k) { return chain_poses ? chain_poses + 3 * k : est + 3 * (int64_t)chain[(size_t)k]; };
     // candidates: active past nodes within the proximity threshold of a chain node (:646-668)
     std::vector<int32_t> cand;
     for (int64_t j = 0; j < n_past && chain_n > 0; ++j) {
         if (!d->active_h[(size_t)j]) continue;
-        for (int32_t v : chain) {
-            const float dx = est[3 * v] - est[3 * j], dy = est[3 * v + 1] - est[3 * j + 1];
+        for (int64_t k = 0; k < chain_n; ++k) {
+            const float* c = cpose(k);
+            const float dx = c[0] - est[3 * j], dy = c[1] - est[3 * j + 1];
             if (sqrtf(dx * dx + dy * dy) <= p.distance_threshold_for_local_submap_nodes) { cand.push_back((int32_t)j); break; }
         }
     }
@@ -888,15 +912,22 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         return finish_call(d, V, 0, t0, st);
     }
     // window: every chain ray stays within its longest range of the lidar
-    for (int32_t v : chain)
-        if (!std::isfinite(est[3 * v]) || !std::isfinite(est[3 * v + 1]) || !std::isfinite(est[3 * v + 2]))
+    float cfr[15][8];   // chain frames at the chain poses
+    int32_t chain_sep = 0;
+    for (int64_t k = 0; k < chain_n; ++k) {
+        const float* c = cpose(k);
+        const int32_t v = chain[(size_t)k];
+        if (!std::isfinite(c[0]) || !std::isfinite(c[1]) || !std::isfinite(c[2]) ||
+            !std::isfinite(est[3 * v]) || !std::isfinite(est[3 * v + 1]) || !std::isfinite(est[3 * v + 2]))
             return dpg_set_error(DPG_ERR_ARG, "non-finite pose in the pose chain");
-    const float* fr = d->h_frames;
+        node_frame(d, c, cfr[k]);
+        if (memcmp(c, est + 3 * v, 3 * sizeof(float)) != 0) chain_sep = 1;
+    }
     double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
-    for (int32_t v : chain) {
-        const double r = d->rmax_beam[(size_t)v];
-        xlo = std::min(xlo, fr[(size_t)(8 * v)] - r); xhi = std::max(xhi, fr[(size_t)(8 * v)] + r);
-        ylo = std::min(ylo, fr[(size_t)(8 * v + 1)] - r); yhi = std::max(yhi, fr[(size_t)(8 * v + 1)] + r);
+    for (int64_t k = 0; k < chain_n; ++k) {
+        const double r = d->rmax_beam[(size_t)chain[(size_t)k]];
+        xlo = std::min(xlo, cfr[k][0] - r); xhi = std::max(xhi, cfr[k][0] + r);
+        ylo = std::min(ylo, cfr[k][1] - r); yhi = std::max(yhi, cfr[k][1] + r);
     }
     Box need;
     need.x0 = (int32_t)floor(xlo / p.occ_grid_resolution) - 4;
@@ -928,7 +959,7 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
         const int32_t v = d->slot_node[q];
         if (v < 0) continue;
         int64_t k = v - (V - chain_n);
-        if (k >= 0 && k < chain_n && memcmp(d->slot_pose[q], est + 3 * v, 3 * sizeof(float)) == 0) {
+        if (k >= 0 && k < chain_n && memcmp(d->slot_pose[q], cpose(k), 3 * sizeof(float)) == 0) {
             slot[(size_t)k] = q;
             keep |= 3u << (2 * q);
         } else {
@@ -940,7 +971,7 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
             int q = 0;
             while (d->slot_node[q] >= 0) ++q;   // chain_n <= 15 planes: always one free
             d->slot_node[q] = chain[(size_t)k];
-            memcpy(d->slot_pose[q], est + 3 * chain[(size_t)k], 3 * sizeof(float));
+            memcpy(d->slot_pose[q], cpose(k), 3 * sizeof(float));
             slot[(size_t)k] = q;
             rast.push_back((int32_t)k);
         }
@@ -948,11 +979,11 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     }
     const int64_t nc = (int64_t)cand.size();
     const int32_t bin_words = (p.num_bins_for_change_detection + 2 + 31) / 32;
-    if (d->stage_cap < 48 + nc) {
+    if (d->stage_cap < kStageCand + nc) {
         if (d->h_stage) (void)hipHostFree(d->h_stage);
         d->h_stage = nullptr;
         d->stage_cap = 0;
-        const int64_t cap = 48 + std::max<int64_t>(2 * nc, 256);
+        const int64_t cap = kStageCand + std::max<int64_t>(2 * nc, 256);
         if (hipHostMalloc(reinterpret_cast<void**>(&d->h_stage), sizeof(int32_t) * cap, hipHostMallocDefault) != hipSuccess)
             return dpg_set_error(DPG_ERR_HIP, "hipHostMalloc(stage) failed");
         d->stage_cap = cap;
@@ -969,13 +1000,15 @@ int dpg_execute_dpg(dpg_dpg* d, int64_t V, int64_t cur_len, const float* est, dp
     memcpy(hs, chain.data(), sizeof(int32_t) * chain_n);
     memcpy(hs + 16, slot.data(), sizeof(int32_t) * chain_n);
     if (!rast.empty()) memcpy(hs + 32, rast.data(), sizeof(int32_t) * rast.size());
-    if (nc) memcpy(hs + 48, cand.data(), sizeof(int32_t) * nc);
-    DTRY(hipMemcpyAsync(d->d_stage.p, hs, sizeof(int32_t) * (48 + nc), hipMemcpyHostToDevice, s));
+    memcpy(hs + 48, cfr, sizeof(float) * 8 * chain_n);
+    if (nc) memcpy(hs + kStageCand, cand.data(), sizeof(int32_t) * nc);
+    DTRY(hipMemcpyAsync(d->d_stage.p, hs, sizeof(int32_t) * (kStageCand + nc), hipMemcpyHostToDevice, s));
     DS ds = make_ds(d);
     ds.n_chain = (int32_t)chain_n;
     ds.n_cand = (int32_t)nc;
     ds.box = box;
     ds.chain_bits = chain_bits;
+    ds.chain_sep = chain_sep;
     ds.keep_mask = keep;
     ds.rebuild = reuse ? 0 : 1;
     const unsigned gx = (unsigned)((d->max_beams + kT - 1) / kT);

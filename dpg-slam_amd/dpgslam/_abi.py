@@ -281,6 +281,7 @@ SIGNATURES = {
     "dpg_dpg_destroy": (None, [P]),
     "dpg_dpg_append": (C.c_int, [P, C.c_int64, I64P, F32P, F32P]),
     "dpg_execute_dpg": (C.c_int, [P, C.c_int64, C.c_int64, F32P, C.POINTER(ChangeStats)]),
+    "dpg_execute_dpg_chain": (C.c_int, [P, C.c_int64, C.c_int64, F32P, F32P, C.POINTER(ChangeStats)]),
     "dpg_dpg_fetch": (C.c_int, [P, U8P, U8P, U8P]),
     "dpg_dpg_load": (C.c_int, [P, U8P, U8P, U8P]),
     "dpg_active_dynamic_points": (C.c_int64, [P, C.c_int64, F32P, F32P, C.c_int64, I64P]),

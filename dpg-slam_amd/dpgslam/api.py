@@ -422,11 +422,19 @@ class DpgStore:
         self.V += len(off) - 1
         self.B += int(off[-1] - off[0])
 
-    def execute_dpg(self, n_nodes: int, current_pass_len: int, est) -> "_abi.ChangeStats":
+    def execute_dpg(self, n_nodes: int, current_pass_len: int, est, chain_poses=None) -> "_abi.ChangeStats":
+        """executeDPG (dpg_slam.cc:865-886).  chain_poses [chain_n][3]: the poses of the pose chain as the
+        reference's current_pass_nodes_ copies hold them (dpg_slam.cc:195,307,598), placing the chain
+        grids and the proximity search (dpg_execute_dpg_chain); None places them at est."""
         e = _f32(est).reshape(-1, 3)
         st = _abi.ChangeStats()
-        check(lib().dpg_execute_dpg(self.handle, n_nodes, current_pass_len, ptr(e, C.c_float), C.byref(st)),
-              "dpg_execute_dpg")
+        if chain_poses is None:
+            check(lib().dpg_execute_dpg(self.handle, n_nodes, current_pass_len, ptr(e, C.c_float), C.byref(st)),
+                  "dpg_execute_dpg")
+        else:
+            c = _f32(chain_poses).reshape(-1, 3)
+            check(lib().dpg_execute_dpg_chain(self.handle, n_nodes, current_pass_len, ptr(e, C.c_float),
+                                              ptr(c, C.c_float), C.byref(st)), "dpg_execute_dpg_chain")
         return st
 
     def fetch(self):

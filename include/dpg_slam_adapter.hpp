@@ -22,6 +22,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -317,12 +318,35 @@ class DpgStore {
     template <class NodeVec, class PointVec>
     dpg_change_stats executeDPG(NodeVec& nodes, size_t current_pass_len, PointVec& active_static,
                                 PointVec& active_added, PointVec& dynamic_removed, PointVec& dynamic_added) {
+        return run(nodes, current_pass_len, static_cast<const NodeVec*>(nullptr), active_static, active_added,
+                   dynamic_removed, dynamic_added);
+    }
+    /* the reference's placement: the pose chain at the poses of the current_pass_nodes_ copies
+       (dpg_slam.cc:195,307,598), dpg_nodes_ (nodes) everywhere else (dpg_execute_dpg_chain) */
+    template <class NodeVec, class PointVec>
+    dpg_change_stats executeDPG(NodeVec& nodes, const NodeVec& current_pass_nodes, PointVec& active_static,
+                                PointVec& active_added, PointVec& dynamic_removed, PointVec& dynamic_added) {
+        return run(nodes, current_pass_nodes.size(), &current_pass_nodes, active_static, active_added,
+                   dynamic_removed, dynamic_added);
+    }
+  private:
+    template <class NodeVec, class PointVec>
+    dpg_change_stats run(NodeVec& nodes, size_t current_pass_len, const NodeVec* pass_nodes, PointVec& active_static,
+                         PointVec& active_added, PointVec& dynamic_removed, PointVec& dynamic_added) {
         using P = typename PointVec::value_type;
         const size_t V = nodes.size();
         std::vector<float> est(3 * V);
         for (size_t i = 0; i < V; ++i) pose_of(nodes[i], &est[3 * i]);
         dpg_change_stats st;
-        check(dpg_execute_dpg(d_, (int64_t)V, (int64_t)current_pass_len, est.data(), &st), "dpg_execute_dpg");
+        if (pass_nodes) {
+            const size_t n = std::min<size_t>(current_pass_len, (size_t)p_.current_pose_chain_len);
+            std::vector<float> chain(3 * n + 3);
+            for (size_t k = 0; k < n; ++k) pose_of((*pass_nodes)[current_pass_len - n + k], &chain[3 * k]);
+            check(dpg_execute_dpg_chain(d_, (int64_t)V, (int64_t)current_pass_len, est.data(), chain.data(), &st),
+                  "dpg_execute_dpg_chain");
+        } else {
+            check(dpg_execute_dpg(d_, (int64_t)V, (int64_t)current_pass_len, est.data(), &st), "dpg_execute_dpg");
+        }
         std::vector<uint8_t> active(V);
         check(dpg_dpg_fetch(d_, nullptr, nullptr, active.data()), "dpg_dpg_fetch");
         for (size_t i = 0; i < V; ++i)
@@ -341,7 +365,6 @@ class DpgStore {
         }
         return st;
     }
-  private:
     dpg_ctx* ctx_;
     dpg_dpg* d_;
     dpg_change_params p_;

@@ -495,6 +495,15 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* beam_offsets, const
  * the last current_pass_len of them; est_poses[n_nodes][3] the estimated node poses. */
 int dpg_execute_dpg(dpg_dpg* d, int64_t n_nodes, int64_t current_pass_len, const float* est_poses,
                     dpg_change_stats* stats);
+/* The same with the pose chain placed where the reference places it: chain_poses[chain_n][3] are the
+ * poses of the last chain_n = min(current_pass_len, current_pose_chain_len) nodes as the host's
+ * current_pass_nodes_ copies hold them (dpg_slam.cc:195,307,598: by-value copies taken at creation
+ * and never refreshed by optimizeGraph).  They place the chain grids (computeLocalSubMap,
+ * :591-620) and the submap proximity search (:646-668); the bin score (:786-800) and the sector
+ * update (:893-898) keep est_poses, as dpg_nodes_ does.  chain_poses == NULL is dpg_execute_dpg
+ * (every use at est_poses, Q8 fix 8 of DESIGN.md section 3). */
+int dpg_execute_dpg_chain(dpg_dpg* d, int64_t n_nodes, int64_t current_pass_len, const float* est_poses,
+                          const float* chain_poses, dpg_change_stats* stats);
 /* Copy the node state back (any pointer may be NULL): labels[B], sector_active[V] (bit s = sector s
  * active), node_active[V]. */
 int dpg_dpg_fetch(dpg_dpg* d, uint8_t* labels, uint8_t* sector_active, uint8_t* node_active);

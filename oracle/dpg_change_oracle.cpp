@@ -78,20 +78,21 @@ struct oracle_dpg {
     std::vector<Node> nodes;
 
     // transformPoint(laser pose, node pose) (dpg_node.cc:34-36, dpg_slam.cc:971-974)
-    void lidar_in_map(const Node& n, float* lx, float* ly, float* la) const {
+    void lidar_in_map(const Node& n, float* lx, float* ly, float* la) const { lidar_at(n.pose, lx, ly, la); }
+    void lidar_at(const float* pose, float* lx, float* ly, float* la) const {
         float rx, ry;
-        rot2f(n.pose[2], p.laser[0], p.laser[1], &rx, &ry);
-        *lx = n.pose[0] + rx;
-        *ly = n.pose[1] + ry;
-        *la = angle_mod_f(n.pose[2] + p.laser[2]);
+        rot2f(pose[2], p.laser[0], p.laser[1], &rx, &ry);
+        *lx = pose[0] + rx;
+        *ly = pose[1] + ry;
+        *la = angle_mod_f(pose[2] + p.laser[2]);
     }
     // MeasurementPoint::getPointInLaserFrame (dpg_measurement.h:102-104) then transformPoint into
     // the map with the lidar pose (dpg_slam.cc:844,979; Q8 fix: once, not twice as :985-986 does)
-    void map_point(const Node& n, int64_t i, float* mx, float* my) const {
+    void map_point(const Node& n, int64_t i, float* mx, float* my, const float* pose = nullptr) const {
         const Beam& b = n.beams[(size_t)i];
         float px = b.range * cosf(b.angle), py = b.range * sinf(b.angle);
         float lx, ly, la, rx, ry;
-        lidar_in_map(n, &lx, &ly, &la);
+        lidar_at(pose ? pose : n.pose, &lx, &ly, &la);
         rot2f(la, px, py, &rx, &ry);
         *mx = lx + rx;
         *my = ly + ry;
@@ -100,20 +101,22 @@ struct oracle_dpg {
     Key key_of(float x, float y) const {
         return Key((int)round((double)x / p.occ_grid_resolution), (int)round((double)y / p.occ_grid_resolution));
     }
-    // occupancyGrid(node) -> calculateOccupancyGrid -> convertLaserRangeToCellKey (dpg_slam.cc:913-1013)
-    Grid node_grid(int64_t v) const {
+    // occupancyGrid(node) -> calculateOccupancyGrid -> convertLaserRangeToCellKey (dpg_slam.cc:913-1013);
+    // pose: the node copy's pose when it differs from dpg_nodes_ (a current_pass_nodes_ entry)
+    Grid node_grid(int64_t v, const float* pose = nullptr) const {
         Grid g;
         const Node& n = nodes[(size_t)v];
         if (!n.active) return g;
+        if (!pose) pose = n.pose;
         float lx, ly, la;
-        lidar_in_map(n, &lx, &ly, &la);
+        lidar_at(pose, &lx, &ly, &la);
         std::vector<Key> occ, fre;
         for (int64_t i = 0; i < (int64_t)n.beams.size(); ++i) {
             const Beam& b = n.beams[(size_t)i];
             if (!n.sector_active[b.sector]) continue;
             // :983-984 with include_static/include_added true; Q8 fix: NOT_YET_LABELED counts as STATIC
             float mx, my;
-            map_point(n, i, &mx, &my);
+            map_point(n, i, &mx, &my, pose);
             Key cell = key_of(mx, my);
             if (b.label != DPG_LABEL_MAX_RANGE) {
                 g.pts[cell].push_back(Pt{v, i});
@@ -156,11 +159,11 @@ struct oracle_dpg {
         return it == g.info.end() ? UNKNOWN : it->second;
     }
 
-    int execute(int64_t V, int64_t cur_len, const float* est, dpg_change_stats* st);
+    int execute(int64_t V, int64_t cur_len, const float* est, const float* chain_poses, dpg_change_stats* st);
     int64_t active_dynamic(int64_t V, const float* est, float* out, int64_t cap, int64_t counts[4]);
 };
 
-int oracle_dpg::execute(int64_t V, int64_t cur_len, const float* est, dpg_change_stats* st) {
+int oracle_dpg::execute(int64_t V, int64_t cur_len, const float* est, const float* chain_poses, dpg_change_stats* st) {
     memset(st, 0, sizeof(*st));
     if (V > (int64_t)nodes.size() || cur_len > V || cur_len < 0) return DPG_ERR_ARG;
     for (int64_t v = 0; v < V; ++v)
@@ -173,8 +176,11 @@ int oracle_dpg::execute(int64_t V, int64_t cur_len, const float* est, dpg_change
     const int64_t chain_n = std::min<int64_t>(cur_len, p.current_pose_chain_len);
     std::vector<int64_t> chain;
     for (int64_t k = 0; k < chain_n; ++k) chain.push_back(V - chain_n + k);
+    // poseChain = current_pass_nodes_ copies (:598): their poses place the chain grids and the
+    // proximity search; without chain_poses they are the estimates (Q8 fix 8)
+    auto cpose = [&](size_t k) { return chain_poses ? chain_poses + 3 * k : nodes[(size_t)chain[k]].pose; };
     std::vector<Grid> chain_grids;
-    for (int64_t v : chain) chain_grids.push_back(node_grid(v));
+    for (size_t k = 0; k < chain.size(); ++k) chain_grids.push_back(node_grid(chain[k], cpose(k)));
     st->n_chain = chain_n;
 
     // getSubMapCoveringCurrPoseChain (:622-701)
@@ -189,9 +195,9 @@ int oracle_dpg::execute(int64_t V, int64_t cur_len, const float* est, dpg_change
         const Node& past = nodes[(size_t)j];
         if (!past.active) continue;
         bool prox = false;
-        for (int64_t v : chain) {
-            const Node& c = nodes[(size_t)v];
-            float dx = c.pose[0] - past.pose[0], dy = c.pose[1] - past.pose[1];
+        for (size_t k = 0; k < chain.size(); ++k) {
+            const float* c = cpose(k);
+            float dx = c[0] - past.pose[0], dy = c[1] - past.pose[1];
             if (sqrtf(dx * dx + dy * dy) <= p.distance_threshold_for_local_submap_nodes) { prox = true; break; }
         }
         if (!prox) continue;
@@ -382,7 +388,12 @@ int oracle_dpg_append(oracle_dpg* o, int64_t n, const int64_t* off, const float*
 }
 
 int oracle_execute_dpg(oracle_dpg* o, int64_t V, int64_t cur_len, const float* est, dpg_change_stats* st) {
-    return o->execute(V, cur_len, est, st);
+    return o->execute(V, cur_len, est, nullptr, st);
+}
+
+int oracle_execute_dpg_chain(oracle_dpg* o, int64_t V, int64_t cur_len, const float* est, const float* chain_poses,
+                             dpg_change_stats* st) {
+    return o->execute(V, cur_len, est, chain_poses, st);
 }
 
 void oracle_dpg_fetch(oracle_dpg* o, uint8_t* labels, uint8_t* sector_active, uint8_t* node_active) {

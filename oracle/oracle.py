@@ -58,6 +58,7 @@ def lib():
             "oracle_dpg_destroy": (None, [P]),
             "oracle_dpg_append": (C.c_int, [P, C.c_int64, I64P, F32P, F32P]),
             "oracle_execute_dpg": (C.c_int, [P, C.c_int64, C.c_int64, F32P, C.POINTER(_abi.ChangeStats)]),
+            "oracle_execute_dpg_chain": (C.c_int, [P, C.c_int64, C.c_int64, F32P, F32P, C.POINTER(_abi.ChangeStats)]),
             "oracle_dpg_fetch": (None, [P, _abi.U8P, _abi.U8P, _abi.U8P]),
             "oracle_dpg_load": (None, [P, _abi.U8P, _abi.U8P, _abi.U8P]),
             "oracle_active_dynamic_points": (C.c_int64, [P, C.c_int64, F32P, F32P, C.c_int64, I64P]),
@@ -333,11 +334,17 @@ class OracleDpgStore:
             lib().oracle_dpg_destroy(self.handle)
             self.handle = None
 
-    def execute_dpg(self, n_nodes, current_pass_len, est):
+    def execute_dpg(self, n_nodes, current_pass_len, est, chain_poses=None):
+        """chain_poses [chain_n][3]: the current_pass_nodes_ copies' poses (dpg_slam.cc:598), or None."""
         from dpgslam import _abi
         e = _f32(est).reshape(-1, 3)
         st = _abi.ChangeStats()
-        rc = lib().oracle_execute_dpg(self.handle, n_nodes, current_pass_len, _p(e, C.c_float), C.byref(st))
+        if chain_poses is None:
+            rc = lib().oracle_execute_dpg(self.handle, n_nodes, current_pass_len, _p(e, C.c_float), C.byref(st))
+        else:
+            c = _f32(chain_poses).reshape(-1, 3)
+            rc = lib().oracle_execute_dpg_chain(self.handle, n_nodes, current_pass_len, _p(e, C.c_float),
+                                                _p(c, C.c_float), C.byref(st))
         assert rc == 0, rc
         return st
 

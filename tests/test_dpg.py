@@ -312,3 +312,83 @@ def test_gpu_append_matches_oracle():
     got = _append_sequence(lambda r, g: api.DpgStore(ctx, r, g), w)
     ref = _append_sequence(lambda r, g: O.OracleDpgStore(r, g), w)
     assert got == ref
+
+
+# ------------------------------------------- reference placement of the pose chain (chain poses)
+def _creation_poses(w, seed=3):
+    """Stand-in for the reference's current_pass_nodes_ copies (dpg_slam.cc:195,307,598): the pose
+    each node had when it was created (odometry-propagated), which optimizeGraph never refreshes --
+    here the estimate plus a seeded drift that grows along the pass."""
+    rng = np.random.default_rng(seed)
+    c = w.est.astype(np.float64).copy()
+    for p in range(len(w.pass_start) - 1):
+        a, b = int(w.pass_start[p]), int(w.pass_start[p + 1])
+        step = rng.normal(0.0, [0.01, 0.01, 0.002], size=(b - a, 3))
+        c[a:b] += np.cumsum(step, axis=0)
+    return c.astype(np.float32)
+
+
+def _chain_of(w, creation, v, cur, chain_len=5):
+    n = min(cur, chain_len)
+    return creation[v + 1 - n:v + 1]
+
+
+def test_oracle_chain_poses_at_estimates_equal_plain():
+    w = _dynamic()
+    a = O.OracleDpgStore(w.ranges, w.geom)
+    b = O.OracleDpgStore(w.ranges, w.geom)
+    for v in range(20, 60):
+        p = w.pass_of[v]
+        cur = int(v - w.pass_start[p] + 1)
+        sa = a.execute_dpg(v + 1, cur, w.est[:v + 1])
+        sb = b.execute_dpg(v + 1, cur, w.est[:v + 1], chain_poses=_chain_of(w, w.est, v, cur))
+        assert sa.counters() == sb.counters(), v
+    _same_state(a, b)
+
+
+def test_oracle_chain_poses_drifted():
+    """Chain grids at drifted creation poses against a submap at the estimates: the misalignment
+    itself reads as change (DESIGN.md section 3, Q8 fix 8) -- more points labelled than with the
+    chain at the estimates; the invariants hold either way."""
+    w = _dynamic()
+    cr = _creation_poses(w)
+    a = O.OracleDpgStore(w.ranges, w.geom)
+    b = O.OracleDpgStore(w.ranges, w.geom)
+    ra = rb = 0
+    for v in range(20, 60):
+        p = w.pass_of[v]
+        cur = int(v - w.pass_start[p] + 1)
+        sa = a.execute_dpg(v + 1, cur, w.est[:v + 1])
+        sb = b.execute_dpg(v + 1, cur, w.est[:v + 1], chain_poses=_chain_of(w, cr, v, cur))
+        assert 0 <= sb.n_uncovered <= sb.n_chain_cells and sb.n_submap_nodes <= sb.n_candidates
+        ra += sa.n_removed + sa.n_added
+        rb += sb.n_removed + sb.n_added
+    assert rb > ra
+
+
+@pytest.mark.gpu
+def test_gpu_chain_poses_parity():
+    """dpg_execute_dpg_chain against the oracle bit for bit with drifted chain poses (every counter
+    and the state after every call, the map lists at the end); with the chain at the estimates it
+    equals dpg_execute_dpg."""
+    w = _dynamic()
+    cr = _creation_poses(w)
+    o = O.OracleDpgStore(w.ranges, w.geom)
+    ctx, g = _gpu_store(w.ranges, w.geom)
+    g2 = __import__("dpgslam.api", fromlist=["api"]).DpgStore(ctx, w.ranges, w.geom)
+    g3 = __import__("dpgslam.api", fromlist=["api"]).DpgStore(ctx, w.ranges, w.geom)
+    for v in range(int(w.pass_start[1]), w.V):
+        p = w.pass_of[v]
+        cur = int(v - w.pass_start[p] + 1)
+        ch = _chain_of(w, cr, v, cur)
+        so = o.execute_dpg(v + 1, cur, w.est[:v + 1], chain_poses=ch)
+        sg = g.execute_dpg(v + 1, cur, w.est[:v + 1], chain_poses=ch)
+        assert sg.counters() == so.counters(), (v, sg.counters(), so.counters())
+        _same_state(g, o)
+        s2 = g2.execute_dpg(v + 1, cur, w.est[:v + 1])
+        s3 = g3.execute_dpg(v + 1, cur, w.est[:v + 1], chain_poses=_chain_of(w, w.est, v, cur))
+        assert s2.counters() == s3.counters(), v
+    _same_state(g2, g3)
+    mo, mg = o.active_dynamic_points(w.V, w.est), g.active_dynamic_points(w.V, w.est)
+    for k in mo:
+        assert np.array_equal(mo[k], mg[k]), k

@@ -238,6 +238,23 @@ int main() {
         printf("executeDPG: %lld candidates, %lld removed, lists %zu %zu %zu %zu\n", (long long)st.n_candidates,
                (long long)st.n_removed, s0.size(), s1.size(), s2.size(), s3.size());
     }
+    // the reference's placement (current_pass_nodes_ copies): copies equal to the estimates give
+    // the same call as the plain form
+    {
+        dpg_adapter::DpgStore store(ctx.get());
+        std::vector<Node> nd(2);
+        auto r0 = room_scan(5.0, 3.0, 0.0, 360);
+        auto r1 = r0;
+        for (int b = 0; b < 72; ++b) r1[(size_t)b] += 2.0f;
+        store.add_scan(r0, (float)-M_PI, (float)M_PI, 30.f);
+        store.add_scan(r1, (float)-M_PI, (float)M_PI, 30.f);
+        const std::vector<Node> pass(nd.begin() + 1, nd.end());
+        std::vector<Vector2f> s0, s1, s2, s3;
+        const dpg_change_stats st = store.executeDPG(nd, pass, s0, s1, s2, s3);
+        EXPECT(st.n_chain == 1 && st.n_candidates == 1);
+        printf("executeDPG (current_pass_nodes_ placement): %lld candidates, %lld removed\n",
+               (long long)st.n_candidates, (long long)st.n_removed);
+    }
     printf(fails ? "adapter check FAILED (%d)\n" : "adapter check ok\n", fails);
     return fails ? 1 : 0;
 }
