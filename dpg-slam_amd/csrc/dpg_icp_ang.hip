@@ -98,6 +98,18 @@ __device__ __forceinline__ int bucket_of(float pa) {
     int b = (int)floorf(pa * kBucketScale);
     return min(max(b, 0), kB - 1);
 }
+// the same bucket with the floor and the conversion in one instruction (v_cvt_flr_i32_f32 is
+// (int)floorf for the finite pa * scale)
+__device__ __forceinline__ int bucket_of_flr(float pa) {
+    int b;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(b) : "v"(pa * kBucketScale));
+    return min(max(b, 0), kB - 1);
+}
+template <int VAR>
+__device__ __forceinline__ int bucket_q(float pa) {
+    if constexpr (VAR >= 2) return bucket_of_flr(pa);
+    else return bucket_of(pa);
+}
 
 __device__ __forceinline__ uint32_t orderable(float f) {
     const uint32_t b = __float_as_uint(f);
@@ -392,7 +404,16 @@ __device__ __forceinline__ int advance(int s, int step, int n) {
 // The sorted positions of the points that can lie within `rad` of q (angle window), as ONE
 // wrapped range: start in [0, n), `count` positions (the whole cloud when the window would span
 // too wide an angle).
+template <int VAR = 1>
+__device__ __forceinline__ int window_pa(const uint16_t* bk, int n, float qx, float qy, float pq, float rad, int& start);
+template <int VAR = 1>
 __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int& start) {
+    return window_pa<VAR>(bk, n, qx, qy, pseudo_angle(qx, qy), rad, start);
+}
+// the same with q's pseudo-angle pq already computed (the forward search computes it once for the
+// unseeded probe and the window)
+template <int VAR>
+__device__ __forceinline__ int window_pa(const uint16_t* bk, int n, float qx, float qy, float pq, float rad, int& start) {
     const float sn = rad * __builtin_amdgcn_rsqf(qx * qx + qy * qy) * 1.0001f + 1e-6f;   // sin of the half-angle
     if (!(sn < 0.7f)) {
         start = 0;
@@ -402,12 +423,11 @@ __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float
     // 1/sqrt(0.51) = 1.40028 at the end), so the half-angle bound needs no reciprocal square root
     // (the window only widens: a superset, exact as above)
     const float half = kPaSlope * sn * fmaf(sn * sn, 0.8172f, 1.0f) * 1.0001f + kPaMargin;
-    const float pq = pseudo_angle(qx, qy);
     float lo = pq - half, hi = pq + half;
     if (lo < 0.0f) lo += kTwoPi;
     if (hi >= kTwoPi) hi -= kTwoPi;
-    int s = bk[bucket_of(lo)];
-    const int end = bk[bucket_of(hi) + 1];
+    int s = bk[bucket_q<VAR>(lo)];
+    const int end = bk[bucket_q<VAR>(hi) + 1];
     const int cnt = lo <= hi ? end - s : (n - s) + end;   // else: straddles pseudo-angle 0
     start = s >= n ? s - n : s;
     return cnt;
@@ -448,14 +468,14 @@ __device__ __forceinline__ double rdlane(double x, int l) {
 // target at q's own bearing first).  Returns the initial best key and sets the radius.  Used by
 // the owner lane and by the cooperative scan with identical arithmetic.
 template <int VAR>
-__device__ __forceinline__ uint64_t forward_init(const Lds& L, int M, int sd, float qx, float qy, float r2f, float rmax,
+__device__ __forceinline__ uint64_t forward_init(const Lds& L, int M, int sd, float qx, float qy, float pq, float r2f, float rmax,
                                                  float rext, float r2ext, float& rad) {
     uint64_t best = dkey(r2f, 0xffffffffu);   // "none": every candidate with d <= r beats it
     rad = rmax;
     if (sd == -1) {
         rad = rext;
         best = dkey(r2ext, 0xffffffffu);
-        int p0 = L.tb[bucket_of(pseudo_angle(qx, qy))];
+        int p0 = L.tb[bucket_q<VAR>(VAR >= 2 ? pq : pseudo_angle(qx, qy))];
         p0 = p0 >= M ? 0 : p0;
         if (M > 0) {
             const Rec r = L.tp[p0];
@@ -496,6 +516,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                                                      dpg_icp_kparams kp, dpg_icp_result* __restrict__ results,
                                                      int32_t* __restrict__ trace, Rec* __restrict__ gscr) {
     constexpr bool kTpL = MODE != 2, kScsL = MODE == 0;   // records in LDS?
+    // issue priority for the synchronised phases (variant 1): 2 from the search barrier to the
+    // next search, 3 for the fit -- the other seven waves of the workgroup wait on them, while the
+    // searches of the CU's other workgroups fill the SIMDs (config 4: kernel -1.5 %, A/B in one
+    // process, profiles/r03/v6_icp_variant_ab.txt)
+    constexpr bool kPrio = VAR >= 1;
     // queue slots: PPT <= 4 packs them into okq / qhi (7 bits each), wider forms keep a byte per point
     constexpr bool kWideQ = PPT >= 8;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -602,6 +627,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     };
     for (;;) {
         ICP_STAMP(c0);
+        if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
         const float i00 = uni((float)L.bc->inv[0]), i01 = uni((float)L.bc->inv[1]);
         const float i10 = uni((float)L.bc->inv[2]), i11 = uni((float)L.bc->inv[3]);
         const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
@@ -636,11 +662,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             // ---- forward 1-NN (target index), seeded radius ----
             const bool search = live && sd >= -1;   // < -1: clearance, provably no target within r
             float rad;
-            uint64_t best = forward_init<VAR>(L, M, search ? sd : 0, qx, qy, r2f, rmax, rext, r2ext, rad);
+            const float pq = VAR >= 2 ? pseudo_angle(qx, qy) : 0.f;   // once for the probe and the window
+            uint64_t best = forward_init<VAR>(L, M, search ? sd : 0, qx, qy, pq, r2f, rmax, rext, r2ext, rad);
             bool pend;   // this point's forward window went to the queue
             {
                 int s = 0;
-                int fc = search ? window(L.tb, M, qx, qy, rad, s) : 0;
+                int fc = search ? (VAR >= 2 ? window_pa<VAR>(L.tb, M, qx, qy, pq, rad, s) : window(L.tb, M, qx, qy, rad, s)) : 0;
                 const int slot = queue_push(fc > dcap, &L.bc->qtail);
                 pend = slot >= 0;
                 if (pend) {
@@ -670,7 +697,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     }
                     s = advance(s, stepM, M);
                 };
-                for (int c = 0; __any(c < fc); c += kU) ftrip();   // exact (d, original index) argmin
+                if constexpr (VAR >= 2) {   // exact (d, original index) argmin
+                    if (__any(0 < fc)) {
+                        int c = 0;
+                        do { ftrip(); c += kU; } while (__any(c < fc));
+                    }
+                } else {
+                    for (int c = 0; __any(c < fc); c += kU) ftrip();
+                }
 
             }
             int bp = -1;
@@ -687,7 +721,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                     // t_j in the source node frame; float error ~1e-6 m, far inside the window margin
                     const float ux = tj.x - ftx, uy = tj.y - fty;
                     const float px = i00 * ux + i01 * uy, py = i10 * ux + i11 * uy;
-                    rc = window(L.sb, N, px, py, bsqrt<VAR>(bd) * 1.0001f + drift, s);
+                    rc = window<VAR>(L.sb, N, px, py, bsqrt<VAR>(bd) * 1.0001f + drift, s);
                 }
                 const int slot = queue_push(ok && rc > dcap, &L.bc->qtail);
                 if (slot >= 0) {
@@ -749,6 +783,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         ICP_STAMP(c1);
         // ---- the cooperative queue: windows too wide for one lane, 64 candidates per trip ----
         __syncthreads();
+        if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);
         const int nq = min((int)uni((uint32_t)L.bc->qtail), kQCap);
         if (nq > 0) {   // nq is the same in every wave (read after the barrier)
             const int w0q = __builtin_amdgcn_readfirstlane(wave);
@@ -762,7 +797,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 uint64_t best = 0;
                 if ((w1 & 1u) == 0u) {   // forward argmin over the window, then the reciprocal test
                     float rad;
-                    const uint64_t b0 = forward_init<VAR>(L, M, (int)(w1 >> 1) - 1, qx, qy, r2f, rmax, rext, r2ext, rad);
+                    const uint64_t b0 = forward_init<VAR>(L, M, (int)(w1 >> 1) - 1, qx, qy, pseudo_angle(qx, qy), r2f, rmax, rext, r2ext, rad);
                     const int fc = window(L.tb, M, qx, qy, rad, s);
                     best = lane == 0 ? b0 : ~0ull;
                     for (int c = lane; c < fc; c += 64) {
@@ -859,6 +894,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         if (__builtin_amdgcn_readlane(last, 0)) {
+            if constexpr (kPrio) __builtin_amdgcn_s_setprio(3);
             double S[kSums];
             if constexpr (VAR >= 1) {   // lane q combines sum q (the same fixed tree), then broadcast
                 const double sq = lane < kSums ? dpg_tree::combine(L.wpart, kSums + 2, lane) : 0.0;
@@ -966,6 +1002,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 st_wmax = 0;
 #endif
             }
+            if constexpr (kPrio) __builtin_amdgcn_s_setprio(2);
         }
         __syncthreads();
         ICP_STAMP(c4);
@@ -1109,19 +1146,20 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     if (chunk <= 0) return DPG_ERR_SIZE;
     Rec* g = reinterpret_cast<Rec*>(scratch);
     const char* ve = getenv("DPG_ICP_VARIANT");   // A/B of kernel variants (tools/icp_var_ab.py)
-    const int var = ve ? atoi(ve) : 1;
+    const int var = ve ? atoi(ve) : 2;
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
 // variant 1 (default): hardware square roots in the window bounds, the candidate distance
 // computed into the record's pad register, reciprocal beats as ballots, the fit's divisions as
-// lane-parallel vector divisions; variant 0: round 2's form of the same arithmetic (A/B reference,
-// DPG_ICP_VARIANT=0).  Both give byte-identical results.
-#define DPG_ANG_LAUNCH(P, M)                                                                                     \
-        if (var == 0) hipLaunchKernelGGL((icp_ang_kernel<P, M, 0>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
-                           results_dev, trace_dev, g);                                                               \
-        else hipLaunchKernelGGL((icp_ang_kernel<P, M, 1>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
+// lane-parallel vector divisions, issue priority for the synchronised phases; variant 0: round
+// 2's form of the same arithmetic (A/B reference, DPG_ICP_VARIANT=0).  Both give byte-identical results.
+#define DPG_ANG_K(P, M, V) hipLaunchKernelGGL((icp_ang_kernel<P, M, V>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
+#define DPG_ANG_LAUNCH(P, M)                                                                                     \
+        if (var == 0) DPG_ANG_K(P, M, 0);                                                                       \
+        else if (var == 1) DPG_ANG_K(P, M, 1);                                                                  \
+        else DPG_ANG_K(P, M, 2)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
             else if (ppt <= 2) DPG_ANG_LAUNCH(2, 0);
@@ -1135,5 +1173,6 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
         if (hipGetLastError() != hipSuccess) return DPG_ERR_HIP;
     }
 #undef DPG_ANG_LAUNCH
+#undef DPG_ANG_K
     return DPG_OK;
 }
