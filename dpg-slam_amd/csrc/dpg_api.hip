@@ -469,6 +469,36 @@ static int scans_append_1(dpg_ctx* c, const float* pts, const int64_t* off, int6
     return DPG_OK;
 }
 
+// The scan store as host copies (the graph checkpoint, dpg_inc_save): node count, downsample
+// ratio, and -- when the arrays are given -- the node offsets [n + 1] and the full clouds [off[n]][2]
+int dpg_scans_export(dpg_ctx* c, int64_t* n_nodes, int32_t* ratio, int64_t* off, float* pts) {
+    if (!c || !n_nodes || !ratio) return fail(DPG_ERR_ARG, "dpg_scans_export: bad arguments");
+    *n_nodes = c->n_nodes;
+    *ratio = c->ratio;
+    if (c->n_nodes <= 0) return DPG_OK;
+    if (off) std::copy(c->full_off.begin(), c->full_off.begin() + c->n_nodes + 1, off);
+    if (pts) {
+        HIP_TRY(hipSetDevice(c->device));
+        const size_t total = (size_t)c->full_off[(size_t)c->n_nodes];
+        if (total) HIP_TRY(hipMemcpyAsync(pts, c->full.p, sizeof(float) * 2 * total, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    return DPG_OK;
+}
+
+// The neighbour index of every stored node (the incremental path builds it node by node as nodes
+// arrive; a store restored from a checkpoint needs all of it before its next dpg_add_node)
+int dpg_scans_index_all(dpg_ctx* c) {
+    if (!c) return fail(DPG_ERR_ARG, "dpg_scans_index_all: ctx is NULL");
+    if (c->n_nodes <= 0 || c->icp_variant != DPG_ICP_ANGULAR) return DPG_OK;   // the other variants index per batch
+    HIP_TRY(hipSetDevice(c->device));
+    const int rc = dpg_launch_angle_index(c->ds.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
+                                          c->buckets.p, c->stream);
+    if (rc) return fail(rc, "angle index build failed");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
 // the scan store back to its first V nodes (dpg_add_node_pairs' rollback); the device arrays keep
 // their capacity, the entries past V are overwritten by the next append
 static void scans_truncate(dpg_ctx* c, int64_t V) {

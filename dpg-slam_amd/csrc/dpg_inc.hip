@@ -28,6 +28,7 @@
 //     its information scaled by u + 1.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
 #include <time.h>
 
@@ -571,6 +572,181 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     S.ms_numeric = t3 - t2;
     if (st) *st = S;
     return DPG_OK;
+}
+
+// ---- graph checkpoint (the reference's state -- dpg_nodes_ and their scans,
+// graph_, isam_ (dpg_slam.h:362,367,372) -- lives only in memory) ----
+// File layout (host byte order, every field fixed-width):
+//   CkptHeader; dpg_factor F[n_factors]; int32 f_created[n_factors]; int32 plo[n_pairs], phi[n_pairs];
+//   double theta[3 V], est[3 V], maxd[V]; int64 scan_off[n_scans + 1]; float scan_pts[scan_off[n_scans]][2]
+// The pairs keep their arrival order (a non-converged loop closure's pair stays an explicit zero
+// block); the scans are the full base_link clouds of the context's store.
+struct CkptHeader {
+    char magic[8];                   // "DPGGRAPH"
+    uint32_t version, sizeof_factor, sizeof_params, pad;
+    dpg_inc_params params;
+    int64_t V, updates, n_factors, n_pairs, n_scans;
+    int32_t ratio, pad2;
+};
+constexpr uint32_t kCkptVersion = 1;
+
+int dpg_inc_save(dpg_inc* q, const char* path) {
+    if (!q || !path) return set_err(DPG_ERR_ARG, "dpg_inc_save: bad arguments");
+    if (q->prepared) return set_err(DPG_ERR_STATE, "dpg_inc_save: an update is prepared but not applied");
+    CkptHeader h;
+    memset(&h, 0, sizeof(h));
+    memcpy(h.magic, "DPGGRAPH", 8);
+    h.version = kCkptVersion;
+    h.sizeof_factor = (uint32_t)sizeof(dpg_factor);
+    h.sizeof_params = (uint32_t)sizeof(dpg_inc_params);
+    h.params = q->P;
+    h.V = q->V;
+    h.updates = q->updates;
+    h.n_factors = (int64_t)q->F.size();
+    h.n_pairs = (int64_t)q->plo.size();
+    int rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, nullptr, nullptr);
+    if (rc) return rc;
+    if (h.n_scans != 0 && h.n_scans < h.V)
+        return set_err(DPG_ERR_STATE, "dpg_inc_save: the scan store holds fewer nodes than the graph");
+    const size_t V = (size_t)h.V;
+    std::vector<double> theta(3 * V), est(3 * V), maxd(V);
+    hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
+    if (hipSetDevice(dpg_ctx_device_of(q->ctx)) != hipSuccess) return set_err(DPG_ERR_HIP, "hipSetDevice failed");
+    if (V && (hipMemcpyAsync(theta.data(), q->theta, sizeof(double) * 3 * V, hipMemcpyDeviceToHost, s) != hipSuccess ||
+              hipMemcpyAsync(est.data(), q->est, sizeof(double) * 3 * V, hipMemcpyDeviceToHost, s) != hipSuccess ||
+              hipMemcpyAsync(maxd.data(), q->maxd, sizeof(double) * V, hipMemcpyDeviceToHost, s) != hipSuccess))
+        return set_err(DPG_ERR_HIP, "dpg_inc_save: read-back failed");
+    if (hipStreamSynchronize(s) != hipSuccess) return set_err(DPG_ERR_HIP, "dpg_inc_save: read-back failed");
+    std::vector<int64_t> off((size_t)h.n_scans + 1, 0);
+    if ((rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, off.data(), nullptr))) return rc;
+    std::vector<float> pts((size_t)(2 * std::max<int64_t>(off[(size_t)h.n_scans], 1)));
+    if ((rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, off.data(), pts.data()))) return rc;
+    FILE* f = fopen(path, "wb");
+    if (!f) return set_err(DPG_ERR_ARG, "dpg_inc_save: cannot open the file for writing");
+    bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+    auto put = [&](const void* p, size_t bytes) { if (ok && bytes) ok = fwrite(p, 1, bytes, f) == bytes; };
+    put(q->F.data(), sizeof(dpg_factor) * q->F.size());
+    put(q->f_created.data(), sizeof(int32_t) * q->f_created.size());
+    put(q->plo.data(), sizeof(int32_t) * q->plo.size());
+    put(q->phi.data(), sizeof(int32_t) * q->phi.size());
+    put(theta.data(), sizeof(double) * theta.size());
+    put(est.data(), sizeof(double) * est.size());
+    put(maxd.data(), sizeof(double) * maxd.size());
+    put(off.data(), sizeof(int64_t) * off.size());
+    put(pts.data(), sizeof(float) * 2 * (size_t)off[(size_t)h.n_scans]);
+    ok = (fclose(f) == 0) && ok;
+    return ok ? DPG_OK : set_err(DPG_ERR_HIP, "dpg_inc_save: write failed");
+}
+
+// A graph restored from dpg_inc_save on ctx (single device): the scan store is replaced by the
+// file's (and indexed), the factors, pairs, linearization points, estimate, per-variable |delta| and
+// update count are the saved ones, so the next dpg_add_node / dpg_inc_update continues the saved
+// run (ISAM2's relinearization schedule included).  The elimination order is computed afresh from
+// the saved pattern (what the saved graph does every reorder_every nodes), so later estimates agree
+// with an uninterrupted run to rounding.  NULL on error (dpg_last_error).
+dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path) {
+    if (!path) {
+        set_err(DPG_ERR_ARG, "dpg_inc_load: bad arguments");
+        return nullptr;
+    }
+    FILE* f = fopen(path, "rb");
+    if (!f) {
+        set_err(DPG_ERR_ARG, "dpg_inc_load: cannot open the file");
+        return nullptr;
+    }
+    CkptHeader h;
+    bool ok = fread(&h, sizeof(h), 1, f) == 1;
+    if (!ok || memcmp(h.magic, "DPGGRAPH", 8) != 0 || h.version != kCkptVersion || h.sizeof_factor != sizeof(dpg_factor) ||
+        h.sizeof_params != sizeof(dpg_inc_params) || h.V < 0 || h.n_factors < 0 || h.n_pairs < 0 || h.n_scans < 0 ||
+        (h.n_scans != 0 && h.n_scans < h.V) ||
+        h.V > ((int64_t)1 << 31) || h.n_factors > ((int64_t)1 << 31) || h.n_pairs > ((int64_t)1 << 31) ||
+        h.n_scans > ((int64_t)1 << 31)) {
+        fclose(f);
+        set_err(DPG_ERR_ARG, "dpg_inc_load: not a graph checkpoint of this version");
+        return nullptr;
+    }
+    const size_t V = (size_t)h.V;
+    std::vector<dpg_factor> F((size_t)h.n_factors);
+    std::vector<int32_t> created((size_t)h.n_factors), plo((size_t)h.n_pairs), phi((size_t)h.n_pairs);
+    std::vector<double> theta(3 * V), est(3 * V), maxd(V);
+    std::vector<int64_t> off((size_t)h.n_scans + 1);
+    auto get = [&](void* p, size_t bytes) { if (ok && bytes) ok = fread(p, 1, bytes, f) == bytes; };
+    get(F.data(), sizeof(dpg_factor) * F.size());
+    get(created.data(), sizeof(int32_t) * created.size());
+    get(plo.data(), sizeof(int32_t) * plo.size());
+    get(phi.data(), sizeof(int32_t) * phi.size());
+    get(theta.data(), sizeof(double) * theta.size());
+    get(est.data(), sizeof(double) * est.size());
+    get(maxd.data(), sizeof(double) * maxd.size());
+    get(off.data(), sizeof(int64_t) * off.size());
+    const int64_t npts = ok ? off[(size_t)h.n_scans] : 0;
+    ok = ok && off[0] == 0 && npts >= 0 && npts < ((int64_t)1 << 31);
+    for (size_t v = 0; ok && v < (size_t)h.n_scans; ++v) ok = off[v + 1] >= off[v];
+    std::vector<float> pts((size_t)(2 * std::max<int64_t>(npts, 1)));
+    get(pts.data(), sizeof(float) * 2 * (size_t)std::max<int64_t>(npts, 0));
+    fclose(f);
+    // the graph must reference only its own nodes and pairs
+    for (int64_t k = 0; ok && k < h.n_pairs; ++k)
+        ok = plo[(size_t)k] >= 0 && plo[(size_t)k] < phi[(size_t)k] && phi[(size_t)k] < h.V;
+    if (!ok) {
+        set_err(DPG_ERR_ARG, "dpg_inc_load: truncated or inconsistent checkpoint");
+        return nullptr;
+    }
+    if (!ctx) {
+        set_err(DPG_ERR_ARG, "dpg_inc_load: ctx is NULL");
+        return nullptr;
+    }
+    if (h.n_scans > 0 && (dpg_scans_upload(ctx, pts.data(), off.data(), h.n_scans, h.ratio) || dpg_scans_index_all(ctx)))
+        return nullptr;
+    dpg_inc* q = dpg_inc_create(ctx, &h.params);
+    if (!q) return nullptr;
+    auto bail = [&](int code, const char* msg) -> dpg_inc* {
+        dpg_inc_destroy(q);
+        set_err(code, msg);
+        return nullptr;
+    };
+    for (int64_t k = 0; k < h.n_pairs; ++k) {
+        if (!q->pair_id.emplace(pkey(plo[(size_t)k], phi[(size_t)k]), (int32_t)k).second)
+            return bail(DPG_ERR_ARG, "dpg_inc_load: a node pair is listed twice");
+    }
+    q->plo = plo;
+    q->phi = phi;
+    for (int64_t k = 0; k < h.n_factors; ++k) {
+        const dpg_factor& fk = F[(size_t)k];
+        int32_t pid = -1;
+        if (fk.kind == DPG_FACTOR_BETWEEN) {
+            const auto it = q->pair_id.find(pkey(std::min(fk.i, fk.j), std::max(fk.i, fk.j)));
+            if (fk.i < 0 || fk.j < 0 || fk.i >= h.V || fk.j >= h.V || it == q->pair_id.end())
+                return bail(DPG_ERR_ARG, "dpg_inc_load: a factor's pair is missing");
+            pid = it->second;
+        } else if (fk.kind != DPG_FACTOR_PRIOR || fk.i < 0 || fk.i >= h.V) {
+            return bail(DPG_ERR_ARG, "dpg_inc_load: a factor references a missing node");
+        }
+        q->f_pair.push_back(pid);
+    }
+    if (h.V == 0) return q;
+    // the structure: a fresh order of the saved pattern (dpg_inc_prepare from an empty symbolic state)
+    if (dpg_inc_prepare(q, h.V, nullptr, 0)) return bail(DPG_ERR_NUMERIC, "dpg_inc_load: symbolic analysis failed");
+    q->prepared = false;
+    q->V = h.V;
+    q->updates = h.updates;
+    q->F = F;
+    q->f_created = created;
+    hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(ctx));
+    if (hipSetDevice(dpg_ctx_device_of(ctx)) != hipSuccess) return bail(DPG_ERR_HIP, "hipSetDevice failed");
+    int rc = 0;
+    rc |= dgrow(&q->theta, &q->c_theta, 3 * V, s, 0);
+    rc |= dgrow(&q->est, &q->c_est, 3 * V, s, 0);
+    rc |= dgrow(&q->maxd, &q->c_maxd, V, s, 0);
+    if (!q->cnt) rc |= hipMalloc(reinterpret_cast<void**>(&q->cnt), sizeof(int32_t)) != hipSuccess;
+    if (rc) return bail(DPG_ERR_HIP, "dpg_inc_load: out of device memory");
+    if (hipMemcpyAsync(q->theta, theta.data(), sizeof(double) * 3 * V, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->est, est.data(), sizeof(double) * 3 * V, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(q->maxd, maxd.data(), sizeof(double) * V, hipMemcpyHostToDevice, s) != hipSuccess)
+        return bail(DPG_ERR_HIP, "dpg_inc_load: upload failed");
+    if ((rc = inc_rebuild(q, s))) return bail(rc, "dpg_inc_load: solver rebuild failed");
+    if (hipStreamSynchronize(s) != hipSuccess) return bail(DPG_ERR_HIP, "dpg_inc_load: upload failed");
+    return q;
 }
 
 int dpg_inc_get_poses(dpg_inc* q, double* poses, int64_t n) {

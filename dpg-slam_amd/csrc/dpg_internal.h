@@ -21,6 +21,10 @@ dpg_ctx* dpg_inc_ctx(dpg_inc* g);   /* the context an incremental graph runs on 
 int dpg_inc_prepare(dpg_inc* g, int64_t n_new, const int32_t* pairs, int64_t n_pairs);
 int dpg_inc_abort_prepare(dpg_inc* g);
 int dpg_ctx_is_multi(dpg_ctx* c);
+/* the scan store as host copies, and the neighbour index of every stored node (the graph
+ * checkpoint, dpg_inc_save / dpg_inc_load in dpg_inc.hip) */
+int dpg_scans_export(dpg_ctx* c, int64_t* n_nodes, int32_t* ratio, int64_t* off, float* pts);
+int dpg_scans_index_all(dpg_ctx* c);
 void* dpg_ctx_stream_of(dpg_ctx* c);
 int dpg_ctx_device_of(dpg_ctx* c);
 

@@ -296,6 +296,8 @@ SIGNATURES = {
     "dpg_inc_update": (C.c_int, [P, C.c_int64, F64P, P, C.c_int64, C.POINTER(IncStats)]),
     "dpg_inc_num_nodes": (C.c_int64, [P]),
     "dpg_inc_get_poses": (C.c_int, [P, F64P, C.c_int64]),
+    "dpg_inc_save": (C.c_int, [P, C.c_char_p]),
+    "dpg_inc_load": (P, [P, C.c_char_p]),
     "dpg_scans_append": (C.c_int, [P, F32P, I64P, C.c_int64, C.c_int32]),
     "dpg_add_node": (C.c_int, [P, F32P, C.c_int64, I32P, F32P, P, C.c_int64, C.POINTER(IcpParams),
                                C.POINTER(ReoptParams), C.c_int32, C.POINTER(AddNodeStats)]),

@@ -13,6 +13,7 @@ batched runIcp calls of reoptimize (dpg_slam.cc:85-106)  Context.upload_scans / 
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 from dataclasses import dataclass
 
@@ -523,6 +524,23 @@ class IncGraph:
         X = np.zeros((max(n, 1), 3), np.float64)
         check(lib().dpg_inc_get_poses(self.handle, ptr(X, C.c_double), n), "dpg_inc_get_poses")
         return X[:n]
+
+    def save(self, path: str):
+        """dpg_inc_save: the graph and its context's scan store to one checkpoint file."""
+        check(lib().dpg_inc_save(self.handle, os.fsencode(path)), "dpg_inc_save")
+
+    @classmethod
+    def load(cls, ctx: Context, path: str) -> "IncGraph":
+        """dpg_inc_load: a graph restored from a checkpoint on ctx (ctx's scan store is replaced)."""
+        g = cls.__new__(cls)
+        g.ctx = ctx
+        g.params = None
+        g.handle = lib().dpg_inc_load(ctx.handle if ctx is not None else None, os.fsencode(path))
+        if not g.handle:
+            raise _abi.DpgError("dpg_inc_load failed: " + (lib().dpg_last_error() or b"").decode())
+        if ctx is not None:
+            ctx._children.add(g)
+        return g
 
     def add_node(self, cloud, passes, init_pose, extra=None, icp_params=None, reopt_params=None,
                  non_successive=True) -> "_abi.AddNodeStats":

@@ -391,6 +391,19 @@ int64_t dpg_inc_num_nodes(const dpg_inc* g);
 /* calculateEstimate() of the first n nodes: poses[n][3] */
 int dpg_inc_get_poses(dpg_inc* g, double* poses, int64_t n);
 
+/* Graph checkpoint ("optional binary dump of the graph (poses, edges,
+ * measurements)"; the reference keeps dpg_nodes_ with their scans, graph_ and isam_ only in memory,
+ * dpg_slam.h:362,367,372).  dpg_inc_save writes the graph's factors, node pairs (arrival order),
+ * linearization points, estimate, per-variable |delta|, update count and parameters, and the
+ * context's scan store (full clouds, downsample ratio), to one binary file.  dpg_inc_load restores
+ * it on ctx (single device; its scan store is replaced by the file's and indexed): the next
+ * dpg_add_node / dpg_inc_update continues the saved run, ISAM2's relinearization schedule
+ * included; the elimination order is recomputed from the saved pattern, so later estimates agree
+ * with an uninterrupted run to rounding.  dpg_inc_load returns NULL on error (dpg_last_error);
+ * a file of another version or layout is rejected. */
+int dpg_inc_save(dpg_inc* g, const char* path);
+dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path);
+
 /* Append nodes to the uploaded scan store (dpg_scans_upload's layout): pts_xy = the new nodes' full
  * clouds concatenated, node_offsets[n_new + 1] relative to pts_xy; the downsample ratio must match
  * the store's.  Only the new nodes' neighbour indexes are built. */

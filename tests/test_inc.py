@@ -195,3 +195,79 @@ def test_gpu_add_node_failure_keeps_store_and_graph_in_step():
     assert g.V == 3 and st.n_icp_edges >= 1
     g.close()
     ctx.close()
+
+
+def test_checkpoint_rejects_foreign_files(tmp_path):
+    """dpg_inc_load validates the file before it touches a device: a file that is not a graph
+    checkpoint of this version (or is truncated) is rejected with DPG_ERR_ARG."""
+    from dpgslam import api
+    bad = tmp_path / "not_a_graph.bin"
+    bad.write_bytes(b"DPGGRAPH" + b"\x07" * 200)
+    with pytest.raises(_abi.DpgError, match="not a graph checkpoint"):
+        api.IncGraph.load(None, str(bad))
+    with pytest.raises(_abi.DpgError, match="cannot open"):
+        api.IncGraph.load(None, str(tmp_path / "missing.bin"))
+
+
+@pytest.mark.gpu
+def test_gpu_checkpoint_resume_update_path(ctx, tmp_path):
+    """dpg_inc_save / dpg_inc_load (SURVEY section 5 graph dump): a 300-node ISAM2 graph is saved,
+    restored on a fresh context, and both continue with the same 150 updates -- the restored run
+    agrees with the uninterrupted one to rounding (a fresh elimination order) and with the oracle;
+    the relinearization schedule continues (update count restored: the 310th update relinearizes)."""
+    from dpgslam import api
+    X0, F = _sequence("config3", 450)
+    key = _per_node(F)
+    g = api.IncGraph(ctx, mode="isam2", reorder_every=64)
+    o = O.OracleIncGraph(mode="isam2")
+    for v in range(300):
+        g.update(X0[v:v + 1], F[key == v])
+        o.update(X0[v:v + 1], F[key == v])
+    path = str(tmp_path / "graph.dpg")
+    g.save(path)
+    ctx2 = api.Context(0)
+    h = api.IncGraph.load(ctx2, path)
+    assert h.V == 300 and np.array_equal(h.poses(), g.poses())
+    for v in range(300, 450):
+        sg = g.update(X0[v:v + 1], F[key == v])
+        sh = h.update(X0[v:v + 1], F[key == v])
+        o.update(X0[v:v + 1], F[key == v])
+        assert sg.relinearized == sh.relinearized and sg.n_factors == sh.n_factors
+    assert np.abs(pose_diff(h.poses(), g.poses())).max() < 1e-9
+    assert np.abs(pose_diff(h.poses(), o.poses())).max() < 1e-6
+    h.close()
+    g.close()
+    ctx2.close()
+
+
+@pytest.mark.gpu
+def test_gpu_checkpoint_resume_add_node_path(tmp_path):
+    """The checkpoint carries the scan store: a graph built node by node with dpg_add_node (the
+    node's cloud, its successive alignment and loop closures by the reference rule) is saved at 60
+    nodes, restored on a fresh context, and both add the same 40 nodes -- same alignments and
+    factors, poses equal to rounding."""
+    from dpgslam import api
+    w = synth.generate("config3")
+    p = _abi.default_icp_params()
+    prior = np.zeros(1, _abi.FACTOR_DTYPE)
+    prior["kind"], prior["i"], prior["info"] = _abi.DPG_FACTOR_PRIOR, 0, 1.0 / np.array([0.04, 0.04, 0.0225])
+    ctx = api.Context(0)
+    g = api.IncGraph(ctx, mode="isam2", reorder_every=16)
+    passes = np.zeros(100, np.int32)
+    for v in range(60):
+        g.add_node(w.cloud(v), passes[:v + 1], w.est[v], extra=prior if v == 0 else None, icp_params=p)
+    path = str(tmp_path / "graph_scans.dpg")
+    g.save(path)
+    ctx2 = api.Context(0)
+    h = api.IncGraph.load(ctx2, path)
+    assert h.V == 60 and np.array_equal(h.poses(), g.poses())
+    for v in range(60, 100):
+        sg = g.add_node(w.cloud(v), passes[:v + 1], w.est[v], icp_params=p)
+        sh = h.add_node(w.cloud(v), passes[:v + 1], w.est[v], icp_params=p)
+        assert (sg.n_icp_edges, sg.n_loop_closures) == (sh.n_icp_edges, sh.n_loop_closures)
+        assert sg.update.n_factors == sh.update.n_factors
+    assert np.abs(pose_diff(h.poses(), g.poses())).max() < 1e-9
+    h.close()
+    g.close()
+    ctx2.close()
+    ctx.close()
