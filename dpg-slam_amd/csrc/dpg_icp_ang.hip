@@ -82,9 +82,18 @@ constexpr float kPaMargin = 2e-5f;              // absolute pseudo-angle margin 
 // pseudo-angle in [0, 2 pi): atan2 approximated per octant by f(t) = t (pi/4 + 0.273 (1 - t)),
 // t = min(|x|,|y|) / max(|x|,|y|) (max error 1.5e-3 rad, slope ratio to atan in [0.98, 1.0584]);
 // 0 at the origin.
+template <bool kAbsMinMax = false>
 __device__ __forceinline__ float pseudo_angle(float x, float y) {
     const float ax = fabsf(x), ay = fabsf(y);
-    const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+    float mx, mn;
+    if constexpr (kAbsMinMax) {   // max / min of the magnitudes straight from x, y (abs operand
+        // modifiers, no separate canonicalizing max per magnitude; the same values: no NaN here)
+        asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(mx) : "v"(x), "v"(y));
+        asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
+    } else {
+        mx = fmaxf(ax, ay);
+        mn = fminf(ax, ay);
+    }
     if (!(mx > 0.0f)) return 0.0f;
     const float t = mn * __builtin_amdgcn_rcpf(mx);
     const float f = t * (1.0584f - 0.273f * t);
@@ -250,6 +259,8 @@ struct Bcast {
     int qtail;       // cooperative queue: items pushed this iteration (may exceed kQCap)
     int qhead;       // unused
     int iter;        // iterations fitted so far (every wave checks it after the publish barrier)
+    float finv[4];   // the inverse rounded to float, as the reciprocal windows use it (variant 3)
+    float drift;     // the next reciprocal tests' drift margin 1e-4 + 5e-5 (k + 1) m (variant 3)
 };
 
 // fp64 inverse of the 2x2 block of a 2x3 float transform (same expressions every time)
@@ -408,7 +419,7 @@ template <int VAR = 1>
 __device__ __forceinline__ int window_pa(const uint16_t* bk, int n, float qx, float qy, float pq, float rad, int& start);
 template <int VAR = 1>
 __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int& start) {
-    return window_pa<VAR>(bk, n, qx, qy, pseudo_angle(qx, qy), rad, start);
+    return window_pa<VAR>(bk, n, qx, qy, pseudo_angle<(VAR >= 4)>(qx, qy), rad, start);
 }
 // the same with q's pseudo-angle pq already computed (the forward search computes it once for the
 // unseeded probe and the window)
@@ -423,6 +434,22 @@ __device__ __forceinline__ int window_pa(const uint16_t* bk, int n, float qx, fl
     // 1/sqrt(0.51) = 1.40028 at the end), so the half-angle bound needs no reciprocal square root
     // (the window only widens: a superset, exact as above)
     const float half = kPaSlope * sn * fmaf(sn * sn, 0.8172f, 1.0f) * 1.0001f + kPaMargin;
+    if constexpr (VAR >= 3) {
+        // the wrap at pseudo-angle 0 in bucket space: floor((pq -+ half) * scale) taken modulo kB
+        // (a power of two) -- the same buckets as wrapping the angle first, up to a few ulp of the
+        // bucket coordinate, far inside the kPaMargin the half-angle carries; a window that rounds
+        // to more than the cloud is the whole cloud
+        static_assert((kB & (kB - 1)) == 0, "bucket count is a power of two");
+        int blo, bhi;
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(blo) : "v"((pq - half) * kBucketScale));
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(bhi) : "v"((pq + half) * kBucketScale));
+        const bool wrap = blo < 0 || bhi >= kB;   // straddles pseudo-angle 0
+        const int s = bk[blo & (kB - 1)];
+        const int end = bk[(bhi & (kB - 1)) + 1];
+        const int cnt = wrap ? (n - s) + end : end - s;
+        start = s >= n ? s - n : s;
+        return min(cnt, n);
+    }
     float lo = pq - half, hi = pq + half;
     if (lo < 0.0f) lo += kTwoPi;
     if (hi >= kTwoPi) hi -= kTwoPi;
@@ -570,6 +597,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         B.qtail = 0;
         B.qhead = 0;
         B.iter = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) B.finv[q] = (float)B.inv[q];
+        B.drift = 1e-4f + 5e-5f * (float)1;
         *L.bc = B;
         *L.arrive = 0;
     }
@@ -628,10 +658,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     for (;;) {
         ICP_STAMP(c0);
         if constexpr (kPrio) __builtin_amdgcn_s_setprio(0);
-        const float i00 = uni((float)L.bc->inv[0]), i01 = uni((float)L.bc->inv[1]);
-        const float i10 = uni((float)L.bc->inv[2]), i11 = uni((float)L.bc->inv[3]);
+        // variant 3: the inverse and the drift margin arrive as floats (no per-slot conversions)
+        const float i00 = uni(VAR >= 3 ? L.bc->finv[0] : (float)L.bc->inv[0]), i01 = uni(VAR >= 3 ? L.bc->finv[1] : (float)L.bc->inv[1]);
+        const float i10 = uni(VAR >= 3 ? L.bc->finv[2] : (float)L.bc->inv[2]), i11 = uni(VAR >= 3 ? L.bc->finv[3] : (float)L.bc->inv[3]);
         const float ftx = uni(L.bc->F[2]), fty = uni(L.bc->F[5]);
-        const float drift = 1e-4f + 5e-5f * (float)(k + 1);
+        const float drift = VAR >= 3 ? uni(L.bc->drift) : 1e-4f + 5e-5f * (float)(k + 1);
         // bit m: point t + 512 m has a (reciprocal) correspondence; bits 8 + 7 m ..: queue slot + 1
         uint32_t okq = 0;
         static_assert(PPT <= 32, "one ok bit per point");
@@ -662,7 +693,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             // ---- forward 1-NN (target index), seeded radius ----
             const bool search = live && sd >= -1;   // < -1: clearance, provably no target within r
             float rad;
-            const float pq = VAR >= 2 ? pseudo_angle(qx, qy) : 0.f;   // once for the probe and the window
+            const float pq = VAR >= 2 ? pseudo_angle<(VAR >= 4)>(qx, qy) : 0.f;   // once for the probe and the window
             uint64_t best = forward_init<VAR>(L, M, search ? sd : 0, qx, qy, pq, r2f, rmax, rext, r2ext, rad);
             bool pend;   // this point's forward window went to the queue
             {
@@ -963,6 +994,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 B.code = (k + 1 >= kp.max_iter || (cos_angle >= kp.rot_thr && tsq <= kp.eps) ||
                           fabs(mse - prev_mse) < kp.mse_abs) ? 1 : 0;
                 B.prev_mse = mse;
+                B.drift = 1e-4f + 5e-5f * (float)(k + 2);
             } else {
                 const double n = S[0];
                 double a, b;
@@ -1051,7 +1083,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 const double det = (double)Fn[0] * (double)Fn[4] - (double)Fn[1] * (double)Fn[3];
                 const double num = lane == 0 ? (double)Fn[4] : lane == 1 ? -(double)Fn[1] : lane == 2 ? -(double)Fn[3] : (double)Fn[0];
                 const double q = num / det;
-                if (lane < 4) L.bc->inv[lane] = q;
+                if (lane < 4) {
+                    L.bc->inv[lane] = q;
+                    L.bc->finv[lane] = (float)q;
+                }
             } else {
                 inverse2(Fn, inv);
                 if (lane == 0)
@@ -1146,7 +1181,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     if (chunk <= 0) return DPG_ERR_SIZE;
     Rec* g = reinterpret_cast<Rec*>(scratch);
     const char* ve = getenv("DPG_ICP_VARIANT");   // A/B of kernel variants (tools/icp_var_ab.py)
-    const int var = ve ? atoi(ve) : 2;
+    const int var = ve ? atoi(ve) : 3;
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
@@ -1159,7 +1194,9 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
         if (var == 0) DPG_ANG_K(P, M, 0);                                                                       \
         else if (var == 1) DPG_ANG_K(P, M, 1);                                                                  \
-        else DPG_ANG_K(P, M, 2)
+        else if (var == 2) DPG_ANG_K(P, M, 2);                                                                  \
+        else if (var == 3) DPG_ANG_K(P, M, 3);                                                                  \
+        else DPG_ANG_K(P, M, 4)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
             else if (ppt <= 2) DPG_ANG_LAUNCH(2, 0);

@@ -238,6 +238,15 @@ class IncGraph {
         write_back(nodes);
         return st;
     }
+    /* graph checkpoint (dpg_inc_save / dpg_inc_load): the graph and its context's scans in one
+       file; a graph loaded on ctx continues the saved run */
+    void save(const char* path) const { check(dpg_inc_save(g_, path), "dpg_inc_save"); }
+    static IncGraph load(dpg_ctx* ctx, const char* path) {
+        dpg_inc* g = dpg_inc_load(ctx, path);
+        if (!g) throw Error(std::string("dpg_inc_load: ") + (dpg_last_error() ? dpg_last_error() : "?"));
+        return IncGraph(g);
+    }
+    IncGraph(IncGraph&& o) noexcept : g_(o.g_) { o.g_ = nullptr; }
     /* the current estimates -> the nodes (setPosition) */
     template <class NodeVec>
     void write_back(NodeVec& nodes) const {
@@ -248,6 +257,7 @@ class IncGraph {
             nodes[k].setPosition(Vec((float)X[3 * k], (float)X[3 * k + 1]), (float)X[3 * k + 2]);
     }
   private:
+    explicit IncGraph(dpg_inc* g) : g_(g) {}
     dpg_inc* g_;
 };
 

@@ -5,6 +5,7 @@
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <memory>
 #include <vector>
@@ -218,6 +219,29 @@ int main() {
         EXPECT(st5.update.n_nodes == 5 && g.size() == 5);
         printf("IncGraph::reoptimize: %lld factors, %lld ICP edges; then node 5 added\n", (long long)rs.n_factors,
                (long long)rs.n_icp_edges);
+        // checkpoint: save, restore on a third context, both add the same node
+        char path[] = "/tmp/adapter_check_graph_XXXXXX";
+        const int fd = mkstemp(path);
+        EXPECT(fd >= 0);
+        if (fd >= 0) close(fd);
+        g.save(path);
+        dpg_adapter::Context ctx3(0);
+        dpg_adapter::IncGraph g3 = dpg_adapter::IncGraph::load(ctx3.get(), path);
+        unlink(path);
+        EXPECT(g3.size() == 5);
+        passes.push_back(0);
+        float ip5[3] = {ip4[0] + 0.9f, ip4[1], ip4[2]};
+        std::vector<dpg_factor> ex5{dpg_adapter::between_factor(4, 5, 0.9, 0.0, 0.0, info)};
+        const dpg_add_node_stats sa = g.add_node(nodes[2].cloud, passes, ip5, ex5, pgp, true);
+        const dpg_add_node_stats sb = g3.add_node(nodes[2].cloud, passes, ip5, ex5, pgp, true);
+        std::vector<Node> c1(6), c3(6);
+        g.write_back(c1);
+        g3.write_back(c3);
+        double worst = 0.0;
+        for (int k = 0; k < 6; ++k)
+            worst = std::max(worst, (double)std::max(std::fabs(c1[k].loc.x() - c3[k].loc.x()), std::fabs(c1[k].th - c3[k].th)));
+        EXPECT(sa.update.n_factors == sb.update.n_factors && sa.n_icp_edges == sb.n_icp_edges && worst < 1e-5);
+        printf("IncGraph::save/load: node 6 added to both, max pose difference %.3g\n", worst);
     }
     // executeDPG: the store grows scan by scan; a second pass sees the room with a wall moved
     {
