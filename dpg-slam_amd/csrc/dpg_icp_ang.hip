@@ -1181,7 +1181,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     if (chunk <= 0) return DPG_ERR_SIZE;
     Rec* g = reinterpret_cast<Rec*>(scratch);
     const char* ve = getenv("DPG_ICP_VARIANT");   // A/B of kernel variants (tools/icp_var_ab.py)
-    const int var = ve ? atoi(ve) : 3;
+    const int var = ve ? atoi(ve) : 4;
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
