@@ -1185,17 +1185,17 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
-// variant 1 (default): hardware square roots in the window bounds, the candidate distance
-// computed into the record's pad register, reciprocal beats as ballots, the fit's divisions as
-// lane-parallel vector divisions, issue priority for the synchronised phases; variant 0: round
-// 2's form of the same arithmetic (A/B reference, DPG_ICP_VARIANT=0).  Both give byte-identical results.
+// variant 4 (default; the kernel's VAR >= 1..4 steps): hardware square roots in the
+// window bounds, the candidate distance computed into the record's pad register, reciprocal beats
+// as ballots, the fit's divisions as lane-parallel vector divisions, issue priority for the
+// synchronised phases (1); the forward pseudo-angle once per point, fused floor+convert, do-while
+// forward trips (2); float inverse + drift from the fitting wave, bucket-space wrap (3); abs-modifier
+// magnitudes in the query pseudo-angles (4).  Variant 0: round 2's form of the same arithmetic
+// (A/B reference, DPG_ICP_VARIANT=0).  Both give byte-identical results.
 #define DPG_ANG_K(P, M, V) hipLaunchKernelGGL((icp_ang_kernel<P, M, V>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
         if (var == 0) DPG_ANG_K(P, M, 0);                                                                       \
-        else if (var == 1) DPG_ANG_K(P, M, 1);                                                                  \
-        else if (var == 2) DPG_ANG_K(P, M, 2);                                                                  \
-        else if (var == 3) DPG_ANG_K(P, M, 3);                                                                  \
         else DPG_ANG_K(P, M, 4)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
