@@ -606,8 +606,9 @@ int dpg_inc_save(dpg_inc* q, const char* path) {
     h.n_pairs = (int64_t)q->plo.size();
     int rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, nullptr, nullptr);
     if (rc) return rc;
-    if (h.n_scans != 0 && h.n_scans < h.V)
-        return set_err(DPG_ERR_STATE, "dpg_inc_save: the scan store holds fewer nodes than the graph");
+    // the store belongs to the graph when it holds the graph's nodes (the dpg_add_node path); a
+    // graph fed by dpg_inc_update alone is saved without scans (the context may hold any others)
+    if (h.n_scans < h.V) h.n_scans = 0;
     const size_t V = (size_t)h.V;
     std::vector<double> theta(3 * V), est(3 * V), maxd(V);
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
@@ -618,9 +619,12 @@ int dpg_inc_save(dpg_inc* q, const char* path) {
         return set_err(DPG_ERR_HIP, "dpg_inc_save: read-back failed");
     if (hipStreamSynchronize(s) != hipSuccess) return set_err(DPG_ERR_HIP, "dpg_inc_save: read-back failed");
     std::vector<int64_t> off((size_t)h.n_scans + 1, 0);
-    if ((rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, off.data(), nullptr))) return rc;
-    std::vector<float> pts((size_t)(2 * std::max<int64_t>(off[(size_t)h.n_scans], 1)));
-    if ((rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, off.data(), pts.data()))) return rc;
+    std::vector<float> pts(2);
+    if (h.n_scans > 0) {
+        if ((rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, off.data(), nullptr))) return rc;
+        pts.resize((size_t)(2 * std::max<int64_t>(off[(size_t)h.n_scans], 1)));
+        if ((rc = dpg_scans_export(q->ctx, &h.n_scans, &h.ratio, off.data(), pts.data()))) return rc;
+    }
     FILE* f = fopen(path, "wb");
     if (!f) return set_err(DPG_ERR_ARG, "dpg_inc_save: cannot open the file for writing");
     bool ok = fwrite(&h, sizeof(h), 1, f) == 1;

@@ -395,8 +395,10 @@ int dpg_inc_get_poses(dpg_inc* g, double* poses, int64_t n);
  * measurements)"; the reference keeps dpg_nodes_ with their scans, graph_ and isam_ only in memory,
  * dpg_slam.h:362,367,372).  dpg_inc_save writes the graph's factors, node pairs (arrival order),
  * linearization points, estimate, per-variable |delta|, update count and parameters, and the
- * context's scan store (full clouds, downsample ratio), to one binary file.  dpg_inc_load restores
- * it on ctx (single device; its scan store is replaced by the file's and indexed): the next
+ * context's scan store (full clouds, downsample ratio) when it holds the graph's nodes (the
+ * dpg_add_node path; a graph fed by dpg_inc_update alone is saved without scans), to one binary
+ * file.  dpg_inc_load restores it on ctx (single device; a saved scan store replaces ctx's and is
+ * indexed, else ctx's store is left as it is): the next
  * dpg_add_node / dpg_inc_update continues the saved run, ISAM2's relinearization schedule
  * included; the elimination order is recomputed from the saved pattern, so later estimates agree
  * with an uninterrupted run to rounding.  dpg_inc_load returns NULL on error (dpg_last_error);
