@@ -44,8 +44,15 @@ int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, in
 // nested dissection (BFS level separators; parts of <= leaf nodes by minimum degree): shallow trees
 int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                       std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
+// the same with the separator rule of the multi-start search (starts = 0: round 2's rule; bal:
+// both sides >= 1 / bal of the part; score 0 |S|, 1 |S| N / min side, 2 |S| sqrt(N / min side))
+int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
+                          int32_t starts, int32_t bal, int32_t score, std::vector<int32_t>& perm,
+                          std::vector<std::vector<int32_t>>& pat);
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
                                const dpg_chol_opts* opts, dpg_chol_sym* S);
+// the fused factorization's critical-path estimate (us) of an analysis (the chol_plan ticket model)
+double dpg_chol_critical_path_us(const dpg_chol_sym& S);
 // the same from patterns in CSR form: column p's rows are prow[cp[p] .. cp[p + 1]) (sorted)
 int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow,
                           const dpg_chol_opts* opts, dpg_chol_sym* S);

@@ -11,6 +11,7 @@
 //      (relaxed amalgamation), and the supernodal elimination tree
 //   4. level schedule (leaves = level 0) and the maps the GPU kernels need: original H blocks
 //      -> front positions, child update matrix rows -> parent front rows
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -101,10 +102,24 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
 // separator a few nodes wide (a BFS level structure from a pseudo-peripheral node: the smallest
 // level in the middle half), orders both halves recursively and the separator last: height
 // O(log n) separators.  Parts of at most `leaf` nodes are ordered by minimum degree.
+//
+// Separator choice (round 3): `starts` = 0 is round 2's rule (one level structure from the
+// pseudo-peripheral node, the smallest level with a fifth of the part on either side).  With
+// starts > 0 the search covers the cuts between consecutive levels of several level structures
+// (the pseudo-peripheral start, the far end of its BFS, and starts - 1 more spread over its BFS
+// order, for parts of at least 256 nodes), each cut's trimmed separator counted in one pass over
+// the edges, and keeps the cut with both sides >= 1 / bal of the part that minimises
+// |S| sqrt(N / min(|A|, |B|)) (score 2; score 1: |S| N / min, score 0: |S|) -- small separators
+// high in the tree are what the GPU factorization's critical path pays for (dpg_chol_symbolic
+// picks among such orders by that path's estimate).
+struct NdParams {
+    int32_t starts = 0, bal = 5, score = 0;
+};
 struct NdState {
     const int64_t* aptr;
     const int32_t* adj;
     int32_t leaf;
+    NdParams prm;
     int32_t next_id = 0;
     std::vector<int32_t> stamp, lvl, queue;
     std::vector<int32_t>* out;
@@ -153,6 +168,90 @@ void nd_min_degree(NdState& st, const std::vector<int32_t>& sub) {
     for (int32_t l : lp) st.out->push_back(sub[(size_t)l]);
 }
 
+void nd_rec(NdState& st, std::vector<int32_t>& sub);
+
+// the separator search with several level structures (NdParams, starts > 0); src is the part's
+// pseudo-peripheral node, `id` its stamp
+void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t src) {
+    const int64_t N = (int64_t)sub.size();
+    const int T = N >= 256 ? st.prm.starts : 1;
+    std::vector<int32_t> starts{src};
+    {
+        for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+        nd_bfs(st, id, src);
+        const std::vector<int32_t> order(st.queue.begin(), st.queue.end());
+        for (int t = 1; t < T; ++t) starts.push_back(order[(size_t)((int64_t)t * (N - 1) / T)]);
+        starts.push_back(order.back());
+    }
+    int32_t bsrc = -1, bm = -1;
+    bool bupper = false;
+    double bsc = 0.0;
+    int64_t bimb = 0;
+    std::vector<int64_t> slo, shi, cnt;
+    for (int32_t s0 : starts) {
+        for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+        const int32_t hh = nd_bfs(st, id, s0);
+        if (hh < 3) continue;
+        cnt.assign((size_t)hh, 0);
+        slo.assign((size_t)hh, 0);
+        shi.assign((size_t)hh, 0);
+        for (int32_t v : sub) {
+            const int32_t l = st.lvl[(size_t)v];
+            cnt[(size_t)l]++;
+            bool up = false, dn = false;
+            for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
+                const int32_t u = st.adj[(size_t)t];
+                if (st.stamp[(size_t)u] != id) continue;
+                up |= st.lvl[(size_t)u] == l + 1;
+                dn |= st.lvl[(size_t)u] == l - 1;
+            }
+            slo[(size_t)l] += up;                    // on level l, touching l + 1
+            if (l > 0) shi[(size_t)l - 1] += dn;     // on level l, touching l - 1
+        }
+        int64_t below = 0;
+        for (int32_t l = 0; l + 1 < hh; ++l) {   // the cut between levels l and l + 1
+            const bool up = shi[(size_t)l] < slo[(size_t)l];
+            const int64_t sz = up ? shi[(size_t)l] : slo[(size_t)l];
+            const int64_t a_sz = below + cnt[(size_t)l] - (up ? 0 : sz), b_sz = N - a_sz - sz;
+            below += cnt[(size_t)l];
+            if (l == 0 || (int64_t)st.prm.bal * a_sz < N || (int64_t)st.prm.bal * b_sz < N) continue;
+            const double mn = (double)std::min(a_sz, b_sz);
+            const double sc = st.prm.score == 2 ? (double)sz * sqrt((double)N / mn)
+                              : st.prm.score == 1 ? (double)sz * (double)N / mn : (double)sz;
+            const int64_t imb = a_sz > b_sz ? a_sz - b_sz : b_sz - a_sz;
+            if (bm < 0 || sc < bsc || (sc == bsc && imb < bimb)) {
+                bsrc = s0; bm = l; bupper = up; bsc = sc; bimb = imb;
+            }
+        }
+    }
+    if (bm < 0) { nd_min_degree(st, sub); return; }
+    for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+    nd_bfs(st, id, bsrc);
+    auto touches = [&](int32_t v, int32_t l) {
+        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
+            const int32_t u = st.adj[(size_t)t];
+            if (st.stamp[(size_t)u] == id && st.lvl[(size_t)u] == l) return true;
+        }
+        return false;
+    };
+    std::vector<int32_t> A, B, S;
+    for (int32_t v : sub) {
+        const int32_t l = st.lvl[(size_t)v];
+        if (!bupper) {
+            if (l < bm) A.push_back(v);
+            else if (l > bm) B.push_back(v);
+            else (touches(v, bm + 1) ? S : A).push_back(v);
+        } else {
+            if (l <= bm) A.push_back(v);
+            else if (l > bm + 1) B.push_back(v);
+            else (touches(v, bm) ? S : B).push_back(v);
+        }
+    }
+    nd_rec(st, A);
+    nd_rec(st, B);
+    for (int32_t v : S) st.out->push_back(v);
+}
+
 void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     if ((int32_t)sub.size() <= st.leaf) { nd_min_degree(st, sub); return; }
     const int32_t id = ++st.next_id;
@@ -188,6 +287,7 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
         if (best == src) break;
         src = best;
     }
+    if (st.prm.starts > 0) { nd_split_multi(st, sub, id, src); return; }
     for (int32_t v : sub) st.lvl[(size_t)v] = -1;
     h = nd_bfs(st, id, src);
     const int64_t N = (int64_t)sub.size();
@@ -281,6 +381,12 @@ void patterns_of_order(int64_t n, const std::vector<int64_t>& aptr, const std::v
 
 int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                       std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
+    return dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, leaf, 0, 5, 0, perm, pat);
+}
+
+int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
+                          int32_t starts, int32_t bal, int32_t score, std::vector<int32_t>& perm,
+                          std::vector<std::vector<int32_t>>& pat) {
     if (n <= 0) return -1;
     std::vector<int64_t> aptr((size_t)n + 1, 0);
     for (int64_t p = 0; p < n_pairs; ++p) { aptr[(size_t)pair_lo[p] + 1]++; aptr[(size_t)pair_hi[p] + 1]++; }
@@ -297,6 +403,9 @@ int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
     st.aptr = aptr.data();
     st.adj = adj.data();
     st.leaf = std::max<int32_t>(leaf, 4);
+    st.prm.starts = starts;
+    st.prm.bal = std::max<int32_t>(bal, 2);
+    st.prm.score = score;
     st.stamp.assign((size_t)n, 0);
     st.lvl.assign((size_t)n, -1);
     perm.clear();
@@ -343,12 +452,65 @@ int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, in
     return 0;
 }
 
+// The fused factorization's critical path estimate (us) of a symbolic analysis: the same per-front
+// model chol_plan orders its tickets by (dpg_chol.hip: a front of <= 96 rows and <= 8 children is
+// factored in LDS, 4 + 0.06 m3 + 0.9 k3; a larger one by a team, 10 + 20 per 24-column panel),
+// summed along the longest leaf-to-root path
+double dpg_chol_critical_path_us(const dpg_chol_sym& S) {
+    std::vector<double> cp((size_t)S.ns, 0.0);
+    double crit = 0.0;
+    for (int32_t s = S.ns - 1; s >= 0; --s) {   // parents after their children: walk down from the roots
+        const int32_t k = S.sn_c0[(size_t)s + 1] - S.sn_c0[(size_t)s];
+        const int32_t r = (int32_t)(S.sn_rows_ptr[(size_t)s + 1] - S.sn_rows_ptr[(size_t)s]);
+        const int32_t nch = (int32_t)(S.child_ptr[(size_t)s + 1] - S.child_ptr[(size_t)s]);
+        const int32_t m3 = 3 * (k + r);
+        const double est = (m3 <= 96 && nch <= 8) ? 4.0 + 0.06 * m3 + 0.9 * (3 * k) : 10.0 + 20.0 * ((3 * k + 23) / 24);
+        const int32_t p = S.sn_parent[(size_t)s];
+        cp[(size_t)s] = est + (p >= 0 ? cp[(size_t)p] : 0.0);
+        crit = std::max(crit, cp[(size_t)s]);
+    }
+    return crit;
+}
+
+// The batch symbolic analysis (once per pattern): nested-dissection orders under two separator
+// rules (round 2's, and the 8-start search with the sqrt-ratio score), each carried through the
+// supernodal analysis, and the one whose critical-path estimate is shortest is kept.  Config 4
+// (tools/nd_ab_job.sh, profiles/r03/v11_nd_ab.txt): factor + solve 0.860 -> 0.770 ms, chord-step
+// solves 0.250 -> 0.257 ms; config 3 keeps round 2's order (0.282 ms, the others 0.31-0.34).
+// The incremental graph (dpg_incsym_reset) keeps round 2's rule: it reorders every 64 nodes and
+// pays the search each time.  DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order;
+// DPG_CHOL_ND=<k> only candidate k of {round 2, 2-start, 8-start, 4-start ratio} (A/B).
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                       const dpg_chol_opts* opts, dpg_chol_sym* S) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
-    return dpg_chol_sym_from_patterns(n, perm, pat, opts, S);
+    if (getenv("DPG_CHOL_ORDER") || n < 256) {
+        if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+        return dpg_chol_sym_from_patterns(n, perm, pat, opts, S);
+    }
+    struct Cand { int32_t starts, bal, score; };
+    static const Cand cands[] = {{0, 5, 0}, {2, 4, 2}, {8, 4, 2}, {4, 5, 1}};
+    const char* only = getenv("DPG_CHOL_ND");
+    static const int kDefault[] = {0, 2};
+    int pick[2];
+    int np = 0;
+    if (only) pick[np++] = std::max(0, std::min(3, atoi(only)));
+    else for (int k : kDefault) pick[np++] = k;
+    double best = -1.0;
+    for (int j = 0; j < np; ++j) {
+        const int k = pick[j];
+        if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, perm,
+                                  pat))
+            return -1;
+        dpg_chol_sym T;
+        if (dpg_chol_sym_from_patterns(n, perm, pat, opts, &T)) return -1;
+        const double cp = dpg_chol_critical_path_us(T);
+        if (best < 0.0 || cp < best) {
+            best = cp;
+            *S = std::move(T);
+        }
+    }
+    return 0;
 }
 
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,

@@ -1,7 +1,7 @@
 // order_eval.cpp -- compare fill-reducing orders for the GPU Cholesky on a pose graph (host only):
 // minimum degree vs nested dissection (several leaf sizes).  For each: fill (blocks), factor Mflop,
 // supernodes, elimination-tree levels, largest front and the critical-path estimate the fused DAG
-// factorization schedules by (dpg_chol.hip chol_plan: 4 + 0.05 m3 us for a small front, 10 + 20 us
+// factorization schedules by (dpg_chol.hip chol_plan: 4 + 0.06 m3 + 0.9 k3 us for a small front, 10 + 20 us
 // per 24-column panel for a large one, summed along the longest leaf-to-root path), plus the
 // ordering time.
 // usage: order_eval PAIRS.bin        (int32 n, int32 P, then P x (lo, hi))
@@ -33,7 +33,7 @@ static void report(const char* name, double ms, const dpg_chol_sym& S) {
         const int32_t r = (int32_t)(S.sn_rows_ptr[(size_t)s + 1] - S.sn_rows_ptr[(size_t)s]);
         const int32_t nch = (int32_t)(S.child_ptr[(size_t)s + 1] - S.child_ptr[(size_t)s]);
         const int32_t m3 = 3 * (k + r);
-        const double est = (m3 <= 96 && nch <= 8) ? 4.0 + 0.05 * m3 : 10.0 + 20.0 * ((3 * k + 23) / 24);
+        const double est = (m3 <= 96 && nch <= 8) ? 4.0 + 0.06 * m3 + 0.9 * (3 * k) : 10.0 + 20.0 * ((3 * k + 23) / 24);
         const int32_t p = S.sn_parent[(size_t)s];
         cp[(size_t)s] = est + (p >= 0 ? cp[(size_t)p] : 0.0);
         crit = std::max(crit, cp[(size_t)s]);
@@ -65,6 +65,25 @@ int main(int argc, char** argv) {
         dpg_chol_sym S;
         dpg_chol_sym_from_patterns(n, perm, pat, &o, &S);
         report("min-degree", ms, S);
+    }
+    for (int k = 0; k < 4; ++k) {   // the batch analysis' candidates (dpg_chol_symbolic picks the shortest path)
+        static const int prm[4][3] = {{0, 5, 0}, {2, 4, 2}, {8, 4, 2}, {4, 5, 1}};
+        std::vector<int32_t> perm;
+        std::vector<std::vector<int32_t>> pat;
+        const double t = now_ms();
+        if (dpg_chol_order_nd_sep(n, lo.data(), hi.data(), P, 16, prm[k][0], prm[k][1], prm[k][2], perm, pat)) return 3;
+        const double ms = now_ms() - t;
+        dpg_chol_sym S;
+        if (dpg_chol_sym_from_patterns(n, perm, pat, &o, &S)) return 4;
+        char name[32];
+        snprintf(name, sizeof(name), "sep/%d", k);
+        report(name, ms, S);
+    }
+    {
+        const double t = now_ms();
+        dpg_chol_sym S;
+        if (dpg_chol_symbolic(n, lo.data(), hi.data(), P, &o, &S)) return 5;
+        report("batch-pick", now_ms() - t, S);
     }
     for (int leaf : {32, 64, 128, 256, 512}) {
         std::vector<int32_t> perm;
