@@ -477,8 +477,8 @@ double dpg_chol_critical_path_us(const dpg_chol_sym& S) {
 // supernodal analysis, and the one whose critical-path estimate is shortest is kept.  Config 4
 // (tools/nd_ab_job.sh, profiles/r03/v11_nd_ab.txt): factor + solve 0.860 -> 0.770 ms, chord-step
 // solves 0.250 -> 0.257 ms; config 3 keeps round 2's order (0.282 ms, the others 0.31-0.34).
-// The incremental graph (dpg_incsym_reset) keeps round 2's rule: it reorders every 64 nodes and
-// pays the search each time.  DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order;
+// The incremental graph (dpg_incsym_reset) reorders every 64 nodes and uses the 2-start search
+// alone.  DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order;
 // DPG_CHOL_ND=<k> only candidate k of {round 2, 2-start, 8-start, 4-start ratio} (A/B).
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                       const dpg_chol_opts* opts, dpg_chol_sym* S) {
@@ -746,7 +746,15 @@ inline void for_rows_after(const dpg_chol_incsym* I, int64_t j, int64_t after, F
 int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+    // the multi-start separator search with 2 starts and the sqrt-ratio score (config 4's arrival
+    // sequence, tools/incsym_bench: critical-path estimate 915 -> 785 us, fill -14 %, host work per
+    // update 2.02 -> 1.87 ms on the build host); DPG_INC_ND=0 restores round 2's rule,
+    // DPG_INC_ND=<starts> another start count (A/B)
+    static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : 2; }();
+    const int rc = (inc_nd > 0 && !getenv("DPG_CHOL_ORDER"))
+                       ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, perm, pat)
+                       : dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat);
+    if (rc) return -1;
     I->n = n;
     I->words = std::max<int64_t>(64, (n + 63) / 64 * 2);
     I->swords = (I->words + 63) / 64;
