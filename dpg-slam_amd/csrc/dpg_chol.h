@@ -45,9 +45,10 @@ int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, in
 int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                       std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
 // the same with the separator rule of the multi-start search (starts = 0: round 2's rule; bal:
-// both sides >= 1 / bal of the part; score 0 |S|, 1 |S| N / min side, 2 |S| sqrt(N / min side))
+// both sides >= 1 / bal of the part; score 0 |S|, 1 |S| N / min side, 2 |S| sqrt(N / min side);
+// cover: the chosen cut's separator as a minimum vertex cover of its crossing edges)
 int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
-                          int32_t starts, int32_t bal, int32_t score, std::vector<int32_t>& perm,
+                          int32_t starts, int32_t bal, int32_t score, bool cover, std::vector<int32_t>& perm,
                           std::vector<std::vector<int32_t>>& pat);
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
                                const dpg_chol_opts* opts, dpg_chol_sym* S);

@@ -114,6 +114,7 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
 // picks among such orders by that path's estimate).
 struct NdParams {
     int32_t starts = 0, bal = 5, score = 0;
+    bool cover = false;   // the chosen cut's separator as a minimum vertex cover of its crossing edges
 };
 struct NdState {
     const int64_t* aptr;
@@ -121,7 +122,7 @@ struct NdState {
     int32_t leaf;
     NdParams prm;
     int32_t next_id = 0;
-    std::vector<int32_t> stamp, lvl, queue;
+    std::vector<int32_t> stamp, lvl, queue, aux;
     std::vector<int32_t>* out;
 };
 
@@ -235,16 +236,89 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         return false;
     };
     std::vector<int32_t> A, B, S;
-    for (int32_t v : sub) {
-        const int32_t l = st.lvl[(size_t)v];
-        if (!bupper) {
-            if (l < bm) A.push_back(v);
-            else if (l > bm) B.push_back(v);
-            else (touches(v, bm + 1) ? S : A).push_back(v);
-        } else {
-            if (l <= bm) A.push_back(v);
-            else if (l > bm + 1) B.push_back(v);
-            else (touches(v, bm) ? S : B).push_back(v);
+    if (st.prm.cover) {
+        // the cut's crossing edges join X (level bm, touching bm + 1) and Y (level bm + 1, touching
+        // bm); a minimum vertex cover of that bipartite graph (maximum matching, Konig) is the
+        // smallest separator this cut admits -- never larger than either side's boundary
+        std::vector<int32_t> X, Y;
+        for (int32_t v : sub) {
+            const int32_t l = st.lvl[(size_t)v];
+            if (l == bm && touches(v, bm + 1)) { st.aux[(size_t)v] = (int32_t)X.size(); X.push_back(v); }
+            else if (l == bm + 1 && touches(v, bm)) { st.aux[(size_t)v] = (int32_t)Y.size(); Y.push_back(v); }
+        }
+        std::vector<int64_t> xp(X.size() + 1, 0);
+        std::vector<int32_t> xa;
+        for (size_t i = 0; i < X.size(); ++i) {
+            const int32_t v = X[i];
+            for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
+                const int32_t u = st.adj[(size_t)t];
+                if (st.stamp[(size_t)u] == id && st.lvl[(size_t)u] == bm + 1) xa.push_back(st.aux[(size_t)u]);
+            }
+            xp[i + 1] = (int64_t)xa.size();
+        }
+        std::vector<int32_t> mx(X.size(), -1), my(Y.size(), -1), seen(Y.size(), -1);
+        // Kuhn's augmenting paths, iterative (the path stack holds (x, next edge))
+        std::vector<std::pair<int32_t, int64_t>> stk;
+        for (int32_t x0 = 0; x0 < (int32_t)X.size(); ++x0) {
+            stk.assign(1, {x0, xp[(size_t)x0]});
+            bool found = false;
+            while (!stk.empty() && !found) {
+                auto& top = stk.back();
+                const int32_t x = top.first;
+                if (top.second == xp[(size_t)x + 1]) { stk.pop_back(); continue; }
+                const int32_t y = xa[(size_t)top.second++];
+                if (seen[(size_t)y] == x0) continue;
+                seen[(size_t)y] = x0;
+                if (my[(size_t)y] < 0) {   // augment along the stack
+                    int32_t yy = y;
+                    for (size_t k = stk.size(); k-- > 0;) {
+                        const int32_t xx = stk[k].first, prev = mx[(size_t)xx];
+                        mx[(size_t)xx] = yy;
+                        my[(size_t)yy] = xx;
+                        yy = prev;
+                    }
+                    found = true;
+                } else {
+                    stk.push_back({my[(size_t)y], xp[(size_t)my[(size_t)y]]});
+                }
+            }
+        }
+        // Konig: Z = reachable from the unmatched X by alternating paths; cover = (X \ Z) + (Y in Z)
+        std::vector<char> zx(X.size(), 0), zy(Y.size(), 0);
+        std::vector<int32_t> q;
+        for (int32_t x = 0; x < (int32_t)X.size(); ++x)
+            if (mx[(size_t)x] < 0) { zx[(size_t)x] = 1; q.push_back(x); }
+        for (size_t qi = 0; qi < q.size(); ++qi) {
+            const int32_t x = q[qi];
+            for (int64_t t = xp[(size_t)x]; t < xp[(size_t)x + 1]; ++t) {
+                const int32_t y = xa[(size_t)t];
+                if (zy[(size_t)y] || mx[(size_t)x] == y) continue;
+                zy[(size_t)y] = 1;
+                const int32_t x2 = my[(size_t)y];
+                if (x2 >= 0 && !zx[(size_t)x2]) { zx[(size_t)x2] = 1; q.push_back(x2); }
+            }
+        }
+        for (size_t i = 0; i < X.size(); ++i) st.aux[(size_t)X[i]] = zx[i] ? -1 : -2;   // -2: in the cover
+        for (size_t j = 0; j < Y.size(); ++j) st.aux[(size_t)Y[j]] = zy[j] ? -2 : -1;
+        for (int32_t v : sub) {
+            const int32_t l = st.lvl[(size_t)v];
+            const bool in_cover = (l == bm || l == bm + 1) && st.aux[(size_t)v] == -2;
+            (in_cover ? S : l <= bm ? A : B).push_back(v);
+        }
+        for (int32_t v : X) st.aux[(size_t)v] = -1;
+        for (int32_t v : Y) st.aux[(size_t)v] = -1;
+    } else {
+        for (int32_t v : sub) {
+            const int32_t l = st.lvl[(size_t)v];
+            if (!bupper) {
+                if (l < bm) A.push_back(v);
+                else if (l > bm) B.push_back(v);
+                else (touches(v, bm + 1) ? S : A).push_back(v);
+            } else {
+                if (l <= bm) A.push_back(v);
+                else if (l > bm + 1) B.push_back(v);
+                else (touches(v, bm) ? S : B).push_back(v);
+            }
         }
     }
     nd_rec(st, A);
@@ -381,11 +455,11 @@ void patterns_of_order(int64_t n, const std::vector<int64_t>& aptr, const std::v
 
 int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                       std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
-    return dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, leaf, 0, 5, 0, perm, pat);
+    return dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, leaf, 0, 5, 0, false, perm, pat);
 }
 
 int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
-                          int32_t starts, int32_t bal, int32_t score, std::vector<int32_t>& perm,
+                          int32_t starts, int32_t bal, int32_t score, bool cover, std::vector<int32_t>& perm,
                           std::vector<std::vector<int32_t>>& pat) {
     if (n <= 0) return -1;
     std::vector<int64_t> aptr((size_t)n + 1, 0);
@@ -406,6 +480,8 @@ int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair
     st.prm.starts = starts;
     st.prm.bal = std::max<int32_t>(bal, 2);
     st.prm.score = score;
+    st.prm.cover = cover && starts > 0 && getenv("DPG_ND_NOCOVER") == nullptr;
+    st.aux.assign((size_t)n, -1);
     st.stamp.assign((size_t)n, 0);
     st.lvl.assign((size_t)n, -1);
     perm.clear();
@@ -473,13 +549,15 @@ double dpg_chol_critical_path_us(const dpg_chol_sym& S) {
 }
 
 // The batch symbolic analysis (once per pattern): nested-dissection orders under two separator
-// rules (round 2's, and the 8-start search with the sqrt-ratio score), each carried through the
-// supernodal analysis, and the one whose critical-path estimate is shortest is kept.  Config 4
-// (tools/nd_ab_job.sh, profiles/r03/v11_nd_ab.txt): factor + solve 0.860 -> 0.770 ms, chord-step
-// solves 0.250 -> 0.257 ms; config 3 keeps round 2's order (0.282 ms, the others 0.31-0.34).
+// rules (round 2's, and the 8-start search with the sqrt-ratio score and minimum-vertex-cover
+// separators), each carried through the supernodal analysis, and the one whose critical-path
+// estimate is shortest is kept.  Config 4 (tools/nd_ab2_job.sh, profiles/r03/v15_nd_cover_ab.txt):
+// factor + solve 0.860 -> 0.716 ms, chord-step solves 0.251 -> 0.230 ms; config 3 keeps round 2's
+// order (0.282 ms; the others 0.29-0.34).
 // The incremental graph (dpg_incsym_reset) reorders every 64 nodes and uses the 2-start search
-// alone.  DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order;
-// DPG_CHOL_ND=<k> only candidate k of {round 2, 2-start, 8-start, 4-start ratio} (A/B).
+// alone, without the cover step (measured per node: p90 2.50 ms with it, 2.23 without).
+// DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order; DPG_CHOL_ND=<k> only candidate k
+// of {round 2, 2-start, 8-start, 4-start ratio} (A/B); DPG_ND_NOCOVER drops the cover step.
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                       const dpg_chol_opts* opts, dpg_chol_sym* S) {
     std::vector<int32_t> perm;
@@ -499,8 +577,8 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
     double best = -1.0;
     for (int j = 0; j < np; ++j) {
         const int k = pick[j];
-        if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, perm,
-                                  pat))
+        if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, true,
+                                  perm, pat))
             return -1;
         dpg_chol_sym T;
         if (dpg_chol_sym_from_patterns(n, perm, pat, opts, &T)) return -1;
@@ -752,7 +830,7 @@ int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, cons
     // DPG_INC_ND=<starts> another start count (A/B)
     static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : 2; }();
     const int rc = (inc_nd > 0 && !getenv("DPG_CHOL_ORDER"))
-                       ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, perm, pat)
+                       ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, false, perm, pat)
                        : dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat);
     if (rc) return -1;
     I->n = n;

@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
         std::vector<int32_t> perm;
         std::vector<std::vector<int32_t>> pat;
         const double t = now_ms();
-        if (dpg_chol_order_nd_sep(n, lo.data(), hi.data(), P, 16, prm[k][0], prm[k][1], prm[k][2], perm, pat)) return 3;
+        if (dpg_chol_order_nd_sep(n, lo.data(), hi.data(), P, 16, prm[k][0], prm[k][1], prm[k][2], k > 0, perm, pat)) return 3;
         const double ms = now_ms() - t;
         dpg_chol_sym S;
         if (dpg_chol_sym_from_patterns(n, perm, pat, &o, &S)) return 4;
