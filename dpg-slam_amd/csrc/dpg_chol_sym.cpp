@@ -554,8 +554,8 @@ double dpg_chol_critical_path_us(const dpg_chol_sym& S) {
 // estimate is shortest is kept.  Config 4 (tools/nd_ab2_job.sh, profiles/r03/v15_nd_cover_ab.txt):
 // factor + solve 0.860 -> 0.716 ms, chord-step solves 0.251 -> 0.230 ms; config 3 keeps round 2's
 // order (0.282 ms; the others 0.29-0.34).
-// The incremental graph (dpg_incsym_reset) reorders every 64 nodes and uses the 2-start search
-// alone, without the cover step (measured per node: p90 2.50 ms with it, 2.23 without).
+// The incremental graph (dpg_incsym_reset) reorders every 64 nodes with round 2's rule (the
+// 2-start search is an option there, DPG_INC_ND: a gain on config 4's graph, a loss on config 5's).
 // DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order; DPG_CHOL_ND=<k> only candidate k
 // of {round 2, 2-start, 8-start, 4-start ratio} (A/B); DPG_ND_NOCOVER drops the cover step.
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
@@ -824,11 +824,12 @@ inline void for_rows_after(const dpg_chol_incsym* I, int64_t j, int64_t after, F
 int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    // the multi-start separator search with 2 starts and the sqrt-ratio score (config 4's arrival
-    // sequence, tools/incsym_bench: critical-path estimate 915 -> 785 us, fill -14 %, host work per
-    // update 2.02 -> 1.87 ms on the build host); DPG_INC_ND=0 restores round 2's rule,
-    // DPG_INC_ND=<starts> another start count (A/B)
-    static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : 2; }();
+    // round 2's separator rule by default.  DPG_INC_ND=<starts> selects the multi-start search
+    // (sqrt-ratio score, no cover step): on config 4's arrival sequence per-node p50 2.33 -> 2.04 ms
+    // and p90 2.81 -> 2.22 ms (fill -14 %), but on config 5's four-pass route 380 -> 362 nodes/s and
+    // p90 4.2 -> 4.5 ms (the reorders cost more there and the fronts come out no better) --
+    // profiles/r03/v13_inc_nd*.json, v17_c5_inc_nd_ab.txt
+    static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : 0; }();
     const int rc = (inc_nd > 0 && !getenv("DPG_CHOL_ORDER"))
                        ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, false, perm, pat)
                        : dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat);
