@@ -598,6 +598,8 @@ def main():
     ap.add_argument("--cpu-dpg-calls", type=int, default=30, help="executeDPG calls replayed on the oracle")
     ap.add_argument("--dpg-param", action="append", default=[],
                     help="DpgParameters override, e.g. occ_grid_resolution=0.1 or num_sectors=8 (repeatable)")
+    ap.add_argument("--gn-loop", default="native", choices=["native", "python"],
+                    help="N=1 GN loop: dpg_gn_run, or the per-iteration host loop every rank runs at N>1")
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
     ap.add_argument("--inc-nodes", type=int, default=5000)
     ap.add_argument("--cpu-nodes", type=int, default=8, help="nodes in the incremental CPU-baseline sample")
@@ -653,11 +655,16 @@ def main():
     backend = D.DeviceBackend(ctx, hb_size, hb_size - 2, dev)
     allreduce = (lambda hb: dist.all_reduce(hb)) if world > 1 else (lambda hb: None)
     X0 = w.est.astype(np.float64)
+    # one rank has nothing to all-reduce: the loop runs natively (dpg_gn_run, same iterations and
+    # convergence test as dist.gn_loop, no interpreter between the launches)
+    native_gn = world == 1 and args.gn_loop == "native"
 
     def step():
         ctx.icp_run(compute_cov=True)
         ctx.gn_take_icp(w.icp_factor_first + e0, e1 - e0, pl.n_always_local, params)
         ctx.gn_set_poses(X0)
+        if native_gn:
+            return ctx.gn_run()[0]
         return D.gn_loop(backend, allreduce, gp)
 
     def barrier():
@@ -695,7 +702,8 @@ def main():
     stats = {"icp_kernel_ms": k_ms, "cov_kernel_ms": float(np.mean(cov_ms)), "index_build_ms": float(np.mean(idx_ms)), "gn_iterations": float(np.mean(gn_iters)), "gn_factorizations": float(np.mean(n_fact)),
              "ms_per_gn_iter": float(np.mean(gn_ms) / max(1.0, np.mean(gn_iters))),
              "icp_iters_mean": float(res["iterations"].mean()), "icp_iters_max": int(res["iterations"].max()),
-             "final_error": st["final_error"], "pcg_iterations": st["pcg_iterations"]}
+             "final_error": st["final_error"], "pcg_iterations": st["pcg_iterations"],
+             "gn_loop": "native" if native_gn else "python"}
     if world > 1:
         t = torch.tensor([stats["icp_kernel_ms"], stats["ms_per_gn_iter"]], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -771,6 +779,8 @@ def main():
             "ms_per_gn_iter": stats["ms_per_gn_iter"],
             "gn_iterations": stats["gn_iterations"],
             "gn_factorizations": stats["gn_factorizations"],
+            "gn_loop": stats["gn_loop"],
+            "final_error": stats["final_error"],
             "icp_kernel_ms": stats["icp_kernel_ms"],
             "cov_kernel_ms": stats["cov_kernel_ms"],
             "index_build_ms": stats["index_build_ms"],

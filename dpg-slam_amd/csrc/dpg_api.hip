@@ -1091,7 +1091,8 @@ static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0,
             cur = nw;
         }
     }
-    if ((rc = dpg_gn_get_poses(c, poses))) return rc;
+    if (poses && (rc = dpg_gn_get_poses(c, poses))) return rc;
+    if (!poses) HIP_TRY(hipStreamSynchronize(c->stream));
     const double t2 = now_ms();
     S.iterations = it;
     S.final_error = nw;
@@ -1173,6 +1174,17 @@ static int gn_loop_multi(dpg_ctx* c, const dpg_gn_params& P, double* poses, doub
     S.ms_per_iteration = it ? (t2 - t1) / it : 0.0;
     if (st) *st = S;
     return DPG_OK;
+}
+
+// The GN loop on the graph staged by dpg_gn_setup (+ dpg_gn_take_icp_measurements) from the poses
+// of dpg_gn_set_poses, with the setup's parameters: what a host loop over the step API does with
+// one rank, natively (one synchronisation per iteration, no interpreter between the launches)
+int dpg_gn_run(dpg_ctx* c, double* poses_out, dpg_gn_stats* st) {
+    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "dpg_gn_run: graph not set up");
+    if (is_multi(c)) return fail(DPG_ERR_STATE, "dpg_gn_run: a multi-GPU context runs dpg_optimize_graph");
+    HIP_TRY(hipSetDevice(c->device));
+    const double t0 = now_ms();
+    return gn_loop(c, c->gp, poses_out, t0, t0, st);
 }
 
 // every device of a multi-GPU context: the whole graph, linearizing factors [b_k, e_k) (equal

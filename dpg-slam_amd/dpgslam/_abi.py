@@ -267,6 +267,7 @@ SIGNATURES = {
     "dpg_gn_solve_retract_async": (C.c_int, [P, P]),
     "dpg_gn_fetch": (C.c_int, [P, P, F64P]),
     "dpg_gn_factorizations": (C.c_int32, [P]),
+    "dpg_gn_run": (C.c_int, [P, F64P, C.POINTER(GnStats)]),
     "dpg_gn_last_assemble_ms": (C.c_float, [P]),
     "dpg_gn_last_solve_ms": (C.c_float, [P]),
     "icp_cov_calculate": (C.c_int, [P, F32P, C.c_int64, F32P, C.c_int64, F32P, C.c_float, C.c_float,

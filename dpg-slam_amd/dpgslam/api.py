@@ -296,6 +296,15 @@ class Context:
         X = _f64(poses).reshape(-1, 3)
         check(lib().dpg_gn_set_poses(self.handle, ptr(X, C.c_double)), "dpg_gn_set_poses")
 
+    def gn_run(self, V: int | None = None):
+        """The whole GN loop natively (dpg_gn_run) from the poses of gn_set_poses; returns
+        (stats dict, poses [V, 3] or None when V is None)."""
+        X = np.empty((V, 3), np.float64) if V else None
+        st = _abi.GnStats()
+        check(lib().dpg_gn_run(self.handle, ptr(X, C.c_double) if X is not None else None, C.byref(st)),
+              "dpg_gn_run")
+        return {k: getattr(st, k) for k, _ in _abi.GnStats._fields_}, X
+
     def gn_get_poses(self, V: int) -> np.ndarray:
         X = np.empty((V, 3), np.float64)
         check(lib().dpg_gn_get_poses(self.handle, ptr(X, C.c_double)), "dpg_gn_get_poses")

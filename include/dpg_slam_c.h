@@ -272,6 +272,11 @@ int dpg_gn_solve_retract(dpg_ctx* ctx, const double* hb_dev, double* delta_inf, 
  * (0 = ok, 1 = H not positive definite, 2 = solver timeout)}. */
 int dpg_gn_solve_retract_async(dpg_ctx* ctx, const double* hb_dev);
 int dpg_gn_fetch(dpg_ctx* ctx, const double* hb_dev, double out[3]);
+/* The whole Gauss-Newton loop over the step API on one device (assemble, then solve + retract +
+ * re-linearize + one read per iteration, the setup's parameters), from the poses of the last
+ * dpg_gn_set_poses; poses_out[V][3] (may be NULL) receives the result.  A single-device context
+ * (a multi-GPU one runs dpg_optimize_graph). */
+int dpg_gn_run(dpg_ctx* ctx, double* poses_out, dpg_gn_stats* stats);
 /* Cholesky factorizations since the last dpg_gn_set_poses (the other solves reused one). */
 int32_t dpg_gn_factorizations(dpg_ctx* ctx);
 float dpg_gn_last_assemble_ms(dpg_ctx* ctx);

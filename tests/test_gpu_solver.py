@@ -76,6 +76,12 @@ def test_async_gn_loop_matches_optimize_graph(ctx, workload):
     Xa = ctx.gn_get_poses(w.V)
     assert st["iterations"] == sc.iterations
     np.testing.assert_array_equal(Xa, Xc)
+    # dpg_gn_run: the same loop natively, from the same staged graph and poses
+    ctx.gn_set_poses(X0)
+    sn, Xn = ctx.gn_run(w.V)
+    assert sn["iterations"] == sc.iterations
+    assert sn["final_error"] == st["final_error"]
+    np.testing.assert_array_equal(Xn, Xc)
 
 
 @pytest.mark.parametrize("name", ["config3", "config4"])
