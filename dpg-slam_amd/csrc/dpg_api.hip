@@ -28,6 +28,7 @@
 
 #include "../../include/dpg_icp_cov.h"
 #include "../../include/dpg_slam_c.h"
+#include "dpg_gn_pipe.h"
 #include "dpg_internal.h"
 
 namespace {
@@ -140,6 +141,10 @@ struct dpg_ctx {
     bool gn_ready = false;
     dpg_gn_params gp{};
     float asm_ms = 0.f, solve_ms = 0.f;
+    // the pipelined GN loop (dpg_gn_pipe.h): control block, two host-mapped report slots + events
+    dpg_gn_ctl* pipe_ctl = nullptr;
+    dpg_gn_slot* pipe_slot = nullptr;
+    hipEvent_t pipe_ev[2] = {};
     // multi-GPU form (dpg_ctx_create_multi): this context drives device 0 of the set, `peers` are
     // full single-device contexts of the others; one RCCL communicator per device
     // (ncclCommInitAll, one process); `shard[k]` = the caller's edge indices staged on device k
@@ -338,6 +343,9 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     c->s_off.release(); c->s_tree_pts.release(); c->s_tree_idx.release();
     c->buckets.release(); c->s_buckets.release(); c->icp_scratch.release();
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
+    if (c->pipe_ctl) (void)hipFree(c->pipe_ctl);
+    if (c->pipe_slot) (void)hipHostFree(c->pipe_slot);
+    for (auto& e : c->pipe_ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->map_ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1064,6 +1072,8 @@ static int check_conv(const dpg_gn_params* gp, double cur, double nw) {
 
 // The Gauss-Newton loop on a set-up graph whose poses are set: solve + retract + re-linearize
 // enqueued back to back, one synchronisation per iteration.  t1: when the iterations started.
+static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it);
+
 static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0, double t1, dpg_gn_stats* st) {
     dpg_gn_stats S;
     memset(&S, 0, sizeof(S));
@@ -1071,7 +1081,11 @@ static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0,
     if ((rc = dpg_gn_assemble(c, nullptr)) || (rc = read_error(c, &S.initial_error))) return rc;
     double cur = S.initial_error, nw = cur, dinf = 0.0;
     int it = 0;
-    if (!(cur <= 0.0) && P.max_iterations > 0) {
+    static const bool pipe_env = !(getenv("DPG_GN_PIPE") && atoi(getenv("DPG_GN_PIPE")) == 0);
+    const bool pipe = pipe_env && P.linear_solver == DPG_SOLVER_CHOLESKY && c->gn.chol && dpg_chol_gated_ok(c->gn.chol);
+    if (pipe && !(cur <= 0.0) && P.max_iterations > 0) {
+        if ((rc = gn_loop_pipe(c, P, S, nw, dinf, it))) return rc;
+    } else if (!(cur <= 0.0) && P.max_iterations > 0) {
         for (;;) {
             double sc[3];
             if ((rc = dpg_gn_solve_retract_async(c, nullptr)) || (rc = dpg_gn_assemble(c, nullptr)) ||
@@ -1100,6 +1114,57 @@ static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0,
     S.ms_total = t2 - t0;
     S.ms_per_iteration = it ? (t2 - t1) / it : 0.0;
     if (st) *st = S;
+    return DPG_OK;
+}
+
+// gn_loop's iterations with the decisions on the device (dpg_gn_pipe.h): iteration k + 1 is queued
+// before iteration k's report is read, so the GPU never waits for the host
+static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it) {
+    if (!c->pipe_ctl) {
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pipe_ctl), sizeof(dpg_gn_ctl)));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pipe_slot), 2 * sizeof(dpg_gn_slot), hipHostMallocMapped | hipHostMallocCoherent));
+        for (auto& e : c->pipe_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    dpg_gn_dev* g = &c->gn;
+    int rc;
+    if ((rc = dpg_gn_pipe_init(g, &P, c->pipe_ctl, S.initial_error, c->stream)))
+        return fail(rc, "GN pipeline launch failed");
+    volatile dpg_gn_slot* slot = c->pipe_slot;
+    auto issue = [&](int k) -> int {   // iteration k (1-based) reports into slot k & 1
+        int r = dpg_gn_pipe_issue(g, &P, c->pipe_ctl, c->pipe_slot + (k & 1), c->stream);
+        if (r) return fail(r, "GN pipeline launch failed: %s", hipGetErrorString(hipGetLastError()));
+        HIP_TRY(hipEventRecord(c->pipe_ev[k & 1], c->stream));
+        return DPG_OK;
+    };
+    if ((rc = issue(1))) return rc;
+    int issued = 1, nfact = 0, reuse_last = g->last_was_chord;
+    for (int k = 1;; ++k) {
+        if (issued < P.max_iterations) {
+            if ((rc = issue(k + 1))) return rc;
+            ++issued;
+        }
+        HIP_TRY(hipEventSynchronize(c->pipe_ev[k & 1]));
+        const dpg_gn_slot o = const_cast<const dpg_gn_slot&>(slot[k & 1]);
+        if (!o.active || o.it != k) return fail(DPG_ERR_STATE, "GN pipeline out of step (iteration %d)", k);
+        if (o.status != 0.0) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)o.status);
+        }
+        it = k;
+        if (!o.reuse) ++nfact;
+        g->prev_delta_inf = g->last_delta_inf;
+        g->last_delta_inf = o.dinf;
+        reuse_last = o.reuse;
+        dinf = o.dinf;
+        nw = o.error;
+        if (o.final_) break;
+    }
+    // the host bookkeeping the step API continues from (as after the host loop)
+    g->last_was_chord = reuse_last;
+    g->have_factor = 1;
+    g->n_factorizations += nfact;
+    g->last_used_chol = 1;
+    S.pcg_iterations = 0;
     return DPG_OK;
 }
 

@@ -358,6 +358,15 @@ __device__ __forceinline__ void wait_geq_sc1(int32_t* w, int32_t target, int32_t
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// A pipelined Gauss-Newton loop (dpg_gn_pipe.h) enqueues both solve paths of an iteration before
+// the previous one is read: gate[0] = the iteration runs, gate[1] = it reuses the factor.  mode 0
+// runs when active, 1 when active and refactoring, 2 when active and reusing; no gate: always.
+__device__ __forceinline__ bool gate_off(const int32_t* gate, int mode) {
+    if (!gate) return false;
+    const int32_t a = gate[0], r = gate[1];   // written by an earlier launch
+    return !a || (mode == 1 && r) || (mode == 2 && !r);
+}
+
 __device__ __forceinline__ int claim_lds(const int32_t* order, int32_t* ticket, int* slot) {
     if (threadIdx.x == 0) *slot = order[atomicAdd(ticket, 1)];
     __syncthreads();
@@ -766,10 +775,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                        const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm,
                                                        double* __restrict__ ysol, double* acc, int R,
-                                                       const double* __restrict__ dinv) {
+                                                       const double* __restrict__ dinv, const int32_t* gate) {
     extern __shared__ __attribute__((aligned(16))) double smem_fw[];
     double* sm = smem_fw + 2;   // smem_fw[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
+    if (gate_off(gate, 2)) return;
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_fw));
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
@@ -906,10 +916,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                         const SolveSeg* __restrict__ segs,
                                                         const double* __restrict__ fronts,
                                                         const double* __restrict__ ysol, double* xsol, int R,
-                                                        int max_seg, const double* __restrict__ dinv) {
+                                                        int max_seg, const double* __restrict__ dinv,
+                                                        const int32_t* gate) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
+    if (gate_off(gate, 0)) return;
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_b));
     const SnDev S = sns[s];
     BW_MARK(s, 0);
@@ -1658,9 +1670,11 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
                                                        const FChild* __restrict__ fchild,
                                                        const double* __restrict__ hb, const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm, double* fronts,
-                                                       double* __restrict__ ysol, double* acc, int ns, int db) {
+                                                       double* __restrict__ ysol, double* acc, int ns, int db,
+                                                       const int32_t* gate) {
     extern __shared__ __attribute__((aligned(16))) double smem_f[];
     double* sm = smem_f + 2;   // smem_f[0]: the claimed ticket (no static LDS: keeps the base 16-B aligned)
+    if (gate_off(gate, 1)) return;
     const int code = claim_lds(order, sync, reinterpret_cast<int*>(smem_f));
     const int s = code >> 6, mem = code & 63;
     const SnDev S = sns[s];
@@ -2398,12 +2412,12 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
         hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
                            c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
                            c->perm, c->fronts,
-                           c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0);
+                           c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, nullptr);
         if (c->use_dinv && c->n_dblocks > 0)
             hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                            c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg,
-                           c->use_dinv ? c->dinv : nullptr);
+                           c->use_dinv ? c->dinv : nullptr, nullptr);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -2427,9 +2441,9 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
         hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
     const double* di = c->use_dinv ? c->dinv : nullptr;
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di);
+                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2442,9 +2456,39 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
     const double* di = c->use_dinv ? c->dinv : nullptr;   // inverted by the factorization's dpg_chol_solve
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+// one Gauss-Newton iteration's solve with the path chosen on the device (gate, see gate_off):
+// the fused factorization + forward solve, or the forward solve with the last factor, then the
+// backward solve.  Only the fused plan without inverted diagonal blocks (dpg_chol_gated_ok).
+extern "C" int dpg_chol_gated_ok(void* h) {
+    const CholDev* c = reinterpret_cast<const CholDev*>(h);
+    return c && c->fused && !(c->use_dinv && c->n_dblocks > 0) ? 1 : 0;
+}
+
+extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* gate, void* stream) {
+    CholDev* c = reinterpret_cast<CholDev*>(h);
+    if (!dpg_chol_gated_ok(h)) return DPG_ERR_STATE;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const dpg_chol_sym& S = c->sym;
+    const double* g = hb + 9 * c->nnzb_upper;
+    // the status word is read (by the iteration's control kernel) before the next iteration clears it
+    if (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess ||
+        hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess)
+        return DPG_ERR_HIP;
+    hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
+                       c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
+                       c->perm, c->fronts, c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, gate);
+    hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage,
+                       nullptr, gate);
+    hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol,
+                       c->solve_stage, c->solve_maxseg, nullptr, gate);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "dpg_internal.h"
+#include "dpg_gn_pipe.h"
 
 namespace {
 
@@ -90,9 +91,9 @@ __device__ __forceinline__ void atwb_acc(const double* A, const double* w, const
 // g_i term, [21..23] the g_j term, [24] chi2 term.
 constexpr int kContrib = 25;
 __global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X, int64_t fb, int64_t fe,
-                           double* __restrict__ contrib) {
+                           double* __restrict__ contrib, const int32_t* gate) {
     const int64_t fi = fb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (fi >= fe) return;
+    if (fi >= fe || (gate && !gate[0])) return;
     const dpg_factor f = F[fi];
     double e[3], Ai[9];
     linearize(f, X, e, Ai);
@@ -119,9 +120,9 @@ __global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __res
 __global__ void gather_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ contrib,
                               const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
                               int64_t n_nodes, int64_t nnzb_upper, int64_t shard_begin, int64_t shard_end,
-                              double* __restrict__ hb, double* __restrict__ chi2_node) {
+                              double* __restrict__ hb, double* __restrict__ chi2_node, const int32_t* gate) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nnzb_upper) return;
+    if (u >= nnzb_upper || (gate && !gate[0])) return;
     const bool is_diag = u < n_nodes;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     double g[3] = {0, 0, 0};
@@ -178,8 +179,10 @@ __device__ double block_sum(double v, double* red) {
     return s;
 }
 
-__global__ void chi2_kernel(const double* __restrict__ chi2_node, int64_t n, double* __restrict__ out) {
+__global__ void chi2_kernel(const double* __restrict__ chi2_node, int64_t n, double* __restrict__ out,
+                            const int32_t* gate) {
     __shared__ double red[16];
+    if (gate && !gate[0]) return;
     double s = 0.0;
     for (int64_t k = threadIdx.x; k < n; k += blockDim.x) s += chi2_node[k];
     s = block_sum(s, red);
@@ -336,7 +339,8 @@ __global__ void pcg_update_kernel(int it, int64_t n, const double* __restrict__ 
 // X <- X * Pose2(d); partial max |d|.  d is indexed by node, or by elimination position when
 // pos != NULL (the Cholesky's solution vector).
 __global__ void retract_kernel(double* __restrict__ X, const double* __restrict__ d, int64_t n,
-                               const int32_t* __restrict__ pos, double* __restrict__ max_out) {
+                               const int32_t* __restrict__ pos, double* __restrict__ max_out, const int32_t* gate) {
+    if (gate && !gate[0]) return;
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     double m = 0.0;
     if (v < n) {
@@ -529,19 +533,22 @@ extern "C" int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* re
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
-extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_t* gate) {
     double* chi2_node = g->partials + 6 * (size_t)g->n_blocks_rows;
     const int64_t nfs = g->shard_end - g->shard_begin;
     if (nfs > 0)
         hipLaunchKernelGGL(lin_kernel, dim3(nblk(nfs)), dim3(kRowThreads), 0, s, g->factors, g->poses, g->shard_begin,
-                           g->shard_end, g->contrib);
+                           g->shard_end, g->contrib, gate);
     hipLaunchKernelGGL(gather_kernel, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->factors, g->contrib,
                        g->up_cptr, g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, hb,
-                       chi2_node);
+                       chi2_node, gate);
     hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
-                       hb + 9 * g->nnzb_upper + 3 * g->n_nodes);
+                       hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
+    return assemble_gated(g, hb, reinterpret_cast<hipStream_t>(stream), nullptr);
 }
 
 static int pcg_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, hipStream_t s);
@@ -574,7 +581,96 @@ extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg
     }
     if (hipMemsetAsync(g->scal3, 0, sizeof(double), s) != hipSuccess) return DPG_ERR_HIP;
     hipLaunchKernelGGL(retract_kernel, dim3(g->n_blocks_rows), dim3(kRowThreads), 0, s, g->poses, xout, g->n_nodes,
-                       xpos, g->scal3);
+                       xpos, g->scal3, nullptr);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+// ---- the pipelined loop (dpg_gn_pipe.h) ----
+__global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_was_chord, int32_t have_factor,
+                                 double last_dinf, double prev_dinf, double cur, double* max_out) {
+    ctl->active = 1;
+    ctl->reuse = reuse;
+    ctl->last_was_chord = last_was_chord;
+    ctl->have_factor = have_factor;
+    ctl->it = 0;
+    ctl->last_dinf = last_dinf;
+    ctl->prev_dinf = prev_dinf;
+    ctl->cur_error = cur;
+    *max_out = 0.0;
+}
+
+// the end of one iteration: report its scalars, then decide the next one exactly as the host
+// loop does (dpg_api.hip gn_loop: the stop rule; dpg_gn_dev_solve_async: the chord rule)
+__global__ void pipe_ctl_kernel(dpg_gn_ctl* ctl, const double* __restrict__ chi2, const int32_t* __restrict__ status,
+                                double* max_out, dpg_gn_params P, dpg_gn_slot* slot) {
+    dpg_gn_slot o;
+    o.reuse = ctl->reuse;
+    o.active = ctl->active;
+    o.it = ctl->it;
+    o.final_ = 1;
+    o.dinf = 0.0;
+    o.error = 0.0;
+    o.status = 0.0;
+    if (ctl->active) {
+        const double dinf = *max_out, nw = *chi2, st = (double)*status;
+        const int it = ctl->it + 1;
+        o.dinf = dinf;
+        o.error = nw;
+        o.status = st;
+        o.it = it;
+        bool fin = st != 0.0 || it >= P.max_iterations;
+        if (!fin) {
+            const double cur = ctl->cur_error;
+            if (P.use_error_criteria) {
+                bool conv = nw <= 0.0;
+                if (!conv) {
+                    const double abs_dec = cur - nw, rel_dec = abs_dec / cur;
+                    conv = (P.relative_error_tol != 0.0 && rel_dec <= P.relative_error_tol) ||
+                           abs_dec <= P.absolute_error_tol;
+                }
+                fin = conv || !isfinite(cur);
+            } else {
+                fin = dinf < P.delta_tol;
+            }
+        }
+        o.final_ = fin ? 1 : 0;
+        // chord bookkeeping after the fetch: prev <- last, last <- dinf; the step just taken
+        ctl->prev_dinf = ctl->last_dinf;
+        ctl->last_dinf = dinf;
+        ctl->last_was_chord = ctl->reuse;
+        ctl->have_factor = 1;
+        ctl->cur_error = nw;
+        ctl->it = it;
+        const bool slow = ctl->last_was_chord && ctl->last_dinf > 0.1 * ctl->prev_dinf;
+        ctl->reuse = (P.reuse_factorization && ctl->have_factor && ctl->last_dinf < P.refactor_delta && !slow) ? 1 : 0;
+        ctl->active = fin ? 0 : 1;
+        *max_out = 0.0;
+    }
+    *slot = o;
+}
+
+extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, double cur, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // iteration 1's chord decision from the host bookkeeping (as dpg_gn_dev_solve_async takes it)
+    const bool slow = g->last_was_chord && g->last_delta_inf > 0.1 * g->prev_delta_inf;
+    const bool reuse = gp->reuse_factorization && g->have_factor && g->last_delta_inf < gp->refactor_delta && !slow;
+    hipLaunchKernelGGL(pipe_init_kernel, dim3(1), dim3(1), 0, s, ctl, reuse ? 1 : 0, g->last_was_chord, g->have_factor,
+                       g->last_delta_inf, g->prev_delta_inf, cur, g->scal3);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot,
+                                 void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int32_t* gate = &ctl->active;
+    if (!g->chol || !dpg_chol_gated_ok(g->chol)) return DPG_ERR_STATE;
+    int rc = dpg_chol_solve_gated(g->chol, g->hb_own, gate, stream);
+    if (rc) return rc;
+    hipLaunchKernelGGL(retract_kernel, dim3(g->n_blocks_rows), dim3(kRowThreads), 0, s, g->poses, dpg_chol_x_dev(g->chol),
+                       g->n_nodes, dpg_chol_pos_dev(g->chol), g->scal3, gate);
+    if ((rc = assemble_gated(g, g->hb_own, s, gate))) return rc;
+    hipLaunchKernelGGL(pipe_ctl_kernel, dim3(1), dim3(1), 0, s, ctl, g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes,
+                       dpg_chol_status_dev(g->chol), g->scal3, *gp, slot);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
