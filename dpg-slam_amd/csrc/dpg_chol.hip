@@ -31,6 +31,7 @@
 
 #include "dpg_chol.h"
 #include "dpg_internal.h"
+#include "dpg_gn_pipe.h"
 
 namespace {
 
@@ -917,7 +918,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                         const double* __restrict__ fronts,
                                                         const double* __restrict__ ysol, double* xsol, int R,
                                                         int max_seg, const double* __restrict__ dinv,
-                                                        const int32_t* gate) {
+                                                        const int32_t* gate, const int32_t* __restrict__ perm,
+                                                        double* __restrict__ X, double* max_out) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
@@ -958,6 +960,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     __syncthreads();
     if (tid == 0) __hip_atomic_store(sync + 1 + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     BW_MARK(s, 4);
+    if (X) {   // the Gauss-Newton retraction of this front's nodes (retract_kernel's work), max |x|
+        double m = 0.0;
+        for (int j = tid; j < S.k; j += kT)
+            m = fmax(m, pose_retract(X + 3 * (int64_t)perm[S.c0 + j], z[3 * j], z[3 * j + 1], z[3 * j + 2]));
+        if (tid < ((S.k + 63) & ~63)) {   // the waves that own nodes
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
+            if ((tid & 63) == 0)
+                atomicMax(reinterpret_cast<unsigned long long*>(max_out), (unsigned long long)__double_as_longlong(m));
+        }
+    }
 }
 
 // ---- fused factorization + forward solve: ONE launch, fronts as a DAG ----
@@ -2417,7 +2430,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
             hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                            c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg,
-                           c->use_dinv ? c->dinv : nullptr, nullptr);
+                           c->use_dinv ? c->dinv : nullptr, nullptr, nullptr, nullptr, nullptr);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -2443,7 +2456,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr);
+                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2458,7 +2471,7 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr, nullptr, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2470,15 +2483,22 @@ extern "C" int dpg_chol_gated_ok(void* h) {
     return c && c->fused && !(c->use_dinv && c->n_dblocks > 0) ? 1 : 0;
 }
 
-extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* gate, void* stream) {
+extern "C" void dpg_chol_sync_dev(void* h, int32_t** sync, int64_t* n_words) {
+    CholDev* c = reinterpret_cast<CholDev*>(h);
+    *sync = c->sync;
+    *n_words = (int64_t)(c->sync_bytes / sizeof(int32_t));
+}
+
+// prezeroed: the caller's previous launch cleared the status word and the sync counters
+extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* gate, int prezeroed, double* X,
+                                    double* max_out, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!dpg_chol_gated_ok(h)) return DPG_ERR_STATE;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dpg_chol_sym& S = c->sym;
     const double* g = hb + 9 * c->nnzb_upper;
-    // the status word is read (by the iteration's control kernel) before the next iteration clears it
-    if (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess ||
-        hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess)
+    if (!prezeroed && (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess ||
+                       hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess))
         return DPG_ERR_HIP;
     hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
                        c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
@@ -2488,7 +2508,7 @@ extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* ga
                        nullptr, gate);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                        c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol,
-                       c->solve_stage, c->solve_maxseg, nullptr, gate);
+                       c->solve_stage, c->solve_maxseg, nullptr, gate, c->perm, X, max_out);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

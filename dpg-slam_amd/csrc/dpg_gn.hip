@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -85,75 +86,95 @@ __device__ __forceinline__ void atwb_acc(const double* A, const double* w, const
         }
 }
 
-// per-factor linearization, once per factor: the contributions every block it touches needs,
-// computed with exactly the expressions the gather below adds (so the sums are the same as a
-// per-block evaluation):  [0..8] A_i^T W A_i, [9..17] A_i^T W (the (i, j) block), [18..20] the
-// g_i term, [21..23] the g_j term, [24] chi2 term.
-constexpr int kContrib = 25;
-__global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X, int64_t fb, int64_t fe,
-                           double* __restrict__ contrib, const int32_t* gate) {
-    const int64_t fi = fb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (fi >= fe || (gate && !gate[0])) return;
+// linearization by contribution-list entry: entry q of the upper blocks' lists (factor fi, role)
+// gets the 13 doubles its block adds, at rec[13 q] -- role 0 (diag i): A_i^T W A_i, the g_i term,
+// the chi2 term; role 1 (diag j, A_j = I): the diagonal of W, the g_j term; role 2 / 3 (the
+// (i, j) / (j, i) block): A_i^T W.  A factor is linearized once per entry (at most three times),
+// so the gather below reads one contiguous record per entry instead of chasing the factor.
+constexpr int kRec = 13;
+__global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X,
+                           const int32_t* __restrict__ clist, const int32_t* __restrict__ n_entries, int64_t fb,
+                           int64_t fe, double* __restrict__ rec, const int32_t* gate) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= *n_entries || (gate && !gate[0])) return;
+    const int32_t code = clist[q];
+    const int64_t fi = code >> 2;
+    const int role = code & 3;
+    if (fi < fb || fi >= fe) return;   // another rank's factor: the gather skips it
     const dpg_factor f = F[fi];
     double e[3], Ai[9];
     linearize(f, X, e, Ai);
     const double* w = f.info;
-    const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    double C[kContrib];
+    double C[kRec];
 #pragma unroll
-    for (int q = 0; q < 18; ++q) C[q] = 0.0;
-    atwb_acc(Ai, w, Ai, C);
-    atwb_acc(Ai, w, I3, C + 9);
+    for (int k = 0; k < kRec; ++k) C[k] = 0.0;
+    if (role == 0) {
+        atwb_acc(Ai, w, Ai, C);
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        C[18 + r] = Ai[r] * w[0] * e[0] + Ai[3 + r] * w[1] * e[1] + Ai[6 + r] * w[2] * e[2];
-        C[21 + r] = w[r] * e[r];
+        for (int r = 0; r < 3; ++r) C[9 + r] = Ai[r] * w[0] * e[0] + Ai[3 + r] * w[1] * e[1] + Ai[6 + r] * w[2] * e[2];
+        C[12] = 0.5 * (w[0] * e[0] * e[0] + w[1] * e[1] * e[1] + w[2] * e[2] * e[2]);
+    } else if (role == 1) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) { C[r] = w[r]; C[9 + r] = w[r] * e[r]; }
+    } else {
+        const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+        atwb_acc(Ai, w, I3, C);
     }
-    C[24] = 0.5 * (w[0] * e[0] * e[0] + w[1] * e[1] * e[1] + w[2] * e[2] * e[2]);
-    double* o = contrib + kContrib * fi;
+    double* o = rec + kRec * q;
 #pragma unroll
-    for (int q = 0; q < kContrib; ++q) o[q] = C[q];
+    for (int k = 0; k < kRec; ++k) o[k] = C[k];
 }
 
-// one lane per upper 3x3 block of H: adds the contributions of the factors touching it in factor
-// order (deterministic, no float atomics)
-__global__ void gather_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ contrib,
-                              const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
-                              int64_t n_nodes, int64_t nnzb_upper, int64_t shard_begin, int64_t shard_end,
-                              double* __restrict__ hb, double* __restrict__ chi2_node, const int32_t* gate) {
+// one lane per upper 3x3 block of H: adds its entries' records in list (= factor) order
+// (deterministic, no float atomics); kG records are loaded before the first is added
+template <int kG>
+__global__ __launch_bounds__(kRowThreads) void gather_kernel(const double* __restrict__ rec, const int32_t* __restrict__ cptr,
+                              const int32_t* __restrict__ clist, int64_t n_nodes, int64_t nnzb_upper,
+                              int64_t shard_begin, int64_t shard_end, double* __restrict__ hb,
+                              double* __restrict__ chi2_node, const int32_t* gate) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nnzb_upper || (gate && !gate[0])) return;
     const bool is_diag = u < n_nodes;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     double g[3] = {0, 0, 0};
     double chi2 = 0.0;
-    for (int32_t q = cptr[u]; q < cptr[u + 1]; ++q) {
-        const int32_t code = clist[q];
-        const int32_t fi = code >> 2, role = code & 3;
-        if (fi < shard_begin || fi >= shard_end) continue;
-        const double* c = contrib + kContrib * (int64_t)fi;
-        if (role == 0) {          // diag i
+    const int32_t q0 = cptr[u], q1 = cptr[u + 1];
+    for (int32_t qb = q0; qb < q1; qb += kG) {
+        int32_t code[kG];
+        double v[kG][kRec];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) H[k] += c[k];
+        for (int t = 0; t < kG; ++t) {
+            code[t] = qb + t < q1 ? clist[qb + t] : -1;
+            const double* r = rec + kRec * (int64_t)(qb + t < q1 ? qb + t : q0);
 #pragma unroll
-            for (int r = 0; r < 3; ++r) g[r] += c[18 + r];
-            chi2 += c[24];
-        } else if (role == 1) {   // diag j (A_j = I): W
-            const double* w = F[fi].info;
+            for (int k = 0; k < kRec; ++k) v[t][k] = r[k];
+        }
 #pragma unroll
-            for (int r = 0; r < 3; ++r)
+        for (int t = 0; t < kG; ++t) {
+            const int32_t fi = code[t] >> 2, role = code[t] & 3;
+            if (code[t] < 0 || fi < shard_begin || fi >= shard_end) continue;
+            if (role == 0) {          // diag i
 #pragma unroll
-                for (int k = 0; k < 3; ++k) H[3 * r + k] += r == k ? w[r] : 0.0;
+                for (int k = 0; k < 9; ++k) H[k] += v[t][k];
 #pragma unroll
-            for (int r = 0; r < 3; ++r) g[r] += c[21 + r];
-        } else if (role == 2) {   // H(i, j) = A_i^T W, i < j
+                for (int r = 0; r < 3; ++r) g[r] += v[t][9 + r];
+                chi2 += v[t][12];
+            } else if (role == 1) {   // diag j (A_j = I): W
 #pragma unroll
-            for (int k = 0; k < 9; ++k) H[k] += c[9 + k];
-        } else {                  // H(j, i) = W A_i, j < i
+                for (int r = 0; r < 3; ++r)
 #pragma unroll
-            for (int r = 0; r < 3; ++r)
+                    for (int k = 0; k < 3; ++k) H[3 * r + k] += r == k ? v[t][r] : 0.0;
 #pragma unroll
-                for (int k = 0; k < 3; ++k) H[3 * r + k] += c[9 + 3 * k + r];
+                for (int r = 0; r < 3; ++r) g[r] += v[t][9 + r];
+            } else if (role == 2) {   // H(i, j) = A_i^T W, i < j
+#pragma unroll
+                for (int k = 0; k < 9; ++k) H[k] += v[t][k];
+            } else {                  // H(j, i) = W A_i, j < i
+#pragma unroll
+                for (int r = 0; r < 3; ++r)
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) H[3 * r + k] += v[t][3 * k + r];
+            }
         }
     }
     double* o = hb + 9 * u;
@@ -345,17 +366,7 @@ __global__ void retract_kernel(double* __restrict__ X, const double* __restrict_
     double m = 0.0;
     if (v < n) {
         const int64_t di = 3 * (int64_t)(pos ? pos[v] : v);
-        const double c = cos(X[3 * v + 2]), s = sin(X[3 * v + 2]);
-        const double d0 = d[di], d1 = d[di + 1], d2 = d[di + 2];
-        const double cd = cos(d2), sd = sin(d2);
-        const double nx = X[3 * v] + (c * d0 - s * d1);
-        const double ny = X[3 * v + 1] + (s * d0 + c * d1);
-        const double nc = c * cd - s * sd, ns = s * cd + c * sd;
-        X[3 * v] = nx;
-        X[3 * v + 1] = ny;
-        X[3 * v + 2] = atan2(ns, nc);
-        m = fmax(fabs(d0), fmax(fabs(d1), fabs(d2)));
-        if (!(m == m)) m = __longlong_as_double(0x7ff0000000000000ll);   // NaN -> +inf (stops the loop)
+        m = pose_retract(X + 3 * v, d[di], d[di + 1], d[di + 2]);
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) m = fmax(m, __shfl_down(m, off, 64));
@@ -505,7 +516,7 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     rc |= dev_alloc(&g->partials, 6 * (size_t)g->n_blocks_rows + (size_t)n);
     rc |= dev_alloc(&g->scal, 2 * (size_t)65536);
     rc |= dev_alloc(&g->hb_own, (size_t)dpg_gn_dev_hb_size(g));
-    rc |= dev_alloc(&g->contrib, 25 * (size_t)nf);
+    rc |= dev_alloc(&g->contrib, 13 * std::max<size_t>(clist.size(), 1));   // lin_kernel's records
     rc |= dev_alloc(&g->scal3, 4);
     if (!rc && hipHostMalloc(reinterpret_cast<void**>(&g->scal3_host), 4 * sizeof(double)) != hipSuccess) rc = DPG_ERR_HIP;
     if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
@@ -533,17 +544,24 @@ extern "C" int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* re
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
-static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_t* gate) {
+static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_t* gate, bool chi2 = true) {
     double* chi2_node = g->partials + 6 * (size_t)g->n_blocks_rows;
     const int64_t nfs = g->shard_end - g->shard_begin;
+    // upper bound of the list length (a Between factor has 3 entries); the kernel reads the length
     if (nfs > 0)
-        hipLaunchKernelGGL(lin_kernel, dim3(nblk(nfs)), dim3(kRowThreads), 0, s, g->factors, g->poses, g->shard_begin,
-                           g->shard_end, g->contrib, gate);
-    hipLaunchKernelGGL(gather_kernel, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->factors, g->contrib,
-                       g->up_cptr, g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, hb,
-                       chi2_node, gate);
-    hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
-                       hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate);
+        hipLaunchKernelGGL(lin_kernel, dim3(nblk(3 * g->n_factors)), dim3(kRowThreads), 0, s, g->factors, g->poses,
+                           g->up_clist, g->up_cptr + g->nnzb_upper, g->shard_begin, g->shard_end, g->contrib, gate);
+    static const int kg = getenv("DPG_GATHER_G") ? atoi(getenv("DPG_GATHER_G")) : 2;
+#define DPG_GATHER(G)                                                                                               \
+    hipLaunchKernelGGL(gather_kernel<G>, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->contrib, g->up_cptr,  \
+                       g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, hb, chi2_node, gate)
+    if (kg == 1) DPG_GATHER(1);
+    else if (kg == 4) DPG_GATHER(4);
+    else DPG_GATHER(2);
+#undef DPG_GATHER
+    if (chi2)
+        hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
+                           hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -586,8 +604,18 @@ extern "C" int dpg_gn_dev_solve_async(dpg_gn_dev* g, const double* hb, const dpg
 }
 
 // ---- the pipelined loop (dpg_gn_pipe.h) ----
+// clear what the next fused solve counts on (as dpg_chol_solve's memsets)
+__device__ __forceinline__ void clear_sync(int32_t* sync, int64_t n_words, int32_t* status) {
+    int4* s4 = reinterpret_cast<int4*>(sync);   // 16-B aligned, n_words a multiple of 4
+    for (int64_t k = threadIdx.x; k < n_words / 4; k += blockDim.x) s4[k] = make_int4(0, 0, 0, 0);
+    if (threadIdx.x == 0) *status = 0;
+}
+
 __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_was_chord, int32_t have_factor,
-                                 double last_dinf, double prev_dinf, double cur, double* max_out) {
+                                 double last_dinf, double prev_dinf, double cur, double* max_out, int32_t* sync,
+                                 int64_t n_words, int32_t* status) {
+    clear_sync(sync, n_words, status);
+    if (threadIdx.x != 0) return;
     ctl->active = 1;
     ctl->reuse = reuse;
     ctl->last_was_chord = last_was_chord;
@@ -599,10 +627,33 @@ __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_wa
     *max_out = 0.0;
 }
 
-// the end of one iteration: report its scalars, then decide the next one exactly as the host
-// loop does (dpg_api.hip gn_loop: the stop rule; dpg_gn_dev_solve_async: the chord rule)
-__global__ void pipe_ctl_kernel(dpg_gn_ctl* ctl, const double* __restrict__ chi2, const int32_t* __restrict__ status,
-                                double* max_out, dpg_gn_params P, dpg_gn_slot* slot) {
+// the end of one iteration: the error (chi2_kernel's sum, same order), its report, then the next
+// iteration decided exactly as the host loop does (dpg_api.hip gn_loop: the stop rule;
+// dpg_gn_dev_solve_async: the chord rule), and the solver's counters cleared for it
+__global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const double* __restrict__ chi2_node, int64_t n,
+                                                        double* chi2, int32_t* status, double* max_out, dpg_gn_params P,
+                                                        dpg_gn_slot* slot, int32_t* sync, int64_t n_words) {
+    __shared__ double red[16];
+    if (!ctl->active) {   // uniform: nothing ran this iteration
+        if (threadIdx.x == 0) {
+            dpg_gn_slot o;
+            o.reuse = ctl->reuse;
+            o.active = 0;
+            o.it = ctl->it;
+            o.final_ = 1;
+            o.dinf = o.error = o.status = 0.0;
+            *slot = o;
+        }
+        return;
+    }
+    double sum = 0.0;
+    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) sum += chi2_node[k];
+    sum = block_sum(sum, red);
+    const double st_word = (double)*status;
+    __syncthreads();   // every lane has read the status word before it is cleared
+    clear_sync(sync, n_words, status);
+    if (threadIdx.x != 0) return;
+    *chi2 = sum;
     dpg_gn_slot o;
     o.reuse = ctl->reuse;
     o.active = ctl->active;
@@ -612,7 +663,7 @@ __global__ void pipe_ctl_kernel(dpg_gn_ctl* ctl, const double* __restrict__ chi2
     o.error = 0.0;
     o.status = 0.0;
     if (ctl->active) {
-        const double dinf = *max_out, nw = *chi2, st = (double)*status;
+        const double dinf = *max_out, nw = sum, st = st_word;
         const int it = ctl->it + 1;
         o.dinf = dinf;
         o.error = nw;
@@ -654,8 +705,12 @@ extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_c
     // iteration 1's chord decision from the host bookkeeping (as dpg_gn_dev_solve_async takes it)
     const bool slow = g->last_was_chord && g->last_delta_inf > 0.1 * g->prev_delta_inf;
     const bool reuse = gp->reuse_factorization && g->have_factor && g->last_delta_inf < gp->refactor_delta && !slow;
-    hipLaunchKernelGGL(pipe_init_kernel, dim3(1), dim3(1), 0, s, ctl, reuse ? 1 : 0, g->last_was_chord, g->have_factor,
-                       g->last_delta_inf, g->prev_delta_inf, cur, g->scal3);
+    int32_t* sync;
+    int64_t n_words;
+    dpg_chol_sync_dev(g->chol, &sync, &n_words);
+    hipLaunchKernelGGL(pipe_init_kernel, dim3(1), dim3(1024), 0, s, ctl, reuse ? 1 : 0, g->last_was_chord, g->have_factor,
+                       g->last_delta_inf, g->prev_delta_inf, cur, g->scal3, sync, n_words,
+                       const_cast<int32_t*>(dpg_chol_status_dev(g->chol)));
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -664,13 +719,15 @@ extern "C" int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int32_t* gate = &ctl->active;
     if (!g->chol || !dpg_chol_gated_ok(g->chol)) return DPG_ERR_STATE;
-    int rc = dpg_chol_solve_gated(g->chol, g->hb_own, gate, stream);
+    int rc = dpg_chol_solve_gated(g->chol, g->hb_own, gate, 1, g->poses, g->scal3, stream);
     if (rc) return rc;
-    hipLaunchKernelGGL(retract_kernel, dim3(g->n_blocks_rows), dim3(kRowThreads), 0, s, g->poses, dpg_chol_x_dev(g->chol),
-                       g->n_nodes, dpg_chol_pos_dev(g->chol), g->scal3, gate);
-    if ((rc = assemble_gated(g, g->hb_own, s, gate))) return rc;
-    hipLaunchKernelGGL(pipe_ctl_kernel, dim3(1), dim3(1), 0, s, ctl, g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes,
-                       dpg_chol_status_dev(g->chol), g->scal3, *gp, slot);
+    if ((rc = assemble_gated(g, g->hb_own, s, gate, false))) return rc;
+    int32_t* sync;
+    int64_t n_words;
+    dpg_chol_sync_dev(g->chol, &sync, &n_words);
+    hipLaunchKernelGGL(pipe_ctl_kernel, dim3(1), dim3(1024), 0, s, ctl, g->partials + 6 * (size_t)g->n_blocks_rows,
+                       g->n_nodes, g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes,
+                       const_cast<int32_t*>(dpg_chol_status_dev(g->chol)), g->scal3, *gp, slot, sync, n_words);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

@@ -13,6 +13,8 @@
 #ifndef DPG_GN_PIPE_H
 #define DPG_GN_PIPE_H
 
+#include <hip/hip_runtime.h>
+#include <math.h>
 #include <stdint.h>
 
 #include "../../include/dpg_slam_c.h"
@@ -31,10 +33,31 @@ struct dpg_gn_slot {
     int32_t reuse, active, final_, it;
 };
 
+// X_v <- X_v * Pose2(d) (Pose2 retraction); returns max |d|, NaN as +inf.  Shared by the
+// retraction kernel (dpg_gn.hip) and the backward solve that retracts as it goes (dpg_chol.hip).
+__device__ __forceinline__ double pose_retract(double* __restrict__ Xv, double d0, double d1, double d2) {
+    const double c = cos(Xv[2]), s = sin(Xv[2]);
+    const double cd = cos(d2), sd = sin(d2);
+    const double nx = Xv[0] + (c * d0 - s * d1);
+    const double ny = Xv[1] + (s * d0 + c * d1);
+    const double nc = c * cd - s * sd, ns = s * cd + c * sd;
+    Xv[0] = nx;
+    Xv[1] = ny;
+    Xv[2] = atan2(ns, nc);
+    double m = fmax(fabs(d0), fmax(fabs(d1), fabs(d2)));
+    if (!(m == m)) m = __longlong_as_double(0x7ff0000000000000ll);   // NaN -> +inf (stops the loop)
+    return m;
+}
+
 extern "C" {
 // the fused Cholesky of this graph can run gated (dpg_chol.hip)
 int dpg_chol_gated_ok(void* chol);
-int dpg_chol_solve_gated(void* chol, const double* hb, const int32_t* gate, void* stream);
+// X != NULL: the backward solve also retracts the poses X (by node) with the solution and keeps
+// max |x| in *max_out (retract_kernel's work)
+int dpg_chol_solve_gated(void* chol, const double* hb, const int32_t* gate, int prezeroed, double* X, double* max_out,
+                         void* stream);
+// the fused solve's synchronisation words (cleared before every solve)
+void dpg_chol_sync_dev(void* chol, int32_t** sync, int64_t* n_words);
 // set the control block for iteration 1 from the host state (g's chord bookkeeping) and the
 // initial error
 int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, double cur_error, void* stream);

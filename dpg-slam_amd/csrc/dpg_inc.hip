@@ -196,7 +196,7 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
     rc |= dgrow(&g.up_cptr, &q->c_cptr, cnt.size(), s, 0);
     rc |= dgrow(&g.up_clist, &q->c_clist, clist.size(), s, 0);
     rc |= dgrow(&g.hb_own, &q->c_hb, (size_t)(9 * nu + 3 * n + 2), s, 0);
-    rc |= dgrow(&g.contrib, &q->c_contrib, (size_t)(25 * nf), s, 0);
+    rc |= dgrow(&g.contrib, &q->c_contrib, 13 * std::max<size_t>(clist.size(), 1), s, 0);   // lin_kernel's records
     rc |= dgrow(&g.partials, &q->c_partials, (size_t)(6 * g.n_blocks_rows + n), s, 0);
     if (!g.scal3) {
         rc |= hipMalloc(reinterpret_cast<void**>(&g.scal3), 4 * sizeof(double)) != hipSuccess;
