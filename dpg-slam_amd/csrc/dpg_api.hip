@@ -101,6 +101,10 @@ struct dpg_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev[8] = {};
+    // the batch covariance runs on `aux` beside what follows the ICP on `stream` (the pose graph
+    // does not read it): ev[2] marks its end, cov_pending until `stream` has been made to wait
+    hipStream_t aux = nullptr;
+    bool cov_pending = false, cov_on_aux = false;
     int32_t icp_variant = DPG_ICP_ANGULAR;
     int32_t defer_cap = 256;        // angular ICP: cooperative-queue threshold (dpg_ctx_set_icp_defer_cap)
     float map_ms = 0.f;             // last dpg_get_map kernel (HIP events map_ev)
@@ -159,6 +163,12 @@ inline dpg_ctx* dev_ctx(dpg_ctx* c, int k) { return k == 0 ? c : c->peers[(size_
 // made by dpg_ctx_create_multi (even for one GPU: its calls then take the sharded paths, RCCL
 // all-reduce included, with one rank)
 inline bool is_multi(const dpg_ctx* c) { return !c->comms.empty(); }
+// order `stream` after the last batch covariance (before anything rewrites its inputs or reads it)
+inline int join_cov(dpg_ctx* c) {
+    if (!c->cov_pending) return DPG_OK;
+    c->cov_pending = false;
+    return hipStreamWaitEvent(c->stream, c->ev[2], 0) == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
 }  // namespace
 
 namespace {
@@ -197,7 +207,8 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     if (maxp > 16384) return fail(DPG_ERR_SIZE, "downsampled cloud of %d points exceeds 16384", maxp);
     if (maxp > 4096 && c->icp_variant != DPG_ICP_ANGULAR)
         return fail(DPG_ERR_SIZE, "downsampled cloud of %d points: only the angular ICP variant takes more than 4096", maxp);
-    int rc = 0;
+    int rc = join_cov(c);
+    if (rc) return fail(rc, "stream wait failed");
     if (timed) HIP_TRY(hipEventRecord(c->ev[6], c->stream));
     if (c->icp_variant == DPG_ICP_KDTREE) {
         rc = dpg_launch_kdtree_build(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, c->stream);
@@ -229,6 +240,18 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     }
     if (rc) return fail(rc, "ICP kernel launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
     if (timed) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    static const bool overlap = !(getenv("DPG_COV_OVERLAP") && atoi(getenv("DPG_COV_OVERLAP")) == 0);
+    if (hess_dev && timed && overlap) {   // beside the pose graph: on aux, after the ICP
+        if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        HIP_TRY(hipStreamWaitEvent(c->aux, c->ev[1], 0));
+        rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->aux);
+        if (rc) return fail(rc, "covariance kernel launch failed");
+        HIP_TRY(hipEventRecord(c->ev[2], c->aux));
+        c->cov_pending = true;
+        c->cov_on_aux = true;
+        return DPG_OK;
+    }
+    if (timed) c->cov_on_aux = false;
     if (hess_dev) {
         rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->stream);
         if (rc) return fail(rc, "covariance kernel launch failed");
@@ -336,7 +359,9 @@ void dpg_ctx_destroy(dpg_ctx* c) {
         if (m) (void)ncclCommDestroy(m);
     c->comms.clear();
     (void)hipSetDevice(c->device);
+    (void)join_cov(c);
     (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     c->full.release(); c->ds.release(); c->edges.release(); c->res.release(); c->hess.release();
     c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
     c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release();
@@ -355,6 +380,7 @@ void dpg_ctx_destroy(dpg_ctx* c) {
 
 int dpg_ctx_set_stream(dpg_ctx* c, void* s) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    if (join_cov(c)) return fail(DPG_ERR_HIP, "stream wait failed");
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     c->stream = reinterpret_cast<hipStream_t>(s);
@@ -366,6 +392,7 @@ int dpg_ctx_synchronize(dpg_ctx* c) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
     for (int k = 0; k < n_dev(c); ++k) {
         HIP_TRY(hipSetDevice(dev_ctx(c, k)->device));
+        if (join_cov(dev_ctx(c, k))) return fail(DPG_ERR_HIP, "stream wait failed");
         HIP_TRY(hipStreamSynchronize(dev_ctx(c, k)->stream));
     }
     HIP_TRY(hipSetDevice(c->device));
@@ -400,6 +427,10 @@ static int scans_upload_1(dpg_ctx* c, const float* pts, const int64_t* off, int6
     if (!c || !pts || !off || V <= 0) return fail(DPG_ERR_ARG, "dpg_scans_upload: bad arguments");
     if (ratio < 1) ratio = 1;
     HIP_TRY(hipSetDevice(c->device));
+    if (c->cov_pending) {   // the store may be re-allocated under a running covariance
+        HIP_TRY(hipEventSynchronize(c->ev[2]));
+        c->cov_pending = false;
+    }
     const int64_t total = off[V];
     if (total >= ((int64_t)1 << 31)) return fail(DPG_ERR_SIZE, "too many points (%lld)", (long long)total);
     c->full_off.assign(off, off + V + 1);
@@ -434,6 +465,11 @@ static int scans_append_1(dpg_ctx* c, const float* pts, const int64_t* off, int6
     if (!c || !pts || !off || k <= 0) return fail(DPG_ERR_ARG, "dpg_scans_append: bad arguments");
     if (ratio < 1) ratio = 1;
     if (c->n_nodes == 0) return scans_upload_1(c, pts, off, k, ratio);
+    if (c->cov_pending) {   // the store may be re-allocated under a running covariance
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipEventSynchronize(c->ev[2]));
+        c->cov_pending = false;
+    }
     if (ratio != c->ratio) return fail(DPG_ERR_STATE, "scans were uploaded with downsample ratio %d", c->ratio);
     HIP_TRY(hipSetDevice(c->device));
     const int64_t V0 = c->n_nodes, V1 = V0 + k;
@@ -528,6 +564,7 @@ static int batch_prepare_1(dpg_ctx* c, const int32_t* edges, int64_t ne, const f
     int rc = set_kparams(&c->kp, p);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
+    if ((rc = join_cov(c))) return fail(rc, "stream wait failed");
     c->h_edges.resize((size_t)std::max<int64_t>(ne, 1));
     int32_t ms = 0, mt = 0;
     for (int64_t e = 0; e < ne; ++e) {
@@ -710,6 +747,7 @@ int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
 static int batch_fetch_1(dpg_ctx* c, dpg_icp_result* results, double* hess) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
     HIP_TRY(hipSetDevice(c->device));
+    if (join_cov(c)) return fail(DPG_ERR_HIP, "stream wait failed");
     if (results && c->n_edges > 0)
         HIP_TRY(hipMemcpyAsync(results, c->res.p, sizeof(dpg_icp_result) * (size_t)c->n_edges, hipMemcpyDeviceToHost,
                                c->stream));
@@ -752,6 +790,8 @@ static float batch_ms(dpg_ctx* c, int a, int b) {
 float dpg_icp_batch_kernel_ms(dpg_ctx* c) { return batch_ms(c, 0, 1); }
 
 float dpg_cov_batch_kernel_ms(dpg_ctx* c) { return batch_ms(c, 1, 2); }
+
+int32_t dpg_cov_batch_overlapped(dpg_ctx* c) { return c && c->cov_on_aux ? 1 : 0; }
 
 static double batch_bytes_1(dpg_ctx* c);
 

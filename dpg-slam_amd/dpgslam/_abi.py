@@ -251,6 +251,7 @@ SIGNATURES = {
     "dpg_icp_batch_fetch_trace": (C.c_int, [P, I32P, I64P]),
     "dpg_icp_batch_kernel_ms": (C.c_float, [P]),
     "dpg_cov_batch_kernel_ms": (C.c_float, [P]),
+    "dpg_cov_batch_overlapped": (C.c_int32, [P]),
     "dpg_kdtree_build_ms": (C.c_float, [P]),
     "dpg_ctx_set_icp_variant": (C.c_int, [P, C.c_int32]),
     "dpg_ctx_set_icp_defer_cap": (C.c_int, [P, C.c_int32]),

@@ -265,6 +265,10 @@ class Context:
     def cov_kernel_ms(self) -> float:
         return float(lib().dpg_cov_batch_kernel_ms(self.handle))
 
+    def cov_overlapped(self) -> bool:
+        """The last batch's covariance ran beside the pose graph (its own stream)."""
+        return bool(lib().dpg_cov_batch_overlapped(self.handle))
+
     def icp_algorithmic_bytes(self) -> float:
         return float(lib().dpg_icp_batch_algorithmic_bytes(self.handle))
 

@@ -224,6 +224,9 @@ int dpg_icp_batch_fetch_trace(dpg_ctx* ctx, int32_t* trace /*[E][trace_iters][ma
 /* Device time of the last ICP / covariance kernels (ms, HIP events on the context stream). */
 float dpg_icp_batch_kernel_ms(dpg_ctx* ctx);
 float dpg_cov_batch_kernel_ms(dpg_ctx* ctx);
+/* 1: the last batch's covariance kernel ran on the context's second stream, beside what followed
+ * the ICP on its stream (the pose graph does not read it; DPG_COV_OVERLAP=0 keeps stream order) */
+int32_t dpg_cov_batch_overlapped(dpg_ctx* ctx);
 /* Device time of the per-node index build (k-d trees / angle index) that precedes the ICP kernel. */
 float dpg_kdtree_build_ms(dpg_ctx* ctx);
 /* Nearest-neighbour machinery of the ICP kernel; all give bit-identical results. */

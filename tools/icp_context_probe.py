@@ -18,6 +18,10 @@ p = _abi.default_icp_params()
 gp = _abi.default_gn_params()
 ms = {k: [] for k in ("a_back_to_back", "b_after_gn", "c_after_gn_sleep5ms", "d_after_gn_nocov", "e_after_gn_cov_icp")}
 with api.Context(0) as ctx:
+    if os.environ.get("PROBE_TORCH_STREAM") == "1":   # bench.py's setting: torch's current stream
+        import torch
+        ctx.set_stream(torch.cuda.current_stream(torch.device("cuda", 0)).cuda_stream)
+        print("on torch's current stream")
     ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
     ctx.icp_prepare(w.edges, w.est, p)
     F = w.factors_placeholder()
