@@ -154,7 +154,7 @@ def main_incremental(args):
     prof, pbuf = [], (C.c_double * 8)()
     lat, icp_ms, sym_ms, num_ms, reord, relin = [], [], [], [], 0, 0
     with api.Context(0) as ctx:
-        g = api.IncGraph(ctx, mode=args.inc_mode)
+        g = api.IncGraph(ctx, mode=args.inc_mode, reorder_every=args.inc_reorder_every)
         for v in range(V):
             extra = w.base_factors[v:v + 1]
             ts = time.perf_counter()
@@ -602,6 +602,7 @@ def main():
                     help="N=1 GN loop: dpg_gn_run, or the per-iteration host loop every rank runs at N>1")
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
     ap.add_argument("--inc-nodes", type=int, default=5000)
+    ap.add_argument("--inc-reorder-every", type=int, default=64, help="incremental: a fresh order every this many nodes")
     ap.add_argument("--cpu-nodes", type=int, default=8, help="nodes in the incremental CPU-baseline sample")
     args = ap.parse_args()
     if args.workload == "incremental":

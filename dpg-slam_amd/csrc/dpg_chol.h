@@ -77,6 +77,11 @@ struct dpg_chol_incsym {
 };
 // a fresh minimum-degree order of the graph (pairs) -> state
 int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+// the two halves of dpg_incsym_reset: the order and column patterns of the graph (a pure function
+// of its arguments, safe on a worker thread), and the state built from them (perm, pat consumed)
+int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                     std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
+void dpg_incsym_init(dpg_chol_incsym* I, int64_t n, std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
 // nodes n .. n + k - 1 appended at the end of the order
 void dpg_incsym_append(dpg_chol_incsym* I, int64_t k);
 // edge (a, b) of the graph (nodes); returns the number of pattern entries it added (fill)

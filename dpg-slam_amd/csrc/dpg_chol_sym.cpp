@@ -554,8 +554,8 @@ double dpg_chol_critical_path_us(const dpg_chol_sym& S) {
 // estimate is shortest is kept.  Config 4 (tools/nd_ab2_job.sh, profiles/r03/v15_nd_cover_ab.txt):
 // factor + solve 0.860 -> 0.716 ms, chord-step solves 0.251 -> 0.230 ms; config 3 keeps round 2's
 // order (0.282 ms; the others 0.29-0.34).
-// The incremental graph (dpg_incsym_reset) reorders every 64 nodes with round 2's rule (the
-// 2-start search is an option there, DPG_INC_ND: a gain on config 4's graph, a loss on config 5's).
+// The incremental graph (dpg_incsym_order) reorders every 64 nodes with the same pick, on a worker
+// thread (dpg_inc.hip); DPG_INC_ND selects a single rule there.
 // DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order; DPG_CHOL_ND=<k> only candidate k
 // of {round 2, 2-start, 8-start, 4-start ratio} (A/B); DPG_ND_NOCOVER drops the cover step.
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
@@ -821,25 +821,62 @@ inline void for_rows_after(const dpg_chol_incsym* I, int64_t j, int64_t after, F
 
 }  // namespace
 
+int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                     std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
+    // Default (DPG_INC_ND unset or -1): the batch analysis's pick -- round 2's separator rule or the
+    // 8-start search with cover separators, each carried through the supernodal analysis under the
+    // incremental solver's options, the shorter critical-path estimate kept.  It costs two orders
+    // and two analyses per reorder, which dpg_inc computes on a worker thread ahead of time
+    // (dpg_inc.hip, kBgLead), so the per-node latency does not pay for it: config 4 at V = 5000
+    // p50 2.14 -> 1.96 ms, 456 -> 487 nodes/s; config 5 413 vs 411 nodes/s
+    // (profiles/r03/v24_incbg_ab.txt).  DPG_INC_ND=0: round 2's rule alone (round 2 and the earlier
+    // round-3 default); k > 0: the k-start search alone (sqrt-ratio score, no cover step); -k: the
+    // pick between round 2's rule and the k-start search without cover.
+    static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : -1; }();
+    int rc = 0;
+    if (inc_nd < 0 && !getenv("DPG_CHOL_ORDER") && n >= 256) {
+        const dpg_chol_opts o{64, 0.3};   // dpg_inc's solver options
+        double best = -1.0;
+        std::vector<int32_t> pm;
+        std::vector<std::vector<int32_t>> pt;
+        for (int k = 0; k < 2; ++k) {
+            rc = k == 0 ? dpg_chol_order(n, pair_lo, pair_hi, n_pairs, pm, pt)
+                 : inc_nd == -1 ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, pm, pt)
+                                : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, -inc_nd, 4, 2, false, pm, pt);
+            if (rc) return -1;
+            dpg_chol_sym T;
+            if (dpg_chol_sym_from_patterns(n, pm, pt, &o, &T)) return -1;
+            const double cp = dpg_chol_critical_path_us(T);
+            if (best < 0.0 || cp < best) {
+                best = cp;
+                perm.swap(pm);
+                pat.swap(pt);
+            }
+        }
+    } else {
+        rc = (inc_nd > 0 && !getenv("DPG_CHOL_ORDER"))
+                 ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, false, perm, pat)
+                 : dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat);
+    }
+    return rc ? -1 : 0;
+}
+
 int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    // round 2's separator rule by default.  DPG_INC_ND=<starts> selects the multi-start search
-    // (sqrt-ratio score, no cover step): on config 4's arrival sequence per-node p50 2.33 -> 2.04 ms
-    // and p90 2.81 -> 2.22 ms (fill -14 %), but on config 5's four-pass route 380 -> 362 nodes/s and
-    // p90 4.2 -> 4.5 ms (the reorders cost more there and the fronts come out no better) --
-    // profiles/r03/v13_inc_nd*.json, v17_c5_inc_nd_ab.txt
-    static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : 0; }();
-    const int rc = (inc_nd > 0 && !getenv("DPG_CHOL_ORDER"))
-                       ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, false, perm, pat)
-                       : dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat);
-    if (rc) return -1;
+    if (dpg_incsym_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+    dpg_incsym_init(I, n, perm, pat);
+    return 0;
+}
+
+void dpg_incsym_init(dpg_chol_incsym* I, int64_t n, std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
     I->n = n;
     I->words = std::max<int64_t>(64, (n + 63) / 64 * 2);
     I->swords = (I->words + 63) / 64;
-    I->perm = perm;
+    I->perm.swap(perm);
     I->pos.assign((size_t)n, 0);
-    for (int64_t p = 0; p < n; ++p) I->pos[(size_t)perm[(size_t)p]] = (int32_t)p;
+    const std::vector<int32_t>& pm = I->perm;
+    for (int64_t p = 0; p < n; ++p) I->pos[(size_t)pm[(size_t)p]] = (int32_t)p;
     I->bits.assign((size_t)(n * I->words), 0ull);
     I->summ.assign((size_t)(n * I->swords), 0ull);
     I->parent.assign((size_t)n, -1);
@@ -854,7 +891,6 @@ int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, cons
         if (!pat[(size_t)p].empty()) I->parent[(size_t)p] = pat[(size_t)p][0];
         I->nnz += (int64_t)pat[(size_t)p].size();
     }
-    return 0;
 }
 
 void dpg_incsym_append(dpg_chol_incsym* I, int64_t k) {

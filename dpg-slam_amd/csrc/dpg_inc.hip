@@ -33,6 +33,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <future>
 #include <unordered_map>
 #include <vector>
 
@@ -138,6 +139,11 @@ struct dpg_inc {
     int32_t* cnt = nullptr;                    // relinearized variables of the last update
     size_t c_theta = 0, c_est = 0, c_maxd = 0;
     std::vector<dpg_factor> h_dev_factors;     // staging (Q1 scaling)
+    int64_t n_dev_f = 0;                       // leading factors already on the device as given (no Q1)
+    int32_t* h_lists = nullptr;                // pinned staging of the contribution lists
+    size_t c_lists = 0;
+    hipEvent_t lists_ev = nullptr;             // recorded after the lists' copies
+    bool lists_ev_set = false;
     bool prepared = false;                     // inc_prepare ran for the coming update (its pairs are in)
     int64_t prep_new = 0;                      // ... for this many new nodes
     int64_t prep_pairs0 = 0;                   // number of unique pairs before that prepare (rollback)
@@ -145,6 +151,15 @@ struct dpg_inc {
     double* est_bak = nullptr;                 // [V][3] estimate before a batch update (rollback)
     size_t c_theta_bak = 0, c_est_bak = 0;
     bool prep_reordered = false;
+    // the next fresh order, computed on a worker thread from a snapshot of the graph taken
+    // kBgLead nodes before it is due, then extended by the nodes and pairs that arrived since
+    struct BgOrder {
+        int64_t n = 0, n_pairs = 0;
+        int rc = 0;
+        std::vector<int32_t> perm;
+        std::vector<std::vector<int32_t>> pat;
+    };
+    std::future<BgOrder> bg;
     double prep_ms[3] = {};                    // its incsym, derive, chol plan times
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
                                                // chol upload (ms); factor Mflop, largest front (blocks),
@@ -153,12 +168,33 @@ struct dpg_inc {
 
 namespace {
 
-// contribution lists (gather_kernel) of every upper block, in factor order, and the device copies
+// contribution lists (gather_kernel) of every upper block, in factor order, and the device copies.
+// The factor list only grows between resets (a failed update truncates it again), so without Q1
+// scaling only the factors the device does not hold yet go up; the lists are rebuilt (a new factor
+// lands in the middle of the CSR) straight into a pinned staging buffer and copied without a
+// synchronisation -- the next rebuild comes after this update's fetch.
 int inc_rebuild(dpg_inc* q, hipStream_t s) {
     dpg_gn_dev& g = q->g;
     const int64_t n = q->V, nf = (int64_t)q->F.size(), P = (int64_t)q->plo.size();
     const int64_t nu = n + P;
-    std::vector<int32_t> cnt((size_t)nu + 1, 0);
+    int64_t n_list = 0;
+    for (int64_t k = 0; k < nf; ++k) n_list += q->F[(size_t)k].kind == DPG_FACTOR_BETWEEN ? 3 : 1;
+    // the last rebuild's copies out of the staging buffer must be done before it is rewritten
+    if (q->lists_ev_set && hipEventSynchronize(q->lists_ev) != hipSuccess) return DPG_ERR_HIP;
+    const size_t need = (size_t)(nu + 1 + n_list);
+    if (need > q->c_lists) {
+        const size_t nc = std::max(need, q->c_lists + q->c_lists / 2) + 4096;
+        if (q->h_lists) {
+            (void)hipHostFree(q->h_lists);
+            q->h_lists = nullptr;
+            q->c_lists = 0;
+        }
+        if (hipHostMalloc(reinterpret_cast<void**>(&q->h_lists), nc * sizeof(int32_t)) != hipSuccess) return DPG_ERR_HIP;
+        q->c_lists = nc;
+    }
+    int32_t* cnt = q->h_lists;
+    int32_t* clist = q->h_lists + nu + 1;
+    std::fill(cnt, cnt + nu + 1, 0);
     for (int64_t k = 0; k < nf; ++k) {
         const dpg_factor& f = q->F[(size_t)k];
         cnt[(size_t)f.i + 1]++;
@@ -168,8 +204,7 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
         }
     }
     for (int64_t u = 0; u < nu; ++u) cnt[(size_t)u + 1] += cnt[(size_t)u];
-    std::vector<int32_t> clist((size_t)cnt[(size_t)nu]);
-    std::vector<int32_t> cur(cnt.begin(), cnt.end() - 1);
+    std::vector<int32_t> cur(cnt, cnt + nu);
     for (int64_t k = 0; k < nf; ++k) {
         const dpg_factor& f = q->F[(size_t)k];
         clist[(size_t)cur[(size_t)f.i]++] = (int32_t)(k << 2 | 0);
@@ -178,41 +213,48 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
             clist[(size_t)cur[(size_t)(n + q->f_pair[(size_t)k])]++] = (int32_t)(k << 2 | (f.i < f.j ? 2 : 3));
         }
     }
-    // factors as the device sees them: Q1 multiplicity folded into the information
-    q->h_dev_factors = q->F;
-    if (q->P.duplicate_factors)
-        for (int64_t k = 0; k < nf; ++k) {
-            const double mult = (double)(q->updates - q->f_created[(size_t)k] + 1);
-            for (int c = 0; c < 3; ++c) q->h_dev_factors[(size_t)k].info[c] *= mult;
-        }
     g.n_nodes = n;
     g.n_factors = nf;
     g.nnzb_upper = nu;
     g.shard_begin = 0;
     g.shard_end = nf;
     g.n_blocks_rows = (int32_t)nblk(n);
+    const int64_t keep = q->P.duplicate_factors ? 0 : std::min(q->n_dev_f, nf);
     int rc = 0;
-    rc |= dgrow(&g.factors, &q->c_factors, (size_t)nf, s, 0);
-    rc |= dgrow(&g.up_cptr, &q->c_cptr, cnt.size(), s, 0);
-    rc |= dgrow(&g.up_clist, &q->c_clist, clist.size(), s, 0);
+    rc |= dgrow(&g.factors, &q->c_factors, (size_t)nf, s, (size_t)keep);
+    rc |= dgrow(&g.up_cptr, &q->c_cptr, (size_t)(nu + 1), s, 0);
+    rc |= dgrow(&g.up_clist, &q->c_clist, (size_t)n_list, s, 0);
     rc |= dgrow(&g.hb_own, &q->c_hb, (size_t)(9 * nu + 3 * n + 2), s, 0);
-    rc |= dgrow(&g.contrib, &q->c_contrib, 13 * std::max<size_t>(clist.size(), 1), s, 0);   // lin_kernel's records
+    rc |= dgrow(&g.contrib, &q->c_contrib, 13 * std::max<size_t>((size_t)n_list, 1), s, 0);   // lin_kernel's records
     rc |= dgrow(&g.partials, &q->c_partials, (size_t)(6 * g.n_blocks_rows + n), s, 0);
     if (!g.scal3) {
         rc |= hipMalloc(reinterpret_cast<void**>(&g.scal3), 4 * sizeof(double)) != hipSuccess;
         if (!rc) rc |= hipHostMalloc(reinterpret_cast<void**>(&g.scal3_host), 4 * sizeof(double)) != hipSuccess;
     }
     if (rc) return DPG_ERR_HIP;
-    if (nf && hipMemcpyAsync(g.factors, q->h_dev_factors.data(), sizeof(dpg_factor) * (size_t)nf, hipMemcpyHostToDevice,
-                             s) != hipSuccess)
+    if (q->P.duplicate_factors) {   // factors as the device sees them: Q1 multiplicity folded into the information
+        q->h_dev_factors = q->F;
+        for (int64_t k = 0; k < nf; ++k) {
+            const double mult = (double)(q->updates - q->f_created[(size_t)k] + 1);
+            for (int c = 0; c < 3; ++c) q->h_dev_factors[(size_t)k].info[c] *= mult;
+        }
+        if (nf && hipMemcpyAsync(g.factors, q->h_dev_factors.data(), sizeof(dpg_factor) * (size_t)nf,
+                                 hipMemcpyHostToDevice, s) != hipSuccess)
+            return DPG_ERR_HIP;
+    } else if (nf > keep) {
+        // pageable source: the copy is staged before the call returns, and q->F changes only later
+        if (hipMemcpyAsync(g.factors + keep, q->F.data() + keep, sizeof(dpg_factor) * (size_t)(nf - keep),
+                           hipMemcpyHostToDevice, s) != hipSuccess)
+            return DPG_ERR_HIP;
+    }
+    q->n_dev_f = q->P.duplicate_factors ? 0 : nf;
+    if (hipMemcpyAsync(g.up_cptr, cnt, sizeof(int32_t) * (size_t)(nu + 1), hipMemcpyHostToDevice, s) != hipSuccess)
         return DPG_ERR_HIP;
-    if (hipMemcpyAsync(g.up_cptr, cnt.data(), sizeof(int32_t) * cnt.size(), hipMemcpyHostToDevice, s) != hipSuccess)
+    if (n_list && hipMemcpyAsync(g.up_clist, clist, sizeof(int32_t) * (size_t)n_list, hipMemcpyHostToDevice, s) != hipSuccess)
         return DPG_ERR_HIP;
-    if (!clist.empty() &&
-        hipMemcpyAsync(g.up_clist, clist.data(), sizeof(int32_t) * clist.size(), hipMemcpyHostToDevice, s) != hipSuccess)
-        return DPG_ERR_HIP;
-    // the host vectors above must outlive the async copies
-    if (hipStreamSynchronize(s) != hipSuccess) return DPG_ERR_HIP;
+    if (!q->lists_ev && hipEventCreateWithFlags(&q->lists_ev, hipEventDisableTiming) != hipSuccess) return DPG_ERR_HIP;
+    if (hipEventRecord(q->lists_ev, s) != hipSuccess) return DPG_ERR_HIP;
+    q->lists_ev_set = true;
     const double t = now_ms();
     const int rc2 = dpg_chol_create_sym_upload(&g.chol);   // planned by inc_prepare
     q->prof[3] = now_ms() - t + q->prep_ms[2];
@@ -230,6 +272,16 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
 }
 
 int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
+
+// background ordering (DPG_INC_BG_ORDER=0 turns it off: every fresh order on the calling thread)
+constexpr int64_t kBgLead = 16;
+bool bg_order_on() {
+    static const bool on = [] { const char* e = getenv("DPG_INC_BG_ORDER"); return !(e && atoi(e) == 0); }();
+    return on;
+}
+void bg_discard(dpg_inc* q) {
+    if (q->bg.valid()) (void)q->bg.get();   // joins the worker
+}
 
 }  // namespace
 
@@ -267,9 +319,11 @@ dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
 
 int dpg_inc_reset(dpg_inc* q) {
     if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_reset: NULL");
+    bg_discard(q);
     q->V = 0;
     q->updates = 0;
     q->F.clear();
+    q->n_dev_f = 0;
     q->f_created.clear();
     q->f_pair.clear();
     q->pair_id.clear();
@@ -289,6 +343,7 @@ int dpg_inc_reset(dpg_inc* q) {
 int dpg_inc_abort_prepare(dpg_inc* q) {
     if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_abort_prepare: NULL");
     if (!q->prepared) return DPG_OK;
+    bg_discard(q);   // its snapshot may hold the pairs that leave now; the next prepare reorders anyway
     for (size_t k = (size_t)q->prep_pairs0; k < q->plo.size(); ++k) q->pair_id.erase(pkey(q->plo[k], q->phi[k]));
     q->plo.resize((size_t)q->prep_pairs0);
     q->phi.resize((size_t)q->prep_pairs0);
@@ -308,6 +363,8 @@ void dpg_inc_destroy(dpg_inc* q) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (q->g.scal3_host) (void)hipHostFree(q->g.scal3_host);
+    if (q->h_lists) (void)hipHostFree(q->h_lists);
+    if (q->lists_ev) (void)hipEventDestroy(q->lists_ev);
     if (q->g.chol) dpg_chol_destroy(q->g.chol);
     delete q;
 }
@@ -361,23 +418,51 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
         }
     }
     // ordering: extended, or fresh every reorder_every nodes / after 1.5x fill growth
-    bool reordered = false;
+    // (the order due every reorder_every nodes comes from the worker thread when one was started
+    // for it: the snapshot's order, the nodes since appended at its end and the pairs since added,
+    // as between reorders)
+    bool reordered = false, from_bg = false;
     const double expect = q->V_at_order > 0 ? (double)q->nnz_at_order * (double)V1 / (double)q->V_at_order : 0.0;
     if (q->I.n == 0 || V1 - q->V_at_order >= q->P.reorder_every) {
         reordered = true;
+        from_bg = q->I.n > 0 && q->bg.valid();
     } else {
         for (auto& pr : new_pairs) dpg_incsym_add_edge(&q->I, pr.first, pr.second);
         if ((double)q->I.nnz > 1.5 * expect + 64.0) reordered = true;
     }
-    if (reordered) {
+    if (from_bg) {
+        dpg_inc::BgOrder r = q->bg.get();
+        if (r.rc || r.n > V1 || r.n_pairs > (int64_t)q->plo.size()) {
+            from_bg = false;
+        } else {
+            dpg_incsym_init(&q->I, r.n, r.perm, r.pat);
+            dpg_incsym_append(&q->I, V1 - r.n);
+            for (int64_t k = r.n_pairs; k < (int64_t)q->plo.size(); ++k) dpg_incsym_add_edge(&q->I, q->plo[(size_t)k], q->phi[(size_t)k]);
+        }
+    }
+    if (reordered && !from_bg) {
+        bg_discard(q);
         if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size())) {
             q->prepared = true;
             dpg_inc_abort_prepare(q);
             return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic analysis failed");
         }
+    }
+    if (reordered) {
         q->V_at_order = V1;
         q->nnz_at_order = q->I.nnz;
         q->reorders += 1;
+    }
+    if (bg_order_on() && !q->bg.valid() && V1 >= 256 && V1 - q->V_at_order >= q->P.reorder_every - kBgLead) {
+        const int64_t P = (int64_t)q->plo.size();
+        std::vector<int32_t> lo(q->plo), hi(q->phi);
+        q->bg = std::async(std::launch::async, [V1, P, lo = std::move(lo), hi = std::move(hi)]() {
+            dpg_inc::BgOrder r;
+            r.n = V1;
+            r.n_pairs = P;
+            r.rc = dpg_incsym_order(V1, lo.data(), hi.data(), P, r.perm, r.pat);
+            return r;
+        });
     }
     const double t1a = now_ms();
     if (dpg_incsym_derive(&q->I, &q->opts, &q->S)) {
@@ -472,6 +557,7 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     auto rollback = [&](int code, const char* msg) -> int {
         (void)hipStreamSynchronize(s);
         q->F.resize((size_t)nF0);
+        q->n_dev_f = std::min(q->n_dev_f, nF0);
         q->f_created.resize((size_t)nF0);
         q->f_pair.resize((size_t)nF0);
         q->V = V0;
@@ -735,6 +821,7 @@ dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path) {
     q->V = h.V;
     q->updates = h.updates;
     q->F = F;
+    q->n_dev_f = 0;
     q->f_created = created;
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(ctx));
     if (hipSetDevice(dpg_ctx_device_of(ctx)) != hipSuccess) return bail(DPG_ERR_HIP, "hipSetDevice failed");
