@@ -1684,12 +1684,13 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
         if ((rc = dpg_icp_batch_prepare(c, edges.data(), E, pf.data(), &I))) return rc;
         if ((rc = icp_batch_run_from(c, V))) return rc;
         // while the GPU aligns: the update's structure on the host, with every pair a factor may
-        // come from (a loop closure that does not converge stays an explicit zero block)
+        // come from (a loop closure that does not converge stays an explicit zero block) -- its
+        // symbolic half on a worker thread, joined by dpg_inc_update once the factors are staged
         {
             std::vector<int32_t> pr(edges);
             for (int64_t k = 0; k < n_extra; ++k)
                 if (extra[k].kind == DPG_FACTOR_BETWEEN) { pr.push_back(extra[k].i); pr.push_back(extra[k].j); }
-            if ((rc = dpg_inc_prepare(g, 1, pr.data(), (int64_t)pr.size() / 2))) return rc;
+            if ((rc = dpg_inc_prepare_async(g, 1, pr.data(), (int64_t)pr.size() / 2))) return rc;
         }
         std::vector<dpg_icp_result> res((size_t)E);
         if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;

@@ -1768,7 +1768,11 @@ struct CholDev {
     size_t c_stage = 0;
     char* arena = nullptr;        // device: every structure array above (sns .. upd_tasks), one copy
     size_t c_arena = 0;
+    void* host = nullptr;         // CholHost of the build in progress (a plan and its upload may run
+                                  // on different threads, one after the other)
 };
+
+void free_host(void* p);
 
 }  // namespace
 
@@ -1780,6 +1784,7 @@ extern "C" void dpg_chol_destroy(void* h) {
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stage) (void)hipHostFree(c->stage);
+    free_host(c->host);
     delete c;
 }
 
@@ -2345,21 +2350,22 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     return rc ? DPG_ERR_HIP : DPG_OK;
 }
 
-// the host structures of the build in progress on this thread (a plan and its upload may be split:
-// dpg_chol_create_sym_plan / _upload)
-CholHost& build_host() {
-    thread_local CholHost H;
-    return H;
+// the host structures of c's build in progress (a plan and its upload may be split:
+// dpg_chol_create_sym_plan / _upload, possibly on two threads one after the other)
+CholHost& build_host(CholDev* c) {
+    if (!c->host) c->host = new CholHost();
+    return *static_cast<CholHost*>(c->host);
 }
+void free_host(void* p) { delete static_cast<CholHost*>(p); }
 int chol_build_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
     const double t_b0 = wall_ms();
-    const int rc = chol_plan(c, n, pair_lo, pair_hi, n_pairs, build_host());
+    const int rc = chol_plan(c, n, pair_lo, pair_hi, n_pairs, build_host(c));
     c->t_build[0] = wall_ms() - t_b0;
     return rc;
 }
 int chol_build_upload(CholDev* c) {
     const double t_b1 = wall_ms();
-    const int rc = chol_upload(c, c->n, build_host());
+    const int rc = chol_upload(c, c->n, build_host(c));
     c->t_build[1] = wall_ms() - t_b1;
     return rc;
 }
@@ -2370,7 +2376,7 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
 }  // namespace
 
 // dpg_chol_create_sym in two halves: the plan (host only: no device call, so it may run while the
-// caller's stream still works) and the upload of what it planned (same thread, nothing between)
+// caller's stream still works, on any thread) and the upload of what it planned (nothing between)
 int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                              dpg_chol_sym* S) {
     CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();

@@ -33,7 +33,13 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <future>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -112,6 +118,57 @@ inline uint64_t pkey(int32_t lo, int32_t hi) { return ((uint64_t)(uint32_t)lo <<
 
 }  // namespace
 
+// One persistent worker per graph for the prepare's symbolic half (DPG_INC_ASYNC=1; off by
+// default): its scratch (the derive's thread-local buffers, the symbolic state) stays warm on one
+// thread -- a fresh std::async thread per node measured slower than no overlap at all.  Measured
+// (profiles/r03/v25_incasync_ab.txt, v26_incworker_ab.txt): config 4 p50 1.95 -> 2.02 ms (the
+// plan runs ~25 % slower off the thread that built the pairs), config 5 411 -> 424 nodes/s.
+struct dpg_inc_worker {
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::function<int()> job;
+    bool quit = false;
+    std::atomic<int> state{0};   // 0 idle, 1 submitted / running, 2 done
+    int rc = 0;
+    dpg_inc_worker() : th([this] { loop(); }) {}
+    ~dpg_inc_worker() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            quit = true;
+        }
+        cv.notify_one();
+        th.join();
+    }
+    void loop() {
+        std::unique_lock<std::mutex> lk(m);
+        for (;;) {
+            cv.wait(lk, [&] { return quit || (bool)job; });
+            if (quit) return;
+            std::function<int()> j = std::move(job);
+            job = nullptr;
+            lk.unlock();
+            const int r = j();
+            lk.lock();
+            rc = r;
+            state.store(2, std::memory_order_release);
+        }
+    }
+    void submit(std::function<int()> f) {
+        {
+            std::lock_guard<std::mutex> g(m);
+            job = std::move(f);
+            state.store(1, std::memory_order_relaxed);
+        }
+        cv.notify_one();
+    }
+    int wait() {   // the caller has nothing else to do: spin (yielding) until the job is done
+        while (state.load(std::memory_order_acquire) != 2) std::this_thread::yield();
+        state.store(0, std::memory_order_relaxed);
+        return rc;
+    }
+};
+
 struct dpg_inc {
     dpg_ctx* ctx = nullptr;
     dpg_inc_params P{};
@@ -160,6 +217,9 @@ struct dpg_inc {
         std::vector<std::vector<int32_t>> pat;
     };
     std::future<BgOrder> bg;
+    std::unique_ptr<dpg_inc_worker> worker;    // the symbolic half of a prepare (dpg_inc_prepare_async)
+    bool prep_running = false;
+    const char* prep_msg = "";                 // its failure message
     double prep_ms[3] = {};                    // its incsym, derive, chol plan times
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
                                                // chol upload (ms); factor Mflop, largest front (blocks),
@@ -173,7 +233,7 @@ namespace {
 // scaling only the factors the device does not hold yet go up; the lists are rebuilt (a new factor
 // lands in the middle of the CSR) straight into a pinned staging buffer and copied without a
 // synchronisation -- the next rebuild comes after this update's fetch.
-int inc_rebuild(dpg_inc* q, hipStream_t s) {
+int inc_rebuild_lists(dpg_inc* q, hipStream_t s) {
     dpg_gn_dev& g = q->g;
     const int64_t n = q->V, nf = (int64_t)q->F.size(), P = (int64_t)q->plo.size();
     const int64_t nu = n + P;
@@ -255,6 +315,12 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
     if (!q->lists_ev && hipEventCreateWithFlags(&q->lists_ev, hipEventDisableTiming) != hipSuccess) return DPG_ERR_HIP;
     if (hipEventRecord(q->lists_ev, s) != hipSuccess) return DPG_ERR_HIP;
     q->lists_ev_set = true;
+    return DPG_OK;
+}
+
+// the Cholesky structures planned by the prepare go up
+int inc_rebuild_chol(dpg_inc* q) {
+    dpg_gn_dev& g = q->g;
     const double t = now_ms();
     const int rc2 = dpg_chol_create_sym_upload(&g.chol);   // planned by inc_prepare
     q->prof[3] = now_ms() - t + q->prep_ms[2];
@@ -271,6 +337,11 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
     return rc2;
 }
 
+int inc_rebuild(dpg_inc* q, hipStream_t s) {
+    const int rc = inc_rebuild_lists(q, s);
+    return rc ? rc : inc_rebuild_chol(q);
+}
+
 int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
 
 // background ordering (DPG_INC_BG_ORDER=0 turns it off: every fresh order on the calling thread)
@@ -279,6 +350,7 @@ bool bg_order_on() {
     static const bool on = [] { const char* e = getenv("DPG_INC_BG_ORDER"); return !(e && atoi(e) == 0); }();
     return on;
 }
+int prep_join(dpg_inc* q);
 void bg_discard(dpg_inc* q) {
     if (q->bg.valid()) (void)q->bg.get();   // joins the worker
 }
@@ -319,6 +391,7 @@ dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
 
 int dpg_inc_reset(dpg_inc* q) {
     if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_reset: NULL");
+    (void)prep_join(q);
     bg_discard(q);
     q->V = 0;
     q->updates = 0;
@@ -342,6 +415,7 @@ int dpg_inc_reset(dpg_inc* q) {
 // so the next prepare orders the graph afresh from the pairs that remain.
 int dpg_inc_abort_prepare(dpg_inc* q) {
     if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_abort_prepare: NULL");
+    (void)prep_join(q);
     if (!q->prepared) return DPG_OK;
     bg_discard(q);   // its snapshot may hold the pairs that leave now; the next prepare reorders anyway
     for (size_t k = (size_t)q->prep_pairs0; k < q->plo.size(); ++k) q->pair_id.erase(pkey(q->plo[k], q->phi[k]));
@@ -356,6 +430,7 @@ int dpg_inc_abort_prepare(dpg_inc* q) {
 
 void dpg_inc_destroy(dpg_inc* q) {
     if (!q) return;
+    (void)prep_join(q);
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
     (void)hipStreamSynchronize(s);
     void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.contrib, q->g.partials, q->g.scal3,
@@ -395,7 +470,19 @@ int64_t dpg_inc_pairs(const dpg_inc* q, int32_t* lo, int32_t* hi, int64_t n) {
 // pair without factors is an explicit zero block), the symbolic analysis is extended or redone and
 // the Cholesky planned.  dpg_add_node_pairs runs it while the GPU aligns the node's edges; the
 // next dpg_inc_update (for the same n_new) uploads the plan and solves.
-int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs) {
+}  // extern "C"
+
+namespace {
+
+// The structural half of an update, in two parts.  prep_pairs (calling thread): validation, and
+// the update's new node pairs enter the pattern (pair ids in arrival order).  prep_symbolic: the
+// order extended or refreshed, the derived structures and the Cholesky plan -- host only; it touches
+// the symbolic state (I, S, the plan inside g.chol, the ordering bookkeeping) and nothing the
+// numeric half of the update reads before it joins, so dpg_add_node_pairs runs it on a worker
+// thread (dpg_inc_prepare_async) while the GPU aligns and the calling thread stages the factors.
+// It reports failures through its return code and prep_msg; the caller aborts the prepare.
+int prep_pairs(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs,
+               std::vector<std::pair<int32_t, int32_t>>& new_pairs) {
     if (!q || n_new < 0 || n_pairs < 0 || (n_pairs > 0 && !pairs)) return set_err(DPG_ERR_ARG, "dpg_inc_prepare: bad arguments");
     const int64_t V1 = q->V + n_new;
     for (int64_t e = 0; e < n_pairs; ++e)
@@ -404,10 +491,8 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
             return set_err(DPG_ERR_ARG, "dpg_inc_prepare: a pair references a missing node");
     if (V1 == 0) return set_err(DPG_ERR_STATE, "dpg_inc_prepare: empty graph");
     if (q->prepared) return set_err(DPG_ERR_STATE, "dpg_inc_prepare: an update is already prepared");
-    const double t1 = now_ms();
     q->prep_pairs0 = (int64_t)q->plo.size();
-    if (q->I.n > 0) dpg_incsym_append(&q->I, n_new);
-    std::vector<std::pair<int32_t, int32_t>> new_pairs;
+    new_pairs.clear();
     for (int64_t e = 0; e < n_pairs; ++e) {
         const int32_t lo = std::min(pairs[2 * e], pairs[2 * e + 1]), hi = std::max(pairs[2 * e], pairs[2 * e + 1]);
         if (q->pair_id.find(pkey(lo, hi)) == q->pair_id.end()) {
@@ -417,6 +502,14 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
             new_pairs.emplace_back(lo, hi);
         }
     }
+    q->prep_new = n_new;
+    q->prepared = true;
+    return DPG_OK;
+}
+
+int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::pair<int32_t, int32_t>>& new_pairs) {
+    const double t1 = now_ms();
+    if (q->I.n > 0) dpg_incsym_append(&q->I, n_new);
     // ordering: extended, or fresh every reorder_every nodes / after 1.5x fill growth
     // (the order due every reorder_every nodes comes from the worker thread when one was started
     // for it: the snapshot's order, the nodes since appended at its end and the pairs since added,
@@ -443,9 +536,8 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
     if (reordered && !from_bg) {
         bg_discard(q);
         if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size())) {
-            q->prepared = true;
-            dpg_inc_abort_prepare(q);
-            return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic analysis failed");
+            q->prep_msg = "dpg_inc_prepare: symbolic analysis failed";
+            return DPG_ERR_NUMERIC;
         }
     }
     if (reordered) {
@@ -466,23 +558,61 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
     }
     const double t1a = now_ms();
     if (dpg_incsym_derive(&q->I, &q->opts, &q->S)) {
-        q->prepared = true;
-        dpg_inc_abort_prepare(q);
-        return set_err(DPG_ERR_NUMERIC, "dpg_inc_prepare: symbolic derivation failed");
+        q->prep_msg = "dpg_inc_prepare: symbolic derivation failed";
+        return DPG_ERR_NUMERIC;
     }
     const double t1b = now_ms();
     const int rc = dpg_chol_create_sym_plan(&q->g.chol, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size(), &q->S);
     if (rc) {
-        q->prepared = true;
-        dpg_inc_abort_prepare(q);
-        return set_err(rc, "dpg_inc_prepare: Cholesky plan failed");
+        q->prep_msg = "dpg_inc_prepare: Cholesky plan failed";
+        return rc;
     }
     q->prep_ms[0] = t1a - t1;
     q->prep_ms[1] = t1b - t1a;
     q->prep_ms[2] = now_ms() - t1b;
     q->prep_reordered = reordered;
-    q->prep_new = n_new;
-    q->prepared = true;
+    return DPG_OK;
+}
+
+// the symbolic part's result once it is done (0 when none is running)
+int prep_join(dpg_inc* q) {
+    if (!q->prep_running) return DPG_OK;
+    q->prep_running = false;
+    return q->worker->wait();
+}
+
+bool prep_async_on() {
+    static const bool on = [] { const char* e = getenv("DPG_INC_ASYNC"); return e && atoi(e) != 0; }();
+    return on;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs) {
+    std::vector<std::pair<int32_t, int32_t>> new_pairs;
+    int rc = prep_pairs(q, n_new, pairs, n_pairs, new_pairs);
+    if (rc) return rc;
+    if ((rc = prep_symbolic(q, q->V + n_new, n_new, new_pairs))) {
+        const char* msg = q->prep_msg;
+        dpg_inc_abort_prepare(q);
+        return set_err(rc, msg);
+    }
+    return DPG_OK;
+}
+
+// dpg_inc_prepare with its symbolic part on a worker thread (DPG_INC_ASYNC=1; default: this thread);
+// the next dpg_inc_update (or abort / reset / destroy) joins it
+int dpg_inc_prepare_async(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs) {
+    if (!prep_async_on()) return dpg_inc_prepare(q, n_new, pairs, n_pairs);
+    std::vector<std::pair<int32_t, int32_t>> new_pairs;
+    const int rc = prep_pairs(q, n_new, pairs, n_pairs, new_pairs);
+    if (rc) return rc;
+    const int64_t V1 = q->V + n_new;
+    if (!q->worker) q->worker.reset(new dpg_inc_worker());
+    q->prep_running = true;
+    q->worker->submit([q, V1, n_new, np = std::move(new_pairs)]() { return prep_symbolic(q, V1, n_new, np); });
     return DPG_OK;
 }
 
@@ -568,16 +698,24 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         if (est_saved) (void)hipMemcpy(q->est, q->est_bak, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice);
         return set_err(code, msg);
     };
-    const bool reordered = q->prep_reordered;
+    // a prepare still running on its worker thread (dpg_inc_prepare_async): the contribution lists
+    // and, in ISAM2 mode, the relinearization and the assembly go first -- none of them reads the
+    // symbolic state -- and the update joins it before the Cholesky structures go up
+    const bool async_prep = q->prep_running;
+    const bool early = async_prep && q->P.mode == DPG_INC_ISAM2;
     const double t1b = now_ms();
-    if ((rc = inc_rebuild(q, s))) return rollback(rc, "dpg_inc_update: solver rebuild failed");
-    const double t2 = now_ms();
-    q->prof[0] = q->prep_ms[0];
-    q->prof[1] = q->prep_ms[1];
-    q->prof[2] = t2 - t1b - (q->prof[3] - q->prep_ms[2]);
+    if ((rc = inc_rebuild_lists(q, s))) return rollback(rc, "dpg_inc_update: contribution lists failed");
+    q->prof[2] = now_ms() - t1b;
+    auto join_and_upload = [&]() -> int {
+        const int prc = prep_join(q);
+        if (prc) return rollback(prc, q->prep_msg);
+        const int urc = inc_rebuild_chol(q);
+        return urc ? rollback(urc, "dpg_inc_update: solver rebuild failed") : DPG_OK;
+    };
+    if (!early && (rc = join_and_upload())) return rc;
+    double t2 = now_ms();
     dpg_inc_stats S;
     memset(&S, 0, sizeof(S));
-    S.reordered = reordered ? 1 : 0;
     if (q->P.mode == DPG_INC_ISAM2) {
         // 1. relinearize the variables whose delta passed the threshold (before the new factors)
         if (relin) {
@@ -596,6 +734,10 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
             return rollback(DPG_ERR_HIP, "dpg_inc_update: out of device memory");
         q->g.poses = q->theta;
         if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return rollback(rc, "assembly failed");
+        if (early) {
+            if ((rc = join_and_upload())) return rc;
+            t2 = now_ms();
+        }
         if ((rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s))) return rollback(rc, "Cholesky launch failed");
         if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return rollback(DPG_ERR_HIP, "memset");
         hipLaunchKernelGGL(inc_estimate_kernel, dim3(nblk(V1)), dim3(kThreads), 0, s, q->theta, dpg_chol_x_dev(q->g.chol),
@@ -650,6 +792,9 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         S.last_delta_inf = sc[0];
     }
     const double t3 = now_ms();
+    S.reordered = q->prep_reordered ? 1 : 0;
+    q->prof[0] = q->prep_ms[0];
+    q->prof[1] = q->prep_ms[1];
     S.n_nodes = V1;
     S.n_factors = (int64_t)q->F.size();
     S.nnz_l = q->I.nnz;

@@ -19,6 +19,7 @@ dpg_ctx* dpg_inc_ctx(dpg_inc* g);   /* the context an incremental graph runs on 
 /* the structural half of the next dpg_inc_update (host only: n_new nodes, node pairs that may carry
  * its Between factors), so that it can run while the GPU aligns the node's edges (dpg_inc.hip) */
 int dpg_inc_prepare(dpg_inc* g, int64_t n_new, const int32_t* pairs, int64_t n_pairs);
+int dpg_inc_prepare_async(dpg_inc* g, int64_t n_new, const int32_t* pairs, int64_t n_pairs);
 int dpg_inc_abort_prepare(dpg_inc* g);
 int dpg_ctx_is_multi(dpg_ctx* c);
 /* the scan store as host copies, and the neighbour index of every stored node (the graph
