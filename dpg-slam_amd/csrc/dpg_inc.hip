@@ -209,7 +209,7 @@ struct dpg_inc {
     size_t c_theta_bak = 0, c_est_bak = 0;
     bool prep_reordered = false;
     // the next fresh order, computed on a worker thread from a snapshot of the graph taken
-    // kBgLead nodes before it is due, then extended by the nodes and pairs that arrived since
+    // bg_lead() nodes before it is due, then extended by the nodes and pairs that arrived since
     struct BgOrder {
         int64_t n = 0, n_pairs = 0;
         int rc = 0;
@@ -345,7 +345,10 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
 int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
 
 // background ordering (DPG_INC_BG_ORDER=0 turns it off: every fresh order on the calling thread)
-constexpr int64_t kBgLead = 16;
+int64_t bg_lead() {   // nodes between the snapshot and the reorder it is for (DPG_INC_BG_LEAD, A/B)
+    static const int64_t v = [] { const char* e = getenv("DPG_INC_BG_LEAD"); return e ? (int64_t)atoi(e) : (int64_t)16; }();
+    return v;
+}
 bool bg_order_on() {
     static const bool on = [] { const char* e = getenv("DPG_INC_BG_ORDER"); return !(e && atoi(e) == 0); }();
     return on;
@@ -384,6 +387,7 @@ dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
     if (p) q->P = *p;
     else dpg_inc_params_default(&q->P);
     if (q->P.relinearize_skip < 1) q->P.relinearize_skip = 1;
+    if (const char* e = getenv("DPG_INC_REORDER_EVERY")) q->P.reorder_every = atoi(e);   // A/B override
     if (q->P.reorder_every < 1) q->P.reorder_every = 1;
     q->P.gn.linear_solver = DPG_SOLVER_CHOLESKY;
     return q;
@@ -545,7 +549,7 @@ int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::
         q->nnz_at_order = q->I.nnz;
         q->reorders += 1;
     }
-    if (bg_order_on() && !q->bg.valid() && V1 >= 256 && V1 - q->V_at_order >= q->P.reorder_every - kBgLead) {
+    if (bg_order_on() && !q->bg.valid() && V1 >= 256 && V1 - q->V_at_order >= q->P.reorder_every - bg_lead()) {
         const int64_t P = (int64_t)q->plo.size();
         std::vector<int32_t> lo(q->plo), hi(q->phi);
         q->bg = std::async(std::launch::async, [V1, P, lo = std::move(lo), hi = std::move(hi)]() {
