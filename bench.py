@@ -602,7 +602,7 @@ def main():
                     help="N=1 GN loop: dpg_gn_run, or the per-iteration host loop every rank runs at N>1")
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
     ap.add_argument("--inc-nodes", type=int, default=5000)
-    ap.add_argument("--inc-reorder-every", type=int, default=64, help="incremental: a fresh order every this many nodes")
+    ap.add_argument("--inc-reorder-every", type=int, default=32, help="incremental: a fresh order every this many nodes")
     ap.add_argument("--cpu-nodes", type=int, default=8, help="nodes in the incremental CPU-baseline sample")
     args = ap.parse_args()
     if args.workload == "incremental":

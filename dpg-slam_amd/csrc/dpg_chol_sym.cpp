@@ -827,7 +827,7 @@ int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, 
     // 8-start search with cover separators, each carried through the supernodal analysis under the
     // incremental solver's options, the shorter critical-path estimate kept.  It costs two orders
     // and two analyses per reorder, which dpg_inc computes on a worker thread ahead of time
-    // (dpg_inc.hip, kBgLead), so the per-node latency does not pay for it: config 4 at V = 5000
+    // (dpg_inc.hip, DPG_INC_BG_LEAD), so the per-node latency does not pay for it: config 4 at V = 5000
     // p50 2.14 -> 1.96 ms, 456 -> 487 nodes/s; config 5 413 vs 411 nodes/s
     // (profiles/r03/v24_incbg_ab.txt).  DPG_INC_ND=0: round 2's rule alone (round 2 and the earlier
     // round-3 default); k > 0: the k-start search alone (sqrt-ratio score, no cover step); -k: the

@@ -346,7 +346,7 @@ int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
 
 // background ordering (DPG_INC_BG_ORDER=0 turns it off: every fresh order on the calling thread)
 int64_t bg_lead() {   // nodes between the snapshot and the reorder it is for (DPG_INC_BG_LEAD, A/B)
-    static const int64_t v = [] { const char* e = getenv("DPG_INC_BG_LEAD"); return e ? (int64_t)atoi(e) : (int64_t)16; }();
+    static const int64_t v = [] { const char* e = getenv("DPG_INC_BG_LEAD"); return e ? (int64_t)atoi(e) : (int64_t)8; }();
     return v;
 }
 bool bg_order_on() {
@@ -369,7 +369,7 @@ void dpg_inc_params_default(dpg_inc_params* p) {
     p->relinearize_skip = 10;
     p->relinearize_threshold = 0.1;
     p->duplicate_factors = 0;
-    p->reorder_every = 64;
+    p->reorder_every = 32;
     dpg_gn_params_default(&p->gn);
 }
 

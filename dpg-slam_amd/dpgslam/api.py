@@ -489,7 +489,7 @@ class IncGraph:
     (dpg_slam.cc:255-329), device-resident, growing in place.  mode: "isam2" (ISAM2 defaults: partial
     relinearization, threshold 0.1, skip 10) or "batch" (Gauss-Newton to convergence per update)."""
 
-    def __init__(self, ctx: Context, mode: str = "isam2", duplicate_factors: bool = False, reorder_every: int = 64,
+    def __init__(self, ctx: Context, mode: str = "isam2", duplicate_factors: bool = False, reorder_every: int = 32,
                  gn_params=None):
         self.ctx = ctx
         p = _abi.default_inc_params()

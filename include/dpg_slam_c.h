@@ -369,7 +369,7 @@ typedef struct dpg_inc_params {
     int32_t relinearize_skip;        /* 10 (ISAM2Params::relinearizeSkip) */
     double relinearize_threshold;    /* 0.1 (ISAM2Params::relinearizeThreshold) */
     int32_t duplicate_factors;       /* 0; 1: SURVEY Q1 */
-    int32_t reorder_every;           /* 64: a fresh fill-reducing order every this many new nodes */
+    int32_t reorder_every;           /* 32: a fresh fill-reducing order every this many new nodes */
     dpg_gn_params gn;                /* DPG_INC_BATCH: the Gauss-Newton loop (Cholesky) */
 } dpg_inc_params;
 
