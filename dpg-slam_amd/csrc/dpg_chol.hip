@@ -1850,6 +1850,8 @@ struct CholHost {
     std::vector<int2> panel_t;
     std::vector<int4> upd_t;
     std::vector<int2> dblocks;
+    std::vector<int32_t> tcnt, tfill;   // per-tile child counts / fill cursors of one large front
+    std::vector<char> tused;
     int64_t acc_total = 0;
 };
 
@@ -2035,25 +2037,61 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         for (int32_t c = 0; c < k3; c += kFNB) cuts.push_back(c);
         for (int32_t c = k3; c < m3; c += kFNB) cuts.push_back(c);
         cuts.push_back(m3);
-        for (size_t t = 0; t + 1 < cuts.size(); ++t) {
-            const int32_t c0 = cuts[t], c1 = cuts[t + 1];
-            FTask ft{0, 0, (int32_t)fchild.size(), 0};
+        // the children's column ranges per tile, tile-major and child order within a tile: each
+        // child visits only the tiles its rows reach (its rows map to increasing front rows, so
+        // the tiles' boundaries fall at increasing j), counted, then placed
+        const int32_t nt = (int32_t)cuts.size() - 1;
+        std::vector<int32_t>& tcnt = H.tcnt;
+        tcnt.assign((size_t)nt + 1, 0);
+        const int64_t ch0 = S.child_ptr[(size_t)s], ch1 = S.child_ptr[(size_t)s + 1];
+        // the tile holding front row c: [0, k3) in kFNB steps, then [k3, m3) in kFNB steps
+        const int32_t nt_k = (k3 + kFNB - 1) / kFNB;
+        auto tile_of = [&](int32_t c) { return c < k3 ? c / kFNB : nt_k + (c - k3) / kFNB; };
+        for (int64_t ci = ch0; ci < ch1; ++ci) {
+            const SnDev& cd = sns[(size_t)S.child_list[(size_t)ci]];
+            if (cd.r == 0) continue;
+            const int32_t* rm = S.relmap.data() + cd.rows_off;
+            const int32_t ta = tile_of(3 * rm[0]), tb = tile_of(3 * rm[cd.r - 1] + 2);
+            for (int32_t t = ta; t <= tb; ++t) tcnt[(size_t)t + 1]++;   // an upper bound: empty ranges drop below
+        }
+        const size_t base = fchild.size();
+        for (int32_t t = 0; t < nt; ++t) tcnt[(size_t)t + 1] += tcnt[(size_t)t];
+        fchild.resize(base + (size_t)tcnt[(size_t)nt]);
+        std::vector<int32_t>& tfill = H.tfill;
+        tfill.assign(tcnt.begin(), tcnt.end() - 1);
+        std::vector<char>& used = H.tused;
+        used.assign(fchild.size() - base, 0);
+        for (int64_t ci = ch0; ci < ch1; ++ci) {
+            const SnDev& cd = sns[(size_t)S.child_list[(size_t)ci]];
+            if (cd.r == 0) continue;
+            const int32_t* rm = S.relmap.data() + cd.rows_off;
+            const int32_t ta = tile_of(3 * rm[0]), tb = tile_of(3 * rm[cd.r - 1] + 2);
+            int32_t ja = first_at_or_after(rm, cd.r, cuts[(size_t)ta]);
+            for (int32_t t = ta; t <= tb; ++t) {
+                const int32_t jb = first_at_or_after(rm, cd.r, cuts[(size_t)t + 1]);
+                const size_t at = (size_t)tfill[(size_t)t]++;
+                if (jb > ja) {
+                    fchild[base + at] = FChild{ja, jb, cd.k, cd.r, cd.front_off, cd.rows_off};
+                    used[at] = 1;
+                }
+                ja = jb;
+            }
+        }
+        // compact (a child whose rows skip a whole tile left an unused slot there)
+        size_t w = base;
+        for (int32_t t = 0; t < nt; ++t) {
+            const int32_t c0 = cuts[(size_t)t], c1 = cuts[(size_t)t + 1];
+            FTask ft{0, 0, (int32_t)w, 0};
             ft.om_b = (int32_t)d.omap_off + (int32_t)(std::lower_bound(ob, ob + d.omap_n, c0 / 3,
                           [](const OEnt& o, int32_t v) { return o.b < v; }) - ob);
             ft.om_e = (int32_t)d.omap_off + (int32_t)(std::upper_bound(ob, ob + d.omap_n, (c1 - 1) / 3,
                           [](int32_t v, const OEnt& o) { return v < o.b; }) - ob);
-            for (int64_t ci = S.child_ptr[(size_t)s]; ci < S.child_ptr[(size_t)s + 1]; ++ci) {
-                const int32_t ch = S.child_list[(size_t)ci];
-                const SnDev& cd = sns[(size_t)ch];
-                const int32_t* rm = S.relmap.data() + cd.rows_off;
-                if (cd.r == 0 || 3 * rm[cd.r - 1] + 2 < c0 || 3 * rm[0] >= c1) continue;   // misses the tile
-                const int32_t ja = first_at_or_after(rm, cd.r, c0);
-                const int32_t jb = first_at_or_after(rm, cd.r, c1);
-                if (jb > ja) fchild.push_back(FChild{ja, jb, cd.k, cd.r, cd.front_off, cd.rows_off});
-            }
-            ft.ch_cnt = (int32_t)fchild.size() - ft.ch_off;
+            for (int32_t a = tcnt[(size_t)t]; a < tcnt[(size_t)t + 1]; ++a)
+                if (used[(size_t)a]) fchild[w++] = fchild[base + (size_t)a];
+            ft.ch_cnt = (int32_t)w - ft.ch_off;
             ftasks.push_back(ft);
         }
+        fchild.resize(w);
     }
     // fused tickets (front * 64 + team member) in critical-path order: a front's priority is its
     // estimated time plus its parent's priority (the longest remaining path to the root), so
