@@ -31,6 +31,16 @@ def test_incremental_symbolic_matches_elimination(incsym_bin, n0, steps, seed, s
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("n0,steps,seed,split,lead", [(500, 120, 9, "-", 8), (300, 100, 4, "split", 16),
+                                                      (260, 80, 2, "-", 40)])
+def test_background_order_extended_matches_elimination(incsym_bin, n0, steps, seed, split, lead):
+    """The background reorder's state (dpg_inc.hip): the order of a snapshot taken `lead` nodes
+    earlier, extended by the nodes and edges since, keeps column patterns equal to a from-scratch
+    elimination of the whole graph in that order, through later growth."""
+    r = subprocess.run([incsym_bin, str(n0), str(steps), str(seed), split, str(lead)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
 def test_solver_plan_matches_straightforward_construction(tmp_path):
     """The GPU solver's host plan (dpg_chol.hip chol_plan: H-block -> front map by column buckets,
     child column ranges by binary search, critical-path front order) equals the straightforward

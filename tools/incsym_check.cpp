@@ -2,7 +2,7 @@
 // pose graph grown node by node (chain + loop closures to older nodes, some between two older
 // nodes), starting from a minimum-degree order of its first part; after every step the maintained
 // column patterns must equal a from-scratch symbolic elimination of the current graph in the
-// maintained order.  usage: incsym_check N0 STEPS SEED [split]   (exit 0 = all equal)
+// maintained order.  usage: incsym_check N0 STEPS SEED [split|-] [LEAD]   (exit 0 = all equal)
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -47,7 +47,23 @@ int main(int argc, char** argv) {
     std::vector<int32_t> lo, hi;
     for (auto& e : edges) { lo.push_back(e.first); hi.push_back(e.second); }
     dpg_chol_incsym I;
-    if (dpg_incsym_reset(&I, n0, lo.data(), hi.data(), (int64_t)lo.size())) return 3;
+    // lead > 0: the background reorder's path (dpg_inc.hip) -- the order of a snapshot of the graph
+    // `lead` nodes earlier (dpg_incsym_order + dpg_incsym_init), the nodes since appended at its
+    // end and their edges added, instead of a fresh order of the whole initial graph
+    const int lead = argc > 5 ? atoi(argv[5]) : 0;
+    if (lead > 0 && lead < n0) {
+        const int ns = n0 - lead;
+        int64_t k = 0;
+        while (k < (int64_t)edges.size() && edges[(size_t)k].second < ns) ++k;   // edges arrive by their later node
+        std::vector<int32_t> perm;
+        std::vector<std::vector<int32_t>> pat;
+        if (dpg_incsym_order(ns, lo.data(), hi.data(), k, perm, pat)) return 3;
+        dpg_incsym_init(&I, ns, perm, pat);
+        dpg_incsym_append(&I, lead);
+        for (int64_t q = k; q < (int64_t)edges.size(); ++q) dpg_incsym_add_edge(&I, edges[(size_t)q].first, edges[(size_t)q].second);
+    } else if (dpg_incsym_reset(&I, n0, lo.data(), hi.data(), (int64_t)lo.size())) {
+        return 3;
+    }
     int64_t n = n0;
     for (int s = 0; s < steps; ++s) {
         dpg_incsym_append(&I, 1);
