@@ -706,7 +706,10 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     // and, in ISAM2 mode, the relinearization and the assembly go first -- none of them reads the
     // symbolic state -- and the update joins it before the Cholesky structures go up
     const bool async_prep = q->prep_running;
-    const bool early = async_prep && q->P.mode == DPG_INC_ISAM2;
+    // (DPG_INC_EARLY_ASM=1: also without the worker -- the assembly then runs on the GPU while the
+    // host stages the Cholesky upload; not yet measured on the GPU, off by default)
+    static const bool early_asm = [] { const char* e = getenv("DPG_INC_EARLY_ASM"); return e && atoi(e) != 0; }();
+    const bool early = (async_prep || early_asm) && q->P.mode == DPG_INC_ISAM2;
     const double t1b = now_ms();
     if ((rc = inc_rebuild_lists(q, s))) return rollback(rc, "dpg_inc_update: contribution lists failed");
     q->prof[2] = now_ms() - t1b;
