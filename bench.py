@@ -598,8 +598,14 @@ def main():
     ap.add_argument("--cpu-dpg-calls", type=int, default=30, help="executeDPG calls replayed on the oracle")
     ap.add_argument("--dpg-param", action="append", default=[],
                     help="DpgParameters override, e.g. occ_grid_resolution=0.1 or num_sectors=8 (repeatable)")
-    ap.add_argument("--gn-loop", default="native", choices=["native", "python"],
-                    help="N=1 GN loop: dpg_gn_run, or the per-iteration host loop every rank runs at N>1")
+    ap.add_argument("--dist", default="native", choices=["native", "torch"],
+                    help="under torchrun: native = libdpg's rank form (its own RCCL communicator, the "
+                         "pipelined GN); torch = the per-rank step API + Python GN loop over torch.distributed")
+    ap.add_argument("--virtual", type=int, default=0,
+                    help="K > 0: K virtual devices on one card (dpg_ctx_create_virtual) -- a rehearsal of "
+                         "the sharded paths, not a scaling number")
+    ap.add_argument("--schedule", default="measured", choices=["measured", "caller"],
+                    help="batched ICP dispatch (dpg_ctx_set_icp_schedule); results are identical")
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
     ap.add_argument("--inc-nodes", type=int, default=5000)
     ap.add_argument("--inc-reorder-every", type=int, default=32, help="incremental: a fresh order every this many nodes")
@@ -615,23 +621,42 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
 
     import torch
     import torch.distributed as dist
     from dpgslam import _abi, api, synth
     from dpgslam import dist as D
 
-    gpu = local_rank % max(1, torch.cuda.device_count())   # == local_rank on a full node
+    # The forms of one job:
+    #   single  -- N = 1: one device context;
+    #   multi   -- N > 1 without a launcher: ONE process over N devices (dpg_ctx_create_multi: sharded
+    #              ICP, the pipelined GN with an in-stream ncclAllReduce per iteration);
+    #   rank    -- under torchrun (WORLD_SIZE = N): one process per GPU, each a rank of one RCCL
+    #              communicator made inside libdpg (dpg_ctx_create_rank), the same native paths;
+    #   virtual -- --virtual K: K virtual devices on one card (rehearsal of the sharded paths);
+    #   torch   -- --dist torch under torchrun: round 2's Python GN loop over torch.distributed.
+    n_vis = torch.cuda.device_count()
+    if world > 1:
+        mode = "torch" if args.dist == "torch" else "rank"
+        if world != args.gpus:
+            log(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    elif args.virtual:
+        mode = "virtual"
+    elif args.gpus > 1:
+        mode = "multi"
+        if n_vis < args.gpus:
+            log(f"error: --gpus {args.gpus} asked, {n_vis} GPU(s) visible")
+            sys.exit(2)
+    else:
+        mode = "single"
+    if mode == "torch":
+        return main_torch_dist(args, rank, world, local_rank)
+
+    gpu = local_rank % max(1, n_vis)   # == local_rank on a full node
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
-        else:
-            dist.init_process_group("gloo")
-
+        dist.init_process_group("gloo")   # host-side barrier / id hand-off; the data path is libdpg's RCCL
     t0 = time.time()
     w = synth.generate(args.config)
     log(f"[rank {rank}] generated {args.config}: V={w.V} E={w.E} points={len(w.pts)} in {time.time() - t0:.1f}s")
@@ -640,35 +665,34 @@ def main():
     if args.refactor_delta is not None:
         gp.refactor_delta = args.refactor_delta
 
-    ctx = api.Context(gpu)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    if mode == "rank":
+        obj = [api.nccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx = api.Context(gpu, rank=(obj[0], rank, world))
+    elif mode == "multi":
+        ctx = api.Context(0, n_gpus=args.gpus)
+    elif mode == "virtual":
+        ctx = api.Context(gpu, virtual=args.virtual)
+    else:
+        ctx = api.Context(gpu)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    n_gpus = {"single": 1, "multi": args.gpus, "rank": world, "virtual": 1}[mode]
     ctx.set_icp_variant(args.icp_variant)
+    ctx.set_icp_schedule(args.schedule)
     ctx.upload_scans(w.pts, w.offsets, params.downsample_icp_points_ratio)
-    n_src = np.diff(w.offsets)[w.edges[:, 1]]
-    n_tgt = np.diff(w.offsets)[w.edges[:, 0]]
-    pl = D.plan(rank, world, w.E, w.n_successive, w.icp_factor_first, edge_cost=n_src * n_tgt,
-                strategy=args.shard)
-    e0, e1 = pl.edge_range
-    my_edges = pl.edges(w.edges)
-    ctx.icp_prepare(my_edges, w.est, params)
-    F = pl.factors(w.factors_placeholder(), w.icp_factor_first)
-    hb_size = ctx.gn_setup(w.V, F, pl.factor_range, gp)
-    backend = D.DeviceBackend(ctx, hb_size, hb_size - 2, dev)
-    allreduce = (lambda hb: dist.all_reduce(hb)) if world > 1 else (lambda hb: None)
+    ctx.icp_prepare(w.edges, w.est, params)   # ALL edges: a multi-device context shards them itself
+    F = w.factors_placeholder()
+    ctx.gn_setup(w.V, F, params=gp)
     X0 = w.est.astype(np.float64)
-    # one rank has nothing to all-reduce: the loop runs natively (dpg_gn_run, same iterations and
-    # convergence test as dist.gn_loop, no interpreter between the launches)
-    native_gn = world == 1 and args.gn_loop == "native"
 
     def step():
         ctx.icp_run(compute_cov=True)
-        ctx.gn_take_icp(w.icp_factor_first + e0, e1 - e0, pl.n_always_local, params)
+        ctx.gn_take_icp(w.icp_factor_first, w.E, w.n_successive, params)   # on the device(s) that aligned them
         ctx.gn_set_poses(X0)
-        if native_gn:
-            return ctx.gn_run()[0]
-        return D.gn_loop(backend, allreduce, gp)
+        return ctx.gn_run()[0]
 
     def barrier():
+        ctx.synchronize()
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -682,7 +706,7 @@ def main():
     for _ in range(args.steps):
         ts = time.perf_counter()
         st = step()
-        torch.cuda.synchronize(dev)
+        ctx.synchronize()
         icp_ms.append(ctx.icp_kernel_ms())
         cov_ms.append(ctx.cov_kernel_ms())
         idx_ms.append(ctx.kdtree_build_ms())
@@ -694,27 +718,29 @@ def main():
         gn_ms.append((time.perf_counter() - ts) * 1e3 - icp_ms[-1] - cov_serial - idx_ms[-1])
     barrier()
     elapsed = time.perf_counter() - t_start
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_step = elapsed * 1e3 / args.steps
-    algo_bytes = ctx.icp_algorithmic_bytes()
-    k_ms = float(np.mean(icp_ms))
-    achieved = algo_bytes / (k_ms * 1e-3) / 1e9
-    res, _ = ctx.icp_fetch(with_hessian=False)
-    stats = {"icp_kernel_ms": k_ms, "cov_kernel_ms": float(np.mean(cov_ms)), "index_build_ms": float(np.mean(idx_ms)), "gn_iterations": float(np.mean(gn_iters)), "gn_factorizations": float(np.mean(n_fact)),
-             "ms_per_gn_iter": float(np.mean(gn_ms) / max(1.0, np.mean(gn_iters))),
-             "icp_iters_mean": float(res["iterations"].mean()), "icp_iters_max": int(res["iterations"].max()),
-             "final_error": st["final_error"], "pcg_iterations": st["pcg_iterations"],
-             "gn_loop": "native" if native_gn else "python"}
-    if world > 1:
-        t = torch.tensor([stats["icp_kernel_ms"], stats["ms_per_gn_iter"]], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        stats["icp_kernel_ms"], stats["ms_per_gn_iter"] = float(t[0]), float(t[1])
 
+    def reduce(vals, op):
+        if world == 1:
+            return vals
+        t = torch.tensor(vals, dtype=torch.float64)
+        dist.all_reduce(t, op=op)
+        return t.tolist()
+
+    elapsed = reduce([elapsed], dist.ReduceOp.MAX if world > 1 else None)[0]
+    ms_step = elapsed * 1e3 / args.steps
+    algo_bytes = reduce([ctx.icp_algorithmic_bytes()], dist.ReduceOp.SUM if world > 1 else None)[0]
+    k_ms, gn_it_ms = reduce([float(np.mean(icp_ms)), float(np.mean(gn_ms) / max(1.0, np.mean(gn_iters)))],
+                            dist.ReduceOp.MAX if world > 1 else None)
+    # one launch per device: the aggregate algorithmic rate against the devices' aggregate peak
+    achieved = algo_bytes / (k_ms * 1e-3) / 1e9
+    res, _ = ctx.icp_fetch(with_hessian=False)   # a collective on the rank form
+    stats = {"icp_kernel_ms": k_ms, "cov_kernel_ms": float(np.mean(cov_ms)), "index_build_ms": float(np.mean(idx_ms)),
+             "gn_iterations": float(np.mean(gn_iters)), "gn_factorizations": float(np.mean(n_fact)),
+             "ms_per_gn_iter": gn_it_ms,
+             "icp_iters_mean": float(res["iterations"].mean()), "icp_iters_max": int(res["iterations"].max()),
+             "final_error": st["final_error"], "pcg_iterations": st["pcg_iterations"], "gn_loop": "native"}
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and mode == "single" and not args.no_cpu_baseline:
         cores = host_cpus()
         cb = cpu_baseline(w, params, args.cpu_sample, threads=1)
         gnb = cpu_gn_baseline(w, res, params)
@@ -739,7 +765,7 @@ def main():
                                   "sample": f"same sample, OpenMP over edges, median of 5 runs ({cm['icp_s']:.2f} s per run)"}
 
     traffic, traffic_src, sq = pmc_traffic(KERNEL_NAME[args.icp_variant])
-    if world > 1:   # the PMC pass measured the whole 1-GPU launch; a rank's launch holds only its shard
+    if mode != "single":   # the PMC pass measured the whole 1-GPU launch; a device's launch holds only its shard
         traffic, traffic_src, sq = None, None, {}
     # the PMC record's provenance, and the kernel against the limiters the counters name: VALU issue
     # (wave64 VALU = 2 cycles on a SIMD-32, 1024 SIMDs at 2.4 GHz) and the LDS array (one access
@@ -751,7 +777,7 @@ def main():
                 "matches_running_kernel": rec.get("src_sha256") == src_now}
     counts = next((v for k, v in rec.get("counts", {}).items() if k.split("<")[0] == KERNEL_NAME[args.icp_variant]), {})
     limiters = []
-    if counts and world == 1:
+    if counts and mode == "single":
         t = k_ms * 1e-3
         if counts.get("SQ_INSTS_VALU"):
             a = counts["SQ_INSTS_VALU"] / t
@@ -768,7 +794,7 @@ def main():
             "metric": "ICP edges/sec + ms/GN-iter on 5k-node/20k-edge synthetic graph, 1->8 GPU",
             "value": w.E * args.steps / elapsed,
             "unit": "edges/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
@@ -779,7 +805,9 @@ def main():
             "data": "synthetic (seeded ray-cast 2D world, 5000-beam scans -> ~1000-pt clouds)",
             "config": {"workload": f"{args.config}: {w.V} nodes / {w.E} ICP edges / {len(F)} factors, "
                                    f"~{int(np.mean(np.diff(w.offsets)) / 5)}-pt downsampled scans",
-                       "nodes": w.V, "icp_edges": w.E, "factors": len(F), "parallelism": f"edge-sharded dp{world}"},
+                       "nodes": w.V, "icp_edges": w.E, "factors": len(F),
+                       "parallelism": f"edge-sharded dp{ctx.n_ranks}" + ("" if mode == "single" else f" ({mode} form)")},
+            "form": mode, "ranks": ctx.n_ranks, "icp_schedule": args.schedule,
             "ms_per_gn_iter": stats["ms_per_gn_iter"],
             "gn_iterations": stats["gn_iterations"],
             "gn_factorizations": stats["gn_factorizations"],
@@ -790,15 +818,15 @@ def main():
             "cov_beside_gn": ctx.cov_overlapped(),
             "index_build_ms": stats["index_build_ms"],
             "icp_variant": args.icp_variant,
-            "icp_edges_per_s_kernel": w.E / world / (stats["icp_kernel_ms"] * 1e-3) * world,
+            "icp_edges_per_s_kernel": w.E / (stats["icp_kernel_ms"] * 1e-3),
             "icp_iters_mean": stats["icp_iters_mean"],
             "icp_iters_max": stats["icp_iters_max"],
             "gn_note": "ms_per_gn_iter averages plain GN steps and chord steps that reuse the last Cholesky "
                        "factor (gn_factorizations of gn_iterations refactor; DESIGN.md section 3)",
             # roofline of the dominant kernel against HBM (SURVEY 8d's algorithmic bytes); the counters
             # say what actually limits it: "limiter" + the SQ fractions of the last committed PMC pass
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS * n_gpus, "unit": "GB/s",
+                         "frac": achieved / (HBM_PEAK_GBS * n_gpus), "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": KERNEL_NAME[args.icp_variant] + " (correspondence search + fit, fused)",
                          "bytes_per_launch": algo_bytes,
                          "limiter": "VALU issue + LDS latency with per-iteration workgroup barriers, not HBM: "
@@ -811,6 +839,83 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    ctx.close()
+
+
+def main_torch_dist(args, rank, world, local_rank):
+    """--dist torch under torchrun: one process per GPU, the per-rank step API of libdpg and the
+    Python GN loop (dpgslam.dist.gn_loop) with torch.distributed's all-reduce (RCCL) of the packed
+    system per iteration -- round 2's form, kept as the alternative to the native rank form."""
+    import torch
+    import torch.distributed as dist
+    from dpgslam import _abi, api, synth
+    from dpgslam import dist as D
+
+    gpu = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)   # RCCL over xGMI
+    else:
+        dist.init_process_group("gloo")
+    w = synth.generate(args.config)
+    params = _abi.default_icp_params()
+    gp = _abi.default_gn_params()
+    if args.refactor_delta is not None:
+        gp.refactor_delta = args.refactor_delta
+    ctx = api.Context(gpu)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctx.set_icp_variant(args.icp_variant)
+    ctx.upload_scans(w.pts, w.offsets, params.downsample_icp_points_ratio)
+    n_src = np.diff(w.offsets)[w.edges[:, 1]]
+    n_tgt = np.diff(w.offsets)[w.edges[:, 0]]
+    pl = D.plan(rank, world, w.E, w.n_successive, w.icp_factor_first, edge_cost=n_src * n_tgt, strategy=args.shard)
+    e0, e1 = pl.edge_range
+    ctx.icp_prepare(pl.edges(w.edges), w.est, params)
+    F = pl.factors(w.factors_placeholder(), w.icp_factor_first)
+    hb_size = ctx.gn_setup(w.V, F, pl.factor_range, gp)
+    backend = D.DeviceBackend(ctx, hb_size, hb_size - 2, dev)
+    X0 = w.est.astype(np.float64)
+
+    def step():
+        ctx.icp_run(compute_cov=True)
+        ctx.gn_take_icp(w.icp_factor_first + e0, e1 - e0, pl.n_always_local, params)
+        ctx.gn_set_poses(X0)
+        return D.gn_loop(backend, lambda hb: dist.all_reduce(hb), gp)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        st = step()
+    barrier()
+    icp_ms, iters = [], []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        torch.cuda.synchronize(dev)
+        icp_ms.append(ctx.icp_kernel_ms())
+        iters.append(st["iterations"])
+    barrier()
+    t = torch.tensor([time.perf_counter() - t_start, float(np.mean(icp_ms))], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, k_ms = float(t[0]), float(t[1])
+    if rank == 0:
+        print(json.dumps({
+            "metric": "ICP edges/sec + ms/GN-iter on 5k-node/20k-edge synthetic graph, 1->8 GPU",
+            "value": w.E * args.steps / elapsed, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "fp32 (ICP) + fp64 (GN)",
+            "data": "synthetic (seeded ray-cast 2D world, 5000-beam scans -> ~1000-pt clouds)",
+            "config": {"workload": f"{args.config}: {w.V} nodes / {w.E} ICP edges / {len(F)} factors",
+                       "nodes": w.V, "icp_edges": w.E, "factors": len(F),
+                       "parallelism": f"edge-sharded dp{world} (torch form)"},
+            "form": "torch", "ranks": world, "icp_kernel_ms": k_ms, "gn_iterations": float(np.mean(iters)),
+            "gn_loop": "python", "roofline": None, "cpu_baseline": None}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
     ctx.close()
 
 

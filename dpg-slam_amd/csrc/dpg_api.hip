@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/dpg_icp_cov.h"
@@ -149,20 +150,37 @@ struct dpg_ctx {
     dpg_gn_ctl* pipe_ctl = nullptr;
     dpg_gn_slot* pipe_slot = nullptr;
     hipEvent_t pipe_ev[2] = {};
-    // multi-GPU form (dpg_ctx_create_multi): this context drives device 0 of the set, `peers` are
-    // full single-device contexts of the others; one RCCL communicator per device
-    // (ncclCommInitAll, one process); `shard[k]` = the caller's edge indices staged on device k
+    // multi-device forms (dpg_ctx_create_multi / _rank / _virtual): this context drives local
+    // device 0 and holds the batch as the caller sees it; `peers` are full single-device contexts
+    // of the other local devices.  Local device k is global rank rank0 + k of `world`.
     std::vector<dpg_ctx*> peers;
-    std::vector<ncclComm_t> comms;
+    std::vector<ncclComm_t> comms;   // RCCL: one communicator per local device
+    int32_t coll = 0;                // kCollNone | kCollRccl | kCollVirtual
+    int32_t world = 1, rank0 = 0;
+    int32_t rank = 0;                // global rank of THIS device context (peers too)
+    // the staged batch, every form: the edges in the caller's order and their assignment --
+    // batch_owner[e] = global rank aligning edge e; shard[k] = the caller indices aligned on local
+    // device k, ascending (local result j of device k is edge shard[k][j])
+    std::vector<dpg_icp_edge> batch;
+    std::vector<int32_t> batch_owner;
     std::vector<std::vector<int64_t>> shard;
+    bool batch_measured = false;     // assignment + dispatch order from measured costs
+    int32_t batch_runs = 0;          // runs of the staged batch so far
+    int32_t schedule = DPG_ICP_SCHEDULE_MEASURED;
+    // measured alignment cost (iterations x (source + target points)) by (target, source) pair,
+    // from earlier runs: the LPT assignment over ranks and the longest-first dispatch order
+    std::unordered_map<uint64_t, float> cost;
+    DevBuf<int32_t> shard_idx;       // per device context: its shard's caller indices
+    DevBuf<float> cost_dev;          // rank form: the all-reduced cost vector of a batch
 };
 
 namespace {
+enum { kCollNone = 0, kCollRccl = 1, kCollVirtual = 2, kMaxVirtual = 16 };
 inline int n_dev(const dpg_ctx* c) { return 1 + (int)c->peers.size(); }
 inline dpg_ctx* dev_ctx(dpg_ctx* c, int k) { return k == 0 ? c : c->peers[(size_t)k - 1]; }
-// made by dpg_ctx_create_multi (even for one GPU: its calls then take the sharded paths, RCCL
-// all-reduce included, with one rank)
-inline bool is_multi(const dpg_ctx* c) { return !c->comms.empty(); }
+// made by dpg_ctx_create_multi / _rank / _virtual (even for one GPU: its calls then take the
+// sharded paths, the all-reduce included, with one rank)
+inline bool is_multi(const dpg_ctx* c) { return c->coll != kCollNone; }
 // order `stream` after the last batch covariance (before anything rewrites its inputs or reads it)
 inline int join_cov(dpg_ctx* c) {
     if (!c->cov_pending) return DPG_OK;
@@ -240,8 +258,7 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     }
     if (rc) return fail(rc, "ICP kernel launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
     if (timed) HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    static const bool overlap = !(getenv("DPG_COV_OVERLAP") && atoi(getenv("DPG_COV_OVERLAP")) == 0);
-    if (hess_dev && timed && overlap) {   // beside the pose graph: on aux, after the ICP
+    if (hess_dev && timed) {   // beside the pose graph: on aux, after the ICP
         if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
         HIP_TRY(hipStreamWaitEvent(c->aux, c->ev[1], 0));
         rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->aux);
@@ -335,6 +352,7 @@ dpg_ctx* dpg_ctx_create_multi(int32_t n_gpus, const int32_t* devices) {
             dpg_ctx_destroy(c);
             return nullptr;
         }
+        q->rank = k;
         c->peers.push_back(q);
     }
     c->comms.assign((size_t)n_gpus, nullptr);
@@ -345,14 +363,101 @@ dpg_ctx* dpg_ctx_create_multi(int32_t n_gpus, const int32_t* devices) {
         fail(DPG_ERR_HIP, "ncclCommInitAll over %d devices failed: %s", n_gpus, ncclGetErrorString(r));
         return nullptr;
     }
+    c->coll = kCollRccl;
+    c->world = n_gpus;
+    (void)hipSetDevice(c->device);
+    return c;
+}
+
+// Test / rehearsal form: k device contexts on ONE device, all on one stream (so the DAG solves of
+// the k "devices" never run concurrently), the all-reduce a device-side sum in rank order.  Every
+// sharded code path of the multi-device forms runs, with k > 1, on one card.
+dpg_ctx* dpg_ctx_create_virtual(int32_t k, int32_t device) {
+    if (k < 1 || k > kMaxVirtual) {
+        fail(DPG_ERR_ARG, "dpg_ctx_create_virtual: %d virtual devices (1 .. %d)", k, kMaxVirtual);
+        return nullptr;
+    }
+    dpg_ctx* c = dpg_ctx_create(device);
+    if (!c) return nullptr;
+    for (int r = 1; r < k; ++r) {
+        dpg_ctx* q = dpg_ctx_create(device);
+        if (!q) {
+            dpg_ctx_destroy(c);
+            return nullptr;
+        }
+        (void)hipStreamDestroy(q->stream);
+        q->stream = c->stream;
+        q->own_stream = false;
+        q->rank = r;
+        c->peers.push_back(q);
+    }
+    c->coll = kCollVirtual;
+    c->world = k;
+    return c;
+}
+
+int dpg_nccl_unique_id(void* id_out) {
+    if (!id_out) return fail(DPG_ERR_ARG, "dpg_nccl_unique_id: NULL");
+    static_assert(sizeof(ncclUniqueId) == DPG_NCCL_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) return fail(DPG_ERR_HIP, "ncclGetUniqueId failed: %s", ncclGetErrorString(r));
+    memcpy(id_out, &id, sizeof(id));
+    return DPG_OK;
+}
+
+// One process per GPU (torchrun): this process's device is global rank `rank` of `world`; the
+// communicator comes from the id rank 0 made (dpg_nccl_unique_id), passed around by the caller.
+dpg_ctx* dpg_ctx_create_rank(int32_t device, const void* nccl_id, int32_t rank, int32_t world) {
+    if (!nccl_id || world < 1 || rank < 0 || rank >= world) {
+        fail(DPG_ERR_ARG, "dpg_ctx_create_rank: rank %d of %d", rank, world);
+        return nullptr;
+    }
+    dpg_ctx* c = dpg_ctx_create(device);
+    if (!c) return nullptr;
+    ncclUniqueId id;
+    memcpy(&id, nccl_id, sizeof(id));
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&comm, world, id, rank);
+    if (r != ncclSuccess) {
+        dpg_ctx_destroy(c);
+        fail(DPG_ERR_HIP, "ncclCommInitRank(rank %d of %d) failed: %s", rank, world, ncclGetErrorString(r));
+        return nullptr;
+    }
+    c->comms.assign(1, comm);
+    c->coll = kCollRccl;
+    c->world = world;
+    c->rank0 = rank;
+    c->rank = rank;
     return c;
 }
 
 int32_t dpg_ctx_num_gpus(dpg_ctx* c) { return c ? n_dev(c) : -1; }
 int dpg_ctx_is_multi(dpg_ctx* c) { return c && is_multi(c) ? 1 : 0; }
+int32_t dpg_ctx_rank(dpg_ctx* c) { return c ? c->rank0 : -1; }
+
+// ranks of the context's collective: ncclCommCount of its communicator (RCCL forms), k (virtual),
+// 1 (single device)
+int32_t dpg_ctx_num_ranks(dpg_ctx* c) {
+    if (!c) return -1;
+    if (c->coll == kCollRccl) {
+        int n = -1;
+        if (ncclCommCount(c->comms[0], &n) != ncclSuccess) return fail(DPG_ERR_HIP, "ncclCommCount failed");
+        return n;
+    }
+    return c->world;
+}
+
+int dpg_ctx_set_icp_schedule(dpg_ctx* c, int32_t schedule) {
+    if (!c || (schedule != DPG_ICP_SCHEDULE_CALLER && schedule != DPG_ICP_SCHEDULE_MEASURED))
+        return fail(DPG_ERR_ARG, "bad ICP schedule");
+    c->schedule = schedule;
+    return DPG_OK;
+}
 
 void dpg_ctx_destroy(dpg_ctx* c) {
     if (!c) return;
+    if (c->coll == kCollVirtual) (void)hipStreamSynchronize(c->stream);   // the peers' work is on it
     for (dpg_ctx* q : c->peers) dpg_ctx_destroy(q);
     c->peers.clear();
     for (ncclComm_t m : c->comms)
@@ -367,6 +472,7 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release();
     c->s_off.release(); c->s_tree_pts.release(); c->s_tree_idx.release();
     c->buckets.release(); c->s_buckets.release(); c->icp_scratch.release();
+    c->shard_idx.release(); c->cost_dev.release();
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     if (c->pipe_ctl) (void)hipFree(c->pipe_ctl);
     if (c->pipe_slot) (void)hipHostFree(c->pipe_slot);
@@ -385,6 +491,8 @@ int dpg_ctx_set_stream(dpg_ctx* c, void* s) {
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
     c->stream = reinterpret_cast<hipStream_t>(s);
     c->own_stream = false;
+    if (c->coll == kCollVirtual)   // the virtual devices keep sharing one stream
+        for (dpg_ctx* q : c->peers) q->stream = c->stream;
     return DPG_OK;
 }
 
@@ -556,22 +664,23 @@ static void scans_truncate(dpg_ctx* c, int64_t V) {
     }
 }
 
-static int batch_prepare_1(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
-    if (!c || (!edges && ne > 0) || !poses || !p) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
+// The kernel's edge records of a batch in the caller's order (R3 guesses, dpg_slam.cc:364-378;
+// pad[0] = the caller's index), the kernel scalars and the largest clouds.
+static int build_batch(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p,
+                       std::vector<dpg_icp_edge>& out, dpg_icp_kparams& kp, int32_t& ms, int32_t& mt) {
+    if (!c || (!edges && ne > 0) || ne < 0 || !poses || !p) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
     if (c->n_nodes <= 0) return fail(DPG_ERR_STATE, "no scans uploaded");
     if (p->downsample_icp_points_ratio != c->ratio && !(p->downsample_icp_points_ratio < 1 && c->ratio == 1))
         return fail(DPG_ERR_STATE, "scans were uploaded with downsample ratio %d", c->ratio);
-    int rc = set_kparams(&c->kp, p);
+    int rc = set_kparams(&kp, p);
     if (rc) return rc;
-    HIP_TRY(hipSetDevice(c->device));
-    if ((rc = join_cov(c))) return fail(rc, "stream wait failed");
-    c->h_edges.resize((size_t)std::max<int64_t>(ne, 1));
-    int32_t ms = 0, mt = 0;
+    out.resize((size_t)ne);
+    ms = mt = 0;
     for (int64_t e = 0; e < ne; ++e) {
         const int32_t t = edges[2 * e], s = edges[2 * e + 1];  // node_1 = target, node_2 = source
         if (t < 0 || s < 0 || t >= c->n_nodes || s >= c->n_nodes)
             return fail(DPG_ERR_ARG, "edge %lld references a missing node", (long long)e);
-        dpg_icp_edge& E = c->h_edges[(size_t)e];
+        dpg_icp_edge& E = out[(size_t)e];
         memset(&E, 0, sizeof(E));
         E.src_node = s;
         E.tgt_node = t;
@@ -588,36 +697,118 @@ static int batch_prepare_1(dpg_ctx* c, const int32_t* edges, int64_t ne, const f
         ms = std::max(ms, E.n_src_ds);
         mt = std::max(mt, E.n_tgt_ds);
     }
-    // Optional dispatch order (DPG_ICP_ORDER=1): one workgroup per edge, so edges that need long
-    // alignments could start first; the predictor is the guess displacement.  Measured on config 4
-    // in bench.py it does not pay (6.55 ms ordered vs 6.49 ms in the caller's order; an oracle order
-    // by the measured iteration counts reached 5.82 ms in tools/icp_order_probe.py), so it is off by
-    // default.  Results are written by pad[0] either way, so the caller's order is unchanged.
-    static const bool order_edges = [] { const char* v = getenv("DPG_ICP_ORDER"); return v && v[0] == '1'; }();
-    if (order_edges && ne > 1) {
-        std::vector<double> key((size_t)ne);
-        for (int64_t e = 0; e < ne; ++e) {
-            const float* g = c->h_edges[(size_t)e].guess;   // [c -s tx; s c ty]
-            key[(size_t)e] = std::hypot((double)g[2], (double)g[5]) + 2.0 * std::fabs(std::atan2((double)g[3], (double)g[0]));
-        }
-        std::vector<int64_t> idx((size_t)ne);
-        for (int64_t e = 0; e < ne; ++e) idx[(size_t)e] = e;
-        std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) { return key[(size_t)a] > key[(size_t)b]; });
-        std::vector<dpg_icp_edge> sorted((size_t)ne);
-        for (int64_t k = 0; k < ne; ++k) sorted[(size_t)k] = c->h_edges[(size_t)idx[(size_t)k]];
-        std::copy(sorted.begin(), sorted.end(), c->h_edges.begin());
-    }
-    if (c->edges.reserve((size_t)std::max<int64_t>(ne, 1)) || c->res.reserve((size_t)std::max<int64_t>(ne, 1)) ||
-        c->hess.reserve((size_t)(9 * std::max<int64_t>(ne, 1))))
-        return fail(DPG_ERR_HIP, "out of device memory for %lld edges", (long long)ne);
+    return DPG_OK;
+}
+
+inline uint64_t pair_key(const dpg_icp_edge& E) { return (uint64_t)(uint32_t)E.tgt_node << 32 | (uint32_t)E.src_node; }
+// what an alignment costs: its iterations, each a search over both clouds
+inline float edge_cost(const dpg_icp_edge& E, int32_t iterations) {
+    return (float)std::max(iterations, 1) * (float)(E.n_src_ds + E.n_tgt_ds);
+}
+
+// device q's share of the staged batch: h = its edges in dispatch order, pad[0] = the local result
+// index; every device sizes its kernel by the batch-wide largest clouds (one kernel form)
+static int stage_device(dpg_ctx* q, std::vector<dpg_icp_edge>& h, const dpg_icp_kparams& kp, int32_t ms, int32_t mt,
+                        const std::vector<int64_t>* idx) {
+    HIP_TRY(hipSetDevice(q->device));
+    int rc = join_cov(q);
+    if (rc) return fail(rc, "stream wait failed");
+    const size_t ne = h.size();
+    if (q->edges.reserve(std::max<size_t>(ne, 1)) || q->res.reserve(std::max<size_t>(ne, 1)) ||
+        q->hess.reserve(9 * std::max<size_t>(ne, 1)))
+        return fail(DPG_ERR_HIP, "out of device memory for %zu edges", ne);
     if (ne > 0)
-        HIP_TRY(hipMemcpyAsync(c->edges.p, c->h_edges.data(), sizeof(dpg_icp_edge) * (size_t)ne,
-                               hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    c->n_edges = ne;
+        HIP_TRY(hipMemcpyAsync(q->edges.p, h.data(), sizeof(dpg_icp_edge) * ne, hipMemcpyHostToDevice, q->stream));
+    if (idx) {   // multi-device: the caller's index of every local result (dpg_gn_take_icp_measurements)
+        std::vector<int32_t> ix(idx->begin(), idx->end());
+        if (q->shard_idx.reserve(std::max<size_t>(ix.size(), 1))) return fail(DPG_ERR_HIP, "out of device memory");
+        if (!ix.empty())
+            HIP_TRY(hipMemcpyAsync(q->shard_idx.p, ix.data(), sizeof(int32_t) * ix.size(), hipMemcpyHostToDevice, q->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(q->stream));
+    q->h_edges.swap(h);
+    q->kp = kp;
+    q->n_edges = (int64_t)ne;
+    q->max_src = ms;
+    q->max_tgt = mt;
+    return DPG_OK;
+}
+
+// The staged batch over the ranks and each rank's dispatch order.  measured: every edge's cost is
+// known from an earlier run -- longest-processing-time assignment (longest first to the least
+// loaded rank; ties: lower index, lower rank) and longest-first dispatch on every rank, so the
+// alignments that bound a launch start first.  Otherwise edge e goes to rank e mod world, in the
+// caller's order (the caller's lists come grouped -- successive pairs, then loop closures nearest
+// first -- so every rank gets the same mix of classes).  Results keep the caller's order either way.
+static int plan_and_stage(dpg_ctx* c, bool measured) {
+    const int64_t ne = (int64_t)c->batch.size();
+    const int W = c->world;
+    std::vector<std::vector<int64_t>> disp((size_t)W);
+    c->batch_owner.assign((size_t)ne, 0);
+    if (measured) {
+        std::vector<float> w((size_t)ne);
+        for (int64_t e = 0; e < ne; ++e) w[(size_t)e] = c->cost.at(pair_key(c->batch[(size_t)e]));
+        std::vector<int64_t> ord((size_t)ne);
+        for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = e;
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return w[(size_t)a] > w[(size_t)b]; });
+        std::vector<double> load((size_t)W, 0.0);
+        for (int64_t e : ord) {
+            int r = 0;
+            for (int q = 1; q < W; ++q)
+                if (load[(size_t)q] < load[(size_t)r]) r = q;
+            c->batch_owner[(size_t)e] = r;
+            load[(size_t)r] += w[(size_t)e];
+            disp[(size_t)r].push_back(e);
+        }
+    } else {
+        for (int64_t e = 0; e < ne; ++e) {
+            const int r = (int)(e % W);
+            c->batch_owner[(size_t)e] = r;
+            disp[(size_t)r].push_back(e);
+        }
+    }
+    const int32_t ms = c->max_src, mt = c->max_tgt;
+    const dpg_icp_kparams kp = c->kp;
+    c->shard.assign((size_t)n_dev(c), {});
+    for (int k = 0; k < n_dev(c); ++k) {
+        const auto& d = disp[(size_t)(c->rank0 + k)];
+        auto& sh = c->shard[(size_t)k];
+        sh = d;
+        std::sort(sh.begin(), sh.end());
+        std::vector<dpg_icp_edge> h(d.size());
+        for (size_t q = 0; q < d.size(); ++q) {
+            h[q] = c->batch[(size_t)d[q]];
+            h[q].pad[0] = (int32_t)(std::lower_bound(sh.begin(), sh.end(), d[q]) - sh.begin());
+        }
+        const int rc = stage_device(dev_ctx(c, k), h, kp, ms, mt, is_multi(c) ? &sh : nullptr);
+        if (rc) return rc;
+    }
+    c->batch_measured = measured;
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
+static bool batch_costs_known(const dpg_ctx* c) {
+    for (const dpg_icp_edge& E : c->batch)
+        if (c->cost.find(pair_key(E)) == c->cost.end()) return false;
+    return true;
+}
+
+// Stage an edge batch on every device.  The assignment uses measured costs when every edge of the
+// batch has been aligned before (a sweep re-aligns the previous sweep's pairs from similar guesses).
+int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
+    if (!c) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
+    int32_t ms = 0, mt = 0;
+    dpg_icp_kparams kp;
+    std::vector<dpg_icp_edge> all;
+    int rc = build_batch(c, edges, ne, poses, p, all, kp, ms, mt);
+    if (rc) return rc;
+    c->batch.swap(all);
+    c->kp = kp;
     c->max_src = ms;
     c->max_tgt = mt;
-    return DPG_OK;
+    c->batch_runs = 0;
+    return plan_and_stage(c, c->schedule == DPG_ICP_SCHEDULE_MEASURED && ne > 0 && batch_costs_known(c));
 }
 
 static int batch_run_1(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
@@ -640,46 +831,54 @@ static int batch_run_1(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
                         compute_cov ? c->hess.p : nullptr, tr, true);
 }
 
-// Multi-GPU form: device k aligns the edges e with e mod n == k (the caller's lists come grouped --
-// successive pairs, then loop closures nearest first -- so every device gets the same mix of
-// classes, whose alignments differ in length and in correspondences per iteration), in the
-// caller's order; results are gathered back into the caller's order by dpg_icp_batch_fetch.
-int dpg_icp_batch_prepare(dpg_ctx* c, const int32_t* edges, int64_t ne, const float* poses, const dpg_icp_params* p) {
-    if (!c) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
-    const int n = n_dev(c);
-    if (!is_multi(c)) return batch_prepare_1(c, edges, ne, poses, p);
-    if ((!edges && ne > 0) || ne < 0) return fail(DPG_ERR_ARG, "dpg_icp_batch_prepare: bad arguments");
-    c->shard.assign((size_t)n, {});
-    std::vector<int32_t> sub;
-    for (int k = 0; k < n; ++k) {
-        auto& ids = c->shard[(size_t)k];
-        sub.clear();
-        for (int64_t e = k; e < ne; e += n) {
-            ids.push_back(e);
-            sub.push_back(edges[2 * e]);
-            sub.push_back(edges[2 * e + 1]);
-        }
-        const int rc = batch_prepare_1(dev_ctx(c, k), sub.empty() ? nullptr : sub.data(), (int64_t)ids.size(), poses, p);
-        if (rc) return rc;
+// the measured cost of every edge of the last run into the cost memory (blocking); on the rank form
+// the ranks' costs are summed into one vector (every edge has one owner, the others add 0), so every
+// rank plans the next run from the same numbers
+static int harvest_costs(dpg_ctx* c) {
+    const int64_t ne = (int64_t)c->batch.size();
+    std::vector<float> w((size_t)std::max<int64_t>(ne, 1), 0.f);
+    std::vector<dpg_icp_result> r;
+    for (int k = 0; k < (int)c->shard.size(); ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        const auto& sh = c->shard[(size_t)k];
+        if (sh.empty()) continue;
+        r.resize(sh.size());
+        HIP_TRY(hipSetDevice(q->device));
+        if (join_cov(q)) return fail(DPG_ERR_HIP, "stream wait failed");
+        HIP_TRY(hipMemcpyAsync(r.data(), q->res.p, sizeof(dpg_icp_result) * sh.size(), hipMemcpyDeviceToHost, q->stream));
+        HIP_TRY(hipStreamSynchronize(q->stream));
+        for (size_t j = 0; j < sh.size(); ++j) w[(size_t)sh[j]] = edge_cost(c->batch[(size_t)sh[j]], r[j].iterations);
     }
-    c->n_edges = ne;   // the whole batch, as the caller sees it (device 0 staged c->shard[0])
+    if (c->coll == kCollRccl && n_dev(c) == 1 && c->world > 1 && ne > 0) {
+        HIP_TRY(hipSetDevice(c->device));
+        if (c->cost_dev.reserve((size_t)ne)) return fail(DPG_ERR_HIP, "out of device memory");
+        HIP_TRY(hipMemcpyAsync(c->cost_dev.p, w.data(), sizeof(float) * (size_t)ne, hipMemcpyHostToDevice, c->stream));
+        const ncclResult_t nr = ncclAllReduce(c->cost_dev.p, c->cost_dev.p, (size_t)ne, ncclFloat, ncclSum, c->comms[0], c->stream);
+        if (nr != ncclSuccess) return fail(DPG_ERR_HIP, "ncclAllReduce (costs) failed: %s", ncclGetErrorString(nr));
+        HIP_TRY(hipMemcpyAsync(w.data(), c->cost_dev.p, sizeof(float) * (size_t)ne, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    for (int64_t e = 0; e < ne; ++e)
+        if (w[(size_t)e] > 0.f) c->cost[pair_key(c->batch[(size_t)e])] = w[(size_t)e];
     HIP_TRY(hipSetDevice(c->device));
     return DPG_OK;
 }
 
+// Run the staged batch on every device (launches only: the devices run concurrently).  A batch
+// run again after its first run (the bench's steps) is re-planned once from its measured costs.
 int dpg_icp_batch_run(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
-    if (!is_multi(c)) return batch_run_1(c, compute_cov, trace_iters);
-    if (trace_iters > 0) return fail(DPG_ERR_STATE, "the correspondence trace is a single-device diagnostic");
-    const int64_t ne = c->n_edges;
-    for (int k = 0; k < n_dev(c); ++k) {   // launches only: the devices run concurrently
-        dpg_ctx* q = dev_ctx(c, k);
-        q->n_edges = (int64_t)c->shard[(size_t)k].size();
-        const int rc = batch_run_1(q, compute_cov, 0);
-        if (rc) return rc;
+    if (trace_iters > 0 && is_multi(c)) return fail(DPG_ERR_STATE, "the correspondence trace is a single-device diagnostic");
+    int rc;
+    if (c->schedule == DPG_ICP_SCHEDULE_MEASURED && !c->batch_measured && c->batch_runs > 0 && trace_iters <= 0 &&
+        !c->batch.empty()) {
+        if (!batch_costs_known(c) && (rc = harvest_costs(c))) return rc;
+        if (batch_costs_known(c) && (rc = plan_and_stage(c, true))) return rc;
     }
-    c->n_edges = ne;
+    for (int k = 0; k < n_dev(c); ++k)
+        if ((rc = batch_run_1(dev_ctx(c, k), compute_cov, trace_iters))) return rc;
     c->have_cov = compute_cov != 0;
+    ++c->batch_runs;
     HIP_TRY(hipSetDevice(c->device));
     return DPG_OK;
 }
@@ -690,6 +889,7 @@ static int icp_batch_run_from(dpg_ctx* c, int64_t tree_from) {
     HIP_TRY(hipSetDevice(c->device));
     c->trace_iters = 0;
     c->have_cov = false;
+    ++c->batch_runs;
     return launch_batch(c, c->ds.p, c->full.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
                         c->buckets.p, c->edges.p, c->n_edges, c->kp, c->max_src, c->max_tgt, c->res.p, nullptr,
                         nullptr, true, tree_from);
@@ -715,48 +915,92 @@ float dpg_kdtree_build_ms(dpg_ctx* c) {
     return ms;
 }
 
-static int batch_fetch_1(dpg_ctx* c, dpg_icp_result* results, double* hess);
-
-int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
-    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
-    const int n = n_dev(c);
-    if (!is_multi(c)) return batch_fetch_1(c, results, hess);
-    if (hess && !c->have_cov) return fail(DPG_ERR_STATE, "last batch ran without compute_cov");
-    const int64_t ne = c->n_edges;
-    std::vector<dpg_icp_result> r;
-    std::vector<double> h;
-    for (int k = 0; k < n; ++k) {
-        dpg_ctx* q = dev_ctx(c, k);
-        const auto& ids = c->shard[(size_t)k];
-        r.resize(std::max<size_t>(ids.size(), 1));
-        if (hess) h.resize(9 * std::max<size_t>(ids.size(), 1));
-        q->n_edges = (int64_t)ids.size();
-        const int rc = batch_fetch_1(q, results ? r.data() : nullptr, hess ? h.data() : nullptr);
-        c->n_edges = ne;
-        if (rc) return rc;
-        for (size_t j = 0; j < ids.size(); ++j) {
-            if (results) results[ids[j]] = r[j];
-            if (hess) memcpy(hess + 9 * ids[j], h.data() + 9 * j, 9 * sizeof(double));
-        }
-    }
-    c->n_edges = ne;
-    HIP_TRY(hipSetDevice(c->device));
+// device q's results (+ covariance blocks) in local order, blocking
+static int fetch_local(dpg_ctx* q, size_t n, dpg_icp_result* results, double* hess) {
+    HIP_TRY(hipSetDevice(q->device));
+    if (join_cov(q)) return fail(DPG_ERR_HIP, "stream wait failed");
+    if (results && n > 0)
+        HIP_TRY(hipMemcpyAsync(results, q->res.p, sizeof(dpg_icp_result) * n, hipMemcpyDeviceToHost, q->stream));
+    if (hess && n > 0)
+        HIP_TRY(hipMemcpyAsync(hess, q->hess.p, sizeof(double) * 9 * n, hipMemcpyDeviceToHost, q->stream));
+    HIP_TRY(hipStreamSynchronize(q->stream));
     return DPG_OK;
 }
 
-static int batch_fetch_1(dpg_ctx* c, dpg_icp_result* results, double* hess) {
-    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+// rank form: every rank's local results, gathered with one ncclAllGather of equal-size slices
+// (the largest share; each rank derives every other rank's share from the common plan)
+static int fetch_allgather(dpg_ctx* c, void* out, size_t rec_bytes, const void* local_dev, std::vector<char>& all,
+                           size_t& slice) {
+    const int W = c->world;
+    std::vector<size_t> cnt((size_t)W, 0);
+    for (int32_t o : c->batch_owner) ++cnt[(size_t)o];
+    slice = std::max<size_t>(*std::max_element(cnt.begin(), cnt.end()), 1);
+    DevBuf<char> send, recv;
+    int rc = DPG_OK;
     HIP_TRY(hipSetDevice(c->device));
-    if (join_cov(c)) return fail(DPG_ERR_HIP, "stream wait failed");
-    if (results && c->n_edges > 0)
-        HIP_TRY(hipMemcpyAsync(results, c->res.p, sizeof(dpg_icp_result) * (size_t)c->n_edges, hipMemcpyDeviceToHost,
-                               c->stream));
-    if (hess && c->n_edges > 0) {
-        if (!c->have_cov) return fail(DPG_ERR_STATE, "last batch ran without compute_cov");
-        HIP_TRY(hipMemcpyAsync(hess, c->hess.p, sizeof(double) * 9 * (size_t)c->n_edges, hipMemcpyDeviceToHost,
-                               c->stream));
+    if (send.reserve(slice * rec_bytes) || recv.reserve(slice * rec_bytes * (size_t)W)) {
+        send.release();
+        recv.release();
+        return fail(DPG_ERR_HIP, "out of device memory for the gather");
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    const size_t mine = c->shard.empty() ? 0 : c->shard[0].size();
+    if (mine && hipMemcpyAsync(send.p, local_dev, mine * rec_bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+        rc = fail(DPG_ERR_HIP, "gather staging copy failed");
+    if (!rc) {
+        const ncclResult_t nr = ncclAllGather(send.p, recv.p, slice * rec_bytes, ncclChar, c->comms[0], c->stream);
+        if (nr != ncclSuccess) rc = fail(DPG_ERR_HIP, "ncclAllGather failed: %s", ncclGetErrorString(nr));
+    }
+    all.resize(slice * rec_bytes * (size_t)W);
+    if (!rc && (hipMemcpyAsync(all.data(), recv.p, all.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = fail(DPG_ERR_HIP, "gather copy failed");
+    send.release();
+    recv.release();
+    if (rc) return rc;
+    std::vector<size_t> pos((size_t)W, 0);
+    char* o = static_cast<char*>(out);
+    for (size_t e = 0; e < c->batch_owner.size(); ++e) {
+        const int r = c->batch_owner[e];
+        memcpy(o + e * rec_bytes, all.data() + ((size_t)r * slice + pos[(size_t)r]++) * rec_bytes, rec_bytes);
+    }
+    return DPG_OK;
+}
+
+// Results of the staged batch in the caller's order (and the covariance blocks).  On the rank form
+// this is a collective: every rank receives every edge's result.
+int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    if (hess && !c->have_cov && !c->batch.empty()) return fail(DPG_ERR_STATE, "last batch ran without compute_cov");
+    const int64_t ne = (int64_t)c->batch.size();
+    std::vector<dpg_icp_result> own;
+    dpg_icp_result* R = results;
+    if (!R) {   // the costs are learnt from every fetch
+        own.resize((size_t)std::max<int64_t>(ne, 1));
+        R = own.data();
+    }
+    int rc;
+    if (c->coll == kCollRccl && n_dev(c) == 1 && c->world > 1) {
+        std::vector<char> buf;
+        size_t slice = 0;
+        if (join_cov(c)) return fail(DPG_ERR_HIP, "stream wait failed");
+        if ((rc = fetch_allgather(c, R, sizeof(dpg_icp_result), c->res.p, buf, slice))) return rc;
+        if (hess && (rc = fetch_allgather(c, hess, 9 * sizeof(double), c->hess.p, buf, slice))) return rc;
+    } else {
+        std::vector<dpg_icp_result> r;
+        std::vector<double> h;
+        for (int k = 0; k < (int)c->shard.size(); ++k) {
+            const auto& ids = c->shard[(size_t)k];
+            r.resize(std::max<size_t>(ids.size(), 1));
+            if (hess) h.resize(9 * std::max<size_t>(ids.size(), 1));
+            if ((rc = fetch_local(dev_ctx(c, k), ids.size(), r.data(), hess ? h.data() : nullptr))) return rc;
+            for (size_t j = 0; j < ids.size(); ++j) {
+                R[ids[j]] = r[j];
+                if (hess) memcpy(hess + 9 * ids[j], h.data() + 9 * j, 9 * sizeof(double));
+            }
+        }
+    }
+    for (int64_t e = 0; e < ne; ++e) c->cost[pair_key(c->batch[(size_t)e])] = edge_cost(c->batch[(size_t)e], R[e].iterations);
+    HIP_TRY(hipSetDevice(c->device));
     return DPG_OK;
 }
 
@@ -772,7 +1016,7 @@ int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t* max_src_out) 
     return DPG_OK;
 }
 
-// event pair (a, b) of the last batch: the slowest device of a multi-GPU context
+// event pair (a, b) of the last batch: the slowest local device
 static float batch_ms(dpg_ctx* c, int a, int b) {
     float worst = -1.f;
     for (int k = 0; k < (c ? n_dev(c) : 0); ++k) {
@@ -793,23 +1037,7 @@ float dpg_cov_batch_kernel_ms(dpg_ctx* c) { return batch_ms(c, 1, 2); }
 
 int32_t dpg_cov_batch_overlapped(dpg_ctx* c) { return c && c->cov_on_aux ? 1 : 0; }
 
-static double batch_bytes_1(dpg_ctx* c);
-
-double dpg_icp_batch_algorithmic_bytes(dpg_ctx* c) {
-    if (!c) return 0.0;
-    if (!is_multi(c)) return batch_bytes_1(c);
-    const int64_t ne = c->n_edges;
-    double b = 0.0;
-    for (int k = 0; k < n_dev(c); ++k) {
-        dev_ctx(c, k)->n_edges = (int64_t)c->shard[(size_t)k].size();
-        (void)hipSetDevice(dev_ctx(c, k)->device);
-        b += batch_bytes_1(dev_ctx(c, k));
-    }
-    c->n_edges = ne;
-    (void)hipSetDevice(c->device);
-    return b;
-}
-
+// the last launch on device q, from its own records: sum over its edges of iterations x (8N + 8M + 8N)
 static double batch_bytes_1(dpg_ctx* c) {
     if (!c || c->n_edges <= 0) return 0.0;
     std::vector<dpg_icp_result> r((size_t)c->n_edges);
@@ -821,6 +1049,20 @@ static double batch_bytes_1(dpg_ctx* c) {
         bytes += (double)r[(size_t)E.pad[0]].iterations * (16.0 * E.n_src_ds + 8.0 * E.n_tgt_ds);
     }
     return bytes;
+}
+
+// the local devices' launches (the rank form: this rank's share)
+double dpg_icp_batch_algorithmic_bytes(dpg_ctx* c) {
+    if (!c) return 0.0;
+    double b = 0.0;
+    for (int k = 0; k < n_dev(c); ++k) {
+        (void)hipSetDevice(dev_ctx(c, k)->device);
+        const double x = batch_bytes_1(dev_ctx(c, k));
+        if (x < 0) return x;
+        b += x;
+    }
+    (void)hipSetDevice(c->device);
+    return b;
 }
 
 // ------------------------------------------------------------------ single alignment / covariance
@@ -995,9 +1237,8 @@ int icp_cov_sandwich(dpg_ctx* c, const float* data, int64_t nd, const float* mod
 }
 
 // ------------------------------------------------------------------ pose graph
-int dpg_gn_setup(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t b, int64_t e,
-                 const dpg_gn_params* gp) {
-    if (!c || !F || V <= 0 || nf < 0) return fail(DPG_ERR_ARG, "dpg_gn_setup: bad arguments");
+static int gn_setup_1(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t b, int64_t e,
+                      const dpg_gn_params* gp) {
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
@@ -1010,22 +1251,57 @@ int dpg_gn_setup(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t
     return DPG_OK;
 }
 
+// Multi-device forms: every local device holds the whole factor list (the sparsity pattern is
+// global) and linearizes the factors f with f mod world == its rank; dpg_gn_take_icp_measurements
+// then hands each ICP slot to the device that aligned the edge.
+int dpg_gn_setup(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t b, int64_t e,
+                 const dpg_gn_params* gp) {
+    if (!c || !F || V <= 0 || nf < 0) return fail(DPG_ERR_ARG, "dpg_gn_setup: bad arguments");
+    if (!is_multi(c)) return gn_setup_1(c, V, F, nf, b, e, gp);
+    if (b != 0 || e != nf) return fail(DPG_ERR_ARG, "dpg_gn_setup: a multi-device context shards the factors itself (0, n_factors)");
+    for (int k = 0; k < n_dev(c); ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        int rc = gn_setup_1(q, V, F, nf, 0, nf, gp);
+        if (!rc && (rc = dpg_gn_dev_set_ownership(&q->gn, c->world, q->rank, q->stream)))
+            rc = fail(rc, "pose-graph ownership setup failed");
+        if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
 int dpg_gn_take_icp_measurements(dpg_ctx* c, int64_t first, int64_t count, int64_t n_always,
                                  const dpg_icp_params* p) {
     if (!c || !c->gn_ready || !p) return fail(DPG_ERR_STATE, "graph not set up");
-    if (is_multi(c))
-        return fail(DPG_ERR_STATE, "the step API is per device: a multi-GPU context solves through dpg_optimize_graph / dpg_reoptimize");
-    if (count > c->n_edges) return fail(DPG_ERR_ARG, "only %lld ICP results available", (long long)c->n_edges);
-    int rc = dpg_gn_dev_icp_to_factors(&c->gn, c->res.p, first, count, n_always, 1.0 / (double)p->laser_x_variance,
-                                       1.0 / (double)p->laser_y_variance, 1.0 / (double)p->laser_theta_variance,
-                                       c->stream);
-    return rc ? fail(rc, "dpg_gn_take_icp_measurements failed") : DPG_OK;
+    const double ix = 1.0 / (double)p->laser_x_variance, iy = 1.0 / (double)p->laser_y_variance,
+                 ith = 1.0 / (double)p->laser_theta_variance;
+    if (!is_multi(c)) {
+        if (count > c->n_edges) return fail(DPG_ERR_ARG, "only %lld ICP results available", (long long)c->n_edges);
+        int rc = dpg_gn_dev_icp_to_factors(&c->gn, c->res.p, first, count, n_always, ix, iy, ith, c->stream);
+        return rc ? fail(rc, "dpg_gn_take_icp_measurements failed") : DPG_OK;
+    }
+    // every slot of the batch: the aligning device's result, on that device only
+    if (count != (int64_t)c->batch.size())
+        return fail(DPG_ERR_ARG, "a multi-device context takes the whole batch (%lld results), not %lld",
+                    (long long)c->batch.size(), (long long)count);
+    for (int k = 0; k < n_dev(c); ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        HIP_TRY(hipSetDevice(q->device));
+        if (!q->gn_ready || !q->gn.mine) return fail(DPG_ERR_STATE, "graph not set up on device %d", k);
+        const int64_t nl = (int64_t)c->shard[(size_t)k].size();
+        const int rc = dpg_gn_dev_icp_to_factors_scatter(&q->gn, q->res.p, q->shard_idx.p, nl, first, count, n_always,
+                                                         ix, iy, ith, q->stream);
+        if (rc) return fail(rc, "dpg_gn_take_icp_measurements failed");
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
 }
 
 int64_t dpg_gn_hb_size(dpg_ctx* c) { return (c && c->gn_ready) ? dpg_gn_dev_hb_size(&c->gn) : -1; }
 
-int dpg_gn_set_poses(dpg_ctx* c, const double* poses) {
-    if (!c || !c->gn_ready || !poses) return fail(DPG_ERR_STATE, "graph not set up");
+static int gn_set_poses_1(dpg_ctx* c, const double* poses) {
+    if (!c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+    HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(c->gn.poses, poses, sizeof(double) * 3 * (size_t)c->gn.n_nodes, hipMemcpyHostToDevice,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1037,16 +1313,35 @@ int dpg_gn_set_poses(dpg_ctx* c, const double* poses) {
     return DPG_OK;
 }
 
+int dpg_gn_set_poses(dpg_ctx* c, const double* poses) {
+    if (!c || !c->gn_ready || !poses) return fail(DPG_ERR_STATE, "graph not set up");
+    for (int k = 0; k < n_dev(c); ++k) {
+        const int rc = gn_set_poses_1(dev_ctx(c, k), poses);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
 int dpg_gn_get_poses(dpg_ctx* c, double* poses) {
     if (!c || !c->gn_ready || !poses) return fail(DPG_ERR_STATE, "graph not set up");
+    HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(poses, c->gn.poses, sizeof(double) * 3 * (size_t)c->gn.n_nodes, hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return DPG_OK;
 }
 
+// the per-iteration step API: one device, the caller's collective between its calls
+#define DPG_STEP_API_1(c)                                                                                        \
+    do {                                                                                                         \
+        if (!(c) || !(c)->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");                             \
+        if (is_multi(c)) return fail(DPG_ERR_STATE, "the step API is per device: a multi-device context runs "   \
+                                                    "dpg_gn_run / dpg_optimize_graph / dpg_reoptimize");         \
+    } while (0)
+
 int dpg_gn_assemble(dpg_ctx* c, double* hb_dev) {
-    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+    DPG_STEP_API_1(c);
     if (!hb_dev) hb_dev = c->gn.hb_own;
     HIP_TRY(hipEventRecord(c->ev[3], c->stream));
     int rc = dpg_gn_dev_assemble(&c->gn, hb_dev, c->stream);
@@ -1056,7 +1351,7 @@ int dpg_gn_assemble(dpg_ctx* c, double* hb_dev) {
 }
 
 int dpg_gn_solve_retract(dpg_ctx* c, const double* hb_dev, double* delta_inf, double* error, int32_t* pcg_iters) {
-    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+    DPG_STEP_API_1(c);
     if (!hb_dev) hb_dev = c->gn.hb_own;
     int rc = dpg_gn_dev_solve(&c->gn, hb_dev, &c->gp, c->stream, delta_inf, error, pcg_iters);
     if (rc) return fail(rc, "PCG solve failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1071,8 +1366,8 @@ int dpg_gn_solve_retract(dpg_ctx* c, const double* hb_dev, double* delta_inf, do
     return DPG_OK;
 }
 
-int dpg_gn_solve_retract_async(dpg_ctx* c, const double* hb_dev) {
-    if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");
+// enqueue solve + retract on one device (no multi check: the multi-device host loop uses it per device)
+static int solve_retract_async_1(dpg_ctx* c, const double* hb_dev) {
     if (!hb_dev) hb_dev = c->gn.hb_own;
     HIP_TRY(hipEventRecord(c->ev[4], c->stream));
     int rc = dpg_gn_dev_solve_async(&c->gn, hb_dev, &c->gp, c->stream);
@@ -1081,10 +1376,14 @@ int dpg_gn_solve_retract_async(dpg_ctx* c, const double* hb_dev) {
     return DPG_OK;
 }
 
+int dpg_gn_solve_retract_async(dpg_ctx* c, const double* hb_dev) {
+    DPG_STEP_API_1(c);
+    return solve_retract_async_1(c, hb_dev);
+}
+
 int32_t dpg_gn_factorizations(dpg_ctx* c) { return (c && c->gn_ready) ? c->gn.n_factorizations : -1; }
 
-int dpg_gn_fetch(dpg_ctx* c, const double* hb_dev, double out[3]) {
-    if (!c || !c->gn_ready || !out) return fail(DPG_ERR_STATE, "graph not set up");
+static int fetch_1(dpg_ctx* c, const double* hb_dev, double out[3]) {
     if (!hb_dev) hb_dev = c->gn.hb_own;
     int rc = dpg_gn_dev_fetch(&c->gn, hb_dev, c->stream, out);
     if (rc) return fail(rc, "fetch failed");
@@ -1093,10 +1392,17 @@ int dpg_gn_fetch(dpg_ctx* c, const double* hb_dev, double out[3]) {
     return DPG_OK;
 }
 
+int dpg_gn_fetch(dpg_ctx* c, const double* hb_dev, double out[3]) {
+    DPG_STEP_API_1(c);
+    if (!out) return fail(DPG_ERR_ARG, "dpg_gn_fetch: out is NULL");
+    return fetch_1(c, hb_dev, out);
+}
+
 float dpg_gn_last_assemble_ms(dpg_ctx* c) { return c ? c->asm_ms : -1.f; }
 float dpg_gn_last_solve_ms(dpg_ctx* c) { return c ? c->solve_ms : -1.f; }
 
 static int read_error(dpg_ctx* c, double* err) {
+    HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipMemcpyAsync(err, c->gn.hb_own + 9 * c->gn.nnzb_upper + 3 * c->gn.n_nodes, sizeof(double),
                            hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1110,112 +1416,26 @@ static int check_conv(const dpg_gn_params* gp, double cur, double nw) {
     return (gp->relative_error_tol != 0.0 && rel_dec <= gp->relative_error_tol) || (abs_dec <= gp->absolute_error_tol);
 }
 
-// The Gauss-Newton loop on a set-up graph whose poses are set: solve + retract + re-linearize
-// enqueued back to back, one synchronisation per iteration.  t1: when the iterations started.
-static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it);
-
-static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0, double t1, dpg_gn_stats* st) {
-    dpg_gn_stats S;
-    memset(&S, 0, sizeof(S));
-    int rc;
-    if ((rc = dpg_gn_assemble(c, nullptr)) || (rc = read_error(c, &S.initial_error))) return rc;
-    double cur = S.initial_error, nw = cur, dinf = 0.0;
-    int it = 0;
-    static const bool pipe_env = !(getenv("DPG_GN_PIPE") && atoi(getenv("DPG_GN_PIPE")) == 0);
-    const bool pipe = pipe_env && P.linear_solver == DPG_SOLVER_CHOLESKY && c->gn.chol && dpg_chol_gated_ok(c->gn.chol);
-    if (pipe && !(cur <= 0.0) && P.max_iterations > 0) {
-        if ((rc = gn_loop_pipe(c, P, S, nw, dinf, it))) return rc;
-    } else if (!(cur <= 0.0) && P.max_iterations > 0) {
-        for (;;) {
-            double sc[3];
-            if ((rc = dpg_gn_solve_retract_async(c, nullptr)) || (rc = dpg_gn_assemble(c, nullptr)) ||
-                (rc = dpg_gn_fetch(c, nullptr, sc)))
-                return rc;
-            if (sc[2] != 0.0) return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)sc[2]);
-            S.pcg_iterations += c->gn.last_pcg_iters;
-            ++it;
-            dinf = sc[0];
-            nw = sc[1];
-            if (it >= P.max_iterations) break;
-            if (P.use_error_criteria) {
-                if (check_conv(&P, cur, nw) || !std::isfinite(cur)) break;
-            } else if (dinf < P.delta_tol) {
-                break;
-            }
-            cur = nw;
-        }
-    }
-    if (poses && (rc = dpg_gn_get_poses(c, poses))) return rc;
-    if (!poses) HIP_TRY(hipStreamSynchronize(c->stream));
-    const double t2 = now_ms();
-    S.iterations = it;
-    S.final_error = nw;
-    S.last_delta_inf = dinf;
-    S.ms_total = t2 - t0;
-    S.ms_per_iteration = it ? (t2 - t1) / it : 0.0;
-    if (st) *st = S;
-    return DPG_OK;
-}
-
-// gn_loop's iterations with the decisions on the device (dpg_gn_pipe.h): iteration k + 1 is queued
-// before iteration k's report is read, so the GPU never waits for the host
-static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it) {
-    if (!c->pipe_ctl) {
-        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->pipe_ctl), sizeof(dpg_gn_ctl)));
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->pipe_slot), 2 * sizeof(dpg_gn_slot), hipHostMallocMapped | hipHostMallocCoherent));
-        for (auto& e : c->pipe_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    dpg_gn_dev* g = &c->gn;
-    int rc;
-    if ((rc = dpg_gn_pipe_init(g, &P, c->pipe_ctl, S.initial_error, c->stream)))
-        return fail(rc, "GN pipeline launch failed");
-    volatile dpg_gn_slot* slot = c->pipe_slot;
-    auto issue = [&](int k) -> int {   // iteration k (1-based) reports into slot k & 1
-        int r = dpg_gn_pipe_issue(g, &P, c->pipe_ctl, c->pipe_slot + (k & 1), c->stream);
-        if (r) return fail(r, "GN pipeline launch failed: %s", hipGetErrorString(hipGetLastError()));
-        HIP_TRY(hipEventRecord(c->pipe_ev[k & 1], c->stream));
-        return DPG_OK;
-    };
-    if ((rc = issue(1))) return rc;
-    int issued = 1, nfact = 0, reuse_last = g->last_was_chord;
-    for (int k = 1;; ++k) {
-        if (issued < P.max_iterations) {
-            if ((rc = issue(k + 1))) return rc;
-            ++issued;
-        }
-        HIP_TRY(hipEventSynchronize(c->pipe_ev[k & 1]));
-        const dpg_gn_slot o = const_cast<const dpg_gn_slot&>(slot[k & 1]);
-        if (!o.active || o.it != k) return fail(DPG_ERR_STATE, "GN pipeline out of step (iteration %d)", k);
-        if (o.status != 0.0) {
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)o.status);
-        }
-        it = k;
-        if (!o.reuse) ++nfact;
-        g->prev_delta_inf = g->last_delta_inf;
-        g->last_delta_inf = o.dinf;
-        reuse_last = o.reuse;
-        dinf = o.dinf;
-        nw = o.error;
-        if (o.final_) break;
-    }
-    // the host bookkeeping the step API continues from (as after the host loop)
-    g->last_was_chord = reuse_last;
-    g->have_factor = 1;
-    g->n_factorizations += nfact;
-    g->last_used_chol = 1;
-    S.pcg_iterations = 0;
-    return DPG_OK;
-}
-
-// ONE all-reduce(sum, fp64) of every device's packed [H upper | g | chi2] buffer, in place, on the
-// devices' own streams (one thread drives every device: grouped)
-static int allreduce_hb(dpg_ctx* c) {
+// The multi-device forms' all-reduce: every local device's hb_part summed into every hb_own --
+// ONE ncclAllReduce(sum, fp64) per device on its own stream (grouped: one thread drives them), or
+// the virtual devices' rank-order sum.  Out of place, so an iteration that a gate turned into
+// no-ops sums the same partial buffers again and leaves hb_own as it was.
+static int coll_sum_hb(dpg_ctx* c) {
     const size_t count = (size_t)dpg_gn_dev_hb_size(&c->gn);
+    if (c->coll == kCollVirtual) {
+        const double* parts[kMaxVirtual];
+        double* outs[kMaxVirtual];
+        for (int k = 0; k < n_dev(c); ++k) {
+            parts[k] = dev_ctx(c, k)->gn.hb_part;
+            outs[k] = dev_ctx(c, k)->gn.hb_own;
+        }
+        const int rc = dpg_launch_vsum(parts, outs, n_dev(c), (int64_t)count, c->stream);   // the shared stream
+        return rc ? fail(rc, "virtual all-reduce launch failed") : DPG_OK;
+    }
     if (ncclGroupStart() != ncclSuccess) return fail(DPG_ERR_HIP, "ncclGroupStart failed");
     for (int k = 0; k < n_dev(c); ++k) {
         dpg_ctx* q = dev_ctx(c, k);
-        const ncclResult_t r = ncclAllReduce(q->gn.hb_own, q->gn.hb_own, count, ncclDouble, ncclSum, c->comms[(size_t)k],
+        const ncclResult_t r = ncclAllReduce(q->gn.hb_part, q->gn.hb_own, count, ncclDouble, ncclSum, c->comms[(size_t)k],
                                              q->stream);
         if (r != ncclSuccess) {
             (void)ncclGroupEnd();
@@ -1226,41 +1446,172 @@ static int allreduce_hb(dpg_ctx* c) {
     return DPG_OK;
 }
 
-// The Gauss-Newton loop of a multi-GPU context: every device holds the whole factor list and
-// linearizes its contiguous shard of it; per iteration each device enqueues solve + retract +
-// re-linearization, then ONE all-reduce of the packed system, then one read of device 0's
-// scalars.  The devices factor and solve the identical reduced system, so their poses stay
-// bitwise equal without a broadcast.
-static int gn_loop_multi(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0, double t1, dpg_gn_stats* st) {
+static int ensure_pipe(dpg_ctx* q) {
+    if (q->pipe_ctl) return DPG_OK;
+    HIP_TRY(hipSetDevice(q->device));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q->pipe_ctl), sizeof(dpg_gn_ctl)));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&q->pipe_slot), 2 * sizeof(dpg_gn_slot),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+    for (auto& e : q->pipe_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return DPG_OK;
+}
+
+// The Gauss-Newton iterations with the decisions on the device (dpg_gn_pipe.h): iteration k + 1 is
+// queued before iteration k's report is read, so the GPU never waits for the host.  Multi-device
+// forms: every device solves the identical all-reduced system and decides for itself (its own
+// control block: the chord rule's bookkeeping stays per device); their reports must agree bit for
+// bit, which the loop checks every iteration.
+static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it) {
+    const int L = n_dev(c);
+    const int part = is_multi(c) ? 1 : 0;
+    int rc;
+    for (int k = 0; k < L; ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        if ((rc = ensure_pipe(q))) return rc;
+        if ((rc = dpg_gn_pipe_init(&q->gn, &P, q->pipe_ctl, S.initial_error, q->stream)))
+            return fail(rc, "GN pipeline launch failed");
+    }
+    auto issue = [&](int i) -> int {   // iteration i (1-based) reports into slot i & 1
+        int r;
+        for (int k = 0; k < L; ++k) {
+            dpg_ctx* q = dev_ctx(c, k);
+            HIP_TRY(hipSetDevice(q->device));
+            if ((r = dpg_gn_pipe_issue_solve(&q->gn, q->pipe_ctl, part, q->stream)))
+                return fail(r, "GN pipeline launch failed: %s", hipGetErrorString(hipGetLastError()));
+        }
+        if (part && (r = coll_sum_hb(c))) return r;
+        for (int k = 0; k < L; ++k) {
+            dpg_ctx* q = dev_ctx(c, k);
+            HIP_TRY(hipSetDevice(q->device));
+            if ((r = dpg_gn_pipe_issue_ctl(&q->gn, &P, q->pipe_ctl, q->pipe_slot + (i & 1), part, q->stream)))
+                return fail(r, "GN pipeline launch failed: %s", hipGetErrorString(hipGetLastError()));
+            HIP_TRY(hipEventRecord(q->pipe_ev[i & 1], q->stream));
+        }
+        return DPG_OK;
+    };
+    if ((rc = issue(1))) return rc;
+    int issued = 1;
+    std::vector<int> nfact((size_t)L, 0), reuse_last((size_t)L, 0);
+    for (int k = 0; k < L; ++k) reuse_last[(size_t)k] = dev_ctx(c, k)->gn.last_was_chord;
+    for (int i = 1;; ++i) {
+        if (issued < P.max_iterations) {
+            if ((rc = issue(i + 1))) return rc;
+            ++issued;
+        }
+        dpg_gn_slot o0{};
+        for (int k = 0; k < L; ++k) {
+            dpg_ctx* q = dev_ctx(c, k);
+            HIP_TRY(hipSetDevice(q->device));
+            HIP_TRY(hipEventSynchronize(q->pipe_ev[i & 1]));
+            dpg_gn_slot o;   // host-mapped, written by the device: read through volatile
+            {
+                const volatile dpg_gn_slot* v = q->pipe_slot + (i & 1);
+                o.dinf = v->dinf;
+                o.error = v->error;
+                o.status = v->status;
+                o.reuse = v->reuse;
+                o.active = v->active;
+                o.final_ = v->final_;
+                o.it = v->it;
+            }
+            if (!o.active || o.it != i) return fail(DPG_ERR_STATE, "GN pipeline out of step (device %d, iteration %d)", k, i);
+            if (k == 0) {
+                o0 = o;
+            } else if (memcmp(&o.dinf, &o0.dinf, sizeof(double)) || memcmp(&o.error, &o0.error, sizeof(double)) ||
+                       o.status != o0.status || o.reuse != o0.reuse || o.final_ != o0.final_) {
+                for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
+                return fail(DPG_ERR_INTERNAL, "devices diverged at GN iteration %d (device %d: |d| %.17g error %.17g, "
+                            "device 0: %.17g %.17g)", i, k, o.dinf, o.error, o0.dinf, o0.error);
+            }
+            if (!o.reuse) ++nfact[(size_t)k];
+            q->gn.prev_delta_inf = q->gn.last_delta_inf;
+            q->gn.last_delta_inf = o.dinf;
+            reuse_last[(size_t)k] = o.reuse;
+        }
+        if (o0.status != 0.0) {
+            for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
+            return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)o0.status);
+        }
+        it = i;
+        dinf = o0.dinf;
+        nw = o0.error;
+        if (o0.final_) break;
+    }
+    // the host bookkeeping the step API continues from (as after the host loop)
+    for (int k = 0; k < L; ++k) {
+        dpg_gn_dev* g = &dev_ctx(c, k)->gn;
+        g->last_was_chord = reuse_last[(size_t)k];
+        g->have_factor = 1;
+        g->n_factorizations += nfact[(size_t)k];
+        g->last_used_chol = 1;
+    }
+    S.pcg_iterations = 0;
+    HIP_TRY(hipSetDevice(c->device));
+    return DPG_OK;
+}
+
+static bool pipe_ok(dpg_ctx* c, const dpg_gn_params& P) {
+    if (P.linear_solver != DPG_SOLVER_CHOLESKY) return false;
+    for (int k = 0; k < n_dev(c); ++k) {
+        const dpg_gn_dev& g = dev_ctx(c, k)->gn;
+        if (!g.chol || !dpg_chol_gated_ok(g.chol)) return false;
+    }
+    return true;
+}
+
+// The Gauss-Newton loop on a set-up graph whose poses are set.  One device: assemble, then the
+// pipelined iterations (or, for the PCG solver / a factorization that cannot run gated, the
+// host-decided loop: solve + retract + re-linearize enqueued back to back, ONE read per iteration).
+// Multi-device forms: the same loops with every device's share assembled into its hb_part and ONE
+// all-reduce into hb_own between the assembly and the decision; every device solves the identical
+// system, so the poses stay bitwise equal on all of them without a broadcast.
+static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0, double t1, dpg_gn_stats* st) {
     dpg_gn_stats S;
     memset(&S, 0, sizeof(S));
-    const int n = n_dev(c);
+    const int L = n_dev(c);
+    const bool multi = is_multi(c);
     int rc;
-    for (int k = 0; k < n; ++k)
-        if ((rc = hipSetDevice(dev_ctx(c, k)->device) != hipSuccess ? DPG_ERR_HIP : 0) ||
-            (rc = dpg_gn_assemble(dev_ctx(c, k), nullptr)))
-            return rc ? rc : fail(DPG_ERR_HIP, "hipSetDevice failed");
-    if ((rc = allreduce_hb(c))) return rc;
-    HIP_TRY(hipSetDevice(c->device));
+    for (int k = 0; k < L; ++k) {
+        dpg_ctx* q = dev_ctx(c, k);
+        HIP_TRY(hipSetDevice(q->device));
+        if (multi) rc = dpg_gn_dev_assemble_part(&q->gn, nullptr, q->stream);
+        else rc = dpg_gn_dev_assemble(&q->gn, q->gn.hb_own, q->stream);
+        if (rc) return fail(rc, "assembly launch failed");
+    }
+    if (multi && (rc = coll_sum_hb(c))) return rc;
     if ((rc = read_error(c, &S.initial_error))) return rc;
     double cur = S.initial_error, nw = cur, dinf = 0.0;
     int it = 0;
-    if (!(cur <= 0.0) && P.max_iterations > 0) {
+    if (pipe_ok(c, P) && !(cur <= 0.0) && P.max_iterations > 0) {
+        if ((rc = gn_loop_pipe(c, P, S, nw, dinf, it))) return rc;
+    } else if (!(cur <= 0.0) && P.max_iterations > 0) {
         for (;;) {
-            for (int k = 0; k < n; ++k) {
+            for (int k = 0; k < L; ++k) {
                 dpg_ctx* q = dev_ctx(c, k);
                 HIP_TRY(hipSetDevice(q->device));
-                if ((rc = dpg_gn_solve_retract_async(q, nullptr)) || (rc = dpg_gn_assemble(q, nullptr))) return rc;
+                if ((rc = solve_retract_async_1(q, nullptr))) return rc;
+                if (multi) rc = dpg_gn_dev_assemble_part(&q->gn, nullptr, q->stream);
+                else rc = dpg_gn_dev_assemble(&q->gn, q->gn.hb_own, q->stream);
+                if (rc) return fail(rc, "assembly launch failed");
             }
-            if ((rc = allreduce_hb(c))) return rc;
-            double sc[3];
-            HIP_TRY(hipSetDevice(c->device));
-            if ((rc = dpg_gn_fetch(c, nullptr, sc))) return rc;
-            if (sc[2] != 0.0) return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)sc[2]);
+            if (multi && (rc = coll_sum_hb(c))) return rc;
+            // every device reads its own scalars: its chord rule's bookkeeping (last / previous
+            // max|delta|) moves with its own solves, and the devices must agree
+            double sc0[3] = {0, 0, 0};
+            for (int k = 0; k < L; ++k) {
+                dpg_ctx* q = dev_ctx(c, k);
+                double sc[3];
+                HIP_TRY(hipSetDevice(q->device));
+                if ((rc = fetch_1(q, nullptr, sc))) return rc;
+                if (k == 0) memcpy(sc0, sc, sizeof(sc));
+                else if (memcmp(sc, sc0, sizeof(sc)))
+                    return fail(DPG_ERR_INTERNAL, "devices diverged at GN iteration %d (device %d)", it + 1, k);
+            }
+            if (sc0[2] != 0.0) return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)sc0[2]);
             S.pcg_iterations += c->gn.last_pcg_iters;
             ++it;
-            dinf = sc[0];
-            nw = sc[1];
+            dinf = sc0[0];
+            nw = sc0[1];
             if (it >= P.max_iterations) break;
             if (P.use_error_criteria) {
                 if (check_conv(&P, cur, nw) || !std::isfinite(cur)) break;
@@ -1270,7 +1621,12 @@ static int gn_loop_multi(dpg_ctx* c, const dpg_gn_params& P, double* poses, doub
             cur = nw;
         }
     }
-    if ((rc = dpg_ctx_synchronize(c)) || (rc = dpg_gn_get_poses(c, poses))) return rc;
+    if (multi && (rc = dpg_ctx_synchronize(c))) return rc;
+    if (poses && (rc = dpg_gn_get_poses(c, poses))) return rc;
+    if (!poses) {
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     const double t2 = now_ms();
     S.iterations = it;
     S.final_error = nw;
@@ -1282,30 +1638,14 @@ static int gn_loop_multi(dpg_ctx* c, const dpg_gn_params& P, double* poses, doub
 }
 
 // The GN loop on the graph staged by dpg_gn_setup (+ dpg_gn_take_icp_measurements) from the poses
-// of dpg_gn_set_poses, with the setup's parameters: what a host loop over the step API does with
-// one rank, natively (one synchronisation per iteration, no interpreter between the launches)
+// of dpg_gn_set_poses, with the setup's parameters: what a host loop over the step API does,
+// natively (no interpreter between the launches; multi-device forms: sharded, one all-reduce per
+// iteration)
 int dpg_gn_run(dpg_ctx* c, double* poses_out, dpg_gn_stats* st) {
     if (!c || !c->gn_ready) return fail(DPG_ERR_STATE, "dpg_gn_run: graph not set up");
-    if (is_multi(c)) return fail(DPG_ERR_STATE, "dpg_gn_run: a multi-GPU context runs dpg_optimize_graph");
     HIP_TRY(hipSetDevice(c->device));
     const double t0 = now_ms();
     return gn_loop(c, c->gp, poses_out, t0, t0, st);
-}
-
-// every device of a multi-GPU context: the whole graph, linearizing factors [b_k, e_k) (equal
-// counts, contiguous), the same initial poses
-static int gn_setup_multi(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params& P,
-                          const double* poses) {
-    const int n = n_dev(c);
-    for (int k = 0; k < n; ++k) {
-        dpg_ctx* q = dev_ctx(c, k);
-        const int64_t b = nf * k / n, e = nf * (k + 1) / n;
-        int rc = dpg_gn_setup(q, V, F, nf, b, e, &P);
-        if (!rc) rc = dpg_gn_set_poses(q, poses);
-        if (rc) return rc;
-    }
-    HIP_TRY(hipSetDevice(c->device));
-    return DPG_OK;
 }
 
 int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F, int64_t nf, const dpg_gn_params* gp,
@@ -1314,12 +1654,7 @@ int dpg_optimize_graph(dpg_ctx* c, double* poses, int64_t V, const dpg_factor* F
     dpg_gn_params P;
     if (gp) P = *gp;
     else dpg_gn_params_default(&P);
-    if (c && is_multi(c)) {
-        if (!F || !poses || V <= 0 || nf < 0) return fail(DPG_ERR_ARG, "dpg_optimize_graph: bad arguments");
-        int rc = gn_setup_multi(c, V, F, nf, P, poses);
-        if (rc) return rc;
-        return gn_loop_multi(c, P, poses, t0, now_ms(), st);
-    }
+    if (!c || !F || !poses || V <= 0 || nf < 0) return fail(DPG_ERR_ARG, "dpg_optimize_graph: bad arguments");
     int rc = dpg_gn_setup(c, V, F, nf, 0, nf, &P);
     if (rc) return rc;
     if ((rc = dpg_gn_set_poses(c, poses))) return rc;
@@ -1527,41 +1862,16 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
     int rc = reopt_sweep(c, V, pass, est, odom, I, R, edges, F, first_icp, n_succ, S, t1);
     if (rc) return rc;
     const int64_t E = S.n_icp_edges;
-    if (is_multi(c)) {   // the alignments ran sharded: their measurements enter the factor slots on the host
-        std::vector<dpg_icp_result> res((size_t)std::max<int64_t>(E, 1));
-        if (E > 0 && (rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
-        const double t2 = now_ms();
-        const double ix = 1.0 / (double)I.laser_x_variance, iy = 1.0 / (double)I.laser_y_variance,
-                     ith = 1.0 / (double)I.laser_theta_variance;
-        for (int64_t e = 0; e < E; ++e) {   // icp_to_factor_kernel's expressions (dpg_gn.hip)
-            const dpg_icp_result& r = res[(size_t)e];
-            dpg_factor& f = F[(size_t)(first_icp + e)];
-            const bool keep = e < n_succ || (r.converged && r.status == DPG_ICP_OK);
-            f.z[0] = r.z[0];
-            f.z[1] = r.z[1];
-            f.z[2] = r.z[2];
-            f.info[0] = keep ? ix : 0.0;
-            f.info[1] = keep ? iy : 0.0;
-            f.info[2] = keep ? ith : 0.0;
-            if (e >= n_succ && keep) ++S.n_loop_closures;
-        }
-        for (int64_t v = 0; v < 3 * V; ++v) poses_out[v] = (double)est[v];
-        if ((rc = gn_setup_multi(c, V, F.data(), (int64_t)F.size(), P, poses_out))) return rc;
-        if ((rc = gn_loop_multi(c, P, poses_out, t2, now_ms(), &S.gn))) return rc;
-        S.n_factors = (int64_t)F.size();
-        S.ms_icp = t2 - t1;
-        S.ms_gn = now_ms() - t2;
-        if (st) *st = S;
-        return DPG_OK;
-    }
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return fail(DPG_ERR_HIP, "ICP batch failed");
+    // the sweep's own results (the caller may fetch them again: the batch stays staged) -- the
+    // alignments end here, and their outcomes give the loop-closure count
+    std::vector<dpg_icp_result> res((size_t)std::max<int64_t>(E, 1));
+    if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
     const double t2 = now_ms();
-    // 5. batch Gauss-Newton from the estimated poses (optimizeGraph, dpg_slam.cc:111-119, 316-329)
+    // 5. batch Gauss-Newton from the estimated poses (optimizeGraph, dpg_slam.cc:111-119, 316-329);
+    //    the ICP slots take the results where they were aligned (multi-device: on each device)
     if ((rc = dpg_gn_setup(c, V, F.data(), (int64_t)F.size(), 0, (int64_t)F.size(), &P))) return rc;
     if ((rc = dpg_gn_take_icp_measurements(c, first_icp, E, n_succ, &I))) return rc;
     {
-        std::vector<dpg_icp_result> res((size_t)E);
-        if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
         for (int64_t e = n_succ; e < E; ++e)
             S.n_loop_closures += (res[(size_t)e].converged && res[(size_t)e].status == DPG_ICP_OK) ? 1 : 0;
     }

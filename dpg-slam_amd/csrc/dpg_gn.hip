@@ -94,13 +94,13 @@ __device__ __forceinline__ void atwb_acc(const double* A, const double* w, const
 constexpr int kRec = 13;
 __global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X,
                            const int32_t* __restrict__ clist, const int32_t* __restrict__ n_entries, int64_t fb,
-                           int64_t fe, double* __restrict__ rec, const int32_t* gate) {
+                           int64_t fe, const uint8_t* __restrict__ mine, double* __restrict__ rec, const int32_t* gate) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= *n_entries || (gate && !gate[0])) return;
     const int32_t code = clist[q];
     const int64_t fi = code >> 2;
     const int role = code & 3;
-    if (fi < fb || fi >= fe) return;   // another rank's factor: the gather skips it
+    if (mine ? !mine[fi] : (fi < fb || fi >= fe)) return;   // another rank's factor: the gather skips it
     const dpg_factor f = F[fi];
     double e[3], Ai[9];
     linearize(f, X, e, Ai);
@@ -130,8 +130,8 @@ __global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __res
 template <int kG>
 __global__ __launch_bounds__(kRowThreads) void gather_kernel(const double* __restrict__ rec, const int32_t* __restrict__ cptr,
                               const int32_t* __restrict__ clist, int64_t n_nodes, int64_t nnzb_upper,
-                              int64_t shard_begin, int64_t shard_end, double* __restrict__ hb,
-                              double* __restrict__ chi2_node, const int32_t* gate) {
+                              int64_t shard_begin, int64_t shard_end, const uint8_t* __restrict__ mine,
+                              double* __restrict__ hb, double* __restrict__ chi2_node, const int32_t* gate) {
     const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nnzb_upper || (gate && !gate[0])) return;
     const bool is_diag = u < n_nodes;
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kRowThreads) void gather_kernel(const double* __res
 #pragma unroll
         for (int t = 0; t < kG; ++t) {
             const int32_t fi = code[t] >> 2, role = code[t] & 3;
-            if (code[t] < 0 || fi < shard_begin || fi >= shard_end) continue;
+            if (code[t] < 0 || (mine ? !mine[fi] : (fi < shard_begin || fi >= shard_end))) continue;
             if (role == 0) {          // diag i
 #pragma unroll
                 for (int k = 0; k < 9; ++k) H[k] += v[t][k];
@@ -419,7 +419,7 @@ extern "C" int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g) { return 9 * g->nnzb_
 extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
     void* ptrs[] = {g->factors, g->up_row, g->up_col, g->up_cptr, g->up_clist, g->node_fptr, g->node_flist,
                     g->rowptr, g->colidx, g->src_up, g->bsr, g->minv, g->poses, g->x, g->r, g->z,
-                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own, g->contrib, g->scal3};
+                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own, g->contrib, g->scal3, g->mine, g->hb_part};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (g->scal3_host) (void)hipHostFree(g->scal3_host);
@@ -546,19 +546,16 @@ extern "C" int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* re
 
 static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_t* gate, bool chi2 = true) {
     double* chi2_node = g->partials + 6 * (size_t)g->n_blocks_rows;
-    const int64_t nfs = g->shard_end - g->shard_begin;
+    const int64_t nfs = g->mine ? g->n_factors : g->shard_end - g->shard_begin;
     // upper bound of the list length (a Between factor has 3 entries); the kernel reads the length
     if (nfs > 0)
         hipLaunchKernelGGL(lin_kernel, dim3(nblk(3 * g->n_factors)), dim3(kRowThreads), 0, s, g->factors, g->poses,
-                           g->up_clist, g->up_cptr + g->nnzb_upper, g->shard_begin, g->shard_end, g->contrib, gate);
-    static const int kg = getenv("DPG_GATHER_G") ? atoi(getenv("DPG_GATHER_G")) : 2;
-#define DPG_GATHER(G)                                                                                               \
-    hipLaunchKernelGGL(gather_kernel<G>, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->contrib, g->up_cptr,  \
-                       g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, hb, chi2_node, gate)
-    if (kg == 1) DPG_GATHER(1);
-    else if (kg == 4) DPG_GATHER(4);
-    else DPG_GATHER(2);
-#undef DPG_GATHER
+                           g->up_clist, g->up_cptr + g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, g->contrib,
+                           gate);
+    // two records in flight per lane (1 and 4 measured slower)
+    hipLaunchKernelGGL(gather_kernel<2>, dim3(nblk(g->nnzb_upper)), dim3(kRowThreads), 0, s, g->contrib, g->up_cptr,
+                       g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, hb, chi2_node,
+                       gate);
     if (chi2)
         hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
                            hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate);
@@ -567,6 +564,85 @@ static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_
 
 extern "C" int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb, void* stream) {
     return assemble_gated(g, hb, reinterpret_cast<hipStream_t>(stream), nullptr);
+}
+
+// ---- multi-device forms ----
+__global__ void own_kernel(uint8_t* __restrict__ mine, int64_t nf, int32_t world, int32_t rank) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < nf) mine[f] = (f % world) == rank ? 1 : 0;
+}
+
+// icp_to_factor_kernel's expressions for this device's results, written to the caller's slots
+__global__ void icp_to_factor_scatter_kernel(const dpg_icp_result* __restrict__ res, const int32_t* __restrict__ idx,
+                                             dpg_factor* __restrict__ F, uint8_t* __restrict__ mine, int64_t first,
+                                             int64_t n_local, int64_t n_always, double ix, double iy, double ith) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_local) return;
+    const int64_t e = idx[j];
+    dpg_factor& f = F[first + e];
+    const dpg_icp_result r = res[j];
+    const bool keep = e < n_always || (r.converged && r.status == DPG_ICP_OK);
+    f.z[0] = r.z[0];
+    f.z[1] = r.z[1];
+    f.z[2] = r.z[2];
+    f.info[0] = keep ? ix : 0.0;
+    f.info[1] = keep ? iy : 0.0;
+    f.info[2] = keep ? ith : 0.0;
+    mine[first + e] = 1;
+}
+
+struct VsumArgs {
+    const double* parts[16];
+    double* outs[16];
+};
+// virtual devices' all-reduce: every output the same rank-order sum
+__global__ void vsum_kernel(VsumArgs a, int32_t k, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double s = a.parts[0][i];
+        for (int32_t q = 1; q < k; ++q) s += a.parts[q][i];
+        for (int32_t q = 0; q < k; ++q) a.outs[q][i] = s;
+    }
+}
+
+extern "C" int dpg_gn_dev_set_ownership(dpg_gn_dev* g, int32_t world, int32_t rank, void* stream) {
+    if (world < 1 || rank < 0 || rank >= world) return DPG_ERR_ARG;
+    if (!g->mine && dev_alloc(&g->mine, (size_t)g->n_factors)) return DPG_ERR_HIP;
+    if (!g->hb_part && dev_alloc(&g->hb_part, (size_t)dpg_gn_dev_hb_size(g))) return DPG_ERR_HIP;
+    g->world = world;
+    g->rank = rank;
+    if (g->n_factors > 0)
+        hipLaunchKernelGGL(own_kernel, dim3(nblk(g->n_factors)), dim3(kRowThreads), 0, reinterpret_cast<hipStream_t>(stream),
+                           g->mine, g->n_factors, world, rank);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_dev_icp_to_factors_scatter(dpg_gn_dev* g, const dpg_icp_result* res, const int32_t* idx,
+                                                 int64_t n_local, int64_t first, int64_t count, int64_t n_always,
+                                                 double ix, double iy, double ith, void* stream) {
+    if (!g->mine || first < 0 || count < n_local || first + count > g->n_factors) return DPG_ERR_ARG;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (count > 0 && hipMemsetAsync(g->mine + first, 0, (size_t)count, s) != hipSuccess) return DPG_ERR_HIP;
+    if (n_local > 0)
+        hipLaunchKernelGGL(icp_to_factor_scatter_kernel, dim3(nblk(n_local)), dim3(kRowThreads), 0, s, res, idx, g->factors,
+                           g->mine, first, n_local, n_always, ix, iy, ith);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_dev_assemble_part(dpg_gn_dev* g, const int32_t* gate, void* stream) {
+    if (!g->hb_part) return DPG_ERR_STATE;
+    return assemble_gated(g, g->hb_part, reinterpret_cast<hipStream_t>(stream), gate, true);
+}
+
+extern "C" int dpg_launch_vsum(const double* const* parts, double* const* outs, int32_t k, int64_t n, void* stream) {
+    if (k < 1 || k > 16 || n <= 0) return k >= 1 && k <= 16 ? DPG_OK : DPG_ERR_ARG;
+    VsumArgs a;
+    for (int q = 0; q < 16; ++q) {
+        a.parts[q] = q < k ? parts[q] : nullptr;
+        a.outs[q] = q < k ? outs[q] : nullptr;
+    }
+    const unsigned blocks = (unsigned)std::min<int64_t>((n + 1023) / 1024, 2048);
+    hipLaunchKernelGGL(vsum_kernel, dim3(blocks), dim3(1024), 0, reinterpret_cast<hipStream_t>(stream), a, k, n);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
 static int pcg_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, hipStream_t s);
@@ -630,9 +706,12 @@ __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_wa
 // the end of one iteration: the error (chi2_kernel's sum, same order), its report, then the next
 // iteration decided exactly as the host loop does (dpg_api.hip gn_loop: the stop rule;
 // dpg_gn_dev_solve_async: the chord rule), and the solver's counters cleared for it
+// chi2_sum != NULL (multi-device forms): the error is the all-reduced sum already in hb, not this
+// device's per-node terms
 __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const double* __restrict__ chi2_node, int64_t n,
-                                                        double* chi2, int32_t* status, double* max_out, dpg_gn_params P,
-                                                        dpg_gn_slot* slot, int32_t* sync, int64_t n_words) {
+                                                        double* chi2, const double* chi2_sum, int32_t* status,
+                                                        double* max_out, dpg_gn_params P, dpg_gn_slot* slot,
+                                                        int32_t* sync, int64_t n_words) {
     __shared__ double red[16];
     if (!ctl->active) {   // uniform: nothing ran this iteration
         if (threadIdx.x == 0) {
@@ -647,8 +726,12 @@ __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const d
         return;
     }
     double sum = 0.0;
-    for (int64_t k = threadIdx.x; k < n; k += blockDim.x) sum += chi2_node[k];
-    sum = block_sum(sum, red);
+    if (chi2_sum) {
+        sum = *chi2_sum;
+    } else {
+        for (int64_t k = threadIdx.x; k < n; k += blockDim.x) sum += chi2_node[k];
+        sum = block_sum(sum, red);
+    }
     const double st_word = (double)*status;
     __syncthreads();   // every lane has read the status word before it is cleared
     clear_sync(sync, n_words, status);
@@ -714,21 +797,32 @@ extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_c
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
-extern "C" int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot,
-                                 void* stream) {
+extern "C" int dpg_gn_pipe_issue_solve(dpg_gn_dev* g, dpg_gn_ctl* ctl, int part, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int32_t* gate = &ctl->active;
-    if (!g->chol || !dpg_chol_gated_ok(g->chol)) return DPG_ERR_STATE;
+    if (!g->chol || !dpg_chol_gated_ok(g->chol) || (part && !g->hb_part)) return DPG_ERR_STATE;
     int rc = dpg_chol_solve_gated(g->chol, g->hb_own, gate, 1, g->poses, g->scal3, stream);
     if (rc) return rc;
-    if ((rc = assemble_gated(g, g->hb_own, s, gate, false))) return rc;
+    return part ? assemble_gated(g, g->hb_part, s, gate, true) : assemble_gated(g, g->hb_own, s, gate, false);
+}
+
+extern "C" int dpg_gn_pipe_issue_ctl(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot,
+                                     int part, void* stream) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int32_t* sync;
     int64_t n_words;
     dpg_chol_sync_dev(g->chol, &sync, &n_words);
+    double* chi2 = g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes;
     hipLaunchKernelGGL(pipe_ctl_kernel, dim3(1), dim3(1024), 0, s, ctl, g->partials + 6 * (size_t)g->n_blocks_rows,
-                       g->n_nodes, g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes,
-                       const_cast<int32_t*>(dpg_chol_status_dev(g->chol)), g->scal3, *gp, slot, sync, n_words);
+                       g->n_nodes, chi2, part ? chi2 : nullptr, const_cast<int32_t*>(dpg_chol_status_dev(g->chol)),
+                       g->scal3, *gp, slot, sync, n_words);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+extern "C" int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot,
+                                 void* stream) {
+    const int rc = dpg_gn_pipe_issue_solve(g, ctl, 0, stream);
+    return rc ? rc : dpg_gn_pipe_issue_ctl(g, gp, ctl, slot, 0, stream);
 }
 
 extern "C" int dpg_gn_dev_fetch(dpg_gn_dev* g, const double* hb, void* stream, double out[3]) {

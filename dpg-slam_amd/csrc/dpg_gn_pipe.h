@@ -64,6 +64,12 @@ int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, do
 // enqueue one gated iteration: solve, retract, re-linearize + assemble into g->hb_own, control
 // kernel (reports into slot, a host-mapped pointer)
 int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot, void* stream);
+// the same in two halves for the multi-device forms (part = 1): solve from hb_own, retract and
+// assemble this device's share into hb_part with its error; [the caller's all-reduce hb_part ->
+// hb_own]; the control kernel, taking the error from hb_own.  part = 0 is dpg_gn_pipe_issue.
+int dpg_gn_pipe_issue_solve(dpg_gn_dev* g, dpg_gn_ctl* ctl, int part, void* stream);
+int dpg_gn_pipe_issue_ctl(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot, int part,
+                          void* stream);
 }
 
 #endif

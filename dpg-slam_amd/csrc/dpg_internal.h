@@ -135,6 +135,11 @@ typedef struct dpg_gn_dev {
     int32_t have_factor;           /* the Cholesky holds a factorization of this graph */
     int32_t last_was_chord;        /* the last solve reused the factor */
     int32_t n_factorizations;      /* since dpg_gn_set_poses */
+    /* multi-device forms: this device linearizes the factors f with mine[f] != 0 (instead of the
+       range [shard_begin, shard_end)) into hb_part; the all-reduce of hb_part gives hb_own */
+    uint8_t* mine;                 /* [n_factors] or NULL */
+    double* hb_part;               /* [hb size] or NULL */
+    int32_t world, rank;
 } dpg_gn_dev;
 
 /* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip). */
@@ -164,6 +169,17 @@ int dpg_gn_dev_solve(dpg_gn_dev* g, const double* hb_dev, const dpg_gn_params* g
 int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* results_dev, int64_t first,
                               int64_t count, int64_t n_always, double info_x, double info_y,
                               double info_th, void* stream);
+/* multi-device forms: factor f is this device's when f mod world == rank (allocates mine + hb_part) */
+int dpg_gn_dev_set_ownership(dpg_gn_dev* g, int32_t world, int32_t rank, void* stream);
+/* ICP slots [first, first + count) of the batch: this device's n_local results (caller indices
+   idx_dev) become its factors, every other slot in the range another device's */
+int dpg_gn_dev_icp_to_factors_scatter(dpg_gn_dev* g, const dpg_icp_result* results_dev, const int32_t* idx_dev,
+                                      int64_t n_local, int64_t first, int64_t count, int64_t n_always, double info_x,
+                                      double info_y, double info_th, void* stream);
+/* this device's share of [H upper | g | chi2] into hb_part (gate: the pipelined loop's, or NULL) */
+int dpg_gn_dev_assemble_part(dpg_gn_dev* g, const int32_t* gate, void* stream);
+/* virtual devices: outs[r] = sum over q in rank order of parts[q], n doubles, r < k <= 16 */
+int dpg_launch_vsum(const double* const* parts, double* const* outs, int32_t k, int64_t n, void* stream);
 
 #ifdef __cplusplus
 }

@@ -222,6 +222,12 @@ SIGNATURES = {
     "dpg_ctx_create": (P, [C.c_int]),
     "dpg_ctx_create_multi": (P, [C.c_int32, I32P]),
     "dpg_ctx_num_gpus": (C.c_int32, [P]),
+    "dpg_ctx_create_virtual": (P, [C.c_int32, C.c_int32]),
+    "dpg_ctx_create_rank": (P, [C.c_int32, P, C.c_int32, C.c_int32]),
+    "dpg_nccl_unique_id": (C.c_int, [P]),
+    "dpg_ctx_num_ranks": (C.c_int32, [P]),
+    "dpg_ctx_rank": (C.c_int32, [P]),
+    "dpg_ctx_set_icp_schedule": (C.c_int, [P, C.c_int32]),
     "dpg_ctx_destroy": (None, [P]),
     "dpg_ctx_set_stream": (C.c_int, [P, P]),
     "dpg_ctx_synchronize": (C.c_int, [P]),

@@ -146,13 +146,33 @@ def results_array(n: int) -> np.ndarray:
 
 
 # ------------------------------------------------------------------------- GPU context
+NCCL_ID_BYTES = 128
+
+
+def nccl_unique_id() -> bytes:
+    """dpg_nccl_unique_id: the id rank 0 of a one-process-per-GPU job hands to every rank."""
+    buf = C.create_string_buffer(NCCL_ID_BYTES)
+    check(lib().dpg_nccl_unique_id(C.cast(buf, C.c_void_p)), "dpg_nccl_unique_id")
+    return buf.raw
+
+
 class Context:
     """One dpg_ctx (one GPU, one HIP stream).  Creating it without a usable GPU raises."""
 
-    def __init__(self, device: int = 0, n_gpus: int | None = None):
+    def __init__(self, device: int = 0, n_gpus: int | None = None, virtual: int | None = None,
+                 rank: tuple | None = None):
         """n_gpus: a multi-GPU context over devices device .. device + n_gpus - 1
-        (dpg_ctx_create_multi: one process, RCCL between the devices); None: one device."""
-        if n_gpus is None:
+        (dpg_ctx_create_multi: one process, RCCL between the devices); virtual=k: k contexts on
+        `device` sharing one stream, the all-reduce a device-side sum (dpg_ctx_create_virtual: the
+        sharded paths on one card); rank=(nccl_id bytes, rank, world): this process's device as one
+        rank of a one-process-per-GPU job (dpg_ctx_create_rank); none of them: one device."""
+        if virtual is not None:
+            self.handle = lib().dpg_ctx_create_virtual(int(virtual), device)
+        elif rank is not None:
+            nid, r, w = rank
+            buf = C.create_string_buffer(bytes(nid), NCCL_ID_BYTES)
+            self.handle = lib().dpg_ctx_create_rank(device, C.cast(buf, C.c_void_p), int(r), int(w))
+        elif n_gpus is None:
             self.handle = lib().dpg_ctx_create(device)
         else:
             devs = np.arange(device, device + int(n_gpus), dtype=np.int32)
@@ -161,6 +181,8 @@ class Context:
             raise _abi.DpgError("dpg_ctx_create failed: " + (lib().dpg_last_error() or b"").decode())
         self.device = device
         self.n_gpus = int(lib().dpg_ctx_num_gpus(self.handle))
+        self.n_ranks = int(lib().dpg_ctx_num_ranks(self.handle))
+        self.rank = int(lib().dpg_ctx_rank(self.handle))
         self.n_edges = 0
         self.V = 0
         self._children = weakref.WeakSet()   # DpgStore / IncGraph objects living on this context
@@ -201,6 +223,12 @@ class Context:
         """Angular ICP: windows of more than `cap` candidates are scanned by a whole wave (0: never);
         results are identical for every value."""
         check(lib().dpg_ctx_set_icp_defer_cap(self.handle, int(cap)), "dpg_ctx_set_icp_defer_cap")
+
+    def set_icp_schedule(self, schedule: str):
+        """'measured' (default): once every edge of the staged batch has a measured cost, LPT over the
+        ranks + longest-first dispatch; 'caller': e mod ranks in the caller's order.  Same results."""
+        v = {"caller": 0, "measured": 1}[schedule]
+        check(lib().dpg_ctx_set_icp_schedule(self.handle, v), "dpg_ctx_set_icp_schedule")
 
     def kdtree_build_ms(self) -> float:
         return float(lib().dpg_kdtree_build_ms(self.handle))
@@ -382,6 +410,7 @@ class Context:
         check(lib().dpg_reoptimize(self.handle, len(e), ptr(ps, C.c_int32), ptr(e, C.c_float), ptr(o, C.c_float),
                                    C.byref(ip), C.byref(gp), C.byref(rp), ptr(X, C.c_double), C.byref(st)),
               "dpg_reoptimize")
+        self.n_edges = int(st.n_icp_edges)   # the sweep's batch stays staged: icp_fetch returns its results
         return X, st
 
     def gn_times_ms(self):

@@ -136,19 +136,50 @@ void dpg_ctx_destroy(dpg_ctx* ctx);
  *   dpg_scans_upload / dpg_scans_append   every device holds every scan;
  *   dpg_icp_batch_prepare / _run / _fetch edge e is aligned on device e mod n_gpus, all devices
  *                                         concurrently; results (and covariance blocks) come back
- *                                         in the caller's order; _kernel_ms is the slowest device;
- *   dpg_optimize_graph, dpg_reoptimize    every device holds the factor list and linearizes a
- *                                         contiguous 1/n of it; per Gauss-Newton iteration ONE
+ *                                         in the caller's order; _kernel_ms is the slowest device
+ *                                         (dpg_ctx_set_icp_schedule: once every edge's cost is
+ *                                         known from an earlier run, a longest-processing-time
+ *                                         assignment instead);
+ *   dpg_optimize_graph, dpg_reoptimize,   every device holds the factor list and linearizes its
+ *   dpg_gn_setup + _take_icp_measurements share (factor f mod n, and each ICP slot on the device
+ *   + _set_poses + dpg_gn_run             that aligned its edge); per Gauss-Newton iteration ONE
  *                                         ncclAllReduce(sum, fp64) of the packed [H upper | g |
  *                                         chi2]; every device factors and solves the identical
- *                                         system (poses bitwise equal on all devices).
+ *                                         system and takes its own (identical) stop / chord
+ *                                         decisions on the device (poses bitwise equal on all
+ *                                         devices; the loop checks their reports agree).
  * dpg_run_icp, icp_cov_calculate / icp_cov_sandwich, dpg_get_map and dpg_loop_closure_candidates
- * run on the first device.  The per-device step API (dpg_gn_take_icp_measurements ...), the trace
- * and the incremental graph (dpg_inc_create: per-node updates are latency-bound, one GPU) need a
- * single-device context.  n_gpus = 1 gives a context whose calls take the sharded paths with one
- * rank (RCCL included): its results equal dpg_ctx_create's byte for byte. */
+ * run on the first device.  The per-iteration step API (dpg_gn_assemble / _solve_retract* /
+ * _fetch), the trace and the incremental graph (dpg_inc_create: per-node updates are
+ * latency-bound, one GPU) need a single-device context.  n_gpus = 1 gives a context whose calls
+ * take the sharded paths with one rank (RCCL included): its results equal dpg_ctx_create's byte
+ * for byte. */
 dpg_ctx* dpg_ctx_create_multi(int32_t n_gpus, const int32_t* devices);
-int32_t dpg_ctx_num_gpus(dpg_ctx* ctx);   /* 1 for dpg_ctx_create */
+/* One process per GPU (torchrun and the like): this process's `device` is global rank `rank` of
+ * `world`; the RCCL communicator is built from the id rank 0 made with dpg_nccl_unique_id and the
+ * caller handed to every rank (ncclCommInitRank).  The batched calls above then act on the whole
+ * job: dpg_icp_batch_prepare takes ALL edges and aligns this rank's share, dpg_icp_batch_fetch
+ * returns every edge's result (a collective: every rank calls it), the Gauss-Newton calls
+ * all-reduce across ranks.  Every rank must make the same calls with the same arguments. */
+#define DPG_NCCL_ID_BYTES 128
+int dpg_nccl_unique_id(void* id_out /*[DPG_NCCL_ID_BYTES]*/);
+dpg_ctx* dpg_ctx_create_rank(int32_t device, const void* nccl_id, int32_t rank, int32_t world);
+/* Test / rehearsal form: k "devices" that are k contexts on ONE device sharing one stream, the
+ * all-reduce a device-side sum in rank order.  Every sharded path of the multi-device forms runs
+ * with k > 1 on one card (k <= 16). */
+dpg_ctx* dpg_ctx_create_virtual(int32_t k, int32_t device);
+int32_t dpg_ctx_num_gpus(dpg_ctx* ctx);   /* local devices: 1 for dpg_ctx_create and the rank form */
+int32_t dpg_ctx_num_ranks(dpg_ctx* ctx);  /* ranks of the collective (ncclCommCount; k virtual; 1) */
+int32_t dpg_ctx_rank(dpg_ctx* ctx);       /* global rank of the first local device */
+/* Batched ICP dispatch (results are identical for both): DPG_ICP_SCHEDULE_CALLER -- edge e on rank
+ * e mod ranks, in the caller's order; DPG_ICP_SCHEDULE_MEASURED (default) -- the same until every
+ * edge of the staged batch has a measured cost (iterations x points, from an earlier run of the
+ * same (target, source) pair: a batch run again, or the next sweep), then a longest-processing-time
+ * assignment over the ranks and longest-first dispatch on each, so that the alignments that bound
+ * a launch start first. */
+#define DPG_ICP_SCHEDULE_CALLER 0
+#define DPG_ICP_SCHEDULE_MEASURED 1
+int dpg_ctx_set_icp_schedule(dpg_ctx* ctx, int32_t schedule);
 /* Run all work of this context on an external hipStream_t (e.g. torch's current stream); on a
  * multi-GPU context it applies to the first device only. */
 int dpg_ctx_set_stream(dpg_ctx* ctx, void* hip_stream);
@@ -254,7 +285,8 @@ int dpg_optimize_graph(dpg_ctx* ctx, double* poses_inout, int64_t n_nodes, const
 int dpg_gn_setup(dpg_ctx* ctx, int64_t n_nodes, const dpg_factor* factors, int64_t n_factors,
                  int64_t shard_begin, int64_t shard_end, const dpg_gn_params* params);
 /* Overwrite the measurement/information of factors [first, first+count) with the ICP batch
- * results of edges [0, count) of the last dpg_icp_batch_run (device to device).  Edges
+ * results of edges [0, count) of the last dpg_icp_batch_run (device to device; multi-device forms:
+ * count = the whole batch, each slot on the device that aligned it).  Edges
  * [0, n_always) always become factors (successive scans, dpg_slam.cc:85-89); the others only when
  * the alignment converged (loop closures, dpg_slam.cc:101-104) -- a dropped edge keeps its slot
  * with zero information, which adds nothing to H, g or the error. */
@@ -275,10 +307,10 @@ int dpg_gn_solve_retract(dpg_ctx* ctx, const double* hb_dev, double* delta_inf, 
  * (0 = ok, 1 = H not positive definite, 2 = solver timeout)}. */
 int dpg_gn_solve_retract_async(dpg_ctx* ctx, const double* hb_dev);
 int dpg_gn_fetch(dpg_ctx* ctx, const double* hb_dev, double out[3]);
-/* The whole Gauss-Newton loop over the step API on one device (assemble, then solve + retract +
- * re-linearize + one read per iteration, the setup's parameters), from the poses of the last
- * dpg_gn_set_poses; poses_out[V][3] (may be NULL) receives the result.  A single-device context
- * (a multi-GPU one runs dpg_optimize_graph). */
+/* The whole Gauss-Newton loop of the setup (its parameters) from the poses of the last
+ * dpg_gn_set_poses, natively: assemble, then per iteration solve + retract + re-linearize with the
+ * stop and chord decisions taken on the device (multi-device forms: sharded assembly and one
+ * all-reduce per iteration); poses_out[V][3] (may be NULL) receives the result. */
 int dpg_gn_run(dpg_ctx* ctx, double* poses_out, dpg_gn_stats* stats);
 /* Cholesky factorizations since the last dpg_gn_set_poses (the other solves reused one). */
 int32_t dpg_gn_factorizations(dpg_ctx* ctx);
