@@ -29,6 +29,7 @@
 
 #include "../../include/dpg_icp_cov.h"
 #include "../../include/dpg_slam_c.h"
+#include "dpg_chol.h"
 #include "dpg_gn_pipe.h"
 #include "dpg_internal.h"
 
@@ -108,6 +109,7 @@ struct dpg_ctx {
     bool cov_pending = false, cov_on_aux = false;
     int32_t icp_variant = DPG_ICP_ANGULAR;
     int32_t defer_cap = 256;        // angular ICP: cooperative-queue threshold (dpg_ctx_set_icp_defer_cap)
+    int32_t kernel_variant = 0;     // angular ICP kernel form (dpg_ctx_set_icp_kernel_variant, A/B)
     float map_ms = 0.f;             // last dpg_get_map kernel (HIP events map_ev)
     hipEvent_t map_ev[2] = {};
     // scan store (batch form)
@@ -172,6 +174,7 @@ struct dpg_ctx {
     std::unordered_map<uint64_t, float> cost;
     DevBuf<int32_t> shard_idx;       // per device context: its shard's caller indices
     DevBuf<float> cost_dev;          // rank form: the all-reduced cost vector of a batch
+    dpg_chol_opts copts;             // solver options (dpg_ctx_set_solver_options)
 };
 
 namespace {
@@ -240,6 +243,7 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     if (c->icp_variant == DPG_ICP_ANGULAR) {
         kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 16);   // record capacity
         kp.defer_cap = c->defer_cap;
+        kp.kernel_variant = c->kernel_variant;
         // large clouds: a record slice per resident edge in global scratch, edges in chunks of <= 2048
         const size_t per_edge = dpg_icp_ang_scratch_per_edge(kp.lds_tgt);
         size_t sbytes = 0;
@@ -447,6 +451,41 @@ int32_t dpg_ctx_num_ranks(dpg_ctx* c) {
     }
     return c->world;
 }
+
+void dpg_solver_options_default(dpg_solver_options* o) {
+    if (!o) return;
+    const dpg_chol_opts d;
+    memset(o, 0, sizeof(*o));
+    o->order = d.order;
+    o->fused = d.fused;
+    o->solve_stage = d.solve_stage;
+    o->solve_maxseg = d.solve_maxseg;
+    o->solve_dinv = d.solve_dinv;
+    o->merge_single = d.merge_single;
+    o->max_supernode_cols = d.max_supernode_cols;
+    o->relax_fraction = d.relax_fraction;
+}
+
+// per context (every device of a multi-device one): applies to the next graph set up on it
+int dpg_ctx_set_solver_options(dpg_ctx* c, const dpg_solver_options* o) {
+    if (!c || !o || o->order < DPG_ORDER_AUTO || o->order > DPG_ORDER_ND || o->max_supernode_cols < 1 ||
+        !(o->relax_fraction >= 0.0))
+        return fail(DPG_ERR_ARG, "bad solver options");
+    for (int k = 0; k < n_dev(c); ++k) {
+        dpg_chol_opts& d = dev_ctx(c, k)->copts;
+        d.order = o->order;
+        d.fused = o->fused ? 1 : 0;
+        d.solve_stage = o->solve_stage;
+        d.solve_maxseg = o->solve_maxseg;
+        d.solve_dinv = o->solve_dinv ? 1 : 0;
+        d.merge_single = o->merge_single ? 1 : 0;
+        d.max_supernode_cols = o->max_supernode_cols;
+        d.relax_fraction = o->relax_fraction;
+    }
+    return DPG_OK;
+}
+
+const dpg_chol_opts* dpg_ctx_chol_opts(dpg_ctx* c) { return &c->copts; }
 
 int dpg_ctx_set_icp_schedule(dpg_ctx* c, int32_t schedule) {
     if (!c || (schedule != DPG_ICP_SCHEDULE_CALLER && schedule != DPG_ICP_SCHEDULE_MEASURED))
@@ -908,6 +947,12 @@ int dpg_ctx_set_icp_defer_cap(dpg_ctx* c, int32_t cap) {
     return DPG_OK;
 }
 
+int dpg_ctx_set_icp_kernel_variant(dpg_ctx* c, int32_t v) {
+    if (!c || v < 0) return fail(DPG_ERR_ARG, "bad kernel variant");
+    for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->kernel_variant = v;
+    return DPG_OK;
+}
+
 float dpg_kdtree_build_ms(dpg_ctx* c) {
     float ms = -1.f;
     if (!c || hipEventSynchronize(c->ev[0]) != hipSuccess) return -1.f;
@@ -1243,7 +1288,7 @@ static int gn_setup_1(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, in
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     c->gn_ready = false;
-    int rc = dpg_gn_dev_alloc(&c->gn, V, F, nf, b, e);
+    int rc = dpg_gn_dev_alloc(&c->gn, V, F, nf, b, e, &c->copts);
     if (rc) return fail(rc, "pose-graph setup failed (invalid factor or out of memory)");
     c->gn_ready = true;
     if (gp) c->gp = *gp;
@@ -1994,13 +2039,12 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
         if ((rc = dpg_icp_batch_prepare(c, edges.data(), E, pf.data(), &I))) return rc;
         if ((rc = icp_batch_run_from(c, V))) return rc;
         // while the GPU aligns: the update's structure on the host, with every pair a factor may
-        // come from (a loop closure that does not converge stays an explicit zero block) -- its
-        // symbolic half on a worker thread, joined by dpg_inc_update once the factors are staged
+        // come from (a loop closure that does not converge stays an explicit zero block)
         {
             std::vector<int32_t> pr(edges);
             for (int64_t k = 0; k < n_extra; ++k)
                 if (extra[k].kind == DPG_FACTOR_BETWEEN) { pr.push_back(extra[k].i); pr.push_back(extra[k].j); }
-            if ((rc = dpg_inc_prepare_async(g, 1, pr.data(), (int64_t)pr.size() / 2))) return rc;
+            if ((rc = dpg_inc_prepare(g, 1, pr.data(), (int64_t)pr.size() / 2))) return rc;
         }
         std::vector<dpg_icp_result> res((size_t)E);
         if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;

@@ -8,9 +8,16 @@
 
 #include <vector>
 
+// The solver's options (the public dpg_solver_options, dpg_slam_c.h, set per context)
 struct dpg_chol_opts {
-    int32_t max_supernode_cols;   // cap on columns (3x3 blocks) per supernode
-    double relax_fraction;        // explicit-zero budget of relaxed amalgamation (0 = fundamental)
+    int32_t max_supernode_cols = 64;   // cap on columns (3x3 blocks) per supernode
+    double relax_fraction = 0.3;       // explicit-zero budget of relaxed amalgamation (0 = fundamental)
+    int32_t order = 0;                 // DPG_ORDER_AUTO | DPG_ORDER_MD | DPG_ORDER_ND
+    int32_t merge_single = 0;          // supernodes merge only along single-child chains (round 1's rule)
+    int32_t fused = 1;                 // one-launch DAG factorization when the fronts fit LDS
+    int32_t solve_stage = -1;          // doubles of L staged in LDS by the solves (-1: what fills 80 KB)
+    int32_t solve_maxseg = -1;         // ancestor row segments in the backward solve (-1: all)
+    int32_t solve_dinv = 0;            // solves with inverted diagonal blocks
 };
 
 // Everything is indexed by block positions p = pos[node] in the elimination order.
@@ -39,8 +46,9 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
                       const dpg_chol_opts* opts, dpg_chol_sym* S);
 // the two halves of dpg_chol_symbolic: the minimum-degree order with the column patterns of L
 // (in elimination positions, sorted), and everything derived from an order + patterns
+// (md: minimum degree alone; otherwise nested dissection with minimum-degree parts of <= 16 nodes)
 int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                   std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
+                   std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat, bool md = false);
 // nested dissection (BFS level separators; parts of <= leaf nodes by minimum degree): shallow trees
 int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                       std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
@@ -76,11 +84,13 @@ struct dpg_chol_incsym {
     std::vector<std::pair<int32_t, int32_t>> added;
 };
 // a fresh minimum-degree order of the graph (pairs) -> state
-int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                     const dpg_chol_opts* opts = nullptr);
 // the two halves of dpg_incsym_reset: the order and column patterns of the graph (a pure function
 // of its arguments, safe on a worker thread), and the state built from them (perm, pat consumed)
 int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                     std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
+                     std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat,
+                     const dpg_chol_opts* opts = nullptr);
 void dpg_incsym_init(dpg_chol_incsym* I, int64_t n, std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
 // nodes n .. n + k - 1 appended at the end of the order
 void dpg_incsym_append(dpg_chol_incsym* I, int64_t k);
@@ -94,11 +104,11 @@ int dpg_incsym_derive(dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sy
 // buffers grow only when needed -- or created when NULL.  On error *h is destroyed and NULL.  The
 // analysis is moved into *h: *S is left holding *h's previous one (or nothing).
 int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                        dpg_chol_sym* S);
+                        dpg_chol_sym* S, const dpg_chol_opts* opts = nullptr);
 // the same in two halves: the plan (host only, no device call) and its upload (the same thread,
 // no other build in between); on error *h is destroyed and NULL
 int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                             dpg_chol_sym* S);
+                             dpg_chol_sym* S, const dpg_chol_opts* opts = nullptr);
 int dpg_chol_create_sym_upload(void** h);
 // host time (ms) of the last build of h: structures, uploads
 void dpg_chol_build_times(void* h, double out[2]);

@@ -1715,6 +1715,7 @@ int dreserve(T** d, size_t* cap, size_t n) {
 }
 
 struct CholDev {
+    dpg_chol_opts opts;   // the context's solver options at creation
     dpg_chol_sym sym;
     int64_t n = 0;
     SnDev* sns = nullptr;
@@ -1794,14 +1795,11 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
 }  // namespace
 
 extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
-                               int64_t n_pairs) {
+                               int64_t n_pairs, const dpg_chol_opts* opts) {
     *out = nullptr;
     CholDev* c = new CholDev();
-    dpg_chol_opts o{64, 0.3};
-    // supernode size / explicit-zero budget (A/B only: DPG_CHOL_MAXCOLS, DPG_CHOL_RELAX)
-    if (const char* e = getenv("DPG_CHOL_MAXCOLS")) o.max_supernode_cols = atoi(e);
-    if (const char* e = getenv("DPG_CHOL_RELAX")) o.relax_fraction = atof(e);
-    if (dpg_chol_symbolic(n, pair_lo, pair_hi, n_pairs, &o, &c->sym)) {
+    if (opts) c->opts = *opts;
+    if (dpg_chol_symbolic(n, pair_lo, pair_hi, n_pairs, &c->opts, &c->sym)) {
         delete c;
         return DPG_ERR_NUMERIC;
     }
@@ -1813,8 +1811,9 @@ extern "C" int dpg_chol_create(void** out, int64_t n, const int32_t* pair_lo, co
 
 // The same from a given symbolic analysis; *h is reused (its buffers grow when needed) or created.
 int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                        dpg_chol_sym* S) {
+                        dpg_chol_sym* S, const dpg_chol_opts* opts) {
     CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
+    if (opts) c->opts = *opts;
     std::swap(c->sym, *S);   // *S gets the previous analysis (its buffers are reused by the next derive)
     const int rc = chol_build(c, n, pair_lo, pair_hi, n_pairs);
     if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
@@ -2193,7 +2192,7 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         c->lds_fused = std::max(c->lds_fused, 8 * fused_lds_doubles(3 * (d.k + d.r), 3 * d.k, true));
     }
     // two panel buffers for the chain when every front fits, else one (the chain step goes through HBM)
-    c->fused_db = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_SINGLE_BUFFER") == nullptr;
+    c->fused_db = c->lds_fused <= 160 * 1024;
     if (!c->fused_db) {
         c->lds_fused = 0;
         for (int32_t s = 0; s < S.ns; ++s) {
@@ -2201,11 +2200,11 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
             c->lds_fused = std::max(c->lds_fused, 8 * fused_lds_doubles(3 * (d.k + d.r), 3 * d.k, false));
         }
     }
-    c->fused = c->lds_fused <= 160 * 1024 && getenv("DPG_CHOL_LEVELS") == nullptr;
+    c->fused = c->lds_fused <= 160 * 1024 && c->opts.fused;
     // LDS of the DAG solves: the largest front
     // the solves' LDS: diagonal block D + staging region R + reciprocals + right-hand side / gathered
     // x + row positions.  Their VGPR budget (the 64-step chains) already holds them to two
-    // workgroups per CU, so R defaults to what fills 80 KB; DPG_SOLVE_STAGE overrides it (doubles,
+    // workgroups per CU, so R defaults to what fills 80 KB; opts.solve_stage overrides it (doubles,
     // 0 = no staging)
     size_t lds_rest = 0;
     for (int32_t s = 0; s < S.ns; ++s) {
@@ -2213,13 +2212,12 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         lds_rest = std::max(lds_rest, (size_t)(kSB * kDL + kSB + m3 + 2 + m3 / 6 + 2 + 2 * kMaxSeg) * sizeof(double));
     }
     {
-        const char* env = getenv("DPG_SOLVE_STAGE");
         const long room = (long)(80 * 1024) - (long)lds_rest;
-        const long want = env ? atol(env) : room / (long)sizeof(double);
+        const long want = c->opts.solve_stage >= 0 ? (long)c->opts.solve_stage : room / (long)sizeof(double);
         const long cap = ((long)(160 * 1024) - (long)lds_rest) / (long)sizeof(double);
         c->solve_stage = (int32_t)std::max<long>(0, std::min<long>(want, cap)) & ~1;
-        const char* ms = getenv("DPG_SOLVE_MAXSEG");   // tests: 0 = every front takes the parent path
-        c->solve_maxseg = ms ? std::max(0, std::min(atoi(ms), kMaxSeg)) : kMaxSeg;
+        // tests: 0 = every front takes the parent path
+        c->solve_maxseg = c->opts.solve_maxseg >= 0 ? std::min(c->opts.solve_maxseg, kMaxSeg) : kMaxSeg;
     }
     c->lds_solve_max = (size_t)c->solve_stage * sizeof(double) + lds_rest;
     if (c->lds_solve_max > 160 * 1024) return DPG_ERR_SIZE;
@@ -2312,8 +2310,8 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     c->n_dblocks = (int64_t)H.dblocks.size();
     // measured (tools/r3_gn_job.sh, profiles/r03): the inversion launch (~55 us at config 4) costs
     // more than the chains it removes from the solves (re-solve 0.250 -> 0.241 ms), so the chains
-    // stay the default; DPG_SOLVE_DINV=1 selects the inverted blocks
-    c->use_dinv = getenv("DPG_SOLVE_DINV") != nullptr;
+    // stay the default; opts.solve_dinv selects the inverted blocks
+    c->use_dinv = c->opts.solve_dinv != 0;
     PLAN_T(7);
     return DPG_OK;
 }
@@ -2416,8 +2414,9 @@ int chol_build(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pai
 // dpg_chol_create_sym in two halves: the plan (host only: no device call, so it may run while the
 // caller's stream still works, on any thread) and the upload of what it planned (nothing between)
 int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                             dpg_chol_sym* S) {
+                             dpg_chol_sym* S, const dpg_chol_opts* opts) {
     CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
+    if (opts) c->opts = *opts;
     std::swap(c->sym, *S);
     const int rc = chol_build_plan(c, n, pair_lo, pair_hi, n_pairs);
     if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }

@@ -480,7 +480,7 @@ int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair
     st.prm.starts = starts;
     st.prm.bal = std::max<int32_t>(bal, 2);
     st.prm.score = score;
-    st.prm.cover = cover && starts > 0 && getenv("DPG_ND_NOCOVER") == nullptr;
+    st.prm.cover = cover && starts > 0;
     st.aux.assign((size_t)n, -1);
     st.stamp.assign((size_t)n, 0);
     st.lvl.assign((size_t)n, -1);
@@ -496,15 +496,12 @@ int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair
 }
 
 int dpg_chol_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                   std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
+                   std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat, bool md) {
     if (n <= 0) return -1;
     // nested dissection with minimum-degree parts of <= 16 nodes (tools/order_job.sh: the GPU
     // factorization 1.1x faster than under plain minimum degree on config 4's graph, 1.5x on config
-    // 3's, 16x on config 5's four-pass route); DPG_CHOL_ORDER=md selects plain minimum degree,
-    // nd:<leaf> another part size
-    const char* e = getenv("DPG_CHOL_ORDER");
-    if (!e || strncmp(e, "md", 2) != 0)
-        return dpg_chol_order_nd(n, pair_lo, pair_hi, n_pairs, e && strncmp(e, "nd:", 3) == 0 ? atoi(e + 3) : 16, perm, pat);
+    // 3's, 16x on config 5's four-pass route); md: plain minimum degree (DPG_ORDER_MD)
+    if (!md) return dpg_chol_order_nd(n, pair_lo, pair_hi, n_pairs, 16, perm, pat);
     // ---- graph
     std::vector<int64_t> aptr((size_t)n + 1, 0);
     for (int64_t p = 0; p < n_pairs; ++p) { aptr[(size_t)pair_lo[p] + 1]++; aptr[(size_t)pair_hi[p] + 1]++; }
@@ -555,28 +552,21 @@ double dpg_chol_critical_path_us(const dpg_chol_sym& S) {
 // factor + solve 0.860 -> 0.716 ms, chord-step solves 0.251 -> 0.230 ms; config 3 keeps round 2's
 // order (0.282 ms; the others 0.29-0.34).
 // The incremental graph (dpg_incsym_order) reorders every 64 nodes with the same pick, on a worker
-// thread (dpg_inc.hip); DPG_INC_ND selects a single rule there.
-// DPG_CHOL_ORDER (md, nd:<leaf>) forces round 2's single order; DPG_CHOL_ND=<k> only candidate k
-// of {round 2, 2-start, 8-start, 4-start ratio} (A/B); DPG_ND_NOCOVER drops the cover step.
+// thread (dpg_inc.hip).
+// opts->order DPG_ORDER_ND (2) keeps round 2's single order, DPG_ORDER_MD (1) plain minimum degree.
 int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                       const dpg_chol_opts* opts, dpg_chol_sym* S) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    if (getenv("DPG_CHOL_ORDER") || n < 256) {
-        if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+    const int32_t order = opts ? opts->order : 0;
+    if (order != 0 || n < 256) {
+        if (dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat, order == 1)) return -1;
         return dpg_chol_sym_from_patterns(n, perm, pat, opts, S);
     }
     struct Cand { int32_t starts, bal, score; };
-    static const Cand cands[] = {{0, 5, 0}, {2, 4, 2}, {8, 4, 2}, {4, 5, 1}};
-    const char* only = getenv("DPG_CHOL_ND");
-    static const int kDefault[] = {0, 2};
-    int pick[2];
-    int np = 0;
-    if (only) pick[np++] = std::max(0, std::min(3, atoi(only)));
-    else for (int k : kDefault) pick[np++] = k;
+    static const Cand cands[] = {{0, 5, 0}, {8, 4, 2}};
     double best = -1.0;
-    for (int j = 0; j < np; ++j) {
-        const int k = pick[j];
+    for (int k = 0; k < 2; ++k) {
         if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, true,
                                   perm, pat))
             return -1;
@@ -634,8 +624,8 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
     // a column joins its child's supernode whatever its other children (they hang off the merged
     // front, whose index set holds their rows): nested dissection's separators become one front
     // each instead of a chain of fronts split at every subtree root attached to them.
-    // DPG_CHOL_MERGE_SINGLE=1 restores the single-child rule.
-    const bool any_child = getenv("DPG_CHOL_MERGE_SINGLE") == nullptr;
+    // opts->merge_single restores the single-child rule.
+    const bool any_child = !(opts && opts->merge_single);
     {
         int32_t s = -1;
         int64_t zeros = 0, cols = 0;
@@ -822,27 +812,26 @@ inline void for_rows_after(const dpg_chol_incsym* I, int64_t j, int64_t after, F
 }  // namespace
 
 int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
-                     std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat) {
-    // Default (DPG_INC_ND unset or -1): the batch analysis's pick -- round 2's separator rule or the
+                     std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat,
+                     const dpg_chol_opts* opts) {
+    // The batch analysis's pick (opts->order DPG_ORDER_AUTO) -- round 2's separator rule or the
     // 8-start search with cover separators, each carried through the supernodal analysis under the
     // incremental solver's options, the shorter critical-path estimate kept.  It costs two orders
     // and two analyses per reorder, which dpg_inc computes on a worker thread ahead of time
     // (dpg_inc.hip, DPG_INC_BG_LEAD), so the per-node latency does not pay for it: config 4 at V = 5000
     // p50 2.14 -> 1.96 ms, 456 -> 487 nodes/s; config 5 413 vs 411 nodes/s
-    // (profiles/r03/v24_incbg_ab.txt).  DPG_INC_ND=0: round 2's rule alone (round 2 and the earlier
-    // round-3 default); k > 0: the k-start search alone (sqrt-ratio score, no cover step); -k: the
-    // pick between round 2's rule and the k-start search without cover.
-    static const int inc_nd = [] { const char* e = getenv("DPG_INC_ND"); return e ? atoi(e) : -1; }();
+    // (profiles/r03/v24_incbg_ab.txt).  DPG_ORDER_ND: round 2's rule alone; DPG_ORDER_MD: minimum
+    // degree.
+    const int32_t order = opts ? opts->order : 0;
     int rc = 0;
-    if (inc_nd < 0 && !getenv("DPG_CHOL_ORDER") && n >= 256) {
-        const dpg_chol_opts o{64, 0.3};   // dpg_inc's solver options
+    if (order == 0 && n >= 256) {
+        const dpg_chol_opts o = opts ? *opts : dpg_chol_opts{};
         double best = -1.0;
         std::vector<int32_t> pm;
         std::vector<std::vector<int32_t>> pt;
         for (int k = 0; k < 2; ++k) {
             rc = k == 0 ? dpg_chol_order(n, pair_lo, pair_hi, n_pairs, pm, pt)
-                 : inc_nd == -1 ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, pm, pt)
-                                : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, -inc_nd, 4, 2, false, pm, pt);
+                        : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, pm, pt);
             if (rc) return -1;
             dpg_chol_sym T;
             if (dpg_chol_sym_from_patterns(n, pm, pt, &o, &T)) return -1;
@@ -854,17 +843,16 @@ int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, 
             }
         }
     } else {
-        rc = (inc_nd > 0 && !getenv("DPG_CHOL_ORDER"))
-                 ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, inc_nd, 4, 2, false, perm, pat)
-                 : dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat);
+        rc = dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat, order == 1);
     }
     return rc ? -1 : 0;
 }
 
-int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs) {
+int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                     const dpg_chol_opts* opts) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    if (dpg_incsym_order(n, pair_lo, pair_hi, n_pairs, perm, pat)) return -1;
+    if (dpg_incsym_order(n, pair_lo, pair_hi, n_pairs, perm, pat, opts)) return -1;
     dpg_incsym_init(I, n, perm, pat);
     return 0;
 }

@@ -428,7 +428,7 @@ extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
 }
 
 extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, int64_t nf,
-                                int64_t shard_begin, int64_t shard_end) {
+                                int64_t shard_begin, int64_t shard_end, const dpg_chol_opts* opts) {
     memset(g, 0, sizeof(*g));
     if (n <= 0 || nf < 0 || n > (int64_t)1 << 28) return DPG_ERR_ARG;
     // unique pairs (lo, hi) of Between factors
@@ -530,7 +530,7 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     // symbolic analysis + device structures of the supernodal Cholesky (once per pattern)
     std::vector<int32_t> plo((size_t)P), phi((size_t)P);
     for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)pairs[(size_t)p].first; phi[(size_t)p] = (int32_t)pairs[(size_t)p].second; }
-    rc = dpg_chol_create(&g->chol, n, plo.data(), phi.data(), P);
+    rc = dpg_chol_create(&g->chol, n, plo.data(), phi.data(), P, opts);
     if (rc) g->chol = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
     return DPG_OK;
 }

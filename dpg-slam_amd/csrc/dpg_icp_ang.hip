@@ -1180,8 +1180,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     const int64_t chunk = mode ? (int64_t)(scratch && per_edge ? scratch_bytes / per_edge : 0) : n_edges;
     if (chunk <= 0) return DPG_ERR_SIZE;
     Rec* g = reinterpret_cast<Rec*>(scratch);
-    const char* ve = getenv("DPG_ICP_VARIANT");   // A/B of kernel variants (tools/icp_var_ab.py)
-    const int var = ve ? atoi(ve) : 4;
+    const int var = kp->kernel_variant;   // A/B of kernel forms (tools/icp_var_ab.py); 0 = the default
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
@@ -1195,7 +1194,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
 #define DPG_ANG_K(P, M, V) hipLaunchKernelGGL((icp_ang_kernel<P, M, V>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
-        if (var == 0) DPG_ANG_K(P, M, 0);                                                                       \
+        if (var == 0) DPG_ANG_K(P, M, 4);                                                                       \
         else DPG_ANG_K(P, M, 4)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);

@@ -118,56 +118,6 @@ inline uint64_t pkey(int32_t lo, int32_t hi) { return ((uint64_t)(uint32_t)lo <<
 
 }  // namespace
 
-// One persistent worker per graph for the prepare's symbolic half (DPG_INC_ASYNC=1; off by
-// default): its scratch (the derive's thread-local buffers, the symbolic state) stays warm on one
-// thread -- a fresh std::async thread per node measured slower than no overlap at all.  Measured
-// (profiles/r03/v25_incasync_ab.txt, v26_incworker_ab.txt): config 4 p50 1.95 -> 2.02 ms (the
-// plan runs ~25 % slower off the thread that built the pairs), config 5 411 -> 424 nodes/s.
-struct dpg_inc_worker {
-    std::thread th;
-    std::mutex m;
-    std::condition_variable cv;
-    std::function<int()> job;
-    bool quit = false;
-    std::atomic<int> state{0};   // 0 idle, 1 submitted / running, 2 done
-    int rc = 0;
-    dpg_inc_worker() : th([this] { loop(); }) {}
-    ~dpg_inc_worker() {
-        {
-            std::lock_guard<std::mutex> g(m);
-            quit = true;
-        }
-        cv.notify_one();
-        th.join();
-    }
-    void loop() {
-        std::unique_lock<std::mutex> lk(m);
-        for (;;) {
-            cv.wait(lk, [&] { return quit || (bool)job; });
-            if (quit) return;
-            std::function<int()> j = std::move(job);
-            job = nullptr;
-            lk.unlock();
-            const int r = j();
-            lk.lock();
-            rc = r;
-            state.store(2, std::memory_order_release);
-        }
-    }
-    void submit(std::function<int()> f) {
-        {
-            std::lock_guard<std::mutex> g(m);
-            job = std::move(f);
-            state.store(1, std::memory_order_relaxed);
-        }
-        cv.notify_one();
-    }
-    int wait() {   // the caller has nothing else to do: spin (yielding) until the job is done
-        while (state.load(std::memory_order_acquire) != 2) std::this_thread::yield();
-        state.store(0, std::memory_order_relaxed);
-        return rc;
-    }
-};
 
 struct dpg_inc {
     dpg_ctx* ctx = nullptr;
@@ -182,7 +132,7 @@ struct dpg_inc {
     dpg_chol_incsym I;
     int64_t V_at_order = 0, nnz_at_order = 0;  // size of the graph at the last full ordering
     dpg_chol_sym S;
-    dpg_chol_opts opts{64, 0.3};
+    dpg_chol_opts opts;
     int64_t reorders = 0;
     // device
     dpg_gn_dev g{};                            // assembly buffers + the Cholesky (g.chol)
@@ -217,8 +167,6 @@ struct dpg_inc {
         std::vector<std::vector<int32_t>> pat;
     };
     std::future<BgOrder> bg;
-    std::unique_ptr<dpg_inc_worker> worker;    // the symbolic half of a prepare (dpg_inc_prepare_async)
-    bool prep_running = false;
     const char* prep_msg = "";                 // its failure message
     double prep_ms[3] = {};                    // its incsym, derive, chol plan times
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
@@ -344,16 +292,6 @@ int inc_rebuild(dpg_inc* q, hipStream_t s) {
 
 int set_err(int code, const char* msg) { return dpg_set_error(code, msg); }
 
-// background ordering (DPG_INC_BG_ORDER=0 turns it off: every fresh order on the calling thread)
-int64_t bg_lead() {   // nodes between the snapshot and the reorder it is for (DPG_INC_BG_LEAD, A/B)
-    static const int64_t v = [] { const char* e = getenv("DPG_INC_BG_LEAD"); return e ? (int64_t)atoi(e) : (int64_t)8; }();
-    return v;
-}
-bool bg_order_on() {
-    static const bool on = [] { const char* e = getenv("DPG_INC_BG_ORDER"); return !(e && atoi(e) == 0); }();
-    return on;
-}
-int prep_join(dpg_inc* q);
 void bg_discard(dpg_inc* q) {
     if (q->bg.valid()) (void)q->bg.get();   // joins the worker
 }
@@ -370,6 +308,7 @@ void dpg_inc_params_default(dpg_inc_params* p) {
     p->relinearize_threshold = 0.1;
     p->duplicate_factors = 0;
     p->reorder_every = 32;
+    p->reorder_lead = 8;
     dpg_gn_params_default(&p->gn);
 }
 
@@ -387,15 +326,15 @@ dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
     if (p) q->P = *p;
     else dpg_inc_params_default(&q->P);
     if (q->P.relinearize_skip < 1) q->P.relinearize_skip = 1;
-    if (const char* e = getenv("DPG_INC_REORDER_EVERY")) q->P.reorder_every = atoi(e);   // A/B override
     if (q->P.reorder_every < 1) q->P.reorder_every = 1;
+    if (q->P.reorder_lead < 0 || q->P.reorder_lead >= q->P.reorder_every) q->P.reorder_lead = 0;
+    q->opts = *dpg_ctx_chol_opts(ctx);   // the context's solver options
     q->P.gn.linear_solver = DPG_SOLVER_CHOLESKY;
     return q;
 }
 
 int dpg_inc_reset(dpg_inc* q) {
     if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_reset: NULL");
-    (void)prep_join(q);
     bg_discard(q);
     q->V = 0;
     q->updates = 0;
@@ -419,7 +358,6 @@ int dpg_inc_reset(dpg_inc* q) {
 // so the next prepare orders the graph afresh from the pairs that remain.
 int dpg_inc_abort_prepare(dpg_inc* q) {
     if (!q) return set_err(DPG_ERR_ARG, "dpg_inc_abort_prepare: NULL");
-    (void)prep_join(q);
     if (!q->prepared) return DPG_OK;
     bg_discard(q);   // its snapshot may hold the pairs that leave now; the next prepare reorders anyway
     for (size_t k = (size_t)q->prep_pairs0; k < q->plo.size(); ++k) q->pair_id.erase(pkey(q->plo[k], q->phi[k]));
@@ -434,7 +372,6 @@ int dpg_inc_abort_prepare(dpg_inc* q) {
 
 void dpg_inc_destroy(dpg_inc* q) {
     if (!q) return;
-    (void)prep_join(q);
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
     (void)hipStreamSynchronize(s);
     void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.contrib, q->g.partials, q->g.scal3,
@@ -482,9 +419,8 @@ namespace {
 // the update's new node pairs enter the pattern (pair ids in arrival order).  prep_symbolic: the
 // order extended or refreshed, the derived structures and the Cholesky plan -- host only; it touches
 // the symbolic state (I, S, the plan inside g.chol, the ordering bookkeeping) and nothing the
-// numeric half of the update reads before it joins, so dpg_add_node_pairs runs it on a worker
-// thread (dpg_inc_prepare_async) while the GPU aligns and the calling thread stages the factors.
-// It reports failures through its return code and prep_msg; the caller aborts the prepare.
+// numeric half of the update reads, so dpg_add_node_pairs runs it while the GPU aligns the node's
+// edges.  It reports failures through its return code and prep_msg; the caller aborts the prepare.
 int prep_pairs(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs,
                std::vector<std::pair<int32_t, int32_t>>& new_pairs) {
     if (!q || n_new < 0 || n_pairs < 0 || (n_pairs > 0 && !pairs)) return set_err(DPG_ERR_ARG, "dpg_inc_prepare: bad arguments");
@@ -539,7 +475,7 @@ int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::
     }
     if (reordered && !from_bg) {
         bg_discard(q);
-        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size())) {
+        if (dpg_incsym_reset(&q->I, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size(), &q->opts)) {
             q->prep_msg = "dpg_inc_prepare: symbolic analysis failed";
             return DPG_ERR_NUMERIC;
         }
@@ -549,14 +485,14 @@ int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::
         q->nnz_at_order = q->I.nnz;
         q->reorders += 1;
     }
-    if (bg_order_on() && !q->bg.valid() && V1 >= 256 && V1 - q->V_at_order >= q->P.reorder_every - bg_lead()) {
+    if (q->P.reorder_lead > 0 && !q->bg.valid() && V1 >= 256 && V1 - q->V_at_order >= q->P.reorder_every - q->P.reorder_lead) {
         const int64_t P = (int64_t)q->plo.size();
         std::vector<int32_t> lo(q->plo), hi(q->phi);
-        q->bg = std::async(std::launch::async, [V1, P, lo = std::move(lo), hi = std::move(hi)]() {
+        q->bg = std::async(std::launch::async, [V1, P, lo = std::move(lo), hi = std::move(hi), o = q->opts]() {
             dpg_inc::BgOrder r;
             r.n = V1;
             r.n_pairs = P;
-            r.rc = dpg_incsym_order(V1, lo.data(), hi.data(), P, r.perm, r.pat);
+            r.rc = dpg_incsym_order(V1, lo.data(), hi.data(), P, r.perm, r.pat, &o);
             return r;
         });
     }
@@ -566,7 +502,8 @@ int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::
         return DPG_ERR_NUMERIC;
     }
     const double t1b = now_ms();
-    const int rc = dpg_chol_create_sym_plan(&q->g.chol, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size(), &q->S);
+    const int rc = dpg_chol_create_sym_plan(&q->g.chol, V1, q->plo.data(), q->phi.data(), (int64_t)q->plo.size(), &q->S,
+                                            &q->opts);
     if (rc) {
         q->prep_msg = "dpg_inc_prepare: Cholesky plan failed";
         return rc;
@@ -576,18 +513,6 @@ int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::
     q->prep_ms[2] = now_ms() - t1b;
     q->prep_reordered = reordered;
     return DPG_OK;
-}
-
-// the symbolic part's result once it is done (0 when none is running)
-int prep_join(dpg_inc* q) {
-    if (!q->prep_running) return DPG_OK;
-    q->prep_running = false;
-    return q->worker->wait();
-}
-
-bool prep_async_on() {
-    static const bool on = [] { const char* e = getenv("DPG_INC_ASYNC"); return e && atoi(e) != 0; }();
-    return on;
 }
 
 }  // namespace
@@ -603,20 +528,6 @@ int dpg_inc_prepare(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_p
         dpg_inc_abort_prepare(q);
         return set_err(rc, msg);
     }
-    return DPG_OK;
-}
-
-// dpg_inc_prepare with its symbolic part on a worker thread (DPG_INC_ASYNC=1; default: this thread);
-// the next dpg_inc_update (or abort / reset / destroy) joins it
-int dpg_inc_prepare_async(dpg_inc* q, int64_t n_new, const int32_t* pairs, int64_t n_pairs) {
-    if (!prep_async_on()) return dpg_inc_prepare(q, n_new, pairs, n_pairs);
-    std::vector<std::pair<int32_t, int32_t>> new_pairs;
-    const int rc = prep_pairs(q, n_new, pairs, n_pairs, new_pairs);
-    if (rc) return rc;
-    const int64_t V1 = q->V + n_new;
-    if (!q->worker) q->worker.reset(new dpg_inc_worker());
-    q->prep_running = true;
-    q->worker->submit([q, V1, n_new, np = std::move(new_pairs)]() { return prep_symbolic(q, V1, n_new, np); });
     return DPG_OK;
 }
 
@@ -702,25 +613,11 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         if (est_saved) (void)hipMemcpy(q->est, q->est_bak, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice);
         return set_err(code, msg);
     };
-    // a prepare still running on its worker thread (dpg_inc_prepare_async): the contribution lists
-    // and, in ISAM2 mode, the relinearization and the assembly go first -- none of them reads the
-    // symbolic state -- and the update joins it before the Cholesky structures go up
-    const bool async_prep = q->prep_running;
-    // (DPG_INC_EARLY_ASM=1: also without the worker -- the assembly then runs on the GPU while the
-    // host stages the Cholesky upload; not yet measured on the GPU, off by default)
-    static const bool early_asm = [] { const char* e = getenv("DPG_INC_EARLY_ASM"); return e && atoi(e) != 0; }();
-    const bool early = (async_prep || early_asm) && q->P.mode == DPG_INC_ISAM2;
     const double t1b = now_ms();
     if ((rc = inc_rebuild_lists(q, s))) return rollback(rc, "dpg_inc_update: contribution lists failed");
     q->prof[2] = now_ms() - t1b;
-    auto join_and_upload = [&]() -> int {
-        const int prc = prep_join(q);
-        if (prc) return rollback(prc, q->prep_msg);
-        const int urc = inc_rebuild_chol(q);
-        return urc ? rollback(urc, "dpg_inc_update: solver rebuild failed") : DPG_OK;
-    };
-    if (!early && (rc = join_and_upload())) return rc;
-    double t2 = now_ms();
+    if ((rc = inc_rebuild_chol(q))) return rollback(rc, "dpg_inc_update: solver rebuild failed");
+    const double t2 = now_ms();
     dpg_inc_stats S;
     memset(&S, 0, sizeof(S));
     if (q->P.mode == DPG_INC_ISAM2) {
@@ -741,10 +638,6 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
             return rollback(DPG_ERR_HIP, "dpg_inc_update: out of device memory");
         q->g.poses = q->theta;
         if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return rollback(rc, "assembly failed");
-        if (early) {
-            if ((rc = join_and_upload())) return rc;
-            t2 = now_ms();
-        }
         if ((rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s))) return rollback(rc, "Cholesky launch failed");
         if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return rollback(DPG_ERR_HIP, "memset");
         hipLaunchKernelGGL(inc_estimate_kernel, dim3(nblk(V1)), dim3(kThreads), 0, s, q->theta, dpg_chol_x_dev(q->g.chol),
@@ -753,13 +646,14 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         q->g.last_used_chol = 1;
         if ((rc = dpg_gn_dev_fetch(&q->g, q->g.hb_own, s, sc))) return rollback(rc, "fetch failed");
         if (sc[2] != 0.0) return rollback(DPG_ERR_NUMERIC, "dpg_inc_update: Cholesky failed (H not positive definite)");
+        // every read that can fail before the commit: a failure rolls the whole update back
+        int32_t nrel = 0;
+        if (relin && hipMemcpy(&nrel, q->cnt, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return rollback(DPG_ERR_HIP, "dpg_inc_update: relinearized-count read-back failed");
         std::swap(q->est, q->est_nxt);
         std::swap(q->c_est, q->c_est_nxt);
         std::swap(q->maxd, q->maxd_nxt);
         std::swap(q->c_maxd, q->c_maxd_nxt);
-        int32_t nrel = 0;
-        if (relin && hipMemcpy(&nrel, q->cnt, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
-            return set_err(DPG_ERR_HIP, "read-back failed");
         S.relinearized = nrel;
         S.gn_iterations = 1;
         S.error = sc[1];
@@ -938,14 +832,21 @@ dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path) {
         set_err(DPG_ERR_ARG, "dpg_inc_load: ctx is NULL");
         return nullptr;
     }
-    if (h.n_scans > 0 && (dpg_scans_upload(ctx, pts.data(), off.data(), h.n_scans, h.ratio) || dpg_scans_index_all(ctx)))
-        return nullptr;
+    // the graph is rebuilt and checked first; the caller's scan store is replaced only once
+    // everything else has succeeded (a failed load leaves the context as it was)
     dpg_inc* q = dpg_inc_create(ctx, &h.params);
     if (!q) return nullptr;
     auto bail = [&](int code, const char* msg) -> dpg_inc* {
         dpg_inc_destroy(q);
         set_err(code, msg);
         return nullptr;
+    };
+    auto take_scans = [&]() -> dpg_inc* {
+        if (h.n_scans > 0 && (dpg_scans_upload(ctx, pts.data(), off.data(), h.n_scans, h.ratio) || dpg_scans_index_all(ctx))) {
+            dpg_inc_destroy(q);
+            return nullptr;   // dpg_last_error is the store's
+        }
+        return q;
     };
     for (int64_t k = 0; k < h.n_pairs; ++k) {
         if (!q->pair_id.emplace(pkey(plo[(size_t)k], phi[(size_t)k]), (int32_t)k).second)
@@ -966,7 +867,7 @@ dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path) {
         }
         q->f_pair.push_back(pid);
     }
-    if (h.V == 0) return q;
+    if (h.V == 0) return take_scans();
     // the structure: a fresh order of the saved pattern (dpg_inc_prepare from an empty symbolic state)
     if (dpg_inc_prepare(q, h.V, nullptr, 0)) return bail(DPG_ERR_NUMERIC, "dpg_inc_load: symbolic analysis failed");
     q->prepared = false;
@@ -989,7 +890,7 @@ dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path) {
         return bail(DPG_ERR_HIP, "dpg_inc_load: upload failed");
     if ((rc = inc_rebuild(q, s))) return bail(rc, "dpg_inc_load: solver rebuild failed");
     if (hipStreamSynchronize(s) != hipSuccess) return bail(DPG_ERR_HIP, "dpg_inc_load: upload failed");
-    return q;
+    return take_scans();
 }
 
 int dpg_inc_get_poses(dpg_inc* q, double* poses, int64_t n) {

@@ -19,7 +19,6 @@ dpg_ctx* dpg_inc_ctx(dpg_inc* g);   /* the context an incremental graph runs on 
 /* the structural half of the next dpg_inc_update (host only: n_new nodes, node pairs that may carry
  * its Between factors), so that it can run while the GPU aligns the node's edges (dpg_inc.hip) */
 int dpg_inc_prepare(dpg_inc* g, int64_t n_new, const int32_t* pairs, int64_t n_pairs);
-int dpg_inc_prepare_async(dpg_inc* g, int64_t n_new, const int32_t* pairs, int64_t n_pairs);
 int dpg_inc_abort_prepare(dpg_inc* g);
 int dpg_ctx_is_multi(dpg_ctx* c);
 /* the scan store as host copies, and the neighbour index of every stored node (the graph
@@ -58,6 +57,7 @@ typedef struct dpg_icp_kparams {
     int32_t trace_stride;
     int32_t defer_cap;  /* angular kernel: windows of more candidates go to the workgroup's
                            cooperative queue (0: never) */
+    int32_t kernel_variant;   /* angular kernel form (dpg_ctx_set_icp_kernel_variant, A/B only) */
 } dpg_icp_kparams;
 
 /* Launchers (defined in dpg_icp.hip).  Return 0 or a negative DPG_ERR_*. */
@@ -142,8 +142,11 @@ typedef struct dpg_gn_dev {
     int32_t world, rank;
 } dpg_gn_dev;
 
-/* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip). */
-int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+/* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip); opts (dpg_chol.h, NULL =
+   defaults) are the context's solver options */
+struct dpg_chol_opts;
+int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                    const struct dpg_chol_opts* opts);
 void dpg_chol_destroy(void* chol);
 /* factor H (upper blocks of hb) and solve H x = -g; x (block positions) stays on device */
 int dpg_chol_solve(void* chol, const double* hb, void* stream);
@@ -155,7 +158,9 @@ const int32_t* dpg_chol_status_dev(void* chol);
 void dpg_chol_stats(void* chol, double out[6]);
 
 int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n_nodes, const dpg_factor* factors, int64_t n_factors,
-                     int64_t shard_begin, int64_t shard_end);
+                     int64_t shard_begin, int64_t shard_end, const struct dpg_chol_opts* opts);
+/* the context's solver options (dpg_ctx_set_solver_options) */
+const struct dpg_chol_opts* dpg_ctx_chol_opts(dpg_ctx* c);
 void dpg_gn_dev_free(dpg_gn_dev* g);
 int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g);
 int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb_dev, void* stream);

@@ -132,8 +132,17 @@ class IncParams(C.Structure):
         ("relinearize_threshold", C.c_double),
         ("duplicate_factors", C.c_int32),
         ("reorder_every", C.c_int32),
+        ("reorder_lead", C.c_int32),
+        ("pad", C.c_int32),
         ("gn", GnParams),
     ]
+
+
+class SolverOptions(C.Structure):
+    """dpg_solver_options -- the supernodal Cholesky's options (per context)."""
+
+    _fields_ = [(n, C.c_int32) for n in ("order", "fused", "solve_stage", "solve_maxseg", "solve_dinv",
+                                          "merge_single", "max_supernode_cols", "pad")] + [("relax_fraction", C.c_double)]
 
 
 class IncStats(C.Structure):
@@ -228,6 +237,8 @@ SIGNATURES = {
     "dpg_ctx_num_ranks": (C.c_int32, [P]),
     "dpg_ctx_rank": (C.c_int32, [P]),
     "dpg_ctx_set_icp_schedule": (C.c_int, [P, C.c_int32]),
+    "dpg_solver_options_default": (None, [C.POINTER(SolverOptions)]),
+    "dpg_ctx_set_solver_options": (C.c_int, [P, C.POINTER(SolverOptions)]),
     "dpg_ctx_destroy": (None, [P]),
     "dpg_ctx_set_stream": (C.c_int, [P, P]),
     "dpg_ctx_synchronize": (C.c_int, [P]),
@@ -261,6 +272,7 @@ SIGNATURES = {
     "dpg_kdtree_build_ms": (C.c_float, [P]),
     "dpg_ctx_set_icp_variant": (C.c_int, [P, C.c_int32]),
     "dpg_ctx_set_icp_defer_cap": (C.c_int, [P, C.c_int32]),
+    "dpg_ctx_set_icp_kernel_variant": (C.c_int, [P, C.c_int32]),
     "dpg_icp_batch_algorithmic_bytes": (C.c_double, [P]),
     "dpg_optimize_graph": (C.c_int, [P, F64P, C.c_int64, P, C.c_int64, C.POINTER(GnParams),
                                      C.POINTER(GnStats)]),
@@ -318,6 +330,12 @@ def default_inc_params() -> IncParams:
     p = IncParams()
     lib().dpg_inc_params_default(C.byref(p))
     return p
+
+
+def default_solver_options() -> SolverOptions:
+    o = SolverOptions()
+    lib().dpg_solver_options_default(C.byref(o))
+    return o
 
 
 def default_reopt_params() -> ReoptParams:

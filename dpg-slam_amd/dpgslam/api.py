@@ -224,11 +224,25 @@ class Context:
         results are identical for every value."""
         check(lib().dpg_ctx_set_icp_defer_cap(self.handle, int(cap)), "dpg_ctx_set_icp_defer_cap")
 
+    def set_solver_options(self, **kw):
+        """dpg_ctx_set_solver_options: the defaults with the given fields changed (order: "auto", "md",
+        "nd" or the DPG_ORDER_* value); taken by the next graph set up on this context."""
+        o = _abi.default_solver_options()
+        for k, v in kw.items():
+            if k == "order" and isinstance(v, str):
+                v = {"auto": 0, "md": 1, "nd": 2}[v]
+            setattr(o, k, v)
+        check(lib().dpg_ctx_set_solver_options(self.handle, C.byref(o)), "dpg_ctx_set_solver_options")
+
     def set_icp_schedule(self, schedule: str):
         """'measured' (default): once every edge of the staged batch has a measured cost, LPT over the
         ranks + longest-first dispatch; 'caller': e mod ranks in the caller's order.  Same results."""
         v = {"caller": 0, "measured": 1}[schedule]
         check(lib().dpg_ctx_set_icp_schedule(self.handle, v), "dpg_ctx_set_icp_schedule")
+
+    def set_icp_kernel_variant(self, v: int):
+        """Diagnostic A/B: the angular kernel's form (0 = default); results must be byte-identical."""
+        check(lib().dpg_ctx_set_icp_kernel_variant(self.handle, int(v)), "dpg_ctx_set_icp_kernel_variant")
 
     def kdtree_build_ms(self) -> float:
         return float(lib().dpg_kdtree_build_ms(self.handle))

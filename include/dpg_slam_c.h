@@ -180,6 +180,27 @@ int32_t dpg_ctx_rank(dpg_ctx* ctx);       /* global rank of the first local devi
 #define DPG_ICP_SCHEDULE_CALLER 0
 #define DPG_ICP_SCHEDULE_MEASURED 1
 int dpg_ctx_set_icp_schedule(dpg_ctx* ctx, int32_t schedule);
+/* Options of the supernodal Cholesky (per context; every device of a multi-device context), taken
+ * by the next graph set up on it (dpg_gn_setup, dpg_optimize_graph, dpg_reoptimize, dpg_inc_create).
+ * The defaults are the measured choices; the others are cross-checks and A/B
+ * references that must give the same solution to rounding. */
+#define DPG_ORDER_AUTO 0   /* nested dissection: the shorter critical path of two separator rules */
+#define DPG_ORDER_MD 1     /* minimum degree */
+#define DPG_ORDER_ND 2     /* nested dissection, round 2's separator rule alone */
+typedef struct dpg_solver_options {
+    int32_t order;               /* DPG_ORDER_AUTO */
+    int32_t fused;               /* 1: one-launch DAG factorization + solves when every front fits LDS;
+                                    0: the level-scheduled factorization */
+    int32_t solve_stage;         /* doubles of L staged in LDS by the DAG solves; -1: what fills 80 KB */
+    int32_t solve_maxseg;        /* ancestor row segments per front in the backward solve; -1: all */
+    int32_t solve_dinv;          /* 1: the solves use inverted diagonal blocks (0: substitution chains) */
+    int32_t merge_single;        /* 1: supernodes merge only along single-child chains (round 1's rule) */
+    int32_t max_supernode_cols;  /* 64 block columns */
+    int32_t pad;
+    double relax_fraction;       /* 0.3: explicit-zero budget of relaxed supernodes */
+} dpg_solver_options;
+void dpg_solver_options_default(dpg_solver_options* o);
+int dpg_ctx_set_solver_options(dpg_ctx* ctx, const dpg_solver_options* o);
 /* Run all work of this context on an external hipStream_t (e.g. torch's current stream); on a
  * multi-GPU context it applies to the first device only. */
 int dpg_ctx_set_stream(dpg_ctx* ctx, void* hip_stream);
@@ -269,6 +290,9 @@ int dpg_ctx_set_icp_variant(dpg_ctx* ctx, int32_t variant);
  * holds more than `cap` candidates is handed to the workgroup's cooperative queue, where a whole
  * wave scans it; 0 scans every window in its own lane.  Default 256. */
 int dpg_ctx_set_icp_defer_cap(dpg_ctx* ctx, int32_t cap);
+/* Diagnostic: the angular ICP kernel's form (0 = the default; others are A/B candidates that must give
+ * byte-identical results, tools/icp_var_ab.py). */
+int dpg_ctx_set_icp_kernel_variant(dpg_ctx* ctx, int32_t variant);
 /* Sum over edges of iterations x (8N + 8M + 8N) -- algorithmic bytes of the correspondence
  * search for the last run, computed on device and copied back. */
 double dpg_icp_batch_algorithmic_bytes(dpg_ctx* ctx);
@@ -402,6 +426,10 @@ typedef struct dpg_inc_params {
     double relinearize_threshold;    /* 0.1 (ISAM2Params::relinearizeThreshold) */
     int32_t duplicate_factors;       /* 0; 1: SURVEY Q1 */
     int32_t reorder_every;           /* 32: a fresh fill-reducing order every this many new nodes */
+    int32_t reorder_lead;            /* 8: that order is computed on a worker thread from a snapshot of
+                                        the graph this many nodes before it is due, then extended by the
+                                        nodes and edges that arrived since; 0: on the calling thread */
+    int32_t pad;
     dpg_gn_params gn;                /* DPG_INC_BATCH: the Gauss-Newton loop (Cholesky) */
 } dpg_inc_params;
 

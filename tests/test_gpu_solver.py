@@ -1,8 +1,6 @@
 """GPU tests of the pose-graph solver itself: the one-launch DAG Cholesky against
 the level-scheduled one, a known-answer mesh graph whose elimination tree has large fronts (the
 multi-workgroup team path), and the asynchronous GN loop against dpg_optimize_graph."""
-import os
-
 import numpy as np
 import pytest
 
@@ -11,17 +9,21 @@ from graphs import consistent_mesh_graph, pose_diff
 pytestmark = pytest.mark.gpu
 
 
-def _optimize(ctx, X0, F, levels=False, **kw):
+def _optimize(ctx, X0, F, levels=False, solver=None, **kw):
+    """dpg_optimize_graph with solver options (dpg_ctx_set_solver_options, taken when the graph is
+    set up), the defaults restored afterwards."""
     from dpgslam import _abi
     gp = _abi.default_gn_params()
     for k, v in kw.items():
         setattr(gp, k, v)
+    opts = dict(solver or {})
     if levels:
-        os.environ["DPG_CHOL_LEVELS"] = "1"   # read when the Cholesky is set up (dpg_chol_create)
+        opts["fused"] = 0
+    ctx.set_solver_options(**opts)
     try:
         return ctx.optimize_graph(X0, F, gp)
     finally:
-        os.environ.pop("DPG_CHOL_LEVELS", None)
+        ctx.set_solver_options()
 
 
 def test_mesh_graph_known_answer(ctx):
@@ -86,8 +88,9 @@ def test_async_gn_loop_matches_optimize_graph(ctx, workload):
 
 @pytest.mark.parametrize("name", ["config3", "config4"])
 def test_orders_agree(ctx, workload, name):
-    """The nested-dissection order (default) and plain minimum degree (DPG_CHOL_ORDER=md) factor the
-    same system: the GN solutions agree to rounding, and against the oracle on config 3."""
+    """The nested-dissection order (default: the better of two separator rules), round 2's rule
+    alone and plain minimum degree (dpg_solver_options.order) factor the same system: the GN
+    solutions agree to rounding, and against the oracle on config 3."""
     from oracle import oracle as O
     from dpgslam import _abi
     w = workload(name)
@@ -97,24 +100,23 @@ def test_orders_agree(ctx, workload, name):
     F = w.factors_with_icp(res, p)
     X0 = w.est.astype(np.float64)
     Xn, sn = _optimize(ctx, X0, F)
-    os.environ["DPG_CHOL_ORDER"] = "md"   # read when the Cholesky is set up
-    try:
-        Xm, sm = _optimize(ctx, X0, F)
-    finally:
-        os.environ.pop("DPG_CHOL_ORDER", None)
+    Xm, sm = _optimize(ctx, X0, F, solver={"order": "md"})
+    Xr, sr = _optimize(ctx, X0, F, solver={"order": "nd"})
     assert np.abs(pose_diff(Xn, Xm)).max() < 1e-9
+    assert np.abs(pose_diff(Xn, Xr)).max() < 1e-9
     if name == "config3":
         Xo, _ = O.optimize_graph(X0, F)
         assert np.abs(pose_diff(Xn, Xo)).max() < 1e-6
 
 
-@pytest.mark.parametrize("env", [{"DPG_SOLVE_STAGE": "0"}, {"DPG_SOLVE_STAGE": "15000"}, {"DPG_SOLVE_MAXSEG": "0"},
-                                 {"DPG_SOLVE_MAXSEG": "1"}, {"DPG_CHOL_MERGE_SINGLE": "1"}])
-def test_solve_paths_agree(ctx, workload, env):
+@pytest.mark.parametrize("opts", [{"solve_stage": 0}, {"solve_stage": 15000}, {"solve_maxseg": 0}, {"solve_maxseg": 1},
+                                  {"merge_single": 1}, {"solve_dinv": 1}])
+def test_solve_paths_agree(ctx, workload, opts):
     """The triangular solves' code paths give the same GN solution on config 4 (chord steps and
     fresh factorizations): no LDS staging, staging of whole fronts up to 15 000 doubles, the
     backward solve with every front waiting for its parent (no row segments) or with segments only
-    where there is one, and the single-child supernode rule -- against the default build."""
+    where there is one, the single-child supernode rule, and the inverted diagonal blocks --
+    against the defaults (dpg_solver_options)."""
     from dpgslam import _abi
     w = workload("config4")
     p = _abi.default_icp_params()
@@ -123,11 +125,6 @@ def test_solve_paths_agree(ctx, workload, env):
     F = w.factors_with_icp(res, p)
     X0 = w.est.astype(np.float64)
     Xd, sd = _optimize(ctx, X0, F)
-    os.environ.update(env)   # read when the Cholesky is set up
-    try:
-        Xe, se = _optimize(ctx, X0, F)
-    finally:
-        for k in env:
-            os.environ.pop(k, None)
+    Xe, se = _optimize(ctx, X0, F, solver=opts)
     assert se.iterations == sd.iterations
     assert np.abs(pose_diff(Xe, Xd)).max() < 1e-9

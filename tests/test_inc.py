@@ -281,3 +281,32 @@ def test_gpu_checkpoint_resume_add_node_path(tmp_path):
     g.close()
     ctx2.close()
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_checkpoint_failed_load_keeps_the_store(tmp_path):
+    """A load that fails after the file was read (here: a multi-device context, which the incremental
+    graph refuses) leaves the caller's scan store as it was -- its own 30 nodes, still aligned bit
+    for bit as before (the store used to be replaced before the checks)."""
+    from dpgslam import api
+    w = synth.generate("config2")
+    p = _abi.default_icp_params()
+    ctx = api.Context(0)
+    g = api.IncGraph(ctx, mode="isam2")
+    prior = np.zeros(1, _abi.FACTOR_DTYPE)
+    prior["kind"], prior["i"], prior["info"] = _abi.DPG_FACTOR_PRIOR, 0, 1.0 / np.array([0.04, 0.04, 0.0225])
+    for v in range(12):
+        g.add_node(w.cloud(v), np.zeros(v + 1, np.int32), w.est[v], extra=prior if v == 0 else None, icp_params=p)
+    path = str(tmp_path / "graph12.dpg")
+    g.save(path)
+    g.close()
+    ctx.close()
+    V = 30
+    with api.Context(0, virtual=2) as m:
+        m.upload_scans(w.pts[:w.offsets[V]], w.offsets[:V + 1], p.downsample_icp_points_ratio)
+        e = np.stack([np.arange(V - 1), np.arange(1, V)], 1).astype(np.int32)
+        before, _ = m.icp_batch(e, w.est[:V], p, compute_cov=False)
+        with pytest.raises(_abi.DpgError):
+            api.IncGraph.load(m, path)
+        after, _ = m.icp_batch(e, w.est[:V], p, compute_cov=False)
+        assert before.tobytes() == after.tobytes()

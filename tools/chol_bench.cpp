@@ -12,7 +12,9 @@
 #include <vector>
 
 extern "C" {
-int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs);
+struct dpg_chol_opts;
+int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
+                    const dpg_chol_opts* opts);
 void dpg_chol_destroy(void* chol);
 int dpg_chol_solve(void* chol, const double* hb, void* stream);
 int dpg_chol_resolve(void* chol, const double* hb, void* stream);
@@ -81,7 +83,7 @@ int main(int argc, char** argv) {
     for (int64_t t = 0; t < 3 * n; ++t) g[t] = U(rng);
 
     void* ch = nullptr;
-    int rc = dpg_chol_create(&ch, n, lo.data(), hi.data(), P);
+    int rc = dpg_chol_create(&ch, n, lo.data(), hi.data(), P, nullptr);
     if (rc) {
         fprintf(stderr, "dpg_chol_create failed %d\n", rc);
         return 1;

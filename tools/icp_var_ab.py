@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B of angular ICP kernel variants (DPG_ICP_VARIANT, read by the launcher at every launch) on a
+"""A/B of angular ICP kernel variants (dpg_ctx_set_icp_kernel_variant, taken at every launch) on a
 config's batched ICP, interleaved rounds in ONE process (cdna_hip_programming.md rule 24).  Every
 variant must give byte-identical results to the first one listed.
 usage: python tools/icp_var_ab.py [variants...] (default 0 1); ICP_CONFIG (config4), AB_ROUNDS (5)"""
@@ -22,10 +22,8 @@ with api.Context(0) as ctx:
     ctx.icp_prepare(w.edges, w.est, p)
     ref = None
     for r in range(rounds + 1):
-        for v in variants:   # "V" or "V:pA" (variant V, wave priority aging every A iterations)
-            var, _, age = v.partition(":p")
-            os.environ["DPG_ICP_VARIANT"] = var
-            os.environ["DPG_ICP_PRIO_AGE"] = age or "0"
+        for v in variants:
+            ctx.set_icp_kernel_variant(int(v))
             ctx.icp_run(compute_cov=False)
             ctx.synchronize()
             k = ctx.icp_kernel_ms()
