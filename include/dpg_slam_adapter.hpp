@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <array>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -41,17 +42,39 @@ inline void check(int rc, const char* what) {
     if (rc != DPG_OK) throw Error(std::string(what) + ": " + (dpg_last_error() ? dpg_last_error() : "?"));
 }
 
-/* One GPU context (device + HIP stream), owned. */
+/* A GPU context, owned: one device (the constructor), or one of the multi-device forms -- every
+ * adapter call below takes any of them (the batched paths shard, dpg_slam_c.h):
+ *   Context::multi(n)              one process over GPUs 0 .. n-1 (the ROS node);
+ *   Context::rank(dev, id, r, w)   one process per GPU, rank r of w (id from nccl_unique_id() on rank 0);
+ *   Context::virtual_devices(k)    k virtual devices on one GPU (tests of the sharded paths). */
 class Context {
   public:
-    explicit Context(int device = 0) : c_(dpg_ctx_create(device)) {
-        if (!c_) throw Error(std::string("dpg_ctx_create: ") + (dpg_last_error() ? dpg_last_error() : "?"));
+    explicit Context(int device = 0) : c_(dpg_ctx_create(device)) { ok("dpg_ctx_create"); }
+    static Context multi(int n_gpus, const int32_t* devices = nullptr) {
+        return Context(dpg_ctx_create_multi(n_gpus, devices), "dpg_ctx_create_multi");
+    }
+    static Context rank(int device, const std::array<unsigned char, DPG_NCCL_ID_BYTES>& id, int rank, int world) {
+        return Context(dpg_ctx_create_rank(device, id.data(), rank, world), "dpg_ctx_create_rank");
+    }
+    static Context virtual_devices(int k, int device = 0) {
+        return Context(dpg_ctx_create_virtual(k, device), "dpg_ctx_create_virtual");
+    }
+    static std::array<unsigned char, DPG_NCCL_ID_BYTES> nccl_unique_id() {
+        std::array<unsigned char, DPG_NCCL_ID_BYTES> id{};
+        check(dpg_nccl_unique_id(id.data()), "dpg_nccl_unique_id");
+        return id;
     }
     ~Context() { if (c_) dpg_ctx_destroy(c_); }
+    Context(Context&& o) noexcept : c_(o.c_) { o.c_ = nullptr; }
     Context(const Context&) = delete;
     Context& operator=(const Context&) = delete;
     dpg_ctx* get() const { return c_; }
+    int ranks() const { return dpg_ctx_num_ranks(c_); }
   private:
+    Context(dpg_ctx* c, const char* what) : c_(c) { ok(what); }
+    void ok(const char* what) {
+        if (!c_) throw Error(std::string(what) + ": " + (dpg_last_error() ? dpg_last_error() : "?"));
+    }
     dpg_ctx* c_;
 };
 

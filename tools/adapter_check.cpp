@@ -158,6 +158,40 @@ int main() {
         EXPECT(st.iterations == st2.iterations);
         printf("optimizeGraph: %d iterations, error %.6g\n", st.iterations, st.final_error);
     }
+    // the multi-device contexts through the same adapter calls: one
+    // process over n GPUs at n = 1 (RCCL with one rank) must equal the single device byte for byte;
+    // two virtual devices on this GPU run the n > 1 shard / gather / all-reduce paths
+    {
+        const double sig[3] = {0.2, 0.2, 0.15}, info[3] = {2.0, 2.0, 1.0 / 0.3f};
+        std::vector<dpg_factor> F{dpg_adapter::prior_factor(0, 0, 0, 0, sig)};
+        for (int k = 1; k < 4; ++k) F.push_back(dpg_adapter::between_factor(k - 1, k, 0.9, 0.0, 0.03, info));
+        F.push_back(dpg_adapter::between_factor(0, 2, 1.8, 0.0, 0.07, info));
+        std::vector<std::pair<Vector2f, float>> odom;
+        for (int k = 0; k < 4; ++k) odom.emplace_back(Vector2f(0.9f * (float)k, 0.0f), 0.03f * (float)k);
+        std::vector<Node> a1 = nodes, r1 = nodes;
+        dpg_adapter::Context s0(0);   // its own single-device context: reoptimize uploads the scans
+        const dpg_gn_stats s1 = dpg_adapter::optimizeGraph(s0.get(), a1, F);
+        const dpg_reopt_stats q1 = dpg_adapter::reoptimize(s0.get(), r1, odom, pgp);
+        dpg_adapter::Context m1 = dpg_adapter::Context::multi(1);
+        dpg_adapter::Context v2 = dpg_adapter::Context::virtual_devices(2);
+        EXPECT(m1.ranks() == 1 && v2.ranks() == 2);
+        int form = 0;
+        for (dpg_adapter::Context* c : {&m1, &v2}) {
+            std::vector<Node> a2 = nodes, r2 = nodes;
+            const dpg_gn_stats s2 = dpg_adapter::optimizeGraph(c->get(), a2, F);
+            const dpg_reopt_stats q2 = dpg_adapter::reoptimize(c->get(), r2, odom, pgp);
+            double worst = 0.0;
+            for (int k = 0; k < 4; ++k)
+                worst = std::max({worst, (double)std::fabs(a1[k].loc.x() - a2[k].loc.x()), (double)std::fabs(a1[k].th - a2[k].th),
+                                  (double)std::fabs(r1[k].loc.x() - r2[k].loc.x()), (double)std::fabs(r1[k].th - r2[k].th)});
+            EXPECT(s1.iterations == s2.iterations && q1.n_icp_edges == q2.n_icp_edges &&
+                   q1.n_loop_closures == q2.n_loop_closures && q1.gn.iterations == q2.gn.iterations);
+            EXPECT(form == 0 ? worst == 0.0 : worst < 1e-5);   // float poses: 1 ulp
+            printf("%s: optimizeGraph + reoptimize through the adapter, max pose difference %.3g\n",
+                   form == 0 ? "multi(1)" : "virtual(2)", worst);
+            ++form;
+        }
+    }
     // incremental form: one add_node per node
     {
         dpg_adapter::IncGraph g(ctx.get());

@@ -20,6 +20,7 @@ ap.add_argument("config", nargs="?", default="config4")
 ap.add_argument("--cap", action="store_true", help="transformation epsilon 0 and MSE threshold 0: every edge runs "
                                                    "to the iteration cap")
 ap.add_argument("--edges", type=int, default=0, help="only the first N edges")
+ap.add_argument("--variant", type=int, default=0, help="angular kernel form (dpg_ctx_set_icp_kernel_variant)")
 a = ap.parse_args()
 w = synth.generate(a.config)
 p = _abi.default_icp_params()
@@ -34,6 +35,7 @@ st = (C.c_ulonglong * 48)()
 with api.Context(0) as ctx:
     if os.environ.get("DPG_DEFER_CAP"):
         ctx.set_icp_defer_cap(int(os.environ["DPG_DEFER_CAP"]))
+    ctx.set_icp_kernel_variant(a.variant)
     ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
     ctx.icp_prepare(w.edges, w.est, p)
     L.dpg_icp_stats(st, 1)
