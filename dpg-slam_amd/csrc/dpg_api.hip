@@ -109,6 +109,7 @@ struct dpg_ctx {
     bool cov_pending = false, cov_on_aux = false;
     int32_t icp_variant = DPG_ICP_ANGULAR;
     int32_t defer_cap = 256;        // angular ICP: cooperative-queue threshold (dpg_ctx_set_icp_defer_cap)
+    int32_t cov_wg = 0;             // covariance kernel workgroups beside the pose graph (dpg_ctx_set_cov_workgroups)
     int32_t kernel_variant = 0;     // angular ICP kernel form (dpg_ctx_set_icp_kernel_variant, A/B)
     float map_ms = 0.f;             // last dpg_get_map kernel (HIP events map_ev)
     hipEvent_t map_ev[2] = {};
@@ -265,7 +266,7 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     if (hess_dev && timed) {   // beside the pose graph: on aux, after the ICP
         if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
         HIP_TRY(hipStreamWaitEvent(c->aux, c->ev[1], 0));
-        rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->aux);
+        rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->cov_wg, c->aux);
         if (rc) return fail(rc, "covariance kernel launch failed");
         HIP_TRY(hipEventRecord(c->ev[2], c->aux));
         c->cov_pending = true;
@@ -274,7 +275,7 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     }
     if (timed) c->cov_on_aux = false;
     if (hess_dev) {
-        rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, c->stream);
+        rc = dpg_launch_cov(full_dev, edges_dev, ne, res_dev, hess_dev, 0, c->stream);
         if (rc) return fail(rc, "covariance kernel launch failed");
     }
     if (timed) HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -947,6 +948,12 @@ int dpg_ctx_set_icp_defer_cap(dpg_ctx* c, int32_t cap) {
     return DPG_OK;
 }
 
+int dpg_ctx_set_cov_workgroups(dpg_ctx* c, int32_t n) {
+    if (!c || n < 0) return fail(DPG_ERR_ARG, "bad covariance workgroup count");
+    for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->cov_wg = n;
+    return DPG_OK;
+}
+
 int dpg_ctx_set_icp_kernel_variant(dpg_ctx* c, int32_t v) {
     if (!c || v < 0) return fail(DPG_ERR_ARG, "bad kernel variant");
     for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->kernel_variant = v;
@@ -1189,7 +1196,7 @@ int icp_cov_calculate(dpg_ctx* c, const float* data, int64_t nd, const float* mo
     HIP_TRY(hipMemcpyAsync(c->s_pts.p, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->s_edge.p, &E, sizeof(E), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->s_res.p, &R, sizeof(R), hipMemcpyHostToDevice, c->stream));
-    int rc = dpg_launch_cov(c->s_pts.p, c->s_edge.p, 1, c->s_res.p, c->s_hess.p, c->stream);
+    int rc = dpg_launch_cov(c->s_pts.p, c->s_edge.p, 1, c->s_res.p, c->s_hess.p, 0, c->stream);
     if (rc) return fail(rc, "covariance kernel launch failed");
     HIP_TRY(hipMemcpyAsync(hess_out, c->s_hess.p, 9 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1495,7 +1502,7 @@ static int ensure_pipe(dpg_ctx* q) {
     if (q->pipe_ctl) return DPG_OK;
     HIP_TRY(hipSetDevice(q->device));
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q->pipe_ctl), sizeof(dpg_gn_ctl)));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&q->pipe_slot), 2 * sizeof(dpg_gn_slot),
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&q->pipe_slot), 3 * sizeof(dpg_gn_slot),   // + [2]: the initial error
                           hipHostMallocMapped | hipHostMallocCoherent));
     for (auto& e : q->pipe_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return DPG_OK;
@@ -1513,7 +1520,8 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
     for (int k = 0; k < L; ++k) {
         dpg_ctx* q = dev_ctx(c, k);
         if ((rc = ensure_pipe(q))) return rc;
-        if ((rc = dpg_gn_pipe_init(&q->gn, &P, q->pipe_ctl, S.initial_error, q->stream)))
+        const double* cur_dev = q->gn.hb_own + 9 * q->gn.nnzb_upper + 3 * q->gn.n_nodes;   // the assembled error
+        if ((rc = dpg_gn_pipe_init(&q->gn, &P, q->pipe_ctl, cur_dev, q->pipe_slot + 2, q->stream)))
             return fail(rc, "GN pipeline launch failed");
     }
     auto issue = [&](int i) -> int {   // iteration i (1-based) reports into slot i & 1
@@ -1558,6 +1566,17 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
                 o.active = v->active;
                 o.final_ = v->final_;
                 o.it = v->it;
+            }
+            if (i == 1 && k == 0) {   // the initial error, as the device read it (pipe_init_kernel)
+                S.initial_error = static_cast<const volatile dpg_gn_slot*>(q->pipe_slot + 2)->error;
+                if (S.initial_error <= 0.0 && !o.active && o.it == 0) {   // nothing to do: no iteration ran
+                    for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
+                    nw = S.initial_error;
+                    dinf = 0.0;
+                    it = 0;
+                    HIP_TRY(hipSetDevice(c->device));
+                    return DPG_OK;
+                }
             }
             if (!o.active || o.it != i) return fail(DPG_ERR_STATE, "GN pipeline out of step (device %d, iteration %d)", k, i);
             if (k == 0) {
@@ -1624,10 +1643,14 @@ static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0,
         if (rc) return fail(rc, "assembly launch failed");
     }
     if (multi && (rc = coll_sum_hb(c))) return rc;
-    if ((rc = read_error(c, &S.initial_error))) return rc;
-    double cur = S.initial_error, nw = cur, dinf = 0.0;
+    double cur = 0.0, nw = 0.0, dinf = 0.0;
     int it = 0;
-    if (pipe_ok(c, P) && !(cur <= 0.0) && P.max_iterations > 0) {
+    const bool pipe = pipe_ok(c, P) && P.max_iterations > 0;
+    if (!pipe) {   // (the pipelined loop takes the initial error on the device: no round trip)
+        if ((rc = read_error(c, &S.initial_error))) return rc;
+        cur = nw = S.initial_error;
+    }
+    if (pipe) {
         if ((rc = gn_loop_pipe(c, P, S, nw, dinf, it))) return rc;
     } else if (!(cur <= 0.0) && P.max_iterations > 0) {
         for (;;) {

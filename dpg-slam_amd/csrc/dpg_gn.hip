@@ -688,11 +688,13 @@ __device__ __forceinline__ void clear_sync(int32_t* sync, int64_t n_words, int32
 }
 
 __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_was_chord, int32_t have_factor,
-                                 double last_dinf, double prev_dinf, double cur, double* max_out, int32_t* sync,
-                                 int64_t n_words, int32_t* status) {
+                                 double last_dinf, double prev_dinf, const double* cur_dev, dpg_gn_slot* init,
+                                 double* max_out, int32_t* sync, int64_t n_words, int32_t* status) {
     clear_sync(sync, n_words, status);
     if (threadIdx.x != 0) return;
-    ctl->active = 1;
+    const double cur = *cur_dev;   // the assembled initial error (the host loop reads it back first)
+    init->error = cur;
+    ctl->active = !(cur <= 0.0) ? 1 : 0;   // the host loop's entry test
     ctl->reuse = reuse;
     ctl->last_was_chord = last_was_chord;
     ctl->have_factor = have_factor;
@@ -783,7 +785,8 @@ __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const d
     *slot = o;
 }
 
-extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, double cur, void* stream) {
+extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, const double* cur_dev,
+                                dpg_gn_slot* init, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // iteration 1's chord decision from the host bookkeeping (as dpg_gn_dev_solve_async takes it)
     const bool slow = g->last_was_chord && g->last_delta_inf > 0.1 * g->prev_delta_inf;
@@ -792,7 +795,7 @@ extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_c
     int64_t n_words;
     dpg_chol_sync_dev(g->chol, &sync, &n_words);
     hipLaunchKernelGGL(pipe_init_kernel, dim3(1), dim3(1024), 0, s, ctl, reuse ? 1 : 0, g->last_was_chord, g->have_factor,
-                       g->last_delta_inf, g->prev_delta_inf, cur, g->scal3, sync, n_words,
+                       g->last_delta_inf, g->prev_delta_inf, cur_dev, init, g->scal3, sync, n_words,
                        const_cast<int32_t*>(dpg_chol_status_dev(g->chol)));
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }

@@ -60,7 +60,11 @@ int dpg_chol_solve_gated(void* chol, const double* hb, const int32_t* gate, int 
 void dpg_chol_sync_dev(void* chol, int32_t** sync, int64_t* n_words);
 // set the control block for iteration 1 from the host state (g's chord bookkeeping) and the
 // initial error
-int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, double cur_error, void* stream);
+// the initial error comes from the device (cur_dev: the assembled chi2 word, all-reduced on the
+// multi-device forms) and is reported in init->error; a loop whose initial error is not > 0 runs
+// no iteration (iteration 1 reports active = 0)
+int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, const double* cur_dev, dpg_gn_slot* init,
+                     void* stream);
 // enqueue one gated iteration: solve, retract, re-linearize + assemble into g->hb_own, control
 // kernel (reports into slot, a host-mapped pointer)
 int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot, void* stream);

@@ -28,6 +28,8 @@
 // Built with -ffp-contract=off: every float/double expression is one rounding per operation.
 
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <float.h>
 #include <stdint.h>
 
@@ -337,13 +339,16 @@ __global__ __launch_bounds__(kThreads) void icp_edges_kernel(const float2* __res
 }
 
 // R7: [x, y, yaw] block of d2J_dX2 over index-paired full clouds (s < min(n_data, n_model)).
+// A grid smaller than the edge count leaves the rest of the GPU to the pose graph that runs beside
+// it (dpg_ctx_set_cov_workgroups); every edge's sums are the same either way.
 __global__ __launch_bounds__(kThreads) void cov_block_kernel(const float2* __restrict__ full_pts,
-                                                             const dpg_icp_edge* __restrict__ edges,
+                                                             const dpg_icp_edge* __restrict__ edges, int64_t n_edges,
                                                              const dpg_icp_result* __restrict__ results,
                                                              double* __restrict__ hess) {
     __shared__ double red[kWaves][3];
     const int t = threadIdx.x;
-    const dpg_icp_edge E = edges[blockIdx.x];
+    for (int64_t b = blockIdx.x; b < n_edges; b += gridDim.x) {   // edges strided over the grid
+    const dpg_icp_edge E = edges[b];
     const int e = E.pad[0];   // results / hess by the caller's edge index
     const float* T = results[e].T;
     const double a = (double)dpg_atan2f(T[3], T[0]);   // yaw = atan2f(T10, T00) (cov :31)
@@ -378,6 +383,8 @@ __global__ __launch_bounds__(kThreads) void cov_block_kernel(const float2* __res
         o[0] = h00; o[1] = 0.0; o[2] = H02;
         o[3] = 0.0; o[4] = h00; o[5] = H12;
         o[6] = H02; o[7] = H12; o[8] = H22;
+    }
+    __syncthreads();   // red is reused by the next edge
     }
 }
 
@@ -484,11 +491,12 @@ extern "C" int dpg_launch_icp(const float* ds_pts_dev, const dpg_icp_edge* edges
 }
 
 extern "C" int dpg_launch_cov(const float* full_pts_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
-                              const dpg_icp_result* results_dev, double* hess_dev, void* stream) {
+                              const dpg_icp_result* results_dev, double* hess_dev, int32_t max_workgroups, void* stream) {
     if (n_edges <= 0) return DPG_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(cov_block_kernel, dim3((unsigned)n_edges), dim3(kThreads), 0, s,
-                       reinterpret_cast<const float2*>(full_pts_dev), edges_dev, results_dev, hess_dev);
+    const int64_t grid = max_workgroups > 0 ? std::min<int64_t>(n_edges, max_workgroups) : n_edges;
+    hipLaunchKernelGGL(cov_block_kernel, dim3((unsigned)grid), dim3(kThreads), 0, s,
+                       reinterpret_cast<const float2*>(full_pts_dev), edges_dev, n_edges, results_dev, hess_dev);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

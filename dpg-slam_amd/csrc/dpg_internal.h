@@ -65,7 +65,7 @@ int dpg_launch_icp(const float* ds_pts_dev, const dpg_icp_edge* edges_dev, int64
                    const dpg_icp_kparams* kp, int32_t max_points, dpg_icp_result* results_dev,
                    int32_t* trace_dev, void* stream);
 int dpg_launch_cov(const float* full_pts_dev, const dpg_icp_edge* edges_dev, int64_t n_edges,
-                   const dpg_icp_result* results_dev, double* hess_dev, void* stream);
+                   const dpg_icp_result* results_dev, double* hess_dev, int32_t max_workgroups, void* stream);
 size_t dpg_icp_lds_bytes(int32_t lds_tgt, int32_t cells_max);
 /* the 6x6 covariance sums of icp_cov_sandwich (dpg_icp.hip cov6_kernel): out[16] */
 int dpg_launch_cov6(const float* pts_dev, int32_t n_data, int32_t n_model, const float* T6_dev, double* out_dev,

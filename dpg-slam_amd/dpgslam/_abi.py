@@ -272,6 +272,7 @@ SIGNATURES = {
     "dpg_kdtree_build_ms": (C.c_float, [P]),
     "dpg_ctx_set_icp_variant": (C.c_int, [P, C.c_int32]),
     "dpg_ctx_set_icp_defer_cap": (C.c_int, [P, C.c_int32]),
+    "dpg_ctx_set_cov_workgroups": (C.c_int, [P, C.c_int32]),
     "dpg_ctx_set_icp_kernel_variant": (C.c_int, [P, C.c_int32]),
     "dpg_icp_batch_algorithmic_bytes": (C.c_double, [P]),
     "dpg_optimize_graph": (C.c_int, [P, F64P, C.c_int64, P, C.c_int64, C.POINTER(GnParams),

@@ -224,6 +224,11 @@ class Context:
         results are identical for every value."""
         check(lib().dpg_ctx_set_icp_defer_cap(self.handle, int(cap)), "dpg_ctx_set_icp_defer_cap")
 
+    def set_cov_workgroups(self, n: int):
+        """dpg_ctx_set_cov_workgroups: the covariance beside the pose graph on at most n workgroups
+        (0: one per edge); results are identical for every n."""
+        check(lib().dpg_ctx_set_cov_workgroups(self.handle, int(n)), "dpg_ctx_set_cov_workgroups")
+
     def set_solver_options(self, **kw):
         """dpg_ctx_set_solver_options: the defaults with the given fields changed (order: "auto", "md",
         "nd" or the DPG_ORDER_* value); taken by the next graph set up on this context."""

@@ -290,6 +290,10 @@ int dpg_ctx_set_icp_variant(dpg_ctx* ctx, int32_t variant);
  * holds more than `cap` candidates is handed to the workgroup's cooperative queue, where a whole
  * wave scans it; 0 scans every window in its own lane.  Default 256. */
 int dpg_ctx_set_icp_defer_cap(dpg_ctx* ctx, int32_t cap);
+/* The batched covariance that runs beside the pose graph (dpg_icp_batch_run with covariance, its own
+ * stream): at most n workgroups, each taking edges in turn, so the pose graph's kernels find free
+ * compute units while it runs; 0 = one workgroup per edge.  Results are identical for every n. */
+int dpg_ctx_set_cov_workgroups(dpg_ctx* ctx, int32_t n);
 /* Diagnostic: the angular ICP kernel's form (0 = the default; others are A/B candidates that must give
  * byte-identical results, tools/icp_var_ab.py). */
 int dpg_ctx_set_icp_kernel_variant(dpg_ctx* ctx, int32_t variant);

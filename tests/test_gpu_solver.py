@@ -128,3 +128,25 @@ def test_solve_paths_agree(ctx, workload, opts):
     Xe, se = _optimize(ctx, X0, F, solver=opts)
     assert se.iterations == sd.iterations
     assert np.abs(pose_diff(Xe, Xd)).max() < 1e-9
+
+
+def test_zero_initial_error_runs_no_iteration(ctx, workload):
+    """The pipelined loop takes the initial error on the device (no host round trip before the first
+    iteration): a graph already at its optimum runs no iteration, and the reported initial error
+    equals the host-decided loop's (the PCG solver reads it back first) on a real graph."""
+    from dpgslam import _abi, api
+    F = np.concatenate([api.prior_factor(0), api.between_factor(0, 1, (1.0, 0.0, 0.0), sigmas=(0.1, 0.1, 0.05))])
+    X0 = np.array([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0]])
+    for solver in (_abi.DPG_SOLVER_CHOLESKY, _abi.DPG_SOLVER_PCG):
+        X, st = _optimize(ctx, X0, F, linear_solver=solver)
+        assert st.iterations == 0 and st.initial_error == 0.0 and st.final_error == 0.0, (solver, st.iterations)
+        assert np.array_equal(X, X0)
+    w = workload("config3")
+    p = _abi.default_icp_params()
+    ctx.upload_scans(w.pts, w.offsets, 5)
+    res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
+    Fw = w.factors_with_icp(res, p)
+    X0w = w.est.astype(np.float64)
+    _, sc = _optimize(ctx, X0w, Fw)
+    _, sp = _optimize(ctx, X0w, Fw, linear_solver=_abi.DPG_SOLVER_PCG)
+    assert sc.initial_error == sp.initial_error > 0.0
