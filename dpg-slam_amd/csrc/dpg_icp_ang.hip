@@ -78,6 +78,11 @@ constexpr float kTwoPi = 6.28318530717958647692f;
 constexpr float kBucketScale = (float)kB / kTwoPi;
 constexpr float kPaSlope = 1.07f;               // bound on d(pseudo-angle)/d(angle) (max 1.0584)
 constexpr float kPaMargin = 2e-5f;              // absolute pseudo-angle margin (float error ~1e-6)
+// variant 5's window constants (window_pa): the chord bound's coefficient, the slope and the margin
+// in bucket units, each rounded up past the float error of the folded expression
+constexpr float kWinQuad = 0.8172f * 1.001f;
+constexpr float kWinSlope = kPaSlope * 1.0003f * kBucketScale;
+constexpr float kWinMargin = (kPaMargin + 2e-6f) * kBucketScale;
 
 // pseudo-angle in [0, 2 pi): atan2 approximated per octant by f(t) = t (pi/4 + 0.273 (1 - t)),
 // t = min(|x|,|y|) / max(|x|,|y|) (max error 1.5e-3 rad, slope ratio to atan in [0.98, 1.0584]);
@@ -103,6 +108,30 @@ __device__ __forceinline__ float pseudo_angle(float x, float y) {
     return phi;
 }
 
+// variant 5: the same pseudo-angle in bucket units (pseudo_angle<true> * kBucketScale with the scale
+// folded into the constants): the query side only -- within a few ulp of the build side's
+// pa * scale, far inside the windows' margin of kPaMargin * scale buckets
+constexpr float kPaA = 1.0584f * kBucketScale, kPaB = 0.273f * kBucketScale;
+constexpr float kPaQ1 = 1.5707963f * kBucketScale, kPaQ2 = 3.14159265f * kBucketScale, kPaQ4 = kTwoPi * kBucketScale;
+__device__ __forceinline__ float pseudo_angle_b(float x, float y) {
+    float mx, mn;
+    asm("v_max_f32_e64 %0, |%1|, |%2|" : "=v"(mx) : "v"(x), "v"(y));
+    asm("v_min_f32_e64 %0, |%1|, |%2|" : "=v"(mn) : "v"(x), "v"(y));
+    if (!(mx > 0.0f)) return 0.0f;
+    const float t = mn * __builtin_amdgcn_rcpf(mx);
+    const float f = t * (kPaA - kPaB * t);
+    float phi = fabsf(y) > fabsf(x) ? kPaQ1 - f : f;
+    if (x < 0.0f) phi = kPaQ2 - phi;
+    if (y < 0.0f) phi = kPaQ4 - phi;
+    return phi;
+}
+// the query's pseudo-angle as the variant's window takes it (radians; bucket units from variant 5)
+template <int VAR>
+__device__ __forceinline__ float query_angle(float x, float y) {
+    if constexpr (VAR >= 5) return pseudo_angle_b(x, y);
+    else return pseudo_angle<(VAR >= 4)>(x, y);
+}
+
 __device__ __forceinline__ int bucket_of(float pa) {
     int b = (int)floorf(pa * kBucketScale);
     return min(max(b, 0), kB - 1);
@@ -116,6 +145,11 @@ __device__ __forceinline__ int bucket_of_flr(float pa) {
 }
 template <int VAR>
 __device__ __forceinline__ int bucket_q(float pa) {
+    if constexpr (VAR >= 5) {   // pa in bucket units already
+        int b;
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(b) : "v"(pa));
+        return min(max(b, 0), kB - 1);
+    }
     if constexpr (VAR >= 2) return bucket_of_flr(pa);
     else return bucket_of(pa);
 }
@@ -419,12 +453,35 @@ template <int VAR = 1>
 __device__ __forceinline__ int window_pa(const uint16_t* bk, int n, float qx, float qy, float pq, float rad, int& start);
 template <int VAR = 1>
 __device__ __forceinline__ int window(const uint16_t* bk, int n, float qx, float qy, float rad, int& start) {
-    return window_pa<VAR>(bk, n, qx, qy, pseudo_angle<(VAR >= 4)>(qx, qy), rad, start);
+    return window_pa<VAR>(bk, n, qx, qy, query_angle<VAR>(qx, qy), rad, start);
 }
 // the same with q's pseudo-angle pq already computed (the forward search computes it once for the
 // unseeded probe and the window)
 template <int VAR>
 __device__ __forceinline__ int window_pa(const uint16_t* bk, int n, float qx, float qy, float pq, float rad, int& start) {
+    if constexpr (VAR >= 5) {
+        // variant 5: the same bound with its margins folded into three constants, in bucket units.
+        // s0 = rad / |q| is within 4e-7 of the sine; hs >= kPaSlope sn (1 + 0.8172 sn^2) scale +
+        // the absolute margins of the form below (its 1.0001 factors and the 1e-6 on the sine are
+        // inside the 1.0003 and the 2e-6), so the window is a superset of the form below's ideal
+        // one; s0 < 0.6999 keeps sn < 0.7, the chord bound's domain
+        const float s0 = rad * __builtin_amdgcn_rsqf(qx * qx + qy * qy);
+        if (!(s0 < 0.6999f)) {
+            start = 0;
+            return n;
+        }
+        const float hs = fmaf(s0 * fmaf(s0 * s0, kWinQuad, 1.0f), kWinSlope, kWinMargin);
+        const float ps = pq;   // bucket units (query_angle)
+        int blo, bhi;
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(blo) : "v"(ps - hs));
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(bhi) : "v"(ps + hs));
+        const bool wrap = blo < 0 || bhi >= kB;
+        const int s = bk[blo & (kB - 1)];
+        const int end = bk[(bhi & (kB - 1)) + 1];
+        const int cnt = wrap ? (n - s) + end : end - s;
+        start = s >= n ? s - n : s;
+        return min(cnt, n);
+    }
     const float sn = rad * __builtin_amdgcn_rsqf(qx * qx + qy * qy) * 1.0001f + 1e-6f;   // sin of the half-angle
     if (!(sn < 0.7f)) {
         start = 0;
@@ -693,7 +750,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             // ---- forward 1-NN (target index), seeded radius ----
             const bool search = live && sd >= -1;   // < -1: clearance, provably no target within r
             float rad;
-            const float pq = VAR >= 2 ? pseudo_angle<(VAR >= 4)>(qx, qy) : 0.f;   // once for the probe and the window
+            const float pq = VAR >= 2 ? query_angle<VAR>(qx, qy) : 0.f;   // once for the probe and the window
             uint64_t best = forward_init<VAR>(L, M, search ? sd : 0, qx, qy, pq, r2f, rmax, rext, r2ext, rad);
             bool pend;   // this point's forward window went to the queue
             {
@@ -828,7 +885,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 uint64_t best = 0;
                 if ((w1 & 1u) == 0u) {   // forward argmin over the window, then the reciprocal test
                     float rad;
-                    const uint64_t b0 = forward_init<VAR>(L, M, (int)(w1 >> 1) - 1, qx, qy, pseudo_angle(qx, qy), r2f, rmax, rext, r2ext, rad);
+                    const uint64_t b0 = forward_init<VAR>(L, M, (int)(w1 >> 1) - 1, qx, qy, query_angle<VAR>(qx, qy), r2f, rmax, rext, r2ext, rad);
                     const int fc = window(L.tb, M, qx, qy, rad, s);
                     best = lane == 0 ? b0 : ~0ull;
                     for (int c = lane; c < fc; c += 64) {
@@ -1184,7 +1241,10 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     for (int64_t e0 = 0; e0 < n_edges; e0 += chunk) {
         const dim3 grid((unsigned)std::min<int64_t>(chunk, n_edges - e0)), block(kT);
         const dpg_icp_edge* ed = edges_dev + e0;
-// variant 4 (default; the kernel's VAR >= 1..4 steps): hardware square roots in the
+// variant 5 (default): variant 4 with the window bound's margins folded into three constants and the
+// query pseudo-angles in bucket units (-1.6 % at config 4, byte-identical);
+// variant 1 of the diagnostic switch = variant 4, the A/B reference.
+// variant 4 (the kernel's VAR >= 1..4 steps): hardware square roots in the
 // window bounds, the candidate distance computed into the record's pad register, reciprocal beats
 // as ballots, the fit's divisions as lane-parallel vector divisions, issue priority for the
 // synchronised phases (1); the forward pseudo-angle once per point, fused floor+convert, do-while
@@ -1194,8 +1254,8 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
 #define DPG_ANG_K(P, M, V) hipLaunchKernelGGL((icp_ang_kernel<P, M, V>), grid, block, lds, s, ds, ip, idx_orig_dev, buckets_dev, ed, *kp, \
                            results_dev, trace_dev, g)
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
-        if (var == 0) DPG_ANG_K(P, M, 4);                                                                       \
-        else DPG_ANG_K(P, M, 4)
+        if (var == 1) DPG_ANG_K(P, M, 4);                                                                       \
+        else DPG_ANG_K(P, M, 5)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
             else if (ppt <= 2) DPG_ANG_LAUNCH(2, 0);

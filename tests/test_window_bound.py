@@ -68,3 +68,67 @@ def test_pseudo_angle_is_monotone_up_to_float_error():
     back = back[back > -3.0]                     # drop the wrap at 2 pi
     assert back.min() > -2e-5                    # never steps back by more than the margin
     assert abs(p[-1] - 2 * np.pi) < 1e-3 and p[0] == 0.0
+
+
+def _f32_fma(a, b, c):
+    """fmaf in float32: the float64 product of two float32 values is exact, so one rounding of the
+    float64 sum is the fused result (for these magnitudes)."""
+    return (a.astype(np.float64) * b.astype(np.float64) + np.float64(c)).astype(F)
+
+
+def test_variant5_window_contains_every_point_within_radius():
+    """The default kernel form (variant 5): the query's pseudo-angle in bucket units (the scale folded
+    into the octant polynomial's constants) and the half-width's margins folded into three
+    constants (window_pa).  Every cloud point within the radius must land, through the BUILD side's
+    bucket map floor(pseudo_angle(p) * scale), inside [floor(ps - hs), floor(ps + hs)] modulo the
+    bucket count."""
+    rng = np.random.default_rng(5)
+    kB = 1024
+    S = F(F(kB) / TWO_PI)
+    A, B = F(F(1.0584) * S), F(F(0.273) * S)
+    Q1, Q2, Q4 = F(F(1.5707963) * S), F(F(3.14159265) * S), F(TWO_PI * S)
+    QUAD, SL, MG = F(F(0.8172) * F(1.001)), F(F(1.07) * F(1.0003) * S), F((MARGIN + F(2e-6)) * S)
+    n = 600_000
+    r = np.exp(rng.uniform(np.log(0.05), np.log(30.0), n))
+    th = rng.uniform(-np.pi, np.pi, n)
+    th[::5] = rng.choice([0.0, np.pi / 2, np.pi, -np.pi / 2, np.pi / 4], n // 5 + (n % 5 > 0))[: len(th[::5])] \
+        + rng.normal(0, 1e-3, len(th[::5]))
+    qx, qy = (r * np.cos(th)).astype(F), (r * np.sin(th)).astype(F)
+    rho = np.exp(rng.uniform(np.log(1e-5), np.log(0.7), n)).astype(F)
+    d = rho * np.sqrt(rng.uniform(0, 1, n))
+    d[::3] = rho[::3] * (1 - 1e-7)
+    a = rng.uniform(-np.pi, np.pi, n)
+    px, py = (qx + d * np.cos(a)).astype(F), (qy + d * np.sin(a)).astype(F)
+    inside = (px.astype(np.float64) - qx) ** 2 + (py.astype(np.float64) - qy) ** 2 <= rho.astype(np.float64) ** 2
+    # query side (pseudo_angle_b): v_rcp_f32 with one ulp of error either way
+    ax, ay = np.abs(qx), np.abs(qy)
+    mx, mn = np.maximum(ax, ay), np.minimum(ax, ay)
+    rc = (F(1) / mx).astype(F)
+    rc = (rc * (F(1) + F(2 ** -23) * rng.choice([F(-1), F(1)], n))).astype(F)
+    t = (mn * rc).astype(F)
+    f = (t * (A - (B * t).astype(F)).astype(F)).astype(F)
+    ps = np.where(ay > ax, (Q1 - f).astype(F), f).astype(F)
+    ps = np.where(qx < 0, (Q2 - ps).astype(F), ps).astype(F)
+    ps = np.where(qy < 0, (Q4 - ps).astype(F), ps).astype(F)
+    # window_pa<5>: s0 = rad * v_rsq_f32(|q|^2) (one ulp), hs = fma(s0 * fma(s0^2, QUAD, 1), SL, MG)
+    q2 = ((qx * qx).astype(F) + (qy * qy).astype(F)).astype(F)
+    rs = (F(1) / np.sqrt(q2)).astype(F)
+    rs = (rs * (F(1) + F(2 ** -23) * rng.choice([F(-1), F(1)], n))).astype(F)
+    s0 = (rho * rs).astype(F)
+    ok = s0 < F(0.6999)
+    hs = _f32_fma((s0 * _f32_fma((s0 * s0).astype(F), QUAD, 1.0)).astype(F), SL, MG)
+    blo = np.floor((ps - hs).astype(F)).astype(np.int64)
+    bhi = np.floor((ps + hs).astype(F)).astype(np.int64)
+    # build side (angle_index_kernel): bucket_of(pseudo_angle(p)) in radians, then the scale
+    bp = np.clip(np.floor((pseudo_angle(px, py, rng) * S).astype(F)).astype(np.int64), 0, kB - 1)
+    wrap = (blo < 0) | (bhi >= kB)
+    lo, hi = blo % kB, bhi % kB
+    within = np.where(wrap, (bp >= lo) | (bp <= hi), (bp >= lo) & (bp <= hi))
+    sel = inside & ok
+    assert sel.sum() > n // 2
+    assert within[sel].all(), f"{np.sum(~within[sel])} points outside the variant-5 window"
+    # and the continuous bound itself, in bucket units, with room to spare
+    diff = np.abs(pseudo_angle(px, py, rng).astype(np.float64) * np.float64(S) - ps)
+    diff = np.minimum(diff, kB - diff)
+    worst = (diff[sel] / hs[sel]).max()
+    assert worst < 0.995, worst
