@@ -22,7 +22,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -152,7 +155,7 @@ struct dpg_ctx {
     // the pipelined GN loop (dpg_gn_pipe.h): control block, two host-mapped report slots + events
     dpg_gn_ctl* pipe_ctl = nullptr;
     dpg_gn_slot* pipe_slot = nullptr;
-    hipEvent_t pipe_ev[2] = {};
+    uint32_t pipe_loop = 0;            // loops run on this device (tags their reports)
     // multi-device forms (dpg_ctx_create_multi / _rank / _virtual): this context drives local
     // device 0 and holds the batch as the caller sees it; `peers` are full single-device contexts
     // of the other local devices.  Local device k is global rank rank0 + k of `world`.
@@ -516,7 +519,6 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     if (c->gn_ready) dpg_gn_dev_free(&c->gn);
     if (c->pipe_ctl) (void)hipFree(c->pipe_ctl);
     if (c->pipe_slot) (void)hipHostFree(c->pipe_slot);
-    for (auto& e : c->pipe_ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
     for (auto& e : c->map_ev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->stream);
@@ -1504,8 +1506,35 @@ static int ensure_pipe(dpg_ctx* q) {
     HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q->pipe_ctl), sizeof(dpg_gn_ctl)));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&q->pipe_slot), 3 * sizeof(dpg_gn_slot),   // + [2]: the initial error
                           hipHostMallocMapped | hipHostMallocCoherent));
-    for (auto& e : q->pipe_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    memset(q->pipe_slot, 0, 3 * sizeof(dpg_gn_slot));
     return DPG_OK;
+}
+
+// Wait for the report tagged `tag` in a host-mapped slot (the device stores the tag last, after a
+// system-scope fence).  Spins, then yields; every ~2 ms checks the stream: a stream that has
+// drained (or failed) without posting the tag is an error, not a hang.
+static int wait_slot(dpg_ctx* q, const dpg_gn_slot* slot, uint64_t tag) {
+    const volatile uint64_t* t = &slot->tag;
+    auto t0 = std::chrono::steady_clock::now(), last = t0;
+    for (unsigned n = 0;; ++n) {
+        if (*t == tag) {
+            std::atomic_thread_fence(std::memory_order_acquire);
+            return DPG_OK;
+        }
+        if (n < 4096) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        std::this_thread::yield();
+        const auto now = std::chrono::steady_clock::now();
+        if (now - last > std::chrono::milliseconds(2)) {
+            last = now;
+            const hipError_t e = hipStreamQuery(q->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) return fail(DPG_ERR_HIP, "GN pipeline: %s", hipGetErrorString(e));
+            if (e == hipSuccess && *t != tag) return fail(DPG_ERR_STATE, "GN pipeline: the stream drained without the report");
+            if (now - t0 > std::chrono::seconds(60)) return fail(DPG_ERR_HIP, "GN pipeline: no report after 60 s");
+        }
+    }
 }
 
 // The Gauss-Newton iterations with the decisions on the device (dpg_gn_pipe.h): iteration k + 1 is
@@ -1520,8 +1549,9 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
     for (int k = 0; k < L; ++k) {
         dpg_ctx* q = dev_ctx(c, k);
         if ((rc = ensure_pipe(q))) return rc;
+        ++q->pipe_loop;
         const double* cur_dev = q->gn.hb_own + 9 * q->gn.nnzb_upper + 3 * q->gn.n_nodes;   // the assembled error
-        if ((rc = dpg_gn_pipe_init(&q->gn, &P, q->pipe_ctl, cur_dev, q->pipe_slot + 2, q->stream)))
+        if ((rc = dpg_gn_pipe_init(&q->gn, &P, q->pipe_ctl, cur_dev, q->pipe_slot + 2, q->pipe_loop, q->stream)))
             return fail(rc, "GN pipeline launch failed");
     }
     auto issue = [&](int i) -> int {   // iteration i (1-based) reports into slot i & 1
@@ -1538,7 +1568,6 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
             HIP_TRY(hipSetDevice(q->device));
             if ((r = dpg_gn_pipe_issue_ctl(&q->gn, &P, q->pipe_ctl, q->pipe_slot + (i & 1), part, q->stream)))
                 return fail(r, "GN pipeline launch failed: %s", hipGetErrorString(hipGetLastError()));
-            HIP_TRY(hipEventRecord(q->pipe_ev[i & 1], q->stream));
         }
         return DPG_OK;
     };
@@ -1555,7 +1584,20 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
         for (int k = 0; k < L; ++k) {
             dpg_ctx* q = dev_ctx(c, k);
             HIP_TRY(hipSetDevice(q->device));
-            HIP_TRY(hipEventSynchronize(q->pipe_ev[i & 1]));
+            if (i == 1) {   // the initial error, as the device read it (pipe_init_kernel)
+                if ((rc = wait_slot(q, q->pipe_slot + 2, (uint64_t)q->pipe_loop << 32))) return rc;
+                const double e0 = static_cast<const volatile dpg_gn_slot*>(q->pipe_slot + 2)->error;
+                if (!(e0 > 0.0)) {   // nothing to do: no iteration runs (the host loop's entry test)
+                    for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
+                    S.initial_error = e0;
+                    nw = e0;
+                    dinf = 0.0;
+                    it = 0;
+                    HIP_TRY(hipSetDevice(c->device));
+                    return DPG_OK;
+                }
+            }
+            if ((rc = wait_slot(q, q->pipe_slot + (i & 1), ((uint64_t)q->pipe_loop << 32) | (uint32_t)i))) return rc;
             dpg_gn_slot o;   // host-mapped, written by the device: read through volatile
             {
                 const volatile dpg_gn_slot* v = q->pipe_slot + (i & 1);
@@ -1567,17 +1609,7 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
                 o.final_ = v->final_;
                 o.it = v->it;
             }
-            if (i == 1 && k == 0) {   // the initial error, as the device read it (pipe_init_kernel)
-                S.initial_error = static_cast<const volatile dpg_gn_slot*>(q->pipe_slot + 2)->error;
-                if (S.initial_error <= 0.0 && !o.active && o.it == 0) {   // nothing to do: no iteration ran
-                    for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
-                    nw = S.initial_error;
-                    dinf = 0.0;
-                    it = 0;
-                    HIP_TRY(hipSetDevice(c->device));
-                    return DPG_OK;
-                }
-            }
+            if (i == 1 && k == 0) S.initial_error = static_cast<const volatile dpg_gn_slot*>(q->pipe_slot + 2)->error;
             if (!o.active || o.it != i) return fail(DPG_ERR_STATE, "GN pipeline out of step (device %d, iteration %d)", k, i);
             if (k == 0) {
                 o0 = o;

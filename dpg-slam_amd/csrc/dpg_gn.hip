@@ -687,13 +687,32 @@ __device__ __forceinline__ void clear_sync(int32_t* sync, int64_t n_words, int32
     if (threadIdx.x == 0) *status = 0;
 }
 
+// a report into host memory: the fields, a system-scope fence, then the tag the host polls
+__device__ __forceinline__ void post_slot(dpg_gn_slot* slot, const dpg_gn_slot& o, uint64_t tag) {
+    volatile dpg_gn_slot* v = slot;
+    v->dinf = o.dinf;
+    v->error = o.error;
+    v->status = o.status;
+    v->reuse = o.reuse;
+    v->active = o.active;
+    v->final_ = o.final_;
+    v->it = o.it;
+    __threadfence_system();
+    v->tag = tag;
+}
+
 __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_was_chord, int32_t have_factor,
                                  double last_dinf, double prev_dinf, const double* cur_dev, dpg_gn_slot* init,
-                                 double* max_out, int32_t* sync, int64_t n_words, int32_t* status) {
+                                 double* max_out, int32_t* sync, int64_t n_words, int32_t* status, uint32_t loop) {
     clear_sync(sync, n_words, status);
     if (threadIdx.x != 0) return;
     const double cur = *cur_dev;   // the assembled initial error (the host loop reads it back first)
-    init->error = cur;
+    {
+        dpg_gn_slot o{};
+        o.error = cur;
+        post_slot(init, o, (uint64_t)loop << 32);
+    }
+    ctl->loop = loop;
     ctl->active = !(cur <= 0.0) ? 1 : 0;   // the host loop's entry test
     ctl->reuse = reuse;
     ctl->last_was_chord = last_was_chord;
@@ -715,18 +734,7 @@ __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const d
                                                         double* max_out, dpg_gn_params P, dpg_gn_slot* slot,
                                                         int32_t* sync, int64_t n_words) {
     __shared__ double red[16];
-    if (!ctl->active) {   // uniform: nothing ran this iteration
-        if (threadIdx.x == 0) {
-            dpg_gn_slot o;
-            o.reuse = ctl->reuse;
-            o.active = 0;
-            o.it = ctl->it;
-            o.final_ = 1;
-            o.dinf = o.error = o.status = 0.0;
-            *slot = o;
-        }
-        return;
-    }
+    if (!ctl->active) return;   // uniform: nothing ran this iteration, nothing to report
     double sum = 0.0;
     if (chi2_sum) {
         sum = *chi2_sum;
@@ -782,11 +790,11 @@ __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const d
         ctl->active = fin ? 0 : 1;
         *max_out = 0.0;
     }
-    *slot = o;
+    post_slot(slot, o, ((uint64_t)ctl->loop << 32) | (uint32_t)o.it);
 }
 
 extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, const double* cur_dev,
-                                dpg_gn_slot* init, void* stream) {
+                                dpg_gn_slot* init, uint32_t loop, void* stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // iteration 1's chord decision from the host bookkeeping (as dpg_gn_dev_solve_async takes it)
     const bool slow = g->last_was_chord && g->last_delta_inf > 0.1 * g->prev_delta_inf;
@@ -796,7 +804,7 @@ extern "C" int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_c
     dpg_chol_sync_dev(g->chol, &sync, &n_words);
     hipLaunchKernelGGL(pipe_init_kernel, dim3(1), dim3(1024), 0, s, ctl, reuse ? 1 : 0, g->last_was_chord, g->have_factor,
                        g->last_delta_inf, g->prev_delta_inf, cur_dev, init, g->scal3, sync, n_words,
-                       const_cast<int32_t*>(dpg_chol_status_dev(g->chol)));
+                       const_cast<int32_t*>(dpg_chol_status_dev(g->chol)), loop);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

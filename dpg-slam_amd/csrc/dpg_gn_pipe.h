@@ -24,13 +24,18 @@ struct dpg_gn_dev;
 // control block on the device
 struct dpg_gn_ctl {
     int32_t active, reuse;          // the gate of the next iteration (gate_off in dpg_chol.hip)
-    int32_t last_was_chord, have_factor, it, pad[3];
+    int32_t last_was_chord, have_factor, it;
+    uint32_t loop;                  // the host's loop number (tags the reports of this loop)
+    int32_t pad[2];
     double last_dinf, prev_dinf, cur_error, pad2;
 };
-// what the control kernel of iteration k reports (written into host memory)
+// what the control kernel of an ACTIVE iteration k reports (written into host memory; a gated-off
+// iteration writes nothing).  The host polls `tag` = loop << 32 | k, stored after the other fields
+// and a system-scope fence: no event (and no end-of-kernel system release per iteration) is needed
 struct dpg_gn_slot {
     double dinf, error, status;
     int32_t reuse, active, final_, it;
+    uint64_t tag;
 };
 
 // X_v <- X_v * Pose2(d) (Pose2 retraction); returns max |d|, NaN as +inf.  Shared by the
@@ -63,8 +68,9 @@ void dpg_chol_sync_dev(void* chol, int32_t** sync, int64_t* n_words);
 // the initial error comes from the device (cur_dev: the assembled chi2 word, all-reduced on the
 // multi-device forms) and is reported in init->error; a loop whose initial error is not > 0 runs
 // no iteration (iteration 1 reports active = 0)
+// (init->tag = loop << 32 once written; the reports of iteration k carry loop << 32 | k)
 int dpg_gn_pipe_init(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, const double* cur_dev, dpg_gn_slot* init,
-                     void* stream);
+                     uint32_t loop, void* stream);
 // enqueue one gated iteration: solve, retract, re-linearize + assemble into g->hb_own, control
 // kernel (reports into slot, a host-mapped pointer)
 int dpg_gn_pipe_issue(dpg_gn_dev* g, const dpg_gn_params* gp, dpg_gn_ctl* ctl, dpg_gn_slot* slot, void* stream);
