@@ -1831,8 +1831,10 @@ double wall_ms() {
 // host-side structures of one build (kept between builds: the incremental graph rebuilds per update)
 struct CholHost {
     struct Blk { int32_t row, u, tr; };   // an upper block of H in its column's bucket
+    struct Blk4 { int32_t row, col, u, tr; };
     std::vector<int64_t> colptr;
     std::vector<Blk> ent;
+    std::vector<Blk4> byrow;
     std::vector<int32_t> lidx, lstamp;
     std::vector<int64_t> om_ptr, om_cur;
     std::vector<OEnt> omap;
@@ -1893,25 +1895,26 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     std::vector<CholHost::Blk>& ent = H.ent;
     ent.resize((size_t)colptr[(size_t)n]);
     {
-        std::vector<int64_t>& cur = H.om_cur;
-        cur.assign(colptr.begin(), colptr.end() - 1);
-        for (int64_t p = 0; p < n; ++p) ent[(size_t)cur[(size_t)p]++] = CholHost::Blk{(int32_t)p, S.perm[(size_t)p], 0};
+        // two counting sorts: the blocks by row (the pairs' later position; the diagonal block is
+        // its column's first row), then stably into their column buckets -- each bucket comes out
+        // in ascending row order without a per-bucket sort
+        std::vector<int64_t>& rptr = H.om_cur;
+        rptr.assign((size_t)n + 1, 0);
+        for (int64_t p = 0; p < n; ++p) rptr[(size_t)p + 1] = 1;
+        for (int64_t q = 0; q < n_pairs; ++q)
+            rptr[(size_t)std::max(S.pos[(size_t)pair_lo[q]], S.pos[(size_t)pair_hi[q]]) + 1]++;
+        for (int64_t p = 0; p < n; ++p) rptr[(size_t)p + 1] += rptr[(size_t)p];
+        std::vector<CholHost::Blk4>& byrow = H.byrow;
+        byrow.resize(ent.size());
+        for (int64_t p = 0; p < n; ++p) byrow[(size_t)rptr[(size_t)p]++] = CholHost::Blk4{(int32_t)p, (int32_t)p, S.perm[(size_t)p], 0};
         for (int64_t q = 0; q < n_pairs; ++q) {
             const int32_t plo = S.pos[(size_t)pair_lo[q]], phi = S.pos[(size_t)pair_hi[q]];
             // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
-            ent[(size_t)cur[(size_t)std::min(plo, phi)]++] =
-                CholHost::Blk{std::max(plo, phi), (int32_t)(n + q), plo > phi ? 0 : 1};
+            const int32_t r = std::max(plo, phi);
+            byrow[(size_t)rptr[(size_t)r]++] = CholHost::Blk4{r, std::min(plo, phi), (int32_t)(n + q), plo > phi ? 0 : 1};
         }
-        for (int64_t p = 0; p < n; ++p) {   // insertion sort by row: buckets hold a few blocks
-            CholHost::Blk* b = ent.data() + colptr[(size_t)p];
-            const int64_t m = colptr[(size_t)p + 1] - colptr[(size_t)p];
-            for (int64_t i = 1; i < m; ++i) {
-                const CholHost::Blk x = b[i];
-                int64_t j = i - 1;
-                while (j >= 0 && b[j].row > x.row) { b[j + 1] = b[j]; --j; }
-                b[j + 1] = x;
-            }
-        }
+        rptr.assign(colptr.begin(), colptr.end() - 1);   // column cursors
+        for (const CholHost::Blk4& b : byrow) ent[(size_t)rptr[(size_t)b.col]++] = CholHost::Blk{b.row, b.u, b.tr};
     }
     PLAN_T(1);
     std::vector<int64_t>& om_ptr = H.om_ptr;

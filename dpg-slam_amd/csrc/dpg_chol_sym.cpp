@@ -13,6 +13,7 @@
 //      -> front positions, child update matrix rows -> parent front rows
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -603,8 +604,21 @@ static double csr_now() {
 #define CSR_T(k) do { } while (0)
 #endif
 
+static int sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow, const dpg_chol_opts* opts,
+                        dpg_chol_sym* S, bool exact);
+
 int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow,
                           const dpg_chol_opts* opts, dpg_chol_sym* S) {
+    return sym_from_csr(n, perm, cp, prow, opts, S, false);
+}
+
+// exact = the patterns are the exact structure of L (the incremental state: a fresh elimination
+// extended by exact fill updates).  Then every column's pattern minus its parent lies in the
+// parent's pattern (the elimination-tree property), and a supernode is a parent chain, so the row
+// set of a supernode -- the union of its columns' rows past its last column -- is the last column's
+// pattern: no merge, no inclusion test.  Built with DPG_PLAN_VERIFY the union is checked anyway.
+static int sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const int32_t* prow, const dpg_chol_opts* opts,
+                        dpg_chol_sym* S, bool exact) {
     if (n <= 0) return -1;
     CSR_T(0);
     auto psize = [&](int64_t p) { return cp[p + 1] - cp[p]; };
@@ -673,10 +687,24 @@ int dpg_chol_sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, con
         // sorted union of the columns' rows >= c1, merged from the last column down (the last
         // column's rows all qualify; in a fundamental supernode every merge adds nothing)
         rowbuf.assign(prow + cp[c1 - 1], prow + cp[c1]);
+#ifndef DPG_PLAN_VERIFY
+        if (exact) {
+            S->sn_rows.insert(S->sn_rows.end(), rowbuf.begin(), rowbuf.end());
+            S->sn_rows_ptr[(size_t)s + 1] = (int64_t)S->sn_rows.size();
+            if (!rowbuf.empty()) S->sn_parent[(size_t)s] = S->sn_of[(size_t)rowbuf[0]];
+            continue;
+        }
+#endif
         for (int32_t c = c1 - 2; c >= c0; --c) {
             const int32_t* b = std::lower_bound(prow + cp[c], prow + cp[c + 1], c1);
             const int32_t* e = prow + cp[c + 1];
             if (std::includes(rowbuf.begin(), rowbuf.end(), b, e)) continue;
+#ifdef DPG_PLAN_VERIFY
+            if (exact) {
+                fprintf(stderr, "exact patterns: column %d's rows past its supernode are not in the last column's\n", c);
+                abort();
+            }
+#endif
             mergebuf.resize(rowbuf.size() + (size_t)(e - b));
             mergebuf.resize((size_t)(std::set_union(rowbuf.begin(), rowbuf.end(), b, e, mergebuf.begin()) - mergebuf.begin()));
             rowbuf.swap(mergebuf);
@@ -960,5 +988,5 @@ int dpg_incsym_derive(dpg_chol_incsym* I, const dpg_chol_opts* opts, dpg_chol_sy
         I->added.clear();
     }
     if (I->cp[(size_t)n] != I->nnz) return -3;
-    return dpg_chol_sym_from_csr(n, I->perm.data(), I->cp.data(), I->rows.data(), opts, S);
+    return sym_from_csr(n, I->perm.data(), I->cp.data(), I->rows.data(), opts, S, true);
 }
