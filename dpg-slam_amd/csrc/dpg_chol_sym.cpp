@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <functional>
+#include <future>
 #include <queue>
 #include <vector>
 
@@ -566,19 +567,29 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
     }
     struct Cand { int32_t starts, bal, score; };
     static const Cand cands[] = {{0, 5, 0}, {8, 4, 2}};
-    double best = -1.0;
-    for (int k = 0; k < 2; ++k) {
-        if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, true,
-                                  perm, pat))
-            return -1;
+    struct Res {
+        int rc = 0;
+        double cp = 0.0;
         dpg_chol_sym T;
-        if (dpg_chol_sym_from_patterns(n, perm, pat, opts, &T)) return -1;
-        const double cp = dpg_chol_critical_path_us(T);
-        if (best < 0.0 || cp < best) {
-            best = cp;
-            *S = std::move(T);
-        }
-    }
+    };
+    // both candidates at once (thread-local scratch); the first kept unless the second is shorter
+    auto run = [&](int k) {
+        Res r;
+        std::vector<int32_t> pm;
+        std::vector<std::vector<int32_t>> pt;
+        if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, true,
+                                  pm, pt) ||
+            dpg_chol_sym_from_patterns(n, pm, pt, opts, &r.T))
+            r.rc = -1;
+        else
+            r.cp = dpg_chol_critical_path_us(r.T);
+        return r;
+    };
+    std::future<Res> second = std::async(std::launch::async, run, 1);
+    Res r0 = run(0);
+    Res r1 = second.get();
+    if (r0.rc || r1.rc) return -1;
+    *S = std::move(r1.cp < r0.cp ? r1.T : r0.T);
     return 0;
 }
 
@@ -850,26 +861,37 @@ int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, 
     // p50 2.14 -> 1.96 ms, 456 -> 487 nodes/s; config 5 413 vs 411 nodes/s
     // (profiles/r03/v24_incbg_ab.txt).  DPG_ORDER_ND: round 2's rule alone; DPG_ORDER_MD: minimum
     // degree.
+    // The two candidates are independent (their scratch is thread-local): the second is computed on
+    // a thread of its own beside the first (a sweep's fresh order at 10 k nodes is on its caller's
+    // path); the first is kept unless the second's estimate is strictly shorter, as in sequence.
     const int32_t order = opts ? opts->order : 0;
     int rc = 0;
     if (order == 0 && n >= 256) {
         const dpg_chol_opts o = opts ? *opts : dpg_chol_opts{};
-        double best = -1.0;
-        std::vector<int32_t> pm;
-        std::vector<std::vector<int32_t>> pt;
-        for (int k = 0; k < 2; ++k) {
-            rc = k == 0 ? dpg_chol_order(n, pair_lo, pair_hi, n_pairs, pm, pt)
-                        : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, pm, pt);
-            if (rc) return -1;
-            dpg_chol_sym T;
-            if (dpg_chol_sym_from_patterns(n, pm, pt, &o, &T)) return -1;
-            const double cp = dpg_chol_critical_path_us(T);
-            if (best < 0.0 || cp < best) {
-                best = cp;
-                perm.swap(pm);
-                pat.swap(pt);
+        struct Cand {
+            int rc = 0;
+            double cp = 0.0;
+            std::vector<int32_t> pm;
+            std::vector<std::vector<int32_t>> pt;
+        };
+        auto run = [&](int k) {
+            Cand c;
+            c.rc = k == 0 ? dpg_chol_order(n, pair_lo, pair_hi, n_pairs, c.pm, c.pt)
+                          : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, c.pm, c.pt);
+            if (c.rc == 0) {
+                dpg_chol_sym T;
+                if (dpg_chol_sym_from_patterns(n, c.pm, c.pt, &o, &T)) c.rc = -1;
+                else c.cp = dpg_chol_critical_path_us(T);
             }
-        }
+            return c;
+        };
+        std::future<Cand> second = std::async(std::launch::async, run, 1);
+        Cand c0 = run(0);
+        Cand c1 = second.get();
+        if (c0.rc || c1.rc) return -1;
+        Cand& b = c1.cp < c0.cp ? c1 : c0;
+        perm.swap(b.pm);
+        pat.swap(b.pt);
     } else {
         rc = dpg_chol_order(n, pair_lo, pair_hi, n_pairs, perm, pat, order == 1);
     }

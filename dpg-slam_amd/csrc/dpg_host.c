@@ -147,6 +147,21 @@ int dpg_odometry_factor(const float odom_prev[3], const float odom_cur[3], int32
     return DPG_OK;
 }
 
+int dpg_odometry_factors(const float* odom, int64_t n_odom, const int32_t* i_prev, const int32_t* i_cur, int64_t n,
+                         float transl_from_transl, float transl_from_rot, float rot_from_transl, float rot_from_rot,
+                         dpg_factor* out) {
+    if (n < 0 || (n > 0 && (!odom || !i_prev || !i_cur || !out))) return DPG_ERR_ARG;
+    int rc = DPG_OK;
+    for (int64_t k = 0; k < n; ++k) {
+        const int32_t a = i_prev[k], b = i_cur[k];
+        if (a < 0 || b < 0 || a >= n_odom || b >= n_odom) return DPG_ERR_ARG;
+        const int r = dpg_odometry_factor(odom + 3 * (int64_t)a, odom + 3 * (int64_t)b, a, b, transl_from_transl,
+                                          transl_from_rot, rot_from_transl, rot_from_rot, out + k);
+        if (r && rc == DPG_OK) rc = r;
+    }
+    return rc;
+}
+
 /* R9: ICP BetweenFactor (addObservationConstraint, dpg_slam.cc:331-338); the covariance is the
  * constant diagonal of calculate_ICP_COV, which GTSAM's smart Gaussian::Covariance reduces to a
  * Diagonal model with precisions 1/variance. */

@@ -250,6 +250,8 @@ SIGNATURES = {
     "dpg_inverse_transform_point": (None, [F32P, F32P, F32P]),
     "dpg_transform_point": (None, [F32P, F32P, F32P]),
     "dpg_icp_guess": (None, [F32P, F32P, F32P]),
+    "dpg_odometry_factors": (C.c_int, [F32P, C.c_int64, I32P, I32P, C.c_int64, C.c_float, C.c_float, C.c_float,
+                                      C.c_float, C.c_void_p]),
     "dpg_odometry_factor": (C.c_int, [F32P, F32P, C.c_int32, C.c_int32, C.c_float, C.c_float, C.c_float,
                                       C.c_float, C.POINTER(Factor)]),
     "dpg_icp_factor": (None, [C.POINTER(IcpResult), C.c_int32, C.c_int32, C.POINTER(IcpParams),

@@ -92,6 +92,30 @@ def odometry_factor(odom_prev, odom_cur, i_prev, i_cur, motion=(0.4, 0.4, 0.4, 0
     return f
 
 
+def odometry_factors(odom: np.ndarray, i_prev, i_cur, motion=(0.4, 0.4, 0.4, 0.4)) -> np.ndarray:
+    """odometry_factor for n pairs in one call (dpg_odometry_factors): factor k between odom[i_prev[k]]
+    and odom[i_cur[k]] (odom [n_odom, 3] float32); the same factors as n odometry_factor calls."""
+    o = _f32(odom).reshape(-1, 3)
+    a = np.ascontiguousarray(i_prev, np.int32)
+    b = np.ascontiguousarray(i_cur, np.int32)
+    out = np.zeros(len(a), FACTOR_DTYPE)
+    if len(a):
+        check(lib().dpg_odometry_factors(ptr(o, C.c_float), len(o), ptr(a, C.c_int32), ptr(b, C.c_int32), len(a),
+                                         *motion, vptr(out)), "dpg_odometry_factors")
+    return out
+
+
+def prior_factors(nodes, sigmas=(0.2, 0.2, 0.15)) -> np.ndarray:
+    """prior_factor(node, (0, 0, 0), sigmas) for every node of `nodes`."""
+    n = np.asarray(nodes, np.int32).reshape(-1)
+    f = np.zeros(len(n), FACTOR_DTYPE)
+    f["kind"] = _abi.DPG_FACTOR_PRIOR
+    f["i"] = n
+    s = np.asarray(sigmas, np.float32).astype(np.float64)
+    f["info"] = 1.0 / (s * s)
+    return f
+
+
 def prior_factor(node: int, pose=(0.0, 0.0, 0.0), sigmas=(0.2, 0.2, 0.15)) -> np.ndarray:
     """PriorFactor<Pose2> with Diagonal::Sigmas (dpg_slam.cc:44-49); sigmas are the float
     parameters new_pass_{x,y,theta}_std_dev_ (parameters.h:264-274) widened to double."""

@@ -15,6 +15,8 @@ from __future__ import annotations
 import ctypes as C
 import math
 
+import time
+
 import numpy as np
 
 from . import _abi, api
@@ -73,7 +75,7 @@ class GpuBackend:
         """reoptimize's new ISAM2 + new graph and its one update (dpg_slam.cc:36-39,111-119); the
         scan store holds every node's cloud (icp_batch uploaded them)."""
         self.inc.reset()
-        self.inc.update(np.asarray(est, np.float64), F)
+        self.last_rebuild = self.inc.update(np.asarray(est, np.float64), F)
         return self.inc.poses()
 
     def store(self, ranges, geom, offsets, params):
@@ -193,21 +195,29 @@ class DpgSLAM:
         V = len(self.poses)
         if V == 0:
             return
+        t0 = time.perf_counter()
         est = self.poses.copy()
         passes = self.node_pass
         lc = self.be.candidates(est, passes, float(self.within), float(self.across))
+        t1 = time.perf_counter()
         succ = np.stack([np.arange(V - 1), np.arange(1, V)], 1).astype(np.int32)
         edges = np.concatenate([succ, np.asarray(lc, np.int32).reshape(-1, 2)], 0)
         res = None
         if len(edges):
             res = self.be.icp_batch(self._clouds, edges, est, self.icp_params)
-        F, cur = [], None
-        for i in range(V):
-            if i == 0 or passes[i] != cur:
-                F.append(api.prior_factor(i, sigmas=self.prior_sigmas))
-                cur = passes[i]
-            elif self.odometry_constraints:
-                F.append(self._odometry_factor(self.odom_only[i - 1], self.odom_only[i], i - 1, i))
+        t2 = time.perf_counter()
+        # per node, in node order: the pass's prior on its first node, else the odometry Between
+        # from the previous node (dpg_slam.cc:41-75) -- built for all nodes at once
+        pv = np.asarray(passes)
+        start = np.ones(V, bool)
+        start[1:] = pv[1:] != pv[:-1]
+        keep_n = start | bool(self.odometry_constraints)
+        Fn = np.zeros(V, FACTOR_DTYPE)
+        Fn[start] = api.prior_factors(np.nonzero(start)[0], sigmas=self.prior_sigmas)
+        odo = np.nonzero(~start)[0] if self.odometry_constraints else np.zeros(0, np.int64)
+        if len(odo):
+            Fn[odo] = api.odometry_factors(np.asarray(self.odom_only, f32), odo - 1, odo, self.motion)
+        F = [Fn[keep_n]]
         if len(edges):
             # addObservationConstraint per aligned pair (dpg_icp_factor, vectorised): the successive
             # pairs always, a loop closure when its alignment converged (dpg_slam.cc:85-104)
@@ -224,8 +234,16 @@ class DpgSLAM:
         F = np.concatenate([np.asarray(f, FACTOR_DTYPE).reshape(-1) for f in F])
         self.factors = F
         self.n_factors = len(F)
+        t3 = time.perf_counter()
         X = self.be.rebuild_graph(est.astype(np.float64), F)
         self.poses = np.asarray(X, f32).reshape(-1, 3)
+        # the sweep's phases (ms): candidate search, the batched ICP, the factor list, the new graph's update
+        self.last_sweep_ms = {"candidates": (t1 - t0) * 1e3, "icp": (t2 - t1) * 1e3, "factors": (t3 - t2) * 1e3,
+                              "update": (time.perf_counter() - t3) * 1e3, "edges": int(len(edges))}
+        st = getattr(self.be, "last_rebuild", None)
+        if st is not None:
+            self.last_sweep_ms.update(update_symbolic=st.ms_symbolic, update_numeric=st.ms_numeric,
+                                      gn_iterations=int(st.gn_iterations))
 
     # ------------------------------------------------------------------ internals
     def _odometry_factor(self, prev, cur, i, j):

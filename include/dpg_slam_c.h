@@ -233,6 +233,12 @@ int dpg_odometry_factor(const float odom_prev[3], const float odom_cur[3], int32
                         float rot_from_rot, dpg_factor* out);
 void dpg_icp_factor(const dpg_icp_result* r, int32_t from_node, int32_t to_node,
                     const dpg_icp_params* p, dpg_factor* out);
+/* dpg_odometry_factor over n pairs: factor k between odometry poses odom[i_prev[k]] and
+ * odom[i_cur[k]] (odom: [n_odom][3]), into out[k] -- the reference's per-node loop of reoptimize
+ * (dpg_slam.cc:53-75) in one call; returns the first error (out[k] of a failed pair unset). */
+int dpg_odometry_factors(const float* odom, int64_t n_odom, const int32_t* i_prev, const int32_t* i_cur, int64_t n,
+                         float transl_from_transl, float transl_from_rot, float rot_from_transl, float rot_from_rot,
+                         dpg_factor* out);
 
 /* ---- synthetic workload generator (seeded, deterministic) ---- */
 /* World: axis-aligned rooms + random boxes in [0, world_size]^2; segments [n][4] (x0,y0,x1,y1). */

@@ -103,3 +103,25 @@ def test_odometry_factor_noise_model():
     assert (f.i, f.j) == (3, 4)
     assert f.info[0] == 1.0 / (float(st) * float(st)) and f.info[2] == f.info[0]
     assert abs(f.z[2] - 0.1) < 1e-7
+
+
+def test_batched_factor_builders_equal_per_factor_calls():
+    """reoptimize builds its prior / odometry factors for all nodes at once (dpg_odometry_factors,
+    api.prior_factors): byte-identical to the per-node calls of the reference's loop
+    (dpg_slam.cc:41-75), in node order; a zero-motion pair fails the batch as it fails the single call."""
+    from dpgslam import _abi, api
+    from dpgslam._abi import FACTOR_DTYPE
+    rng = np.random.default_rng(7)
+    odom = np.cumsum(rng.normal(0, 0.3, (50, 3)), 0).astype(np.float32)
+    a = np.arange(0, 49, dtype=np.int32)
+    b = a + 1
+    motion = (0.4, 0.3, 0.2, 0.1)
+    Fb = api.odometry_factors(odom, a, b, motion)
+    for k in range(len(a)):
+        f = np.frombuffer(bytes(api.odometry_factor(odom[a[k]], odom[b[k]], int(a[k]), int(b[k]), motion)), FACTOR_DTYPE)
+        assert Fb[k].tobytes() == f.tobytes(), k
+    Pb = api.prior_factors([0, 7, 30], sigmas=(0.2, 0.25, 0.15))
+    for k, n in enumerate([0, 7, 30]):
+        assert Pb[k].tobytes() == api.prior_factor(n, sigmas=(0.2, 0.25, 0.15)).tobytes()
+    with pytest.raises(_abi.DpgError):
+        api.odometry_factors(np.zeros((2, 3), np.float32), [0], [1], motion)
