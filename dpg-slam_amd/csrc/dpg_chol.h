@@ -88,9 +88,11 @@ int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, cons
                      const dpg_chol_opts* opts = nullptr);
 // the two halves of dpg_incsym_reset: the order and column patterns of the graph (a pure function
 // of its arguments, safe on a worker thread), and the state built from them (perm, pat consumed)
+// (concurrent: the two candidates of the automatic rule on two threads -- for callers waiting on
+// the order; the incremental graph's ahead-of-time order on its worker thread runs them in turn)
 int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                      std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat,
-                     const dpg_chol_opts* opts = nullptr);
+                     const dpg_chol_opts* opts = nullptr, bool concurrent = false);
 void dpg_incsym_init(dpg_chol_incsym* I, int64_t n, std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat);
 // nodes n .. n + k - 1 appended at the end of the order
 void dpg_incsym_append(dpg_chol_incsym* I, int64_t k);

@@ -852,7 +852,7 @@ inline void for_rows_after(const dpg_chol_incsym* I, int64_t j, int64_t after, F
 
 int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                      std::vector<int32_t>& perm, std::vector<std::vector<int32_t>>& pat,
-                     const dpg_chol_opts* opts) {
+                     const dpg_chol_opts* opts, bool concurrent) {
     // The batch analysis's pick (opts->order DPG_ORDER_AUTO) -- round 2's separator rule or the
     // 8-start search with cover separators, each carried through the supernodal analysis under the
     // incremental solver's options, the shorter critical-path estimate kept.  It costs two orders
@@ -861,9 +861,10 @@ int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, 
     // p50 2.14 -> 1.96 ms, 456 -> 487 nodes/s; config 5 413 vs 411 nodes/s
     // (profiles/r03/v24_incbg_ab.txt).  DPG_ORDER_ND: round 2's rule alone; DPG_ORDER_MD: minimum
     // degree.
-    // The two candidates are independent (their scratch is thread-local): the second is computed on
-    // a thread of its own beside the first (a sweep's fresh order at 10 k nodes is on its caller's
-    // path); the first is kept unless the second's estimate is strictly shorter, as in sequence.
+    // The two candidates are independent (their scratch is thread-local): with `concurrent` the
+    // second is computed on a thread of its own beside the first (a sweep's fresh order at 10 k
+    // nodes is on its caller's path); the first is kept unless the second's estimate is strictly
+    // shorter.
     const int32_t order = opts ? opts->order : 0;
     int rc = 0;
     if (order == 0 && n >= 256) {
@@ -885,7 +886,7 @@ int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, 
             }
             return c;
         };
-        std::future<Cand> second = std::async(std::launch::async, run, 1);
+        std::future<Cand> second = std::async(concurrent ? std::launch::async : std::launch::deferred, run, 1);
         Cand c0 = run(0);
         Cand c1 = second.get();
         if (c0.rc || c1.rc) return -1;
@@ -902,7 +903,7 @@ int dpg_incsym_reset(dpg_chol_incsym* I, int64_t n, const int32_t* pair_lo, cons
                      const dpg_chol_opts* opts) {
     std::vector<int32_t> perm;
     std::vector<std::vector<int32_t>> pat;
-    if (dpg_incsym_order(n, pair_lo, pair_hi, n_pairs, perm, pat, opts)) return -1;
+    if (dpg_incsym_order(n, pair_lo, pair_hi, n_pairs, perm, pat, opts, true)) return -1;
     dpg_incsym_init(I, n, perm, pat);
     return 0;
 }
