@@ -604,6 +604,8 @@ def main():
     ap.add_argument("--virtual", type=int, default=0,
                     help="K > 0: K virtual devices on one card (dpg_ctx_create_virtual) -- a rehearsal of "
                          "the sharded paths, not a scaling number")
+    ap.add_argument("--kernel-variant", type=int, default=0,
+                    help="diagnostic A/B: the angular ICP kernel's form (dpg_ctx_set_icp_kernel_variant; 0 = default)")
     ap.add_argument("--schedule", default="measured", choices=["measured", "caller"],
                     help="batched ICP dispatch (dpg_ctx_set_icp_schedule); results are identical")
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
@@ -679,6 +681,8 @@ def main():
     n_gpus = {"single": 1, "multi": args.gpus, "rank": world, "virtual": 1}[mode]
     ctx.set_icp_variant(args.icp_variant)
     ctx.set_icp_schedule(args.schedule)
+    if args.kernel_variant:
+        ctx.set_icp_kernel_variant(args.kernel_variant)
     ctx.upload_scans(w.pts, w.offsets, params.downsample_icp_points_ratio)
     ctx.icp_prepare(w.edges, w.est, params)   # ALL edges: a multi-device context shards them itself
     F = w.factors_placeholder()
