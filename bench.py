@@ -229,6 +229,25 @@ def main_incremental(args):
 DPG_BUCKETS = ((0, 1), (1, 10), (10, 50), (50, 1 << 30))
 
 
+def node_tail(rows):
+    """Where the slowest 10 % of the nodes spend their time, against the others: mean wall, node ICP,
+    update (symbolic / numeric), executeDPG ms, and the share of updates that reordered, ICP edges
+    and submap candidates (per-node rows of the dynamic run)."""
+    if not rows:
+        return None
+    a = np.asarray(rows, np.float64)
+    cut = np.percentile(a[:, 0], 90)
+    out = {}
+    for name, m in (("slowest_10pct", a[:, 0] >= cut), ("others", a[:, 0] < cut)):
+        b = a[m]
+        out[name] = {"nodes": int(len(b)), "wall_ms": float(b[:, 0].mean()), "icp_ms": float(b[:, 1].mean()),
+                     "update_ms": float(b[:, 2].mean()), "symbolic_ms": float(b[:, 3].mean()),
+                     "numeric_ms": float(b[:, 4].mean()), "reordered_share": float(b[:, 5].mean()),
+                     "icp_edges": float(b[:, 6].mean()), "dpg_ms": float(b[:, 7].mean()),
+                     "dpg_candidates": float(b[:, 8].mean())}
+    return out
+
+
 def main_dynamic(args):
     """--workload dynamic: BASELINE config 5 ("10k-node graph with DPG node removal +
     re-linearisation sweep") run through DpgSLAM (dpgslam/slam.py on the GPU backend): 4 passes x
@@ -263,6 +282,7 @@ def main_dynamic(args):
     if do_cpu:
         from oracle import oracle as O
     node_ms, add_icp_ms, add_upd_ms, dpg, add_split, prof = [], [], [], [], [], []
+    node_rows = []   # per node: wall, icp, update, symbolic, numeric, reordered, icp edges, executeDPG ms, candidates
     sweeps, active_end, replay_s, pass_tot = [], [], 0.0, {}
     import ctypes as C
     L, pbuf = _abi.lib(), (C.c_double * 12)()
@@ -296,6 +316,10 @@ def main_dynamic(args):
             add_icp_ms.append(la.ms_icp)
             add_upd_ms.append(la.update.ms_total)
             add_split.append((la.update.ms_symbolic, la.update.ms_numeric))
+            dd = slam.last_dpg if p >= 1 else None
+            node_rows.append((dt, la.ms_icp, la.update.ms_total, la.update.ms_symbolic, la.update.ms_numeric,
+                              int(la.update.reordered), int(la.n_icp_edges), float(dd.ms_total) if dd is not None else 0.0,
+                              int(dd.n_candidates) if dd is not None else 0))
             if p == P - 1:   # the last pass: where the symbolic host time goes
                 L.dpg_inc_last_profile(C.c_void_p(slam.be.inc.handle), pbuf, 12)
                 prof.append(list(pbuf)[:11])
@@ -390,6 +414,7 @@ def main_dynamic(args):
                                f"boxes), DpgSLAM defaults", "nodes": V},
         "data": "synthetic (seeded ray-cast building, boxes added/removed between passes, noisy odometry)",
         "wall_s": wall, "nodes_per_pass": [int(np.sum(created == q)) for q in range(P)],
+        "node_tail": node_tail(node_rows),
         "node_ms": {"p50": float(np.median(node_ms)), "p90": float(np.percentile(node_ms, 90)),
                     "mean": float(np.mean(node_ms)), "icp_mean": float(np.mean(add_icp_ms)),
                     "update_mean": float(np.mean(add_upd_ms)),

@@ -577,6 +577,9 @@ struct dpg_dpg {
     std::vector<uint8_t> active_h;    // host mirror of the node activity
     std::vector<float> h_pose;        // [V][3] pose bits the cached frames were computed from (NaN: none)
     float* h_frames = nullptr;        // [V][8] cached node frames, pinned (see upload_frames)
+    int64_t h_cap = 0;                // nodes the pinned mirrors (h_frames, h_act) hold
+    unsigned char* h_app = nullptr;   // pinned staging of dpg_dpg_append's uploads
+    size_t app_cap = 0;
     // pinned staging of the per-call inputs/outputs: one H2D copy of [chain 16 | slot 16 | rast 16 |
     // chain frames 128 | candidates], one D2H of the node activity and the commit flags
     int32_t* h_stage = nullptr;
@@ -747,6 +750,7 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
         hipHostMalloc(reinterpret_cast<void**>(&d->h_commit), sizeof(int32_t) * 16, hipHostMallocDefault) != hipSuccess)
         return bad("hipHostMalloc failed");
     memset(d->h_frames, 0, sizeof(float) * 8 * V);
+    d->h_cap = V;
     hipStream_t s = d->s;
     if (hipMemcpyAsync(d->d_off.p, off, sizeof(int64_t) * (V + 1), hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(d->d_plaser.p, pl.data(), sizeof(float2) * d->B, hipMemcpyHostToDevice, s) != hipSuccess ||
@@ -762,6 +766,12 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
     return d;
 }
 
+// One node per call on the DpgSLAM path: the cost is per call, so nothing here is O(V) -- the
+// device arrays and the pinned mirrors grow by 1.5x with their contents kept, the new nodes' data
+// are built straight into one pinned staging block and go up from it (only the new offsets, not
+// the whole offset array), and the stream is not waited on at the end (the next call, or any
+// executeDPG, is queued behind these copies; the staging block is reused only after the stream
+// synchronisation that opens the next call).
 int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const float* ranges, const float* geom) {
     if (!d || n_new < 0 || (n_new > 0 && (!off_rel || !ranges || !geom))) return dpg_set_error(DPG_ERR_ARG, "bad arguments");
     if (n_new == 0) return DPG_OK;
@@ -769,40 +779,69 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
     hipStream_t s = d->s;
     DTRY(hipStreamSynchronize(s));
     const int64_t V0 = d->V, B0 = d->B, V1 = V0 + n_new, nb_new = off_rel[n_new] - off_rel[0];
-    std::vector<float2> pl((size_t)nb_new);
-    std::vector<uint8_t> lab((size_t)nb_new), sec((size_t)nb_new);
-    std::vector<float> gm((size_t)(4 * n_new));
-    std::vector<int64_t> off(d->off);
-    // the new nodes' largest ranges and the beam maximum are committed to d only after every
-    // check, allocation and copy below succeeded (as off and V)
-    std::vector<float> rmax_new;
     int32_t max_beams = d->max_beams;
     for (int64_t k = 0; k < n_new; ++k) {
         const int64_t nb = off_rel[k + 1] - off_rel[k];
         if (nb < 2 || nb > 65535) return dpg_set_error(DPG_ERR_SIZE, "beams per scan must be in [2, 65535]");
+        max_beams = std::max<int32_t>(max_beams, (int32_t)nb);
+    }
+    // staging layout (16-B aligned parts): offsets [n_new] i64 | plaser [nb] float2 | range [nb] f32 |
+    // geom [n_new] float4 | sect [n_new] u32 | active [n_new] u32 | label [nb] u8 | sector [nb] u8
+    auto al = [](size_t x) { return (x + 15) & ~size_t(15); };
+    const size_t o_off = 0, o_pl = al(o_off + 8 * (size_t)n_new), o_rg = al(o_pl + 8 * (size_t)nb_new),
+                 o_gm = al(o_rg + 4 * (size_t)nb_new), o_sc = al(o_gm + 16 * (size_t)n_new),
+                 o_ac = al(o_sc + 4 * (size_t)n_new), o_lb = al(o_ac + 4 * (size_t)n_new), o_sr = al(o_lb + (size_t)nb_new),
+                 need = al(o_sr + (size_t)nb_new);
+    if (need > d->app_cap) {
+        unsigned char* nb = nullptr;
+        const size_t cap = std::max(need, d->app_cap + d->app_cap / 2);
+        if (hipHostMalloc(reinterpret_cast<void**>(&nb), cap, hipHostMallocDefault) != hipSuccess)
+            return dpg_set_error(DPG_ERR_HIP, "hipHostMalloc(append staging) failed");
+        if (d->h_app) (void)hipHostFree(d->h_app);
+        d->h_app = nb;
+        d->app_cap = cap;
+    }
+    unsigned char* st = d->h_app;
+    int64_t* off_new = reinterpret_cast<int64_t*>(st + o_off);
+    float2* pl = reinterpret_cast<float2*>(st + o_pl);
+    float* rg = reinterpret_cast<float*>(st + o_rg);
+    float* gm = reinterpret_cast<float*>(st + o_gm);
+    uint32_t* sect = reinterpret_cast<uint32_t*>(st + o_sc);
+    uint32_t* act = reinterpret_cast<uint32_t*>(st + o_ac);
+    uint8_t* lab = st + o_lb;
+    uint8_t* sec = st + o_sr;
+    // the new nodes' largest ranges and the beam maximum are committed to d only after every
+    // allocation and copy below succeeded (as off and V)
+    std::vector<float> rmax_new((size_t)n_new);
+    int64_t last = d->off.back();
+    for (int64_t k = 0; k < n_new; ++k) {
+        const int64_t nb = off_rel[k + 1] - off_rel[k];
         const float amin = geom[3 * k], amax = geom[3 * k + 1], rmax = geom[3 * k + 2];
         const float ainc = (float)((double)(amax - amin) / ((double)nb - 1.0));   // createNode (dpg_slam.cc:497)
         const float per_sector = ((float)nb) / (float)d->p.num_sectors;
-        gm[(size_t)(4 * k)] = amin; gm[(size_t)(4 * k + 1)] = amax; gm[(size_t)(4 * k + 2)] = rmax; gm[(size_t)(4 * k + 3)] = ainc;
+        gm[4 * k] = amin; gm[4 * k + 1] = amax; gm[4 * k + 2] = rmax; gm[4 * k + 3] = ainc;
         float rm = 0.f;
         for (int64_t i = 0; i < nb; ++i) {
             const int64_t b = off_rel[k] - off_rel[0] + i;
             const float angle = ainc * (float)i + amin;
             const float r = ranges[b];
-            pl[(size_t)b] = make_float2(r * cosf(angle), r * sinf(angle));
-            lab[(size_t)b] = r >= rmax ? DPG_LABEL_MAX_RANGE : DPG_LABEL_NOT_YET_LABELED;
-            sec[(size_t)b] = (uint8_t)((float)i / per_sector);
+            pl[b] = make_float2(r * cosf(angle), r * sinf(angle));
+            rg[b] = r;
+            lab[b] = r >= rmax ? DPG_LABEL_MAX_RANGE : DPG_LABEL_NOT_YET_LABELED;
+            sec[b] = (uint8_t)((float)i / per_sector);
             rm = std::max(rm, r);
         }
-        off.push_back(off.back() + nb);
-        rmax_new.push_back(rm);
-        max_beams = std::max<int32_t>(max_beams, (int32_t)nb);
+        last += nb;
+        off_new[k] = last;
+        rmax_new[(size_t)k] = rm;
+        sect[k] = (1u << d->p.num_sectors) - 1u;
+        act[k] = 1u;
     }
     // device arrays grow with their contents kept (amortised x1.5)
-    auto grow = [&](auto& b, size_t used, size_t need) -> int {
+    auto grow = [&](auto& b, size_t used, size_t need_n) -> int {
         using T = std::remove_pointer_t<decltype(b.p)>;
-        if (need <= b.cap) return 0;
-        const size_t cap = std::max(need, b.cap + b.cap / 2);
+        if (need_n <= b.cap) return 0;
+        const size_t cap = std::max(need_n, b.cap + b.cap / 2);
         T* np = nullptr;
         if (hipMalloc(reinterpret_cast<void**>(&np), cap * sizeof(T)) != hipSuccess) return -1;
         if (used && hipMemcpyAsync(np, b.p, used * sizeof(T), hipMemcpyDeviceToDevice, s) != hipSuccess) { (void)hipFree(np); return -1; }
@@ -813,39 +852,41 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
         return 0;
     };
     const size_t B1 = (size_t)(B0 + nb_new);
-    if (grow(d->d_off, 0, (size_t)(V1 + 1)) || grow(d->d_plaser, (size_t)B0, B1) || grow(d->d_range, (size_t)B0, B1) ||
+    if (grow(d->d_off, (size_t)(V0 + 1), (size_t)(V1 + 1)) || grow(d->d_plaser, (size_t)B0, B1) || grow(d->d_range, (size_t)B0, B1) ||
         grow(d->d_label, (size_t)B0, B1) || grow(d->d_sector, (size_t)B0, B1) || grow(d->d_geom, (size_t)V0, (size_t)V1) ||
         grow(d->d_sect, (size_t)V0, (size_t)V1) || grow(d->d_active, (size_t)V0, (size_t)V1) ||
         grow(d->d_frame, (size_t)(2 * V0), (size_t)(2 * V1)))
         return dpg_set_error(DPG_ERR_HIP, "hipMalloc(node store growth) failed");
-    // pinned host mirrors
-    float* nf = nullptr;
-    uint32_t* na = nullptr;
-    if (hipHostMalloc(reinterpret_cast<void**>(&nf), sizeof(float) * 8 * V1, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&na), sizeof(uint32_t) * V1, hipHostMallocDefault) != hipSuccess) {
-        if (nf) (void)hipHostFree(nf);
-        return dpg_set_error(DPG_ERR_HIP, "hipHostMalloc(node store growth) failed");
+    // pinned host mirrors, amortised x1.5
+    if (V1 > d->h_cap) {
+        const int64_t cap = std::max<int64_t>(V1, d->h_cap + d->h_cap / 2);
+        float* nf = nullptr;
+        uint32_t* na = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&nf), sizeof(float) * 8 * cap, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc(reinterpret_cast<void**>(&na), sizeof(uint32_t) * cap, hipHostMallocDefault) != hipSuccess) {
+            if (nf) (void)hipHostFree(nf);
+            return dpg_set_error(DPG_ERR_HIP, "hipHostMalloc(node store growth) failed");
+        }
+        memcpy(nf, d->h_frames, sizeof(float) * 8 * V0);
+        (void)hipHostFree(d->h_frames);
+        (void)hipHostFree(d->h_act);
+        d->h_frames = nf;
+        d->h_act = na;
+        d->h_cap = cap;
     }
-    memcpy(nf, d->h_frames, sizeof(float) * 8 * V0);
-    memset(nf + 8 * V0, 0, sizeof(float) * 8 * n_new);
-    (void)hipHostFree(d->h_frames);
-    (void)hipHostFree(d->h_act);
-    d->h_frames = nf;
-    d->h_act = na;
-    std::vector<uint32_t> sect((size_t)n_new, (1u << d->p.num_sectors) - 1u), act((size_t)n_new, 1u);
-    DTRY(hipMemcpyAsync(d->d_off.p, off.data(), sizeof(int64_t) * (V1 + 1), hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_plaser.p + B0, pl.data(), sizeof(float2) * nb_new, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_range.p + B0, ranges, sizeof(float) * nb_new, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_label.p + B0, lab.data(), nb_new, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_sector.p + B0, sec.data(), nb_new, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_geom.p + V0, gm.data(), sizeof(float) * 4 * n_new, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_sect.p + V0, sect.data(), sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
-    DTRY(hipMemcpyAsync(d->d_active.p + V0, act.data(), sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
-    DTRY(hipStreamSynchronize(s));
+    memset(d->h_frames + 8 * V0, 0, sizeof(float) * 8 * n_new);
+    DTRY(hipMemcpyAsync(d->d_off.p + V0 + 1, off_new, sizeof(int64_t) * n_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_plaser.p + B0, pl, sizeof(float2) * nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_range.p + B0, rg, sizeof(float) * nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_label.p + B0, lab, nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_sector.p + B0, sec, nb_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_geom.p + V0, gm, sizeof(float) * 4 * n_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_sect.p + V0, sect, sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
+    DTRY(hipMemcpyAsync(d->d_active.p + V0, act, sizeof(uint32_t) * n_new, hipMemcpyHostToDevice, s));
     d->h_pose.resize((size_t)(3 * V1), NAN);
     d->active_h.resize((size_t)V1, 1);
-    d->geom.insert(d->geom.end(), gm.begin(), gm.end());
-    d->off = off;
+    d->geom.insert(d->geom.end(), gm, gm + 4 * n_new);
+    d->off.insert(d->off.end(), off_new, off_new + n_new);
     d->V = V1;
     d->B = (int64_t)B1;
     d->rmax_beam.insert(d->rmax_beam.end(), rmax_new.begin(), rmax_new.end());
@@ -862,6 +903,7 @@ void dpg_dpg_destroy(dpg_dpg* d) {
     if (d->h_act) (void)hipHostFree(d->h_act);
     if (d->h_commit) (void)hipHostFree(d->h_commit);
     if (d->h_stage) (void)hipHostFree(d->h_stage);
+    if (d->h_app) (void)hipHostFree(d->h_app);
     for (auto& e : d->ev) if (e) (void)hipEventDestroy(e);
     delete d;
 }
