@@ -47,7 +47,15 @@ with api.Context(0) as ctx:
     busy_ms = (time.perf_counter() - t0) * 1e3
     pre = {"after-icp": lambda: ctx.icp_run(compute_cov=False), "after-gn": gn,
            "after-memset-1GiB": lambda: big.fill_(1), "after-busy-compute": busy,
-           "after-idle-4ms": lambda: time.sleep(0.004), "none (sync gap only)": lambda: None}
+           "after-idle-4ms": lambda: time.sleep(0.004), "none (sync gap only)": lambda: None,
+           "after-gn+memset-1GiB": lambda: (gn(), big.fill_(2)),
+           "after-gn+memset-64MiB": lambda: (gn(), big[:1 << 26].fill_(3)),
+           "after-gn+memset-8MiB": lambda: (gn(), big[:1 << 23].fill_(4)),
+           "after-idle+memset-64MiB": lambda: (time.sleep(0.004), big[:1 << 26].fill_(5)),
+           "after-gn+read-1GiB": lambda: (gn(), big.sum(dtype=torch.int64)),
+           "after-gn+busy-compute": lambda: (gn(), busy())}
+    if len(sys.argv) > 2:
+        pre = {k: v for k, v in pre.items() if "+" in k or k in ("after-gn", "after-icp")}
     for k, f in pre.items():
         ms = []
         for r in range(rounds + 1):
