@@ -240,7 +240,8 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
         if (rc) return fail(rc, "k-d tree build launch failed (%d)", rc);
     } else if (c->icp_variant == DPG_ICP_ANGULAR) {
         rc = dpg_launch_angle_index(ds_dev, ds_off_dev + tree_from, n_tree_nodes - tree_from, max_node_pts, tree_pts,
-                                    tree_idx, buckets + tree_from * (int64_t)(dpg_angle_buckets() + 1), c->stream);
+                                    tree_idx, buckets + tree_from * (int64_t)(dpg_angle_buckets() + 1),
+                                    c->kernel_variant == 2, c->stream);
         if (rc) return fail(rc, "angle index build launch failed (%d)", rc);
     }
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -687,7 +688,7 @@ int dpg_scans_index_all(dpg_ctx* c) {
     if (c->n_nodes <= 0 || c->icp_variant != DPG_ICP_ANGULAR) return DPG_OK;   // the other variants index per batch
     HIP_TRY(hipSetDevice(c->device));
     const int rc = dpg_launch_angle_index(c->ds.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
-                                          c->buckets.p, c->stream);
+                                          c->buckets.p, c->kernel_variant == 2, c->stream);
     if (rc) return fail(rc, "angle index build failed");
     HIP_TRY(hipStreamSynchronize(c->stream));
     return DPG_OK;
@@ -2120,7 +2121,8 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
         }
     } else if (c->icp_variant == DPG_ICP_ANGULAR && n_pts > 0) {   // no alignment: only the new node's index
         rc = dpg_launch_angle_index(c->ds.p, c->ds_off_dev.p + V, 1, c->max_ds, c->tree_pts.p, c->tree_idx.p,
-                                    c->buckets.p + V * (int64_t)(dpg_angle_buckets() + 1), c->stream);
+                                    c->buckets.p + V * (int64_t)(dpg_angle_buckets() + 1), c->kernel_variant == 2,
+                                    c->stream);
         if (rc) return fail(rc, "angle index build failed");
     }
     const double init[3] = {(double)init_pose[0], (double)init_pose[1], (double)init_pose[2]};

@@ -159,14 +159,27 @@ __device__ __forceinline__ uint32_t orderable(float f) {
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-// one workgroup per node: points sorted by angle + bucket starts
+// one workgroup per node: the points sorted by (pseudo-angle, original index) and the bucket
+// starts.  A counting sort by bucket -- the bucket is monotone in the pseudo-angle, so the bucket
+// order refines to the key order -- then each bucket (~1 point at kB = 1024) sorted by its full
+// 64-bit key by one thread; a cloud with a bucket of more than kIdxSmall points (a narrow cone)
+// sorts the whole array by a bitonic network instead (so does `bitonic`, the A/B reference: the
+// round-1..4 build).  The keys are unique, so every path gives the same order; bucket b starts at
+// the number of points in buckets < b.  ~8 barriers per cloud instead of the network's 55.
+constexpr int kIdxSmall = 16;
+static_assert(kB == 4 * kTI, "the bucket scan takes four buckets per thread");
 __global__ __launch_bounds__(kTI) void angle_index_kernel(const float2* __restrict__ ds_pts,
                                                          const int64_t* __restrict__ ds_off,
                                                          float2* __restrict__ idx_pts,
                                                          uint16_t* __restrict__ idx_orig,
-                                                         uint16_t* __restrict__ buckets /* [V][kB+1] */) {
+                                                         uint16_t* __restrict__ buckets /* [V][kB+1] */,
+                                                         int32_t bitonic) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int v = blockIdx.x, tid = threadIdx.x;
+    __shared__ int cnt[kB];          // bucket sizes, then the scatter cursors
+    __shared__ int bstart[kB + 1];   // first sorted position of each bucket
+    __shared__ int wsum[kTI / 64];
+    __shared__ int big;
+    const int v = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t off = ds_off[v];
     const int N = (int)(ds_off[v + 1] - off);
     uint16_t* bk = buckets + (size_t)v * (kB + 1);
@@ -174,45 +187,96 @@ __global__ __launch_bounds__(kTI) void angle_index_kernel(const float2* __restri
         for (int b = tid; b <= kB; b += kTI) bk[b] = 0;
         return;
     }
-    int P = 1;
-    while (P < N) P <<= 1;
     uint64_t* key = reinterpret_cast<uint64_t*>(smem);   // [P]: orderable(angle) << 32 | index
-    for (int s = tid; s < P; s += kTI) {
-        if (s < N) {
-            const float2 p = ds_pts[off + s];
-            key[s] = ((uint64_t)orderable(pseudo_angle(p.x, p.y)) << 32) | (uint32_t)s;
-        } else {
-            key[s] = ~0ull;
-        }
+    for (int b = tid; b < kB; b += kTI) cnt[b] = 0;
+    if (tid == 0) big = bitonic;
+    __syncthreads();
+    for (int s = tid; s < N; s += kTI) {
+        const float2 p = ds_pts[off + s];
+        atomicAdd(&cnt[bucket_of(pseudo_angle(p.x, p.y))], 1);
     }
     __syncthreads();
-    for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int q = tid; q < P / 2; q += kTI) {
-                const int i = 2 * q - (q & (j - 1));
-                const int l = i + j;
-                const bool up = (i & k) == 0;
-                const uint64_t a = key[i], b = key[l];
-                if ((a > b) == up) { key[i] = b; key[l] = a; }
+    {   // exclusive scan: thread t owns buckets 4t .. 4t + 3
+        int c[4], run = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            c[j] = cnt[4 * tid + j];
+            run += c[j];
+        }
+        int inc = run;   // inclusive scan of the per-thread sums inside the wave
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int u = __shfl_up(inc, d, 64);
+            if (lane >= d) inc += u;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        int base = inc - run;
+        for (int w = 0; w < wave; ++w) base += wsum[w];
+        int mx = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bstart[4 * tid + j] = base;
+            base += c[j];
+            mx = max(mx, c[j]);
+            cnt[4 * tid + j] = 0;   // only this thread reads these four
+        }
+        if (tid == 0) bstart[kB] = N;
+        if (mx > kIdxSmall) big = 1;
+    }
+    __syncthreads();
+    if (!big) {
+        for (int s = tid; s < N; s += kTI) {
+            const float2 p = ds_pts[off + s];
+            const float pa = pseudo_angle(p.x, p.y);
+            const int b = bucket_of(pa);
+            key[bstart[b] + atomicAdd(&cnt[b], 1)] = ((uint64_t)orderable(pa) << 32) | (uint32_t)s;
+        }
+        __syncthreads();
+        for (int b = tid; b < kB; b += kTI) {   // insertion sort of one bucket by its full keys
+            const int lo = bstart[b], hi = bstart[b + 1];
+            for (int i = lo + 1; i < hi; ++i) {
+                const uint64_t k = key[i];
+                int j = i - 1;
+                while (j >= lo && key[j] > k) {
+                    key[j + 1] = key[j];
+                    --j;
+                }
+                key[j + 1] = k;
             }
-            __syncthreads();
+        }
+        __syncthreads();
+    } else {
+        int P = 1;
+        while (P < N) P <<= 1;
+        for (int s = tid; s < P; s += kTI) {
+            if (s < N) {
+                const float2 p = ds_pts[off + s];
+                key[s] = ((uint64_t)orderable(pseudo_angle(p.x, p.y)) << 32) | (uint32_t)s;
+            } else {
+                key[s] = ~0ull;
+            }
+        }
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int q = tid; q < P / 2; q += kTI) {
+                    const int i = 2 * q - (q & (j - 1));
+                    const int l = i + j;
+                    const bool up = (i & k) == 0;
+                    const uint64_t a = key[i], b = key[l];
+                    if ((a > b) == up) { key[i] = b; key[l] = a; }
+                }
+                __syncthreads();
+            }
         }
     }
     for (int s = tid; s < N; s += kTI) {
         const int o = (int)(key[s] & 0xffffffffu);
-        const float2 p = ds_pts[off + o];
-        idx_pts[off + s] = p;
+        idx_pts[off + s] = ds_pts[off + o];
         idx_orig[off + s] = (uint16_t)o;
-        const int b = bucket_of(pseudo_angle(p.x, p.y));
-        int bp = -1;
-        if (s > 0) {
-            const float2 pp = ds_pts[off + (int)(key[s - 1] & 0xffffffffu)];
-            bp = bucket_of(pseudo_angle(pp.x, pp.y));
-        }
-        for (int bb = bp + 1; bb <= b; ++bb) bk[bb] = (uint16_t)s;   // first sorted position >= bucket
-        if (s == N - 1)
-            for (int bb = b + 1; bb <= kB; ++bb) bk[bb] = (uint16_t)N;
     }
+    for (int b = tid; b <= kB; b += kTI) bk[b] = (uint16_t)bstart[b];
 }
 
 // A point as the search sees it (16 B, one LDS load): coordinates + key = original index << 16 |
@@ -1209,14 +1273,14 @@ extern "C" size_t dpg_icp_ang_scratch_per_edge(int32_t cap) {
 
 extern "C" int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                                       int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
-                                      uint16_t* buckets_dev, void* stream) {
+                                      uint16_t* buckets_dev, int32_t bitonic, void* stream) {
     if (n_nodes <= 0) return DPG_OK;
     int cap = 1;
     while (cap < max_points) cap <<= 1;
     if (cap > kModeMaxPts[2]) return DPG_ERR_SIZE;
     hipLaunchKernelGGL(angle_index_kernel, dim3((unsigned)n_nodes), dim3(kTI), 8 * (size_t)cap,
                        reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float2*>(ds_pts_dev), ds_off_dev,
-                       reinterpret_cast<float2*>(idx_pts_dev), idx_orig_dev, buckets_dev);
+                       reinterpret_cast<float2*>(idx_pts_dev), idx_orig_dev, buckets_dev, bitonic);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -1243,7 +1307,8 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
         const dpg_icp_edge* ed = edges_dev + e0;
 // variant 5 (default): variant 4 with the window bound's margins folded into three constants and the
 // query pseudo-angles in bucket units (-1.6 % at config 4, byte-identical);
-// variant 1 of the diagnostic switch = variant 4, the A/B reference.
+// variant 1 of the diagnostic switch = variant 4, the A/B reference; variant 2 = the default kernel
+// after the angle index built by the bitonic network (dpg_launch_angle_index's A/B reference).
 // variant 4 (the kernel's VAR >= 1..4 steps): hardware square roots in the
 // window bounds, the candidate distance computed into the record's pad register, reciprocal beats
 // as ballots, the fit's divisions as lane-parallel vector divisions, issue priority for the

@@ -89,7 +89,7 @@ int dpg_launch_map_points(const float* pts_dev, const int64_t* off_dev, const fl
                           int32_t fraction, float* out_dev, void* stream);
 int dpg_launch_angle_index(const float* ds_pts_dev, const int64_t* ds_off_dev, int64_t n_nodes,
                            int32_t max_points, float* idx_pts_dev, uint16_t* idx_orig_dev,
-                           uint16_t* buckets_dev, void* stream);
+                           uint16_t* buckets_dev, int32_t bitonic, void* stream);
 /* clouds of more than 4096 points: record slices in global scratch (scratch_bytes of it, used in
    chunks of scratch_bytes / dpg_icp_ang_scratch_per_edge(cap) edges); up to 16384 points */
 int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_dev, const uint16_t* idx_orig_dev,

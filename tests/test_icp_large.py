@@ -47,3 +47,60 @@ def test_large_clouds_16k_mode_bit_exact(ctx):
     res, _ = ctx.icp_batch(w.edges, w.est, p, compute_cov=False)
     ref, _ = O.icp_batch(w.pts, w.offsets, w.edges, w.est, p, O.NN_GRID, threads=8)
     _same(res, ref)
+
+
+def _cone_workload(n_pts=1500, half_width=0.05, n_nodes=3, seed=5):
+    """Clouds seen through a narrow cone (two walls meeting 10 m ahead, +-half_width rad): ~1500
+    points in ~17 of the angle index's 1024 buckets, so the index sorts them by its bitonic path."""
+    rng = np.random.default_rng(seed)
+    clouds = []
+    for _ in range(n_nodes):
+        ang = np.sort(rng.uniform(-half_width, half_width, n_pts))
+        r = np.where(ang < 0, 10.0 / np.cos(ang + 0.6), 10.0 / np.cos(ang - 0.6)) * np.cos(0.6)
+        r = r + rng.normal(0.0, 0.01, ang.shape)
+        clouds.append(np.stack([r * np.cos(ang), r * np.sin(ang)], 1))
+    pts = np.concatenate(clouds).astype(np.float32)
+    offsets = np.arange(n_nodes + 1, dtype=np.int64) * n_pts
+    est = np.array([[0.0, 0.0, 0.0], [0.05, 0.02, 0.004], [0.1, -0.03, -0.004]], np.float32)[:n_nodes]
+    edges = np.array([[0, 1], [1, 2], [0, 2]], np.int32)
+    return pts, offsets, est, edges
+
+
+def test_narrow_cone_clouds_bit_exact(ctx):
+    """The angle index's fallback (a bucket of > 16 points: the bitonic network) against the oracle,
+    and the counting-sort index against the forced network (kernel variant 2) byte for byte."""
+    from dpgslam import _abi
+    from oracle import oracle as O
+    pts, offsets, est, edges = _cone_workload()
+    p = _abi.default_icp_params()
+    p.downsample_icp_points_ratio = 1
+    ctx.upload_scans(pts, offsets, 1)
+    res, _ = ctx.icp_batch(edges, est, p, compute_cov=False)
+    ref, _ = O.icp_batch(pts, offsets, edges, est, p, O.NN_GRID, threads=4)
+    _same(res, ref)
+    ctx.set_icp_kernel_variant(2)
+    try:
+        res2, _ = ctx.icp_batch(edges, est, p, compute_cov=False)
+    finally:
+        ctx.set_icp_kernel_variant(0)
+    assert res2.tobytes() == res.tobytes()
+
+
+@pytest.mark.parametrize("ratio", [5, 1])
+def test_angle_index_forms_identical(ctx, workload, ratio):
+    """The counting-sort angle index (default) and the bitonic network it replaced (kernel variant
+    2) give byte-identical ICP results on config 2 (~1000 and ~5000-point clouds)."""
+    from dpgslam import _abi
+    w = workload("config2")
+    p = _abi.default_icp_params()
+    p.downsample_icp_points_ratio = ratio
+    edges = w.edges[::7][:60]
+    ctx.upload_scans(w.pts, w.offsets, ratio)
+    res, _ = ctx.icp_batch(edges, w.est, p, compute_cov=False)
+    ctx.set_icp_kernel_variant(2)
+    try:
+        res2, _ = ctx.icp_batch(edges, w.est, p, compute_cov=False)
+    finally:
+        ctx.set_icp_kernel_variant(0)
+    assert res2.tobytes() == res.tobytes()
+    assert (res["converged"] != 0).mean() > 0.9
