@@ -112,6 +112,12 @@ int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32
 int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                              dpg_chol_sym* S, const dpg_chol_opts* opts = nullptr);
 int dpg_chol_create_sym_upload(void** h);
+// the plan's first part (H's blocks bucketed by column position) ahead of the next
+// dpg_chol_create_sym_plan of a graph with n nodes and these n_pairs pairs, whose analysis carries
+// the ordering pos / perm; creates *h when NULL.  Host only, not concurrently with a plan or an
+// upload of the same object (the incremental prepare runs it beside dpg_incsym_derive)
+int dpg_chol_plan_blocks(void** h, int64_t n, const int32_t* pos, const int32_t* perm, const int32_t* pair_lo,
+                         const int32_t* pair_hi, int64_t n_pairs);
 // host time (ms) of the last build of h: structures, uploads
 void dpg_chol_build_times(void* h, double out[2]);
 // 1 when h factors with the fused DAG kernel (every front fits its LDS budget), 0 on the level path

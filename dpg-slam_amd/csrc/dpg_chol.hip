@@ -1854,6 +1854,10 @@ struct CholHost {
     std::vector<int32_t> tcnt, tfill;   // per-tile child counts / fill cursors of one large front
     std::vector<char> tused;
     int64_t acc_total = 0;
+    // colptr / ent built ahead by dpg_chol_plan_blocks (the incremental prepare runs it beside the
+    // symbolic derivation) for a graph of blocks_n nodes and blocks_np pairs; the next plan takes them
+    bool blocks_ready = false;
+    int64_t blocks_n = -1, blocks_np = -1;
 };
 
 #ifdef DPG_PLAN_TIMING
@@ -1875,22 +1879,16 @@ inline int32_t first_at_or_after(const int32_t* rm, int32_t r, int32_t c) {
     return lo;
 }
 
-// Host half of chol_build: every device structure, in H; the plan fields of c.
-int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, CholHost& H) {
-    const dpg_chol_sym& S = c->sym;
-    c->lds_fused = 0;
-    c->n_launches = 0;
-    c->n = n;
-    c->nnzb_upper = n + n_pairs;
-    PLAN_T(0);
-    // omap: every upper block of H -> (front, local block row, local block col, transpose), grouped
-    // by front, each front's entries by (column, row): the blocks are bucketed by column position
-    // (counting sort), each bucket sorted by row, and the fronts walked column by column
+// H's upper blocks bucketed by column position, each bucket in ascending row order (the plan's
+// first part; pos / perm: the ordering -- the symbolic analysis's, or the incremental state's it
+// will copy)
+void plan_blocks(CholHost& H, int64_t n, const int32_t* pos, const int32_t* perm, const int32_t* pair_lo,
+                 const int32_t* pair_hi, int64_t n_pairs) {
     std::vector<int64_t>& colptr = H.colptr;
     colptr.assign((size_t)n + 1, 0);
     for (int64_t p = 0; p < n; ++p) colptr[(size_t)p + 1] = 1;   // the diagonal block
     for (int64_t q = 0; q < n_pairs; ++q)
-        colptr[(size_t)std::min(S.pos[(size_t)pair_lo[q]], S.pos[(size_t)pair_hi[q]]) + 1]++;
+        colptr[(size_t)std::min(pos[(size_t)pair_lo[q]], pos[(size_t)pair_hi[q]]) + 1]++;
     for (int64_t p = 0; p < n; ++p) colptr[(size_t)p + 1] += colptr[(size_t)p];
     std::vector<CholHost::Blk>& ent = H.ent;
     ent.resize((size_t)colptr[(size_t)n]);
@@ -1902,13 +1900,13 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         rptr.assign((size_t)n + 1, 0);
         for (int64_t p = 0; p < n; ++p) rptr[(size_t)p + 1] = 1;
         for (int64_t q = 0; q < n_pairs; ++q)
-            rptr[(size_t)std::max(S.pos[(size_t)pair_lo[q]], S.pos[(size_t)pair_hi[q]]) + 1]++;
+            rptr[(size_t)std::max(pos[(size_t)pair_lo[q]], pos[(size_t)pair_hi[q]]) + 1]++;
         for (int64_t p = 0; p < n; ++p) rptr[(size_t)p + 1] += rptr[(size_t)p];
         std::vector<CholHost::Blk4>& byrow = H.byrow;
         byrow.resize(ent.size());
-        for (int64_t p = 0; p < n; ++p) byrow[(size_t)rptr[(size_t)p]++] = CholHost::Blk4{(int32_t)p, (int32_t)p, S.perm[(size_t)p], 0};
+        for (int64_t p = 0; p < n; ++p) byrow[(size_t)rptr[(size_t)p]++] = CholHost::Blk4{(int32_t)p, (int32_t)p, perm[(size_t)p], 0};
         for (int64_t q = 0; q < n_pairs; ++q) {
-            const int32_t plo = S.pos[(size_t)pair_lo[q]], phi = S.pos[(size_t)pair_hi[q]];
+            const int32_t plo = pos[(size_t)pair_lo[q]], phi = pos[(size_t)pair_hi[q]];
             // front wants A(later, earlier) = H(later_node, earlier_node); hb holds H(lo, hi)
             const int32_t r = std::max(plo, phi);
             byrow[(size_t)rptr[(size_t)r]++] = CholHost::Blk4{r, std::min(plo, phi), (int32_t)(n + q), plo > phi ? 0 : 1};
@@ -1916,6 +1914,37 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         rptr.assign(colptr.begin(), colptr.end() - 1);   // column cursors
         for (const CholHost::Blk4& b : byrow) ent[(size_t)rptr[(size_t)b.col]++] = CholHost::Blk{b.row, b.u, b.tr};
     }
+    H.blocks_n = n;
+    H.blocks_np = n_pairs;
+}
+
+// Host half of chol_build: every device structure, in H; the plan fields of c.
+int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, CholHost& H) {
+    const dpg_chol_sym& S = c->sym;
+    c->lds_fused = 0;
+    c->n_launches = 0;
+    c->n = n;
+    c->nnzb_upper = n + n_pairs;
+    PLAN_T(0);
+    // omap: every upper block of H -> (front, local block row, local block col, transpose), grouped
+    // by front, each front's entries by (column, row): the blocks are bucketed by column position
+    // (counting sort), each bucket sorted by row, and the fronts walked column by column
+    const bool pre = H.blocks_ready && H.blocks_n == n && H.blocks_np == n_pairs;
+    H.blocks_ready = false;
+#ifdef DPG_PLAN_VERIFY
+    if (pre) {   // the prebuilt buckets must equal this plan's own
+        const std::vector<int64_t> cp0 = H.colptr;
+        const std::vector<CholHost::Blk> e0 = H.ent;
+        plan_blocks(H, n, S.pos.data(), S.perm.data(), pair_lo, pair_hi, n_pairs);
+        bool same = cp0 == H.colptr && e0.size() == H.ent.size();
+        for (size_t k = 0; same && k < e0.size(); ++k)
+            same = e0[k].row == H.ent[k].row && e0[k].u == H.ent[k].u && e0[k].tr == H.ent[k].tr;
+        if (!same) { fprintf(stderr, "DPG_PLAN_VERIFY: prebuilt H-block buckets differ\n"); abort(); }
+    }
+#endif
+    if (!pre) plan_blocks(H, n, S.pos.data(), S.perm.data(), pair_lo, pair_hi, n_pairs);
+    const std::vector<int64_t>& colptr = H.colptr;
+    const std::vector<CholHost::Blk>& ent = H.ent;
     PLAN_T(1);
     std::vector<int64_t>& om_ptr = H.om_ptr;
     om_ptr.assign((size_t)S.ns + 1, 0);
@@ -2424,6 +2453,20 @@ int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const 
     const int rc = chol_build_plan(c, n, pair_lo, pair_hi, n_pairs);
     if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
     *h = c;
+    return DPG_OK;
+}
+// chol_plan's first part ahead of the plan (pos / perm: the ordering the plan's analysis will
+// carry); creates the solver object when *h is NULL.  Host only; not concurrently with a plan or an
+// upload of the same object.
+int dpg_chol_plan_blocks(void** h, int64_t n, const int32_t* pos, const int32_t* perm, const int32_t* pair_lo,
+                         const int32_t* pair_hi, int64_t n_pairs) {
+    if (!h || n <= 0 || !pos || !perm || n_pairs < 0 || (n_pairs > 0 && (!pair_lo || !pair_hi))) return DPG_ERR_ARG;
+    CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
+    *h = c;
+    CholHost& H = build_host(c);
+    H.blocks_ready = false;
+    plan_blocks(H, n, pos, perm, pair_lo, pair_hi, n_pairs);
+    H.blocks_ready = true;
     return DPG_OK;
 }
 int dpg_chol_create_sym_upload(void** h) {
