@@ -300,8 +300,9 @@ int dpg_ctx_set_icp_defer_cap(dpg_ctx* ctx, int32_t cap);
  * stream): at most n workgroups, each taking edges in turn, so the pose graph's kernels find free
  * compute units while it runs; 0 = one workgroup per edge.  Results are identical for every n. */
 int dpg_ctx_set_cov_workgroups(dpg_ctx* ctx, int32_t n);
-/* Diagnostic: the angular ICP kernel's form (0 = the default; others are A/B candidates that must give
- * byte-identical results, tools/icp_var_ab.py). */
+/* Diagnostic: the angular ICP kernel's form (0 = the default; others are A/B references that must give
+ * byte-identical results, tools/icp_var_ab.py): 1 = the kernel's previous form (variant 4), 2 = the
+ * default kernel after the angle index built by its previous bitonic network. */
 int dpg_ctx_set_icp_kernel_variant(dpg_ctx* ctx, int32_t variant);
 /* Sum over edges of iterations x (8N + 8M + 8N) -- algorithmic bytes of the correspondence
  * search for the last run, computed on device and copied back. */
