@@ -46,7 +46,9 @@ def test_solver_plan_matches_straightforward_construction(tmp_path):
     child column ranges by binary search, critical-path front order) equals the straightforward
     construction (per-block binary search + per-front sort, linear scans, stable sort) after every
     update of a growing graph: tools/incsym_bench.cpp built with DPG_PLAN_VERIFY aborts on the first
-    difference.  Host code only (hipcc compiles it; no device call runs)."""
+    difference -- including the H-block buckets the incremental prepare builds ahead from the
+    incremental state's order (dpg_chol_plan_blocks, every 50th update) and that order against the
+    analysis's.  Host code only (hipcc compiles it; no device call runs)."""
     exe = str(tmp_path / "incsym_bench_v")
     csrc = os.path.join(ROOT, "dpg-slam_amd", "csrc")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-ffp-contract=off",

@@ -104,6 +104,19 @@ int main(int argc, char** argv) {
             dpg_chol_sym_from_csr(n, I.perm.data(), cp.data(), rows.data(), &o, &S2);
             acc[3] += now_ms() - tf;
         }
+#ifdef DPG_PLAN_VERIFY
+        // the incremental prepare builds the plan's H-block buckets from I's order beside the
+        // derivation (dpg_chol_plan_blocks): that order must be the one the analysis carries, and
+        // the plan checks the prebuilt buckets against its own (every 50th update: host only)
+        if (I.perm != S.perm || I.pos != S.pos) { fprintf(stderr, "update %d: I and S orders differ\n", v); abort(); }
+        if (v % 50 == 49) {
+            static void* hv = nullptr;
+            dpg_chol_sym S3 = S;
+            if (dpg_chol_plan_blocks(&hv, V1, I.pos.data(), I.perm.data(), plo.data(), phi.data(), (int64_t)plo.size()) ||
+                dpg_chol_create_sym_plan(&hv, V1, plo.data(), phi.data(), (int64_t)plo.size(), &S3, &o))
+                return 6;
+        }
+#endif
         double plan = 0;
         if (dpg_chol_plan_host(V1, plo.data(), phi.data(), (int64_t)plo.size(), &S, &plan)) return 5;
         if (v >= V - tail) {
