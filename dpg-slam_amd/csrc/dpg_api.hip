@@ -161,7 +161,9 @@ struct dpg_ctx {
     // of the other local devices.  Local device k is global rank rank0 + k of `world`.
     std::vector<dpg_ctx*> peers;
     std::vector<ncclComm_t> comms;   // RCCL: one communicator per local device
-    int32_t coll = 0;                // kCollNone | kCollRccl | kCollVirtual
+    dpg_coll_ops host_ops{};         // kCollHost: the caller's host-memory collectives
+    std::vector<double> host_hb;     // kCollHost: the packed system in host memory
+    int32_t coll = 0;                // kCollNone | kCollRccl | kCollVirtual | kCollHost
     int32_t world = 1, rank0 = 0;
     int32_t rank = 0;                // global rank of THIS device context (peers too)
     // the staged batch, every form: the edges in the caller's order and their assignment --
@@ -182,8 +184,13 @@ struct dpg_ctx {
 };
 
 namespace {
-enum { kCollNone = 0, kCollRccl = 1, kCollVirtual = 2, kMaxVirtual = 16 };
+enum { kCollNone = 0, kCollRccl = 1, kCollVirtual = 2, kCollHost = 3, kMaxVirtual = 16 };
 inline int n_dev(const dpg_ctx* c) { return 1 + (int)c->peers.size(); }
+// one process per GPU with more than one rank (dpg_ctx_create_rank / _rank_ops): the batch's
+// results and costs travel between processes
+inline bool is_rank_form(const dpg_ctx* c) {
+    return (c->coll == kCollRccl || c->coll == kCollHost) && c->peers.empty() && c->world > 1;
+}
 inline dpg_ctx* dev_ctx(dpg_ctx* c, int k) { return k == 0 ? c : c->peers[(size_t)k - 1]; }
 // made by dpg_ctx_create_multi / _rank / _virtual (even for one GPU: its calls then take the
 // sharded paths, the all-reduce included, with one rank)
@@ -306,6 +313,58 @@ int dpg_set_error(int code, const char* msg) { return fail(code, "%s", msg); }
 void* dpg_ctx_stream_of(dpg_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
 int dpg_ctx_device_of(dpg_ctx* c) { return c ? c->device : -1; }
 const char* dpg_version(void) { return "dpg-mi355x 0.1 (gfx950)"; }
+
+// The batch over the ranks (host only).  cost != NULL: longest-processing-time -- edges by cost,
+// longest first (stable: lower index first among equals), each to the least-loaded rank (lower rank
+// among equals), dispatched on its rank in that order, so the alignments that bound a launch start
+// first.  cost == NULL: edge e on rank e mod world in the caller's order (the caller's lists come
+// grouped -- successive pairs, then loop closures nearest first -- so every rank gets the same mix).
+int dpg_shard_plan(const float* cost, int64_t ne, int32_t world, int32_t* owner, int64_t* dispatch, int64_t* counts) {
+    if (ne < 0 || world < 1 || (ne > 0 && (!owner || !dispatch)) || !counts) return fail(DPG_ERR_ARG, "dpg_shard_plan: bad arguments");
+    std::vector<std::vector<int64_t>> disp((size_t)world);
+    if (cost) {
+        std::vector<int64_t> ord((size_t)ne);
+        for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = e;
+        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return cost[a] > cost[b]; });
+        std::vector<double> load((size_t)world, 0.0);
+        for (int64_t e : ord) {
+            int r = 0;
+            for (int q = 1; q < world; ++q)
+                if (load[(size_t)q] < load[(size_t)r]) r = q;
+            owner[e] = r;
+            load[(size_t)r] += cost[e];
+            disp[(size_t)r].push_back(e);
+        }
+    } else {
+        for (int64_t e = 0; e < ne; ++e) {
+            owner[e] = (int32_t)(e % world);
+            disp[(size_t)(e % world)].push_back(e);
+        }
+    }
+    int64_t o = 0;
+    for (int r = 0; r < world; ++r) {
+        counts[r] = (int64_t)disp[(size_t)r].size();
+        for (int64_t e : disp[(size_t)r]) dispatch[o++] = e;
+    }
+    return DPG_OK;
+}
+
+// The rank form's all-gathered results back in the caller's order (host only): slice r holds rank
+// r's records -- its edges ascending, `slice` records of rec_bytes reserved per rank
+int dpg_shard_reassemble(const int32_t* owner, int64_t ne, int32_t world, int64_t slice, int64_t rec_bytes,
+                         const void* gathered, void* out) {
+    if (ne < 0 || world < 1 || slice < 0 || rec_bytes <= 0 || (ne > 0 && (!owner || !gathered || !out)))
+        return fail(DPG_ERR_ARG, "dpg_shard_reassemble: bad arguments");
+    std::vector<int64_t> pos((size_t)world, 0);
+    const char* g = static_cast<const char*>(gathered);
+    char* o = static_cast<char*>(out);
+    for (int64_t e = 0; e < ne; ++e) {
+        const int32_t r = owner[e];
+        if (r < 0 || r >= world || pos[(size_t)r] >= slice) return fail(DPG_ERR_ARG, "dpg_shard_reassemble: edge %lld owner %d out of range", (long long)e, r);
+        memcpy(o + e * rec_bytes, g + (r * slice + pos[(size_t)r]++) * rec_bytes, (size_t)rec_bytes);
+    }
+    return DPG_OK;
+}
 
 dpg_ctx* dpg_ctx_create(int device) {
     int n = 0;
@@ -435,6 +494,27 @@ dpg_ctx* dpg_ctx_create_rank(int32_t device, const void* nccl_id, int32_t rank, 
     }
     c->comms.assign(1, comm);
     c->coll = kCollRccl;
+    c->world = world;
+    c->rank0 = rank;
+    c->rank = rank;
+    return c;
+}
+
+// One process per GPU over the caller's own collectives (blocking, host memory): a host that
+// already runs a communicator (MPI, gloo), or ranks sharing one card (RCCL refuses a second rank
+// on a device).  Every cross-process step of the rank form -- the cost all-reduce of the LPT plan,
+// the results' all-gather, the packed system's all-reduce per Gauss-Newton iteration -- goes
+// through `ops` instead of RCCL; the rest of the rank form is the same code.
+dpg_ctx* dpg_ctx_create_rank_ops(int32_t device, const dpg_coll_ops* ops, int32_t rank, int32_t world) {
+    if (!ops || !ops->allreduce_sum_f64 || !ops->allreduce_sum_f32 || !ops->allgather || world < 1 || rank < 0 ||
+        rank >= world) {
+        fail(DPG_ERR_ARG, "dpg_ctx_create_rank_ops: rank %d of %d (all three collectives are required)", rank, world);
+        return nullptr;
+    }
+    dpg_ctx* c = dpg_ctx_create(device);
+    if (!c) return nullptr;
+    c->host_ops = *ops;
+    c->coll = kCollHost;
     c->world = world;
     c->rank0 = rank;
     c->rank = rank;
@@ -786,35 +866,23 @@ static int stage_device(dpg_ctx* q, std::vector<dpg_icp_edge>& h, const dpg_icp_
 static int plan_and_stage(dpg_ctx* c, bool measured) {
     const int64_t ne = (int64_t)c->batch.size();
     const int W = c->world;
-    std::vector<std::vector<int64_t>> disp((size_t)W);
-    c->batch_owner.assign((size_t)ne, 0);
+    std::vector<float> w;
     if (measured) {
-        std::vector<float> w((size_t)ne);
+        w.resize((size_t)ne);
         for (int64_t e = 0; e < ne; ++e) w[(size_t)e] = c->cost.at(pair_key(c->batch[(size_t)e]));
-        std::vector<int64_t> ord((size_t)ne);
-        for (int64_t e = 0; e < ne; ++e) ord[(size_t)e] = e;
-        std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return w[(size_t)a] > w[(size_t)b]; });
-        std::vector<double> load((size_t)W, 0.0);
-        for (int64_t e : ord) {
-            int r = 0;
-            for (int q = 1; q < W; ++q)
-                if (load[(size_t)q] < load[(size_t)r]) r = q;
-            c->batch_owner[(size_t)e] = r;
-            load[(size_t)r] += w[(size_t)e];
-            disp[(size_t)r].push_back(e);
-        }
-    } else {
-        for (int64_t e = 0; e < ne; ++e) {
-            const int r = (int)(e % W);
-            c->batch_owner[(size_t)e] = r;
-            disp[(size_t)r].push_back(e);
-        }
     }
+    c->batch_owner.assign((size_t)ne, 0);
+    std::vector<int64_t> order((size_t)std::max<int64_t>(ne, 1)), counts((size_t)W, 0);
+    int rc = dpg_shard_plan(measured ? w.data() : nullptr, ne, W, c->batch_owner.data(), order.data(), counts.data());
+    if (rc) return rc;
+    std::vector<int64_t> first((size_t)W + 1, 0);
+    for (int r = 0; r < W; ++r) first[(size_t)r + 1] = first[(size_t)r] + counts[(size_t)r];
     const int32_t ms = c->max_src, mt = c->max_tgt;
     const dpg_icp_kparams kp = c->kp;
     c->shard.assign((size_t)n_dev(c), {});
     for (int k = 0; k < n_dev(c); ++k) {
-        const auto& d = disp[(size_t)(c->rank0 + k)];
+        const int r = c->rank0 + k;
+        const std::vector<int64_t> d(order.begin() + first[(size_t)r], order.begin() + first[(size_t)r + 1]);
         auto& sh = c->shard[(size_t)k];
         sh = d;
         std::sort(sh.begin(), sh.end());
@@ -823,8 +891,7 @@ static int plan_and_stage(dpg_ctx* c, bool measured) {
             h[q] = c->batch[(size_t)d[q]];
             h[q].pad[0] = (int32_t)(std::lower_bound(sh.begin(), sh.end(), d[q]) - sh.begin());
         }
-        const int rc = stage_device(dev_ctx(c, k), h, kp, ms, mt, is_multi(c) ? &sh : nullptr);
-        if (rc) return rc;
+        if ((rc = stage_device(dev_ctx(c, k), h, kp, ms, mt, is_multi(c) ? &sh : nullptr))) return rc;
     }
     c->batch_measured = measured;
     HIP_TRY(hipSetDevice(c->device));
@@ -874,6 +941,56 @@ static int batch_run_1(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
                         compute_cov ? c->hess.p : nullptr, tr, true);
 }
 
+// ---- the rank form's cross-process steps (blocking; every rank makes them in the same order) ----
+// in-place sum of host floats over the ranks
+static int coll_allreduce_f32_host(dpg_ctx* c, float* w, size_t n) {
+    if (c->coll == kCollHost) {
+        if (c->host_ops.allreduce_sum_f32(c->host_ops.user, w, (int64_t)n))
+            return fail(DPG_ERR_HIP, "the caller's float all-reduce failed");
+        return DPG_OK;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->cost_dev.reserve(n)) return fail(DPG_ERR_HIP, "out of device memory");
+    HIP_TRY(hipMemcpyAsync(c->cost_dev.p, w, sizeof(float) * n, hipMemcpyHostToDevice, c->stream));
+    const ncclResult_t nr = ncclAllReduce(c->cost_dev.p, c->cost_dev.p, n, ncclFloat, ncclSum, c->comms[0], c->stream);
+    if (nr != ncclSuccess) return fail(DPG_ERR_HIP, "ncclAllReduce (costs) failed: %s", ncclGetErrorString(nr));
+    HIP_TRY(hipMemcpyAsync(w, c->cost_dev.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DPG_OK;
+}
+
+// every rank's `slice_bytes` (the first mine_bytes of them from local_dev, this rank's records) into
+// `all` on the host, rank order
+static int coll_allgather_to_host(dpg_ctx* c, const void* local_dev, size_t mine_bytes, size_t slice_bytes,
+                                  std::vector<char>& all) {
+    const size_t W = (size_t)c->world;
+    all.assign(slice_bytes * W, 0);
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->coll == kCollHost) {
+        std::vector<char> send(slice_bytes, 0);
+        if (mine_bytes) HIP_TRY(hipMemcpyAsync(send.data(), local_dev, mine_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->host_ops.allgather(c->host_ops.user, send.data(), all.data(), (int64_t)slice_bytes))
+            return fail(DPG_ERR_HIP, "the caller's all-gather failed");
+        return DPG_OK;
+    }
+    DevBuf<char> send, recv;
+    int rc = DPG_OK;
+    if (send.reserve(slice_bytes) || recv.reserve(slice_bytes * W)) rc = fail(DPG_ERR_HIP, "out of device memory for the gather");
+    if (!rc && mine_bytes && hipMemcpyAsync(send.p, local_dev, mine_bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+        rc = fail(DPG_ERR_HIP, "gather staging copy failed");
+    if (!rc) {
+        const ncclResult_t nr = ncclAllGather(send.p, recv.p, slice_bytes, ncclChar, c->comms[0], c->stream);
+        if (nr != ncclSuccess) rc = fail(DPG_ERR_HIP, "ncclAllGather failed: %s", ncclGetErrorString(nr));
+    }
+    if (!rc && (hipMemcpyAsync(all.data(), recv.p, all.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = fail(DPG_ERR_HIP, "gather copy failed");
+    send.release();
+    recv.release();
+    return rc;
+}
+
 // the measured cost of every edge of the last run into the cost memory (blocking); on the rank form
 // the ranks' costs are summed into one vector (every edge has one owner, the others add 0), so every
 // rank plans the next run from the same numbers
@@ -892,15 +1009,8 @@ static int harvest_costs(dpg_ctx* c) {
         HIP_TRY(hipStreamSynchronize(q->stream));
         for (size_t j = 0; j < sh.size(); ++j) w[(size_t)sh[j]] = edge_cost(c->batch[(size_t)sh[j]], r[j].iterations);
     }
-    if (c->coll == kCollRccl && n_dev(c) == 1 && c->world > 1 && ne > 0) {
-        HIP_TRY(hipSetDevice(c->device));
-        if (c->cost_dev.reserve((size_t)ne)) return fail(DPG_ERR_HIP, "out of device memory");
-        HIP_TRY(hipMemcpyAsync(c->cost_dev.p, w.data(), sizeof(float) * (size_t)ne, hipMemcpyHostToDevice, c->stream));
-        const ncclResult_t nr = ncclAllReduce(c->cost_dev.p, c->cost_dev.p, (size_t)ne, ncclFloat, ncclSum, c->comms[0], c->stream);
-        if (nr != ncclSuccess) return fail(DPG_ERR_HIP, "ncclAllReduce (costs) failed: %s", ncclGetErrorString(nr));
-        HIP_TRY(hipMemcpyAsync(w.data(), c->cost_dev.p, sizeof(float) * (size_t)ne, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-    }
+    int rc;
+    if (is_rank_form(c) && ne > 0 && (rc = coll_allreduce_f32_host(c, w.data(), (size_t)ne))) return rc;
     for (int64_t e = 0; e < ne; ++e)
         if (w[(size_t)e] > 0.f) c->cost[pair_key(c->batch[(size_t)e])] = w[(size_t)e];
     HIP_TRY(hipSetDevice(c->device));
@@ -982,43 +1092,18 @@ static int fetch_local(dpg_ctx* q, size_t n, dpg_icp_result* results, double* he
     return DPG_OK;
 }
 
-// rank form: every rank's local results, gathered with one ncclAllGather of equal-size slices
-// (the largest share; each rank derives every other rank's share from the common plan)
-static int fetch_allgather(dpg_ctx* c, void* out, size_t rec_bytes, const void* local_dev, std::vector<char>& all,
-                           size_t& slice) {
+// rank form: every rank's local results, gathered in equal-size slices (the largest share; each
+// rank derives every other rank's share from the common plan), then put in the caller's order
+static int fetch_allgather(dpg_ctx* c, void* out, size_t rec_bytes, const void* local_dev, std::vector<char>& all) {
     const int W = c->world;
     std::vector<size_t> cnt((size_t)W, 0);
     for (int32_t o : c->batch_owner) ++cnt[(size_t)o];
-    slice = std::max<size_t>(*std::max_element(cnt.begin(), cnt.end()), 1);
-    DevBuf<char> send, recv;
-    int rc = DPG_OK;
-    HIP_TRY(hipSetDevice(c->device));
-    if (send.reserve(slice * rec_bytes) || recv.reserve(slice * rec_bytes * (size_t)W)) {
-        send.release();
-        recv.release();
-        return fail(DPG_ERR_HIP, "out of device memory for the gather");
-    }
+    const size_t slice = std::max<size_t>(*std::max_element(cnt.begin(), cnt.end()), 1);
     const size_t mine = c->shard.empty() ? 0 : c->shard[0].size();
-    if (mine && hipMemcpyAsync(send.p, local_dev, mine * rec_bytes, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
-        rc = fail(DPG_ERR_HIP, "gather staging copy failed");
-    if (!rc) {
-        const ncclResult_t nr = ncclAllGather(send.p, recv.p, slice * rec_bytes, ncclChar, c->comms[0], c->stream);
-        if (nr != ncclSuccess) rc = fail(DPG_ERR_HIP, "ncclAllGather failed: %s", ncclGetErrorString(nr));
-    }
-    all.resize(slice * rec_bytes * (size_t)W);
-    if (!rc && (hipMemcpyAsync(all.data(), recv.p, all.size(), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-                hipStreamSynchronize(c->stream) != hipSuccess))
-        rc = fail(DPG_ERR_HIP, "gather copy failed");
-    send.release();
-    recv.release();
+    int rc = coll_allgather_to_host(c, local_dev, mine * rec_bytes, slice * rec_bytes, all);
     if (rc) return rc;
-    std::vector<size_t> pos((size_t)W, 0);
-    char* o = static_cast<char*>(out);
-    for (size_t e = 0; e < c->batch_owner.size(); ++e) {
-        const int r = c->batch_owner[e];
-        memcpy(o + e * rec_bytes, all.data() + ((size_t)r * slice + pos[(size_t)r]++) * rec_bytes, rec_bytes);
-    }
-    return DPG_OK;
+    return dpg_shard_reassemble(c->batch_owner.data(), (int64_t)c->batch_owner.size(), W, (int64_t)slice,
+                                (int64_t)rec_bytes, all.data(), out);
 }
 
 // Results of the staged batch in the caller's order (and the covariance blocks).  On the rank form
@@ -1034,12 +1119,11 @@ int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
         R = own.data();
     }
     int rc;
-    if (c->coll == kCollRccl && n_dev(c) == 1 && c->world > 1) {
+    if (is_rank_form(c)) {
         std::vector<char> buf;
-        size_t slice = 0;
         if (join_cov(c)) return fail(DPG_ERR_HIP, "stream wait failed");
-        if ((rc = fetch_allgather(c, R, sizeof(dpg_icp_result), c->res.p, buf, slice))) return rc;
-        if (hess && (rc = fetch_allgather(c, hess, 9 * sizeof(double), c->hess.p, buf, slice))) return rc;
+        if ((rc = fetch_allgather(c, R, sizeof(dpg_icp_result), c->res.p, buf))) return rc;
+        if (hess && (rc = fetch_allgather(c, hess, 9 * sizeof(double), c->hess.p, buf))) return rc;
     } else {
         std::vector<dpg_icp_result> r;
         std::vector<double> h;
@@ -1487,6 +1571,17 @@ static int coll_sum_hb(dpg_ctx* c) {
         const int rc = dpg_launch_vsum(parts, outs, n_dev(c), (int64_t)count, c->stream);   // the shared stream
         return rc ? fail(rc, "virtual all-reduce launch failed") : DPG_OK;
     }
+    if (c->coll == kCollHost) {   // the caller's collective, through host memory (blocking)
+        c->host_hb.resize(count);
+        HIP_TRY(hipSetDevice(c->device));
+        HIP_TRY(hipMemcpyAsync(c->host_hb.data(), c->gn.hb_part, sizeof(double) * count, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->host_ops.allreduce_sum_f64(c->host_ops.user, c->host_hb.data(), (int64_t)count))
+            return fail(DPG_ERR_HIP, "the caller's all-reduce of the packed system failed");
+        HIP_TRY(hipMemcpyAsync(c->gn.hb_own, c->host_hb.data(), sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return DPG_OK;
+    }
     if (ncclGroupStart() != ncclSuccess) return fail(DPG_ERR_HIP, "ncclGroupStart failed");
     for (int k = 0; k < n_dev(c); ++k) {
         dpg_ctx* q = dev_ctx(c, k);
@@ -1588,7 +1683,7 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
             if (i == 1) {   // the initial error, as the device read it (pipe_init_kernel)
                 if ((rc = wait_slot(q, q->pipe_slot + 2, (uint64_t)q->pipe_loop << 32))) return rc;
                 const double e0 = static_cast<const volatile dpg_gn_slot*>(q->pipe_slot + 2)->error;
-                if (!(e0 > 0.0)) {   // nothing to do: no iteration runs (the host loop's entry test)
+                if (e0 <= 0.0) {   // nothing to do: no iteration runs (pipe_init_kernel's test, NaN runs)
                     for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
                     S.initial_error = e0;
                     nw = e0;
@@ -1627,6 +1722,8 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
         }
         if (o0.status != 0.0) {
             for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
+            if (o0.status == (double)DPG_GN_STATUS_DIVERGED)
+                return fail(DPG_ERR_INTERNAL, "ranks diverged at GN iteration %d (different max |delta| in the vote words)", i);
             return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)o0.status);
         }
         it = i;

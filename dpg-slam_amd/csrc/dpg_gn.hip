@@ -214,13 +214,22 @@ __device__ __forceinline__ double strided_sum(const double* __restrict__ v, int6
     return s;
 }
 
+// vote != NULL (multi-device forms, world > 1): this device's max |delta| and solver status into
+// its own vote words (dpg_gn_dev.n_vote), summed by the all-reduce with the other devices' zeros
 __global__ void chi2_kernel(const double* __restrict__ chi2_node, int64_t n, double* __restrict__ out,
-                            const int32_t* gate) {
+                            const int32_t* gate, double* __restrict__ vote, const double* __restrict__ dinf,
+                            const int32_t* __restrict__ status, int32_t world, int32_t rank) {
     __shared__ double red[16];
     if (gate && !gate[0]) return;
     double s = strided_sum(chi2_node, n, threadIdx.x, blockDim.x);
     s = block_sum(s, red);
-    if (threadIdx.x == 0) *out = s;
+    if (threadIdx.x == 0) {
+        *out = s;
+        if (vote) {
+            vote[rank] = *dinf;
+            vote[world + rank] = (double)*status;
+        }
+    }
 }
 
 // inverse of an SPD 3x3 block (adjugate / determinant)
@@ -427,7 +436,9 @@ inline unsigned nblk(int64_t n) { return (unsigned)((n + kRowThreads - 1) / kRow
 
 }  // namespace
 
-extern "C" int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g) { return 9 * g->nnzb_upper + 3 * g->n_nodes + 2; }
+// [H upper 9 nnzb | g 3n | chi2 | pad | votes n_vote]
+extern "C" int64_t dpg_gn_dev_vote_offset(const dpg_gn_dev* g) { return 9 * g->nnzb_upper + 3 * g->n_nodes + 2; }
+extern "C" int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g) { return dpg_gn_dev_vote_offset(g) + g->n_vote; }
 
 extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
     void* ptrs[] = {g->factors, g->up_row, g->up_col, g->up_cptr, g->up_clist, g->node_fptr, g->node_flist,
@@ -571,9 +582,13 @@ static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_
     hipLaunchKernelGGL(gather_kernel<4>, dim3((unsigned)((g->nnzb_upper + 63) / 64)), dim3(64), 0, s, g->contrib, g->up_cptr,
                        g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, hb, chi2_node,
                        gate);
-    if (chi2)
+    if (chi2) {
+        // the vote words go with the partial buffer only (the sum gives every device all of them)
+        const bool vote = hb == g->hb_part && g->n_vote > 0 && g->chol;
         hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
-                           hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate);
+                           hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate, vote ? hb + dpg_gn_dev_vote_offset(g) : nullptr,
+                           g->scal3, vote ? dpg_chol_status_dev(g->chol) : nullptr, g->world, g->rank);
+    }
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -621,8 +636,20 @@ __global__ void vsum_kernel(VsumArgs a, int32_t k, int64_t n) {
 
 extern "C" int dpg_gn_dev_set_ownership(dpg_gn_dev* g, int32_t world, int32_t rank, void* stream) {
     if (world < 1 || rank < 0 || rank >= world) return DPG_ERR_ARG;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int32_t nv = world > 1 ? 2 * world : 0;
+    if (nv != g->n_vote) {   // the packed buffers grow by the vote words
+        if (hipStreamSynchronize(s) != hipSuccess) return DPG_ERR_HIP;
+        if (g->hb_own) (void)hipFree(g->hb_own);
+        if (g->hb_part) (void)hipFree(g->hb_part);
+        g->hb_own = g->hb_part = nullptr;
+        g->n_vote = nv;
+        if (dev_alloc(&g->hb_own, (size_t)dpg_gn_dev_hb_size(g))) return DPG_ERR_HIP;
+    }
     if (!g->mine && dev_alloc(&g->mine, (size_t)g->n_factors)) return DPG_ERR_HIP;
     if (!g->hb_part && dev_alloc(&g->hb_part, (size_t)dpg_gn_dev_hb_size(g))) return DPG_ERR_HIP;
+    // the other devices' vote words stay zero in this device's partial buffer
+    if (hipMemsetAsync(g->hb_part, 0, sizeof(double) * (size_t)dpg_gn_dev_hb_size(g), s) != hipSuccess) return DPG_ERR_HIP;
     g->world = world;
     g->rank = rank;
     if (g->n_factors > 0)
@@ -743,11 +770,15 @@ __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_wa
 // iteration decided exactly as the host loop does (dpg_api.hip gn_loop: the stop rule;
 // dpg_gn_dev_solve_async: the chord rule), and the solver's counters cleared for it
 // chi2_sum != NULL (multi-device forms): the error is the all-reduced sum already in hb, not this
-// device's per-node terms
+// device's per-node terms.  vote != NULL (world > 1): max |delta| and the status are taken from the
+// all-reduced vote words -- the largest |delta| and the largest status over the devices -- so every
+// device decides from the same numbers; devices whose |delta| differ (they solved different systems)
+// end the loop together with status DPG_GN_STATUS_DIVERGED
 __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const double* __restrict__ chi2_node, int64_t n,
                                                         double* chi2, const double* chi2_sum, int32_t* status,
                                                         double* max_out, dpg_gn_params P, dpg_gn_slot* slot,
-                                                        int32_t* sync, int64_t n_words) {
+                                                        int32_t* sync, int64_t n_words, const double* __restrict__ vote,
+                                                        int32_t world) {
     __shared__ double red[16];
     if (!ctl->active) return;   // uniform: nothing ran this iteration, nothing to report
     double sum = 0.0;
@@ -770,7 +801,20 @@ __global__ __launch_bounds__(1024) void pipe_ctl_kernel(dpg_gn_ctl* ctl, const d
     o.error = 0.0;
     o.status = 0.0;
     if (ctl->active) {
-        const double dinf = *max_out, nw = sum, st = st_word;
+        double dinf = *max_out, st = st_word;
+        if (vote) {
+            const unsigned long long d0 = (unsigned long long)__double_as_longlong(vote[0]);
+            bool diverged = false;
+            dinf = vote[0];
+            st = vote[world];
+            for (int32_t r = 1; r < world; ++r) {
+                diverged |= (unsigned long long)__double_as_longlong(vote[r]) != d0;
+                dinf = fmax(dinf, vote[r]);
+                st = fmax(st, vote[world + r]);
+            }
+            if (diverged) st = (double)DPG_GN_STATUS_DIVERGED;
+        }
+        const double nw = sum;
         const int it = ctl->it + 1;
         o.dinf = dinf;
         o.error = nw;
@@ -840,7 +884,8 @@ extern "C" int dpg_gn_pipe_issue_ctl(dpg_gn_dev* g, const dpg_gn_params* gp, dpg
     double* chi2 = g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes;
     hipLaunchKernelGGL(pipe_ctl_kernel, dim3(1), dim3(1024), 0, s, ctl, g->partials + 6 * (size_t)g->n_blocks_rows,
                        g->n_nodes, chi2, part ? chi2 : nullptr, const_cast<int32_t*>(dpg_chol_status_dev(g->chol)),
-                       g->scal3, *gp, slot, sync, n_words);
+                       g->scal3, *gp, slot, sync, n_words,
+                       part && g->n_vote > 0 ? g->hb_own + dpg_gn_dev_vote_offset(g) : nullptr, g->world);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 

@@ -21,6 +21,10 @@
 
 struct dpg_gn_dev;
 
+// the control kernel's status when the devices of a multi-device form report different max |delta|
+// (after the chol status words: 1 not positive definite, 2 a bounded wait expired)
+#define DPG_GN_STATUS_DIVERGED 3
+
 // control block on the device
 struct dpg_gn_ctl {
     int32_t active, reuse;          // the gate of the next iteration (gate_off in dpg_chol.hip)

@@ -140,6 +140,12 @@ typedef struct dpg_gn_dev {
     uint8_t* mine;                 /* [n_factors] or NULL */
     double* hb_part;               /* [hb size] or NULL */
     int32_t world, rank;
+    /* world > 1: the packed buffer ends in 2 world "vote" words -- this device's max |delta| at
+       [rank] and its solver status at [world + rank], zeros elsewhere -- so after the sum every
+       device holds every device's pair and takes its stop / chord decision from the same numbers
+       (dpg_gn_pipe.h): the ranks cannot disagree on the iteration count, and with it on the number
+       of collectives they issue */
+    int32_t n_vote;
 } dpg_gn_dev;
 
 /* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip); opts (dpg_chol.h, NULL =
@@ -163,6 +169,7 @@ int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n_nodes, const dpg_factor* factors, 
 const struct dpg_chol_opts* dpg_ctx_chol_opts(dpg_ctx* c);
 void dpg_gn_dev_free(dpg_gn_dev* g);
 int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g);
+int64_t dpg_gn_dev_vote_offset(const dpg_gn_dev* g);   /* first vote word of the packed buffer */
 int dpg_gn_dev_assemble(dpg_gn_dev* g, double* hb_dev, void* stream);
 /* enqueue the solve + retraction (max |delta| kept on device); no host synchronisation for the
    Cholesky solver */

@@ -223,6 +223,18 @@ class ChangeStats(C.Structure):
         return {k: int(getattr(self, k)) for k in self.COUNTERS}
 
 
+ALLREDUCE_F64 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int64)
+ALLREDUCE_F32 = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int64)
+ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+
+
+class CollOps(C.Structure):
+    """dpg_coll_ops -- the caller's blocking host-memory collectives (dpg_ctx_create_rank_ops)."""
+
+    _fields_ = [("user", C.c_void_p), ("allreduce_sum_f64", ALLREDUCE_F64), ("allreduce_sum_f32", ALLREDUCE_F32),
+                ("allgather", ALLGATHER)]
+
+
 SIGNATURES = {
     "dpg_last_error": (C.c_char_p, []),
     "dpg_version": (C.c_char_p, []),
@@ -233,6 +245,9 @@ SIGNATURES = {
     "dpg_ctx_num_gpus": (C.c_int32, [P]),
     "dpg_ctx_create_virtual": (P, [C.c_int32, C.c_int32]),
     "dpg_ctx_create_rank": (P, [C.c_int32, P, C.c_int32, C.c_int32]),
+    "dpg_ctx_create_rank_ops": (P, [C.c_int32, C.POINTER(CollOps), C.c_int32, C.c_int32]),
+    "dpg_shard_plan": (C.c_int, [F32P, C.c_int64, C.c_int32, I32P, I64P, I64P]),
+    "dpg_shard_reassemble": (C.c_int, [I32P, C.c_int64, C.c_int32, C.c_int64, C.c_int64, P, P]),
     "dpg_nccl_unique_id": (C.c_int, [P]),
     "dpg_ctx_num_ranks": (C.c_int32, [P]),
     "dpg_ctx_rank": (C.c_int32, [P]),

@@ -169,6 +169,28 @@ def results_array(n: int) -> np.ndarray:
     return np.zeros(n, RESULT_DTYPE)
 
 
+def shard_plan(n_edges: int, world: int, cost=None):
+    """dpg_shard_plan (host only): (owner[e], dispatch order, counts per rank) of the multi-device
+    forms -- LPT over `cost` when given, else e mod world."""
+    owner = np.zeros(max(n_edges, 1), np.int32)
+    disp = np.zeros(max(n_edges, 1), np.int64)
+    counts = np.zeros(world, np.int64)
+    c = None if cost is None else _f32(cost)
+    check(lib().dpg_shard_plan(ptr(c, C.c_float) if c is not None else None, n_edges, world, ptr(owner, C.c_int32),
+                               ptr(disp, C.c_int64), ptr(counts, C.c_int64)), "dpg_shard_plan")
+    return owner[:n_edges], disp[:n_edges], counts
+
+
+def shard_reassemble(owner: np.ndarray, world: int, slice_: int, gathered: np.ndarray, rec_bytes: int) -> np.ndarray:
+    """dpg_shard_reassemble (host only): the rank form's gathered slices back in the caller's order."""
+    owner = np.ascontiguousarray(owner, np.int32)
+    g = np.ascontiguousarray(gathered).view(np.uint8)
+    out = np.zeros(len(owner) * rec_bytes, np.uint8)
+    check(lib().dpg_shard_reassemble(ptr(owner, C.c_int32), len(owner), world, slice_, rec_bytes, vptr(g), vptr(out)),
+          "dpg_shard_reassemble")
+    return out
+
+
 # ------------------------------------------------------------------------- GPU context
 NCCL_ID_BYTES = 128
 
@@ -184,14 +206,21 @@ class Context:
     """One dpg_ctx (one GPU, one HIP stream).  Creating it without a usable GPU raises."""
 
     def __init__(self, device: int = 0, n_gpus: int | None = None, virtual: int | None = None,
-                 rank: tuple | None = None):
+                 rank: tuple | None = None, rank_ops: tuple | None = None):
         """n_gpus: a multi-GPU context over devices device .. device + n_gpus - 1
         (dpg_ctx_create_multi: one process, RCCL between the devices); virtual=k: k contexts on
         `device` sharing one stream, the all-reduce a device-side sum (dpg_ctx_create_virtual: the
         sharded paths on one card); rank=(nccl_id bytes, rank, world): this process's device as one
-        rank of a one-process-per-GPU job (dpg_ctx_create_rank); none of them: one device."""
+        rank of a one-process-per-GPU job (dpg_ctx_create_rank); rank_ops=(collective, rank, world):
+        the same over the caller's host collectives (dpg_ctx_create_rank_ops, e.g.
+        dist.HostCollective over gloo); none of them: one device."""
+        self._coll = None
         if virtual is not None:
             self.handle = lib().dpg_ctx_create_virtual(int(virtual), device)
+        elif rank_ops is not None:
+            coll, r, w = rank_ops
+            self._coll = coll   # its callbacks must outlive the context
+            self.handle = lib().dpg_ctx_create_rank_ops(device, C.byref(coll.ops), int(r), int(w))
         elif rank is not None:
             nid, r, w = rank
             buf = C.create_string_buffer(bytes(nid), NCCL_ID_BYTES)

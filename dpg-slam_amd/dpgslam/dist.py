@@ -157,3 +157,60 @@ class DeviceBackend:
 
     def fetch(self, hb):
         return self.ctx.gn_fetch(hb.data_ptr())
+
+
+class HostCollective:
+    """libdpg's rank form over a torch.distributed process group instead of RCCL
+    (dpg_ctx_create_rank_ops): the three blocking host-memory collectives of dpg_coll_ops -- the
+    cost all-reduce of the LPT plan, the results' all-gather, the packed system's all-reduce per
+    Gauss-Newton iteration -- as gloo calls.  The world > 1 rank form then runs where RCCL cannot
+    (several ranks on one card); `calls` counts what each rank issued (they must agree)."""
+
+    def __init__(self, group=None):
+        import ctypes as C
+        import torch
+        import torch.distributed as dist
+        from . import _abi
+        self.group, self.dist, self.torch, self.C = group, dist, torch, C
+        self.world = dist.get_world_size(group)
+        self.calls = {"allreduce_f64": 0, "allreduce_f32": 0, "allgather": 0}
+        self.error = None
+        # the C side keeps the function pointers: these thunks live as long as this object
+        self._f64 = _abi.ALLREDUCE_F64(self._allreduce_f64)
+        self._f32 = _abi.ALLREDUCE_F32(self._allreduce_f32)
+        self._ag = _abi.ALLGATHER(self._allgather)
+        self.ops = _abi.CollOps(None, self._f64, self._f32, self._ag)
+
+    def _guard(self, fn):
+        try:
+            fn()
+            return 0
+        except Exception as e:   # reported to libdpg as a failed collective
+            self.error = e
+            return 1
+
+    def _allreduce(self, buf, n, dtype, key):
+        def run():
+            a = np.ctypeslib.as_array(buf, shape=(int(n),))
+            t = self.torch.from_numpy(a)          # shares the C buffer: summed in place
+            self.dist.all_reduce(t, group=self.group)
+            self.calls[key] += 1
+        return self._guard(run)
+
+    def _allreduce_f64(self, user, buf, n):
+        return self._allreduce(buf, n, np.float64, "allreduce_f64")
+
+    def _allreduce_f32(self, user, buf, n):
+        return self._allreduce(buf, n, np.float32, "allreduce_f32")
+
+    def _allgather(self, user, send, recv, nbytes):
+        def run():
+            nb = int(nbytes)
+            src = np.ctypeslib.as_array(self.C.cast(send, self.C.POINTER(self.C.c_uint8)), shape=(nb,))
+            dst = np.ctypeslib.as_array(self.C.cast(recv, self.C.POINTER(self.C.c_uint8)), shape=(nb * self.world,))
+            outs = [self.torch.empty(nb, dtype=self.torch.uint8) for _ in range(self.world)]
+            self.dist.all_gather(outs, self.torch.from_numpy(src.copy()), group=self.group)
+            for r, o in enumerate(outs):
+                dst[r * nb:(r + 1) * nb] = o.numpy()
+            self.calls["allgather"] += 1
+        return self._guard(run)

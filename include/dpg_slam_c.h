@@ -164,6 +164,29 @@ dpg_ctx* dpg_ctx_create_multi(int32_t n_gpus, const int32_t* devices);
 #define DPG_NCCL_ID_BYTES 128
 int dpg_nccl_unique_id(void* id_out /*[DPG_NCCL_ID_BYTES]*/);
 dpg_ctx* dpg_ctx_create_rank(int32_t device, const void* nccl_id, int32_t rank, int32_t world);
+/* The same one-process-per-GPU form over the CALLER's collectives instead of RCCL: a host that
+ * already runs a communicator (MPI, gloo), or ranks that share one card (RCCL refuses a second rank
+ * on a device -- the one-GPU test box runs the world > 1 rank form this way).  Three blocking calls
+ * on host memory, made by every rank in the same order with the same sizes, each returning 0 on
+ * success: the float sum of the alignment costs (the LPT plan), the all-gather of the results, the
+ * fp64 sum of the packed [H upper | g | chi2 | votes] per Gauss-Newton iteration. */
+typedef struct dpg_coll_ops {
+    void* user;
+    int (*allreduce_sum_f64)(void* user, double* buf, int64_t n);               /* in place */
+    int (*allreduce_sum_f32)(void* user, float* buf, int64_t n);                /* in place */
+    int (*allgather)(void* user, const void* send, void* recv, int64_t bytes);  /* recv: world * bytes, rank order */
+} dpg_coll_ops;
+dpg_ctx* dpg_ctx_create_rank_ops(int32_t device, const dpg_coll_ops* ops, int32_t rank, int32_t world);
+/* Host helpers of the multi-device forms (no device call): the batch's assignment over `world` ranks
+ * -- cost == NULL: edge e on rank e mod world in the caller's order; else longest-processing-time
+ * (longest first to the least-loaded rank; ties: lower index, lower rank) -- as owner[e] and every
+ * rank's dispatch order (rank 0's counts[0] edges first, then rank 1's, ...); and the rank form's
+ * all-gathered results (slice r = rank r's records, its edges ascending, `slice` records reserved
+ * per rank) back into the caller's order. */
+int dpg_shard_plan(const float* cost, int64_t n_edges, int32_t world, int32_t* owner, int64_t* dispatch,
+                   int64_t* counts);
+int dpg_shard_reassemble(const int32_t* owner, int64_t n_edges, int32_t world, int64_t slice, int64_t rec_bytes,
+                         const void* gathered, void* out);
 /* Test / rehearsal form: k "devices" that are k contexts on ONE device sharing one stream, the
  * all-reduce a device-side sum in rank order.  Every sharded path of the multi-device forms runs
  * with k > 1 on one card (k <= 16). */

@@ -169,3 +169,86 @@ def test_interleaved_shares(world):
     F["i"], F["j"] = np.arange(first + E), -1
     G = plans[0].factors(F, first)
     assert np.array_equal(G["i"][:first], np.arange(first)) and np.array_equal(G["i"][first:], first + perm)
+
+
+def _lpt_reference(cost, world):
+    """longest-processing-time, restated: edges by cost descending (stable), each to the rank with
+    the least load so far (lowest rank among equals)."""
+    order = sorted(range(len(cost)), key=lambda e: -float(np.float32(cost[e])))
+    load = [0.0] * world
+    owner = [0] * len(cost)
+    disp = [[] for _ in range(world)]
+    for e in order:
+        r = min(range(world), key=lambda q: (load[q], q))
+        owner[e] = r
+        load[r] += float(np.float32(cost[e]))
+        disp[r].append(e)
+    return owner, disp
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("measured", [False, True])
+def test_shard_plan_and_rank_form_gather(world, measured):
+    """dpg_shard_plan / dpg_shard_reassemble (libdpg host code, no GPU): the assignment equals the
+    restated LPT (or e mod world), every rank's dispatch list covers its edges, and the rank form's
+    all-gather -- each rank's results in its local order (its edges ascending, as stage_device
+    numbers them), padded to the largest share -- comes back in the caller's order, record for record
+    (the rank form's reassembly was only reachable with world > 1 on GPUs)."""
+    from dpgslam import api
+    rng = np.random.default_rng(world * 10 + measured)
+    ne = 997
+    cost = (rng.integers(1, 60, ne) * rng.integers(200, 1200, ne)).astype(np.float32) if measured else None
+    if measured:
+        cost[::50] = cost[1]   # ties: lower index first
+    owner, disp, counts = api.shard_plan(ne, world, cost)
+    if measured:
+        ro, rd = _lpt_reference(cost, world)
+        assert owner.tolist() == ro
+        assert np.concatenate([np.asarray(d, np.int64) for d in rd]).tolist() == disp.tolist()
+    else:
+        assert np.array_equal(owner, np.arange(ne) % world)
+    assert counts.sum() == ne and np.array_equal(np.sort(disp), np.arange(ne))
+    first = np.r_[0, np.cumsum(counts)]
+    rec = 24
+    slice_ = int(max(counts.max(), 1))
+    gathered = np.zeros((world, slice_, rec), np.uint8)
+    for r in range(world):
+        mine = disp[first[r]:first[r + 1]]
+        assert np.all(owner[mine] == r)
+        local = np.sort(mine)                                # result j of rank r is edge local[j]
+        for j, e in enumerate(local):
+            gathered[r, j] = np.frombuffer(np.array([e, e * 7 + r, -e], np.int64).tobytes(), np.uint8)
+    out = api.shard_reassemble(owner, world, slice_, gathered.reshape(-1), rec).view(np.int64).reshape(ne, 3)
+    assert np.array_equal(out[:, 0], np.arange(ne)) and np.array_equal(out[:, 1], np.arange(ne) * 7 + owner)
+
+
+def _coll_worker(rank, world, port, out):
+    import ctypes as C
+    import torch.distributed as dist
+    from dpgslam import dist as D
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    coll = D.HostCollective()
+    a = np.arange(5, dtype=np.float64) * (rank + 1)
+    f = np.full(3, rank + 0.5, np.float32)
+    send = np.frombuffer(bytes([rank] * 7), np.uint8).copy()
+    recv = np.zeros(7 * world, np.uint8)
+    rc = [coll.ops.allreduce_sum_f64(None, a.ctypes.data_as(C.POINTER(C.c_double)), 5),
+          coll.ops.allreduce_sum_f32(None, f.ctypes.data_as(C.POINTER(C.c_float)), 3),
+          coll.ops.allgather(None, send.ctypes.data, recv.ctypes.data, 7)]
+    out[rank] = (rc, a.copy(), f.copy(), recv.copy(), dict(coll.calls))
+    dist.destroy_process_group()
+
+
+def test_host_collective_over_gloo():
+    """dist.HostCollective -- the dpg_coll_ops callbacks libdpg's rank form calls through
+    dpg_ctx_create_rank_ops -- sums in place and gathers in rank order over gloo (world 2)."""
+    import torch.multiprocessing as mp
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_coll_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        rc, a, f, recv, calls = out[r]
+        assert rc == [0, 0, 0]
+        assert np.array_equal(a, np.arange(5) * 3.0) and np.array_equal(f, np.full(3, 2.0, np.float32))
+        assert recv.tolist() == [0] * 7 + [1] * 7
+        assert calls == {"allreduce_f64": 1, "allreduce_f32": 1, "allgather": 1}

@@ -10,39 +10,7 @@ factorization counts for dpg_optimize_graph, dpg_reoptimize and the step form th
 import numpy as np
 import pytest
 
-from conftest import angle_wrap
-
-
-def _perr(A, B):
-    return float(np.abs(np.concatenate([A[:, :2] - B[:, :2], angle_wrap(A[:, 2:] - B[:, 2:])], 1)).max())
-
-
-def _run_all(ctx, w, p):
-    """ICP batch (+ covariance) twice (the second run re-plans from the first run's costs), the
-    graph solve, the bench's step form, and a sweep."""
-    from dpgslam import _abi
-    ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
-    res1, hess1 = ctx.icp_batch(w.edges, w.est, p, compute_cov=True)
-    ctx.icp_run(compute_cov=True)           # again: the measured schedule now (LPT + longest first)
-    res2, hess2 = ctx.icp_fetch(with_hessian=True)
-    F = w.factors_with_icp(res1, p)
-    X, st = ctx.optimize_graph(w.est.astype(np.float64), F)
-    # the bench's step: the staged batch's results become factors on the device(s) that aligned them
-    ctx.icp_prepare(w.edges, w.est, p)
-    ctx.icp_run(compute_cov=False)
-    gp = _abi.default_gn_params()
-    ctx.gn_setup(w.V, w.factors_placeholder(), params=gp)
-    ctx.gn_take_icp(w.icp_factor_first, w.E, w.n_successive, p)
-    ctx.gn_set_poses(w.est.astype(np.float64))
-    sst, Xs = ctx.gn_run(w.V)
-    nfs = ctx.gn_factorizations()
-    passes = np.zeros(w.V, np.int32)
-    passes[w.V // 2:] = 1
-    Xr, sr = ctx.reoptimize(passes, w.est, w.odom)
-    rr, _ = ctx.icp_fetch(with_hessian=False)
-    return dict(res1=res1.tobytes(), hess1=np.asarray(hess1).tobytes(), res2=res2.tobytes(),
-                hess2=np.asarray(hess2).tobytes(), X=X, it=st.iterations, Xs=Xs, its=sst["iterations"], nfs=nfs,
-                err_s=sst["final_error"], Xr=Xr, itr=sr.gn.iterations, nlc=sr.n_loop_closures, rr=rr.tobytes())
+from multi_common import compare, perr, run_all, run_step
 
 
 @pytest.fixture(scope="module")
@@ -51,7 +19,7 @@ def single_run(workload):
     w = workload("config3")
     p = _abi.default_icp_params()
     with api.Context(0) as c:
-        return _run_all(c, w, p)
+        return run_all(c, w, p)
 
 
 @pytest.mark.gpu
@@ -62,14 +30,40 @@ def test_virtual_devices_equal_single_device(workload, single_run, k):
     p = _abi.default_icp_params()
     with api.Context(0, virtual=k) as c:
         assert c.n_gpus == k and c.n_ranks == k
-        out = _run_all(c, w, p)
-    a = single_run
-    for key in ("res1", "hess1", "res2", "hess2", "rr"):
-        assert out[key] == a[key], f"{key} differs from the single-device context"
-    assert out["it"] == a["it"] and _perr(out["X"], a["X"]) < 1e-9
-    assert out["its"] == a["its"] and out["nfs"] == a["nfs"] and _perr(out["Xs"], a["Xs"]) < 1e-9
-    assert abs(out["err_s"] - a["err_s"]) <= 1e-9 * max(1.0, abs(a["err_s"]))
-    assert out["itr"] == a["itr"] and out["nlc"] == a["nlc"] and _perr(out["Xr"], a["Xr"]) < 1e-9
+        out = run_all(c, w, p)
+    compare(out, single_run)
+
+
+@pytest.fixture(scope="module")
+def single_step4(workload):
+    from dpgslam import _abi, api
+    w = workload("config4")
+    p = _abi.default_icp_params()
+    with api.Context(0) as c:
+        c.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
+        return run_step(c, w, p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("schedule", ["caller", "measured"])
+def test_virtual8_config4_equals_single_device(workload, single_step4, schedule):
+    """The target world size at the headline size (BASELINE config 4, 8 GPUs): k = 8 virtual
+    devices run the bench step twice (the second run planned from measured costs under 'measured')
+    -- every ICP result and covariance block byte-identical to one device, the same GN iterations
+    and factorizations, poses within 1e-9."""
+    from dpgslam import _abi, api
+    w = workload("config4")
+    p = _abi.default_icp_params()
+    with api.Context(0, virtual=8) as c:
+        assert c.n_gpus == 8 and c.n_ranks == 8
+        c.set_icp_schedule(schedule)
+        c.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
+        out = run_step(c, w, p)
+    for k in (0, 1):
+        assert out[f"rs{k}"] == single_step4[f"rs{k}"], f"ICP results of run {k} differ"
+        assert out[f"hs{k}"] == single_step4[f"hs{k}"], f"covariance blocks of run {k} differ"
+        assert out[f"its{k}"] == single_step4[f"its{k}"] and out[f"nfs{k}"] == single_step4[f"nfs{k}"]
+        assert perr(out[f"Xs{k}"], single_step4[f"Xs{k}"]) < 1e-9
 
 
 @pytest.mark.gpu
@@ -80,18 +74,13 @@ def test_multi_ctx_one_gpu_equals_single_device(workload, single_run):
     p = _abi.default_icp_params()
     with api.Context(0, n_gpus=1) as c:
         assert c.n_gpus == 1 and c.n_ranks == 1
-        out = _run_all(c, w, p)
+        out = run_all(c, w, p)
         # the per-iteration step API and the incremental graph want a single-device context
         with pytest.raises(_abi.DpgError):
             api.IncGraph(c)
         with pytest.raises(_abi.DpgError):
             c.gn_assemble()
-    a = single_run
-    for key in ("res1", "hess1", "res2", "hess2", "rr"):
-        assert out[key] == a[key], key
-    assert out["X"].tobytes() == a["X"].tobytes() and out["it"] == a["it"]
-    assert out["Xs"].tobytes() == a["Xs"].tobytes() and out["its"] == a["its"] and out["nfs"] == a["nfs"]
-    assert out["Xr"].tobytes() == a["Xr"].tobytes() and out["itr"] == a["itr"] and out["nlc"] == a["nlc"]
+    compare(out, single_run, exact_poses=True)
 
 
 @pytest.mark.gpu
@@ -104,11 +93,36 @@ def test_rank_form_one_rank_equals_single_device(workload, single_run):
     assert len(nid) == api.NCCL_ID_BYTES
     with api.Context(0, rank=(nid, 0, 1)) as c:
         assert c.n_ranks == 1 and c.rank == 0
-        out = _run_all(c, w, p)
-    a = single_run
-    for key in ("res1", "hess1", "res2", "rr"):
-        assert out[key] == a[key], key
-    assert out["Xs"].tobytes() == a["Xs"].tobytes() and out["its"] == a["its"]
+        out = run_all(c, w, p)
+    compare(out, single_run, exact_poses=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["config3", "config4"])
+def test_rank_form_two_ranks_on_one_card(cfg):
+    """dpg_ctx_create_rank_ops at world = 2: two processes share the card, libdpg's rank form with
+    gloo as its collective (tools/rank_check.py) -- the cost all-reduce of the LPT plan, the results'
+    all-gather, factor ownership by global rank and the packed system's all-reduce per iteration all
+    run for real.  Both schedules; each rank's results byte-identical to a single-device context, the
+    same iteration / factorization counts, poses within 1e-9, and the ranks issued the same
+    collectives."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([root, os.path.join(root, "dpg-slam_amd"),
+                                                         os.path.join(root, "tests")]))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(root, "tools", "rank_check.py"), cfg],
+                       capture_output=True, text=True, timeout=240, env=env)
+    print(r.stdout[-3000:])
+    assert r.returncode == 0 and r.stdout.count("rank check ok") == 2, (r.stdout + r.stderr)[-4000:]
 
 
 @pytest.mark.gpu
