@@ -59,7 +59,7 @@ def compare(out, ref, exact_poses=False):
     for key in BYTE_KEYS:
         if key in ref:
             assert out[key] == ref[key], f"{key} differs from the single-device context"
-    pose_keys = [("X", "it"), ("Xs0", "its0"), ("Xs1", "its1")] + ([("Xr", "itr")] if "Xr" in ref else [])
+    pose_keys = [(x, i) for x, i in (("X", "it"), ("Xs0", "its0"), ("Xs1", "its1"), ("Xr", "itr")) if x in ref]
     for xk, ik in pose_keys:
         assert out[ik] == ref[ik], (ik, out[ik], ref[ik])
         if exact_poses:

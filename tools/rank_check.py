@@ -12,6 +12,8 @@ usage: python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.
 import os
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dpg-slam_amd"), os.path.join(ROOT, "tests")]
 
@@ -33,9 +35,19 @@ def main():
 
     def run(c):
         if small:
-            return run_all(c, w, p)
-        c.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
-        return run_step(c, w, p)
+            out = run_all(c, w, p)
+        else:
+            c.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
+            out = run_step(c, w, p)
+        # pairs never aligned before (the edges reversed), run twice before any fetch: under the
+        # measured schedule the second run plans from the first run's costs, all-reduced over ranks
+        e2 = np.ascontiguousarray(w.edges[:, ::-1])
+        c.icp_prepare(e2, w.est, p)
+        c.icp_run(compute_cov=False)
+        c.icp_run(compute_cov=False)
+        r2, _ = c.icp_fetch(with_hessian=False)
+        out["rev"] = r2.tobytes()
+        return out
 
     coll = D.HostCollective()
     outs = {}
@@ -49,6 +61,7 @@ def main():
         ref = run(s)
     for sched, out in outs.items():
         try:
+            assert out["rev"] == ref["rev"], "reversed-pair batch differs"
             compare(out, ref)
         except AssertionError as e:
             raise AssertionError(f"rank {rank}, schedule {sched}: {e}") from None
