@@ -835,6 +835,30 @@ int dpg_inc_save(dpg_inc* q, const char* path) {
     return ok ? DPG_OK : set_err(DPG_ERR_HIP, "dpg_inc_save: write failed");
 }
 
+// The graph's state as host copies -- dpg_inc_save's arrays without the scans (a test's oracle
+// takes over from it: tests/test_config5.py lockstep)
+int64_t dpg_inc_export(dpg_inc* q, int64_t* updates, dpg_factor* F, int32_t* created, int64_t cap_factors, double* theta,
+                       double* est, double* maxd) {
+    if (!q || cap_factors < 0) return set_err(DPG_ERR_ARG, "dpg_inc_export: bad arguments");
+    if (q->prepared) return set_err(DPG_ERR_STATE, "dpg_inc_export: an update is prepared but not applied");
+    const int64_t nf = (int64_t)q->F.size();
+    if (updates) *updates = q->updates;
+    const size_t k = (size_t)std::min(nf, cap_factors);
+    if (F && k) memcpy(F, q->F.data(), sizeof(dpg_factor) * k);
+    if (created && k) memcpy(created, q->f_created.data(), sizeof(int32_t) * k);
+    const size_t V = (size_t)q->V;
+    hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
+    if (V && (theta || est || maxd)) {
+        if (hipSetDevice(dpg_ctx_device_of(q->ctx)) != hipSuccess) return set_err(DPG_ERR_HIP, "hipSetDevice failed");
+        if ((theta && hipMemcpyAsync(theta, q->theta, sizeof(double) * 3 * V, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+            (est && hipMemcpyAsync(est, q->est, sizeof(double) * 3 * V, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+            (maxd && hipMemcpyAsync(maxd, q->maxd, sizeof(double) * V, hipMemcpyDeviceToHost, s) != hipSuccess) ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return set_err(DPG_ERR_HIP, "dpg_inc_export: read-back failed");
+    }
+    return nf;
+}
+
 // A graph restored from dpg_inc_save on ctx (single device): the scan store is replaced by the
 // file's (and indexed), the factors, pairs, linearization points, estimate, per-variable |delta| and
 // update count are the saved ones, so the next dpg_add_node / dpg_inc_update continues the saved

@@ -336,6 +336,7 @@ SIGNATURES = {
     "dpg_inc_get_poses": (C.c_int, [P, F64P, C.c_int64]),
     "dpg_inc_save": (C.c_int, [P, C.c_char_p]),
     "dpg_inc_load": (P, [P, C.c_char_p]),
+    "dpg_inc_export": (C.c_int64, [P, I64P, P, I32P, C.c_int64, F64P, F64P, F64P]),
     "dpg_scans_append": (C.c_int, [P, F32P, I64P, C.c_int64, C.c_int32]),
     "dpg_add_node": (C.c_int, [P, F32P, C.c_int64, I32P, F32P, P, C.c_int64, C.POINTER(IcpParams),
                                C.POINTER(ReoptParams), C.c_int32, C.POINTER(AddNodeStats)]),

@@ -643,6 +643,25 @@ class IncGraph:
         """dpg_inc_save: the graph and its context's scan store to one checkpoint file."""
         check(lib().dpg_inc_save(self.handle, os.fsencode(path)), "dpg_inc_save")
 
+    def export_state(self) -> dict:
+        """dpg_inc_export: the update count, factors (+ the update that added each), linearization
+        points, estimate and last max |delta| per node, as host arrays."""
+        L = lib()
+        n = L.dpg_inc_export(self.handle, None, None, None, 0, None, None, None)
+        if n < 0:
+            check(int(n), "dpg_inc_export")
+        V = self.V
+        upd = C.c_int64(0)
+        F = np.zeros(max(n, 1), FACTOR_DTYPE)
+        cr = np.zeros(max(n, 1), np.int32)
+        th, es, md = np.zeros((max(V, 1), 3)), np.zeros((max(V, 1), 3)), np.zeros(max(V, 1))
+        m = L.dpg_inc_export(self.handle, C.byref(upd), vptr(F), ptr(cr, C.c_int32), n, ptr(th, C.c_double),
+                             ptr(es, C.c_double), ptr(md, C.c_double))
+        if m < 0:
+            check(int(m), "dpg_inc_export")
+        return {"updates": int(upd.value), "factors": F[:n], "created": cr[:n], "theta": th[:V], "est": es[:V],
+                "maxd": md[:V]}
+
     @classmethod
     def load(cls, ctx: Context, path: str) -> "IncGraph":
         """dpg_inc_load: a graph restored from a checkpoint on ctx (ctx's scan store is replaced)."""

@@ -507,6 +507,12 @@ int dpg_inc_get_poses(dpg_inc* g, double* poses, int64_t n);
  * a file of another version or layout is rejected. */
 int dpg_inc_save(dpg_inc* g, const char* path);
 dpg_inc* dpg_inc_load(dpg_ctx* ctx, const char* path);
+/* The graph's state as host copies (the checkpoint's arrays without the scans): the update count,
+ * the factors and the update that added each (up to cap_factors of them), the linearization points
+ * theta [3 V], the estimate [3 V] and the last max |delta| per node [V] (V = dpg_inc_num_nodes);
+ * any pointer may be NULL.  Returns the number of factors, negative on error. */
+int64_t dpg_inc_export(dpg_inc* g, int64_t* updates, dpg_factor* factors, int32_t* created, int64_t cap_factors,
+                       double* theta, double* est, double* maxd);
 
 /* Append nodes to the uploaded scan store (dpg_scans_upload's layout): pts_xy = the new nodes' full
  * clouds concatenated, node_offsets[n_new + 1] relative to pts_xy; the downsample ratio must match

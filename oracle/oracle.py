@@ -460,3 +460,14 @@ class OracleIncGraph:
 
     def poses(self):
         return self.est.copy()
+
+    def load_state(self, st):
+        """Take over another graph's state (api.IncGraph.export_state: the GPU graph's update count,
+        factors with their creating update, theta, estimate, max |delta|) -- the lockstep tests run
+        the next update from exactly the GPU's state."""
+        self.updates = int(st["updates"])
+        self.F = np.asarray(st["factors"], self._abi.FACTOR_DTYPE).copy()
+        self.created = np.asarray(st["created"], np.int64).copy()
+        self.theta = np.asarray(st["theta"], np.float64).reshape(-1, 3).copy()
+        self.est = np.asarray(st["est"], np.float64).reshape(-1, 3).copy()
+        self.maxd = np.asarray(st["maxd"], np.float64).copy()

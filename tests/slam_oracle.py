@@ -33,8 +33,10 @@ class OracleSlamBackend:
                     edges.append((i, pv))
         F = [np.asarray(extra, _abi.FACTOR_DTYPE).reshape(-1)]
         n_icp = 0
+        self.last_edges, self.last_results = edges, []
         for k, (a, b) in enumerate(edges):
             res, _, _ = O.run_icp(self.clouds[b], self.clouds[a], pf[b], pf[a], icp_params, O.NN_GRID)
+            self.last_results.append(bytes(res))
             ok = bool(res.converged) and res.status == _abi.DPG_ICP_OK
             if k == 0 or ok:
                 F.append(_icp_factor(res, a, b, icp_params))

@@ -48,20 +48,30 @@ def test_slam_driver_oracle_backend():
 
 @pytest.mark.gpu
 def test_slam_driver_gpu_matches_oracle():
-    """Same nodes and factors after every scan, exactly.  Poses to 1e-5, labels to 0.1 %: the two
-    incremental solves agree to ~1e-13 relative (their Cholesky factors sum in different orders),
-    and the driver keeps float32 poses (dpg_nodes_ positions are float); a double that differs in
-    its last bits across a float rounding boundary moves an ICP guess by one float ulp, which can
-    change that alignment's last iterations (bit-exact ICP parity holds for equal inputs,
-    tests/test_gpu_parity.py) and, through the graph, later poses by ~1e-6 and the occupancy cell
-    of a point on a cell boundary."""
+    """The GPU run against the oracle in lockstep (tests/slam_lockstep.py): at EVERY node the oracle
+    takes over the GPU graph's state and repeats dpg_add_node -- the node's alignments bit for bit,
+    its ISAM2-semantics update within 1e-9 -- and every executeDPG call from the GPU store's state,
+    counters and node state bit for bit; the reoptimize sweep's candidates, alignments and update
+    likewise.  A free-running oracle run besides gives the same nodes and factors after every scan.
+    (The free-running poses alone could only be compared to ~1e-5: the driver keeps float poses,
+    dpg_slam.cc:327, so a 1e-13 solver difference can flip an ulp of a guess and reroute a later
+    alignment; the lockstep removes that drift from the comparison.)"""
+    from dpgslam import api
+    from slam_lockstep import LockstepBackend
     w = _workload()
-    so, sg = DpgSLAM(backend=OracleSlamBackend()), DpgSLAM(backend="gpu")
-    to, tg = _drive(so, w, 14), _drive(sg, w, 14)
-    assert to == tg                                    # same nodes and factors after every scan
-    Xo, Xg = np.stack(so.poses), np.stack(sg.poses)
-    assert np.abs(Xo - Xg).max() < 1e-5, np.abs(Xo - Xg).max()
-    lo, _, ao = so._store.fetch()
-    lg, _, ag = sg._store.fetch()
-    assert np.array_equal(ao, ag) and (lo != lg).mean() < 1e-3
-    np.testing.assert_allclose(sg.GetMap(), so.GetMap(), atol=1e-4)
+    ctx = api.Context(0)
+    be = LockstepBackend(ctx, every=1, dpg_every=1, sweep_sample=10 ** 6)
+    sg = DpgSLAM(backend=be)
+    be.clouds_of = lambda: sg.clouds
+    tg = _drive(sg, w, 14)
+    so = DpgSLAM(backend=OracleSlamBackend())
+    assert _drive(so, w, 14) == tg                      # same nodes and factors after every scan
+    V = len(sg.poses)
+    n_later = int(np.sum(np.asarray(sg.node_pass) >= 1))
+    assert be.checked["nodes"] == V and be.checked["dpg"] == n_later and be.checked["sweeps"] == 1, be.checked
+    assert be.checked["icp"] >= V - 1 and be.checked["sweep_icp"] >= V - 1
+    print("lockstep", be.checked, "max pose diff", be.max_pose_diff)
+    from oracle import oracle as O
+    pts, offs = sg._clouds()
+    assert np.array_equal(sg.GetMap(), O.get_map(pts, offs, sg.poses, sg.fraction))
+    ctx.close()
