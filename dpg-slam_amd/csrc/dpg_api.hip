@@ -112,7 +112,7 @@ struct dpg_ctx {
     bool cov_pending = false, cov_on_aux = false;
     int32_t icp_variant = DPG_ICP_ANGULAR;
     int32_t defer_cap = 256;        // angular ICP: cooperative-queue threshold (dpg_ctx_set_icp_defer_cap)
-    int32_t cov_wg = 0;             // covariance kernel workgroups beside the pose graph (dpg_ctx_set_cov_workgroups)
+    int32_t cov_wg = 256;           // covariance kernel workgroups beside the pose graph (dpg_ctx_set_cov_workgroups)
     int32_t kernel_variant = 0;     // angular ICP kernel form (dpg_ctx_set_icp_kernel_variant, A/B)
     float map_ms = 0.f;             // last dpg_get_map kernel (HIP events map_ev)
     hipEvent_t map_ev[2] = {};
@@ -638,6 +638,7 @@ static int scans_append_1(dpg_ctx* c, const float* pts, const int64_t* off, int6
 // clouds per device), so any edge can be aligned on any device
 int dpg_scans_upload(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V, int32_t ratio) {
     if (!c) return fail(DPG_ERR_ARG, "dpg_scans_upload: bad arguments");
+    c->cost.clear();   // a new store: node ids name other scans
     for (int k = 0; k < n_dev(c); ++k) {
         const int rc = scans_upload_1(dev_ctx(c, k), pts, off, V, ratio);
         if (rc) return rc;
@@ -823,6 +824,7 @@ static int build_batch(dpg_ctx* c, const int32_t* edges, int64_t ne, const float
     return DPG_OK;
 }
 
+constexpr size_t kCostMemoryCap = (size_t)1 << 22;   // pairs remembered (~100 MB of hash map at most)
 inline uint64_t pair_key(const dpg_icp_edge& E) { return (uint64_t)(uint32_t)E.tgt_node << 32 | (uint32_t)E.src_node; }
 // what an alignment costs: its iterations, each a search over both clouds
 inline float edge_cost(const dpg_icp_edge& E, int32_t iterations) {
@@ -1107,8 +1109,13 @@ static int fetch_allgather(dpg_ctx* c, void* out, size_t rec_bytes, const void* 
 }
 
 // Results of the staged batch in the caller's order (and the covariance blocks).  On the rank form
-// this is a collective: every rank receives every edge's result.
-int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
+// this is a collective: every rank receives every edge's result.  learn: the alignment costs go into
+// the context's cost memory (the next plan of the same pairs); the per-node path, whose pairs are
+// never re-planned, does not learn (the memory grew by every node's pairs).
+static int batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess, bool learn);
+int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) { return batch_fetch(c, results, hess, true); }
+
+static int batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess, bool learn) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
     if (hess && !c->have_cov && !c->batch.empty()) return fail(DPG_ERR_STATE, "last batch ran without compute_cov");
     const int64_t ne = (int64_t)c->batch.size();
@@ -1138,10 +1145,17 @@ int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) {
             }
         }
     }
-    for (int64_t e = 0; e < ne; ++e) c->cost[pair_key(c->batch[(size_t)e])] = edge_cost(c->batch[(size_t)e], R[e].iterations);
+    if (learn) {
+        if (c->cost.size() + (size_t)ne > kCostMemoryCap) c->cost.clear();   // bounded: a long session's old pairs go
+        for (int64_t e = 0; e < ne; ++e) c->cost[pair_key(c->batch[(size_t)e])] = edge_cost(c->batch[(size_t)e], R[e].iterations);
+    }
     HIP_TRY(hipSetDevice(c->device));
     return DPG_OK;
 }
+
+// edges of the staged batch (dpg_icp_batch_prepare's, or the one a sweep / dpg_add_node staged):
+// what dpg_icp_batch_fetch writes
+int64_t dpg_icp_batch_size(dpg_ctx* c) { return c ? (int64_t)c->batch.size() : fail(DPG_ERR_ARG, "ctx is NULL"); }
 
 int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t* max_src_out) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
@@ -2200,7 +2214,7 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
             if ((rc = dpg_inc_prepare(g, 1, pr.data(), (int64_t)pr.size() / 2))) return rc;
         }
         std::vector<dpg_icp_result> res((size_t)E);
-        if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+        if ((rc = batch_fetch(c, res.data(), nullptr, false))) return rc;
         S.ms_icp = now_ms() - t0;
         S.n_icp_edges = E;
         for (int64_t e = 0; e < E; ++e)   // a failed kernel self-check is an error, never a factor

@@ -118,6 +118,8 @@ int dpg_chol_create_sym_upload(void** h);
 // upload of the same object (the incremental prepare runs it beside dpg_incsym_derive)
 int dpg_chol_plan_blocks(void** h, int64_t n, const int32_t* pos, const int32_t* perm, const int32_t* pair_lo,
                          const int32_t* pair_hi, int64_t n_pairs);
+/* drops buckets prebuilt by dpg_chol_plan_blocks (the next plan builds its own) */
+void dpg_chol_blocks_invalidate(void* h);
 // host time (ms) of the last build of h: structures, uploads
 void dpg_chol_build_times(void* h, double out[2]);
 // 1 when h factors with the fused DAG kernel (every front fits its LDS budget), 0 on the level path

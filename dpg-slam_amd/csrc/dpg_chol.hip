@@ -2469,6 +2469,11 @@ int dpg_chol_plan_blocks(void** h, int64_t n, const int32_t* pos, const int32_t*
     H.blocks_ready = true;
     return DPG_OK;
 }
+// drop prebuilt H-block buckets (their ordering was not the one the next plan will carry: the
+// derivation they were built beside failed)
+void dpg_chol_blocks_invalidate(void* h) {
+    if (h) build_host(reinterpret_cast<CholDev*>(h)).blocks_ready = false;
+}
 int dpg_chol_create_sym_upload(void** h) {
     CholDev* c = reinterpret_cast<CholDev*>(*h);
     if (!c) return DPG_ERR_STATE;

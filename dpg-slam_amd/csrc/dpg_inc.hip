@@ -549,15 +549,19 @@ int prep_symbolic(dpg_inc* q, int64_t V1, int64_t n_new, const std::vector<std::
     // the plan's first part needs only the order (I's, which the derivation copies into S) and the
     // pairs: on the helper thread while this one derives the column patterns and supernodes
     const bool ahead = V1 >= 256;
+    int hrc = DPG_OK;
     if (ahead) {
         if (!q->helper) q->helper.reset(new dpg_inc_helper());
-        q->helper->post([q, V1] {
-            (void)dpg_chol_plan_blocks(&q->g.chol, V1, q->I.pos.data(), q->I.perm.data(), q->plo.data(), q->phi.data(),
+        q->helper->post([q, V1, &hrc] {
+            hrc = dpg_chol_plan_blocks(&q->g.chol, V1, q->I.pos.data(), q->I.perm.data(), q->plo.data(), q->phi.data(),
                                        (int64_t)q->plo.size());
         });
     }
     const int drc = dpg_incsym_derive(&q->I, &q->opts, &q->S);
     if (ahead) q->helper->wait();
+    // buckets built for a derivation that failed (or a helper that failed) must not reach a later
+    // plan of the same size: the plan then builds its own
+    if (ahead && (drc || hrc)) dpg_chol_blocks_invalidate(q->g.chol);
     if (drc) {
         q->prep_msg = "dpg_inc_prepare: symbolic derivation failed";
         return DPG_ERR_NUMERIC;

@@ -283,6 +283,7 @@ SIGNATURES = {
     "dpg_icp_batch_run": (C.c_int, [P, C.c_int32, C.c_int32]),
     "dpg_icp_batch_fetch": (C.c_int, [P, P, F64P]),
     "dpg_icp_batch_fetch_trace": (C.c_int, [P, I32P, I64P]),
+    "dpg_icp_batch_size": (C.c_int64, [P]),
     "dpg_icp_batch_kernel_ms": (C.c_float, [P]),
     "dpg_cov_batch_kernel_ms": (C.c_float, [P]),
     "dpg_cov_batch_overlapped": (C.c_int32, [P]),

@@ -342,8 +342,14 @@ class Context:
         check(lib().dpg_icp_batch_run(self.handle, int(compute_cov), int(trace_iters)), "dpg_icp_batch_run")
 
     def icp_fetch(self, with_hessian=True):
-        res = results_array(self.n_edges)
-        hess = np.zeros((self.n_edges, 9), np.float64) if with_hessian else None
+        """Results of the staged batch, whichever call staged it (its size from dpg_icp_batch_size:
+        dpg_add_node and the sweeps stage batches inside the C calls)."""
+        n = int(lib().dpg_icp_batch_size(self.handle))
+        if n < 0:
+            check(n, "dpg_icp_batch_size")
+        self.n_edges = n
+        res = results_array(n)
+        hess = np.zeros((n, 9), np.float64) if with_hessian else None
         check(lib().dpg_icp_batch_fetch(self.handle, vptr(res), ptr(hess, C.c_double)), "dpg_icp_batch_fetch")
         return res, (hess.reshape(-1, 3, 3) if hess is not None else None)
 
@@ -490,6 +496,16 @@ class Context:
 
 
 # ------------------------------------------------------------------ DPG change detection
+def _ctx_gone(child) -> bool:
+    """The context a DpgStore / IncGraph lives on is already destroyed.  Context.close closes its
+    children first, but when both sit in one reference cycle the garbage collector clears the
+    context's weak child set before any finalizer runs, and may finalize the context first; the
+    child's native destroy would then touch freed context state, so it is skipped (the device
+    memory went with the context's)."""
+    ctx = getattr(child, "ctx", None)
+    return ctx is not None and getattr(ctx, "handle", None) is None
+
+
 class DpgStore:
     """The dynamic node state of DpgSLAM (per-beam labels and sectors, per-node sector activation and
     activity, dpg_measurement.h / dpg_node.h), resident on the context's GPU, and executeDPG over it
@@ -515,6 +531,9 @@ class DpgStore:
 
     def close(self):
         if getattr(self, "handle", None):
+            if _ctx_gone(self):   # finalized after its context in one garbage cycle: nothing safe to free
+                self.handle = None
+                return
             lib().dpg_dpg_destroy(self.handle)
             self.handle = None
 
@@ -607,6 +626,9 @@ class IncGraph:
 
     def close(self):
         if getattr(self, "handle", None):
+            if _ctx_gone(self):   # finalized after its context in one garbage cycle: nothing safe to free
+                self.handle = None
+                return
             lib().dpg_inc_destroy(self.handle)
             self.handle = None
 

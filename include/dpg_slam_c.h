@@ -300,6 +300,9 @@ int dpg_icp_batch_prepare(dpg_ctx* ctx, const int32_t* edges, int64_t n_edges, c
 int dpg_icp_batch_run(dpg_ctx* ctx, int32_t compute_cov, int32_t trace_iters);
 /* 4) copy results back (any pointer may be NULL). */
 int dpg_icp_batch_fetch(dpg_ctx* ctx, dpg_icp_result* results, double* hess /*[E][9]*/);
+/* Edges of the staged batch -- dpg_icp_batch_prepare's, or the batch a sweep (dpg_reoptimize) or
+ * dpg_add_node staged last: the number of records dpg_icp_batch_fetch writes. */
+int64_t dpg_icp_batch_size(dpg_ctx* ctx);
 int dpg_icp_batch_fetch_trace(dpg_ctx* ctx, int32_t* trace /*[E][trace_iters][max_src]*/,
                               int64_t* max_src_out);
 /* Device time of the last ICP / covariance kernels (ms, HIP events on the context stream). */
@@ -321,7 +324,9 @@ int dpg_ctx_set_icp_variant(dpg_ctx* ctx, int32_t variant);
 int dpg_ctx_set_icp_defer_cap(dpg_ctx* ctx, int32_t cap);
 /* The batched covariance that runs beside the pose graph (dpg_icp_batch_run with covariance, its own
  * stream): at most n workgroups, each taking edges in turn, so the pose graph's kernels find free
- * compute units while it runs; 0 = one workgroup per edge.  Results are identical for every n. */
+ * compute units while it runs; 0 = one workgroup per edge.  Default 256 -- one per compute unit
+ * (config 4, one process A/B: 8.567 ms per step at 0, 8.524 at 256, 8.742 at 512; fewer than 64
+ * stretch it past the pose graph).  Results are identical for every n. */
 int dpg_ctx_set_cov_workgroups(dpg_ctx* ctx, int32_t n);
 /* Diagnostic: the angular ICP kernel's form (0 = the default; others are A/B references that must give
  * byte-identical results, tools/icp_var_ab.py): 1 = the kernel's previous form (variant 4), 2 = the

@@ -59,7 +59,7 @@ def _drive(slam, w, trace, sweeps):
             trace.append((len(slam.poses), slam.n_factors))
 
 
-def test_config5_slam_sweep_full_geometry(ctx):
+def test_config5_slam_sweep_full_geometry():
     """Two passes of the patrol at full scan geometry, GPU against the oracle in lockstep at every
     node, every executeDPG call and the pass-boundary sweep (tests/slam_lockstep.py); a free-running
     oracle run gives the same nodes and factors after every reading."""
@@ -67,13 +67,14 @@ def test_config5_slam_sweep_full_geometry(ctx):
     from slam_oracle import OracleSlamBackend
     w = synth.make_patrol(n_passes=2, steps=40)
     assert w.ranges.shape[1] == 5000
-    be = LockstepBackend(ctx, every=1, dpg_every=1, sweep_sample=10 ** 6)
-    sg = DpgSLAM(backend=be, ctx=ctx)
-    be.clouds_of = lambda: sg.clouds
     so = DpgSLAM(backend=OracleSlamBackend())
     to, tg, swo, swg = [], [], [], []
     _drive(so, w, to, swo)
-    _drive(sg, w, tg, swg)
+    with api.Context(0) as ctx:   # its own scan store
+        be = LockstepBackend(ctx, every=1, dpg_every=1, sweep_sample=10 ** 6)
+        sg = DpgSLAM(backend=be, ctx=ctx)
+        be.clouds_of = lambda: sg.clouds
+        _drive(sg, w, tg, swg)
     assert to == tg                                    # same nodes and factors after every reading
     V = len(sg.poses)
     n_later = int(np.sum(np.asarray(sg.node_pass) >= 1))
@@ -82,28 +83,30 @@ def test_config5_slam_sweep_full_geometry(ctx):
 
 
 @pytest.mark.slow
-def test_config5_10k_lockstep(ctx):
+def test_config5_10k_lockstep():
     """BASELINE config 5 at its stated size: DpgSLAM over the 4 x 2500-reading patrol (10 000 nodes)
     on the GPU -- per node dpg_add_node, executeDPG from pass 1 on, the reoptimize sweep at every pass
     boundary and once more at 10 k nodes (dpg_slam.cc:25-120,255-329,865-886) -- with the oracle in
-    lockstep on a fixed sample: every 250th node (its alignments bit-exact, its update within 1e-9 of
-    the oracle's from the GPU's state), every 250th executeDPG call (counters and node state bit for
+    lockstep on a fixed sample: every 250th node (its alignments bit-exact, its update within 1e-8 of
+    the oracle's from the GPU's state, tests/slam_lockstep.py POSE_TOL), every 250th executeDPG call (counters and node state bit for
     bit), and each sweep (candidate set equal, 64 of its alignments bit-exact, its update within
-    1e-9)."""
+    1e-7: one solve of the whole ill-conditioned graph, tests/slam_lockstep.py SWEEP_TOL)."""
     import time
     from slam_lockstep import LockstepBackend
     t0 = time.time()
     w = synth.make_patrol(n_passes=4, steps=2500)
-    be = LockstepBackend(ctx, every=250, dpg_every=250, sweep_sample=64)
-    sg = DpgSLAM(backend=be, ctx=ctx)
-    be.clouds_of = lambda: sg.clouds
     trace, sweeps = [], []
-    _drive(sg, w, trace, sweeps)
-    sg.reoptimize()                                    # the sweep at 10 k nodes
+    with api.Context(0) as ctx:   # its own scan store
+        be = LockstepBackend(ctx, every=250, dpg_every=250, sweep_sample=64)
+        sg = DpgSLAM(backend=be, ctx=ctx)
+        be.clouds_of = lambda: sg.clouds
+        _drive(sg, w, trace, sweeps)
+        sg.reoptimize()                                # the sweep at 10 k nodes
     V = len(sg.poses)
     assert V == 10000 and len(sweeps) == 3
     later = np.nonzero(np.asarray(sg.node_pass) >= 1)[0] + 1          # node counts at the executeDPG calls
     assert be.checked["nodes"] == 40 and be.checked["sweeps"] == 4, be.checked
     assert be.checked["dpg"] == int(np.sum((later - 1) % 250 == 0)) >= 25, be.checked
     assert be.checked["sweep_icp"] == 4 * 64 and be.checked["icp"] >= 40
-    print(f"config5 10k lockstep in {time.time() - t0:.0f} s:", be.checked, "max pose diff", be.max_pose_diff)
+    print(f"config5 10k lockstep in {time.time() - t0:.0f} s:", be.checked, "node update diffs max",
+          max(be.node_diffs), "sweep diffs", be.sweep_diffs)

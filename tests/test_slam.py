@@ -59,7 +59,12 @@ def test_slam_driver_gpu_matches_oracle():
     from dpgslam import api
     from slam_lockstep import LockstepBackend
     w = _workload()
-    ctx = api.Context(0)
+    with api.Context(0) as ctx:
+        _lockstep_run(ctx, w)
+
+
+def _lockstep_run(ctx, w):
+    from slam_lockstep import LockstepBackend
     be = LockstepBackend(ctx, every=1, dpg_every=1, sweep_sample=10 ** 6)
     sg = DpgSLAM(backend=be)
     be.clouds_of = lambda: sg.clouds
@@ -74,4 +79,3 @@ def test_slam_driver_gpu_matches_oracle():
     from oracle import oracle as O
     pts, offs = sg._clouds()
     assert np.array_equal(sg.GetMap(), O.get_map(pts, offs, sg.poses, sg.fraction))
-    ctx.close()

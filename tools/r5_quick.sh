@@ -10,7 +10,7 @@ export PYTHONPATH=$ROOT:$ROOT/dpg-slam_amd:$ROOT/tests
 cd "$ROOT"
 export TMPDIR=/tmp
 if [ "$SEL" != "none" ]; then
-  timeout -k 10 900 python -u -m pytest $SEL -x -v -m gpu --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1
+  timeout -k 10 900 python -u -m pytest $SEL -x -v -m gpu --tb=short --timeout 300 --timeout-method thread > "$OUT/tests.log" 2>&1
   rc=$?; echo "tests exit $rc"; tail -3 "$OUT/tests.log"; [ $rc -eq 0 ] || exit $rc
 fi
 if [ -n "$BENCH" ]; then
