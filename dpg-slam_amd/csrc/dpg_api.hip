@@ -549,11 +549,12 @@ void dpg_solver_options_default(dpg_solver_options* o) {
     o->merge_single = d.merge_single;
     o->max_supernode_cols = d.max_supernode_cols;
     o->relax_fraction = d.relax_fraction;
+    o->solve_inv_cols = d.solve_inv_cols;
 }
 
 // per context (every device of a multi-device one): applies to the next graph set up on it
 int dpg_ctx_set_solver_options(dpg_ctx* c, const dpg_solver_options* o) {
-    if (!c || !o || o->order < DPG_ORDER_AUTO || o->order > DPG_ORDER_ND || o->max_supernode_cols < 1 ||
+    if (!c || !o || o->order < DPG_ORDER_AUTO || o->order > DPG_ORDER_ND || o->max_supernode_cols < 1 || o->solve_inv_cols < 0 ||
         !(o->relax_fraction >= 0.0))
         return fail(DPG_ERR_ARG, "bad solver options");
     for (int k = 0; k < n_dev(c); ++k) {
@@ -566,6 +567,7 @@ int dpg_ctx_set_solver_options(dpg_ctx* c, const dpg_solver_options* o) {
         d.merge_single = o->merge_single ? 1 : 0;
         d.max_supernode_cols = o->max_supernode_cols;
         d.relax_fraction = o->relax_fraction;
+        d.solve_inv_cols = o->solve_inv_cols;
     }
     return DPG_OK;
 }

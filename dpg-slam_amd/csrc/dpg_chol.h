@@ -18,6 +18,10 @@ struct dpg_chol_opts {
     int32_t solve_stage = -1;          // doubles of L staged in LDS by the solves (-1: what fills 80 KB)
     int32_t solve_maxseg = -1;         // ancestor row segments in the backward solve (-1: all)
     int32_t solve_dinv = 0;            // solves with inverted diagonal blocks
+    int32_t solve_inv_cols = 0;        // fronts of at least this many pivot columns get L11^-1 after the
+                                       // factorization: the solves' diagonal part is then one product
+                                       // instead of a substitution chain (0: never; measured slower,
+                                       // DESIGN.md K4 round 5)
 };
 
 // Everything is indexed by block positions p = pos[node] in the elimination order.

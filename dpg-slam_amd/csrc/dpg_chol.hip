@@ -85,7 +85,8 @@ struct SnDev {
     int64_t acc_off;            // doubles (3r pending row updates of the forward solve)
     int32_t omap_n, parent;     // parent supernode, -1 at a root
     int32_t G, need;            // fused factorization: team size, sum of the children's team sizes
-    int32_t ftask, pad;         // large fronts: first tile task
+    int32_t ftask;              // large fronts: first tile task
+    int32_t inv;                // L11^-1 of the front at linv + inv (k3 x k3, column-major), -1: none
     int32_t seg_off, seg_n;     // backward solve: the row segments by owning supernode (SolveSeg)
 };
 
@@ -374,6 +375,151 @@ __device__ __forceinline__ int claim_lds(const int32_t* order, int32_t* ticket, 
     return *slot;
 }
 
+// 16-lane groups: sum of a partial over the group (xor butterfly: every lane gets the total)
+__device__ __forceinline__ double group16_sum(double a) {
+    a += __shfl_xor(a, 8, 16);
+    a += __shfl_xor(a, 4, 16);
+    a += __shfl_xor(a, 2, 16);
+    a += __shfl_xor(a, 1, 16);
+    return a;
+}
+
+// ---- L11^-1 of the large fronts (opts.solve_inv_cols) ----
+// The triangular solves spend their critical path in the top fronts' diagonal parts: a chain of
+// dependent substitution steps per 64-column block, each waiting on its block's loads (profiles/r05
+// chol timing: 59 of the backward's 122 us).  After each factorization this kernel inverts L11 of
+// every front with at least solve_inv_cols pivot columns; the solves then apply it as ONE product
+// (all loads in flight at once).  Task (s, j0): columns [j0, j0 + 16) of X = L11^-1 by column-parallel
+// forward substitution -- 16 lanes per column, lane l owning rows j0 + l + 16 q; step i broadcasts
+// x_i from its owner and every lane adds L(r, i) x_i to its rows r > i (ascending i: a fixed
+// summation order).  L11's columns are staged in LDS 16 at a time.
+// One WAVE per column j of X = L11^-1 (four per workgroup): lane l owns rows j + l + 64 q (q < 3:
+// fronts up to 192 pivot columns); step i broadcasts x_i from its owner (one readlane) and every lane
+// adds L(r, i) x_i to its rows r > i.  L's columns come straight from the fronts (L2), 16 steps'
+// worth loaded ahead into registers; no LDS, so many columns run per compute unit.
+constexpr int kInvCols = 4;              // columns (waves) per workgroup
+constexpr int kInvThreads = 64 * kInvCols;
+constexpr int kInvMaxQ = 3;              // rows per lane
+constexpr int kInvAhead = 16;            // steps of L loaded ahead
+__device__ __forceinline__ double rdlane_(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__global__ __launch_bounds__(kInvThreads) void chol_inv_l11(const int2* __restrict__ tasks, const SnDev* __restrict__ sns,
+                                                            const double* __restrict__ fronts, double* __restrict__ linv,
+                                                            const int32_t* gate) {
+    if (gate_off(gate, 1)) return;
+    const int2 tk = tasks[blockIdx.x];
+    const SnDev S = sns[tk.x];
+    const int lane = threadIdx.x & 63;
+    const int j = tk.y + (int)(threadIdx.x >> 6);      // this wave's column
+    const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k;
+    if (j >= k3) return;                                // whole wave
+    const int nr = k3 - j;                              // rows j .. k3 - 1
+    const double* F = fronts + S.front_off;
+    double* Li = linv + S.inv;
+    double sacc[kInvMaxQ], xo[kInvMaxQ], rd[kInvMaxQ];
+#pragma unroll
+    for (int q = 0; q < kInvMaxQ; ++q) {
+        const int b = lane + 64 * q;
+        sacc[q] = xo[q] = 0.0;
+        rd[q] = b < nr ? 1.0 / F[(int64_t)(j + b) * m3 + j + b] : 0.0;
+    }
+    // L(j + b, j + a) of this lane's rows b = lane + 64 q, 0 where b <= a or past the front
+    auto ld = [&](int a, int q) -> double {
+        const int b = lane + 64 * q;
+        const bool in = b > a && b < nr && a < nr;
+        const double t = F[(int64_t)(j + (a < nr ? a : 0)) * m3 + j + (in ? b : 0)];
+        return in ? t : 0.0;
+    };
+    double cur[kInvAhead][kInvMaxQ], nxt[kInvAhead][kInvMaxQ];
+#pragma unroll
+    for (int u = 0; u < kInvAhead; ++u)
+#pragma unroll
+        for (int q = 0; q < kInvMaxQ; ++q) cur[u][q] = ld(u, q);
+    for (int a0 = 0; a0 < nr; a0 += kInvAhead) {
+#pragma unroll
+        for (int u = 0; u < kInvAhead; ++u)   // the next 16 steps' columns, in flight during these 16
+#pragma unroll
+            for (int q = 0; q < kInvMaxQ; ++q) nxt[u][q] = ld(a0 + kInvAhead + u, q);
+#pragma unroll
+        for (int u = 0; u < kInvAhead; ++u) {
+            const int a = a0 + u;                       // step: row j + a
+            if (a >= nr) break;                         // (uniform)
+            const int own = a & 63, qa = a >> 6;
+            double s_own = sacc[0], r_own = rd[0];
+#pragma unroll
+            for (int q = 1; q < kInvMaxQ; ++q)
+                if (qa == q) { s_own = sacc[q]; r_own = rd[q]; }
+            const double v = a == 0 ? r_own : -s_own * r_own;   // meaningful on lane own
+#pragma unroll
+            for (int q = 0; q < kInvMaxQ; ++q)
+                if (qa == q && lane == own) xo[q] = v;
+            const double x = rdlane_(v, own);
+#pragma unroll
+            for (int q = 0; q < kInvMaxQ; ++q) sacc[q] = fma(cur[u][q], x, sacc[q]);   // (0 above the rows)
+        }
+#pragma unroll
+        for (int u = 0; u < kInvAhead; ++u)
+#pragma unroll
+            for (int q = 0; q < kInvMaxQ; ++q) cur[u][q] = nxt[u][q];
+    }
+#pragma unroll
+    for (int q = 0; q < kInvMaxQ; ++q) {
+        const int b = lane + 64 * q;
+        if (b < nr) Li[(int64_t)j * k3 + j + b] = xo[q];
+    }
+}
+
+// y[0, k3) <- L11^-1 y (tmp: k3 doubles of LDS): one thread per output row, the columns in
+// ascending order over four accumulators; the loads of a column are contiguous across the rows
+__device__ __forceinline__ void inv_apply_lower(const double* __restrict__ Li, int k3, double* y, double* tmp) {
+    const int tid = threadIdx.x;
+    for (int t = tid; t < k3; t += kT) tmp[t] = y[t];
+    __syncthreads();
+    for (int i = tid; i < k3; i += kT) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int k = 0;
+#pragma unroll 2
+        for (; k + 3 <= i; k += 4) {
+            a0 = fma(Li[(int64_t)k * k3 + i], tmp[k], a0);
+            a1 = fma(Li[(int64_t)(k + 1) * k3 + i], tmp[k + 1], a1);
+            a2 = fma(Li[(int64_t)(k + 2) * k3 + i], tmp[k + 2], a2);
+            a3 = fma(Li[(int64_t)(k + 3) * k3 + i], tmp[k + 3], a3);
+        }
+        for (; k <= i; ++k) a0 = fma(Li[(int64_t)k * k3 + i], tmp[k], a0);
+        y[i] = (a0 + a1) + (a2 + a3);
+    }
+    __syncthreads();
+}
+// z[0, k3) <- L11^-T z (tmp: k3 doubles of LDS): 16 lanes per output k, the dot down column k of
+// L11^-1 (rows k .. k3, contiguous)
+__device__ __forceinline__ void inv_apply_upper(const double* __restrict__ Li, int k3, double* z, double* tmp) {
+    const int tid = threadIdx.x, g = tid >> 4, gl = tid & 15;
+    for (int t = tid; t < k3; t += kT) tmp[t] = z[t];
+    __syncthreads();
+    for (int k0 = 0; k0 < k3; k0 += kT / 16) {
+        const int k = k0 + g;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        if (k < k3) {
+            const double* cl = Li + (int64_t)k * k3;
+            int i = k + gl;
+#pragma unroll 2
+            for (; i + 48 < k3; i += 64) {
+                a0 = fma(cl[i], tmp[i], a0);
+                a1 = fma(cl[i + 16], tmp[i + 16], a1);
+                a2 = fma(cl[i + 32], tmp[i + 32], a2);
+                a3 = fma(cl[i + 48], tmp[i + 48], a3);
+            }
+            for (; i < k3; i += 16) a0 = fma(cl[i], tmp[i], a0);
+        }
+        const double a = group16_sum((a0 + a1) + (a2 + a3));
+        if (k < k3 && gl == 0) z[k] = a;
+    }
+    __syncthreads();
+}
+
 // forward: L y = -g.  A front gathers its children's pending row updates (child order: fixed
 // summation order), solves its diagonal blocks (one wave, LDS), then hands L21 y to its parent.
 __device__ __forceinline__ double rdlane(double v, int l) {
@@ -619,14 +765,6 @@ __device__ __forceinline__ void stage_l21(double* dst, const double* F, int m3, 
     }
 }
 
-// 16-lane groups: sum of a partial over the group (xor butterfly: every lane gets the total)
-__device__ __forceinline__ double group16_sum(double a) {
-    a += __shfl_xor(a, 8, 16);
-    a += __shfl_xor(a, 4, 16);
-    a += __shfl_xor(a, 2, 16);
-    a += __shfl_xor(a, 1, 16);
-    return a;
-}
 
 // z[j] -= sum_t A[j * lda + t] x[t] for j < nj, t < nt (A column-major, the dot runs down a
 // column: contiguous): 16 lanes per j, so a long dot is 1/16 of the serial chain.
@@ -696,11 +834,13 @@ __device__ __forceinline__ void sub_coldots(double* z, const double* A, int64_t 
 // (the first one prestaged) and L21s the first C columns of L21.
 template <bool kFull>
 __device__ __forceinline__ void fwd_front(const SnDev& S, const double* F, double* Rg, double* D, const double* L21s,
-                                          int C, double* rd, double* y, double* aR, double* acc, const double* dinv_f) {
+                                          int C, double* rd, double* y, double* aR, double* acc, const double* dinv_f,
+                                          const double* Li) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* A = kFull ? Rg : F;   // the front's columns, ld m3
-    for (int jb = 0; jb < k3; jb += kSB) {
+    if (Li) inv_apply_lower(Li, k3, y, D);   // y_p <- L11^-1 y_p: the whole diagonal part as one product
+    for (int jb = 0; jb < (Li ? 0 : k3); jb += kSB) {
         const int bw = min(kSB, k3 - jb);
         if (jb > 0) {   // the first block was loaded before the wait
             if (dinv_f) load_dinv<false>(D, dinv_f, jb, bw);
@@ -776,7 +916,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                        const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm,
                                                        double* __restrict__ ysol, double* acc, int R,
-                                                       const double* __restrict__ dinv, const int32_t* gate) {
+                                                       const double* __restrict__ dinv, const int32_t* gate,
+                                                       const double* __restrict__ linv) {
     extern __shared__ __attribute__((aligned(16))) double smem_fw[];
     double* sm = smem_fw + 2;   // smem_fw[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
@@ -786,7 +927,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     const double* dinv_f = dinv ? dinv + 3 * (int64_t)S.c0 * kSB : nullptr;   // inverted diagonal blocks
-    double* D = sm;                  // kSB x kDL diagonal block
+    const double* Li = (linv && S.inv >= 0) ? linv + S.inv : nullptr;          // L11^-1
+    double* D = sm;                  // kSB x kDL diagonal block (with Li: k3 doubles of scratch)
     double* Rg = D + kSB * kDL;      // staging region, R doubles (Stage)
     double* L21s = Rg;               // (not full) first C columns of L21
     double* rd = Rg + R;             // kSB reciprocals of the diagonal block's diagonal
@@ -799,7 +941,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
         y[t] = -g[3 * node + t % 3];
     }
     for (int t = tid; t < r3; t += kT) aR[t] = 0.0;
-    if (dinv_f) load_dinv<false>(D, dinv_f, 0, min(kSB, k3));
+    if (Li) {
+    } else if (dinv_f) load_dinv<false>(D, dinv_f, 0, min(kSB, k3));
     else load_diag(D, rd, F, m3, 0, min(kSB, k3));
     if (P.full) stage_copy(Rg, F, m3 * k3);
     else stage_l21(L21s, F, m3, k3, P.C);
@@ -820,8 +963,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
         }
         __syncthreads();
     }
-    if (P.full) fwd_front<true>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc, dinv_f);
-    else fwd_front<false>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc, dinv_f);
+    if (P.full) fwd_front<true>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc, dinv_f, Li);
+    else fwd_front<false>(S, F, Rg, D, L21s, P.C, rd, y, aR, acc, dinv_f, Li);
     for (int t = tid; t < k3; t += kT) ysol[3 * (int64_t)S.c0 + t] = y[t];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -881,7 +1024,7 @@ template <bool kFull>
 __device__ __forceinline__ void bwd_front(int s, const SnDev& S, int nseg, const SolveSeg* sg, const int32_t* rp,
                                           int32_t* sync, int32_t* status, double* xsol, const double* F, double* Rg,
                                           double* D, const double* L21s, int C, double* rd, double* z, double* xr,
-                                          const double* dinv_f) {
+                                          const double* dinv_f, const double* Li) {
     const int tid = threadIdx.x;
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     if (nseg == 0) {   // the root (no rows), or too many segments: wait for the parent, take every row
@@ -908,7 +1051,8 @@ __device__ __forceinline__ void bwd_front(int s, const SnDev& S, int nseg, const
     }
     __syncthreads();
     BW_MARK(s, 2);
-    bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z, dinv_f);
+    if (Li) inv_apply_upper(Li, k3, z, D);   // x_p <- L11^-T z_p: one product
+    else bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z, dinv_f);
 }
 
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,
@@ -919,7 +1063,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
                                                         const double* __restrict__ ysol, double* xsol, int R,
                                                         int max_seg, const double* __restrict__ dinv,
                                                         const int32_t* gate, const int32_t* __restrict__ perm,
-                                                        double* __restrict__ X, double* max_out) {
+                                                        double* __restrict__ X, double* max_out,
+                                                        const double* __restrict__ linv) {
     extern __shared__ __attribute__((aligned(16))) double smem_b[];
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
@@ -930,7 +1075,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
     const double* F = fronts + S.front_off;
     const double* dinv_f = dinv ? dinv + 3 * (int64_t)S.c0 * kSB : nullptr;   // inverted diagonal blocks
-    double* D = sm;                  // kSB x kDL diagonal block
+    // the inverse is valid on the gated loop's chord iterations (a refactoring iteration's is being
+    // computed beside this solve) and whenever the caller passes it ungated
+    const double* Li = (linv && S.inv >= 0 && (!gate || gate[1])) ? linv + S.inv : nullptr;   // L11^-1
+    double* D = sm;                  // kSB x kDL diagonal block (with Li: k3 doubles of scratch)
     double* Rg = D + kSB * kDL;      // staging region, R doubles (Stage)
     double* L21s = Rg;               // (not full) first C columns of L21
     double* rd = Rg + R;             // kSB reciprocals of the diagonal block's diagonal
@@ -944,7 +1092,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     for (int j = tid; j < k3; j += kT) z[j] = ysol[3 * (int64_t)S.c0 + j];
     for (int t = tid; t < S.r; t += kT) rp[t] = rows[S.rows_off + t];
     for (int q = tid; q < nseg; q += kT) sg[q] = segs[S.seg_off + q];
-    {
+    if (!Li) {
         const int jb = ((k3 + kSB - 1) / kSB - 1) * kSB;
         if (dinv_f) load_dinv<true>(D, dinv_f, jb, k3 - jb);
         else load_diag(D, rd, F, m3, jb, k3 - jb);
@@ -952,8 +1100,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     if (P.full) stage_copy(Rg, F, m3 * k3);
     else stage_l21(L21s, F, m3, k3, P.C);
     __syncthreads();
-    if (P.full) bwd_front<true>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f);
-    else bwd_front<false>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f);
+    if (P.full) bwd_front<true>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f, Li);
+    else bwd_front<false>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f, Li);
     BW_MARK(s, 3);
     for (int j = tid; j < k3; j += kT) st_agent(xsol + 3 * (int64_t)S.c0 + j, z[j]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1731,6 +1879,10 @@ struct CholDev {
     double* xsol = nullptr;
     int32_t* status = nullptr;
     double* dinv = nullptr;            // inverted diagonal blocks of the solves ([3n][kSB])
+    double* linv = nullptr;            // L11^-1 of the large fronts (SnDev.inv offsets)
+    int2* inv_tasks = nullptr;         // chol_inv_l11: (front, first column) per workgroup
+    int64_t n_inv_tasks = 0, linv_total = 0;
+    size_t lds_inv = 0, c_linv = 0;
     int2* dblocks = nullptr;           // (front, jb) of every diagonal block
     int64_t n_dblocks = 0;
     bool use_dinv = false;             // DPG_SOLVE_DINV=1: inverted diagonal blocks (measured slower)
@@ -1762,6 +1914,14 @@ struct CholDev {
     bool fused = false;
     size_t lds_fused = 0;
     bool fused_db = true;
+    // L11^-1 (chol_inv_l11): valid for the last factorization (inv_valid: computed by an ungated
+    // solve); the gated loop computes it on `aux` beside each refactoring iteration's backward solve
+    // and its chord iterations wait for it (ev_inv of the previous iteration)
+    bool inv_valid = false;
+    bool keep_inv = false;   // ungated solves compute L11^-1 after their backward solve (for dpg_chol_resolve)
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_fac = nullptr, ev_inv[2] = {nullptr, nullptr};
+    int inv_par = 0;
     // capacities (elements) of the device buffers above, for rebuilds
     size_t c_fronts = 0, c_acc = 0, c_ysol = 0, c_xsol = 0, c_status = 0, c_sync = 0, c_dinv = 0;
     double t_build[2] = {0, 0};   // last chol_build: host structures, uploads (ms)
@@ -1781,10 +1941,15 @@ extern "C" void dpg_chol_destroy(void* h) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!c) return;
     // (the structure arrays live in c->arena)
-    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync, c->dinv};
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
+    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync, c->dinv, c->linv};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stage) (void)hipHostFree(c->stage);
+    if (c->ev_fac) (void)hipEventDestroy(c->ev_fac);
+    for (hipEvent_t e : c->ev_inv)
+        if (e) (void)hipEventDestroy(e);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     free_host(c->host);
     delete c;
 }
@@ -1851,6 +2016,7 @@ struct CholHost {
     std::vector<int2> panel_t;
     std::vector<int4> upd_t;
     std::vector<int2> dblocks;
+    std::vector<int2> inv_t;            // chol_inv_l11 tasks (front, first column)
     std::vector<int32_t> tcnt, tfill;   // per-tile child counts / fill cursors of one large front
     std::vector<char> tused;
     int64_t acc_total = 0;
@@ -2036,6 +2202,23 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     }
     for (int32_t s = 0; s < S.ns; ++s)
         if (sns[(size_t)s].parent >= 0) sns[(size_t)sns[(size_t)s].parent].need += sns[(size_t)s].G;
+    // L11^-1 of the fronts with at least solve_inv_cols pivot columns (and at most 64 kInvMaxQ = 192)
+    H.inv_t.clear();
+    c->linv_total = 0;
+    c->lds_inv = 0;
+    for (int32_t s = 0; s < S.ns; ++s) {
+        SnDev& d = sns[(size_t)s];
+        const int32_t k3 = 3 * d.k;
+        d.inv = -1;
+        if (c->opts.solve_inv_cols <= 0 || k3 < c->opts.solve_inv_cols || k3 > 64 * kInvMaxQ ||
+            c->linv_total + (int64_t)k3 * k3 > INT32_MAX)
+            continue;
+        d.inv = (int32_t)c->linv_total;
+        c->linv_total += (int64_t)k3 * k3;
+        for (int32_t j0 = 0; j0 < k3; j0 += kInvCols) H.inv_t.push_back(make_int2(s, j0));
+        c->lds_inv = 0;
+    }
+    c->n_inv_tasks = (int64_t)H.inv_t.size();
     std::vector<SolveSeg>& segs = H.segs;
     segs.clear();
     for (int32_t s = 0; s < S.ns; ++s) {
@@ -2374,6 +2557,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     add(&c->order_bwd, H.bwd);
     add(&c->segs, H.segs);
     add(&c->dblocks, H.dblocks);
+    add(&c->inv_tasks, H.inv_t);
     if (!c->fused) {
         add(&c->asm_tasks, H.asm_t);
         add(&c->asm_child, H.asm_c);
@@ -2412,6 +2596,7 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
     rc |= dreserve(&c->xsol, &c->c_xsol, (size_t)(3 * n));
     rc |= dreserve(&c->status, &c->c_status, 1);
     rc |= dreserve(&c->dinv, &c->c_dinv, (size_t)(3 * n) * kSB);
+    rc |= dreserve(&c->linv, &c->c_linv, (size_t)std::max<int64_t>(c->linv_total, 1));
     if (!rc) rc |= hipMemsetAsync(c->status, 0, sizeof(int32_t), nullptr) != hipSuccess;
     // the staging buffer is reused by the next build: wait for the copy (always, even after an error)
     rc |= hipStreamSynchronize(nullptr) != hipSuccess;
@@ -2508,6 +2693,14 @@ void dpg_chol_build_times(void* h, double out[2]) {
     out[1] = c ? c->t_build[1] : 0.0;
 }
 
+// L11^-1 of the large fronts from the fronts just factored (gate: the pipelined loop's, refactoring
+// iterations only)
+static void launch_inv(CholDev* c, hipStream_t st, const int32_t* gate) {
+    if (c->n_inv_tasks > 0)
+        hipLaunchKernelGGL(chol_inv_l11, dim3((unsigned)c->n_inv_tasks), dim3(kInvThreads), c->lds_inv, st, c->inv_tasks, c->sns,
+                           c->fronts, c->linv, gate);
+}
+
 extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -2524,7 +2717,11 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
             hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                            c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg,
-                           c->use_dinv ? c->dinv : nullptr, nullptr, nullptr, nullptr, nullptr);
+                           c->use_dinv ? c->dinv : nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+        // the inverse after the backward (which, as a refactoring iteration of the gated loop, chains):
+        // the chord steps of dpg_chol_resolve then do the same arithmetic as the gated loop's
+        c->inv_valid = c->keep_inv && c->n_inv_tasks > 0;
+        if (c->inv_valid) launch_inv(c, st, nullptr);
         return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
     }
     int pid = 0;
@@ -2548,9 +2745,13 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
         hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
     const double* di = c->use_dinv ? c->dinv : nullptr;
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, sync_f, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr,
+                       nullptr);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd, sync_b, c->status,
-                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr, nullptr, nullptr, nullptr);
+                       c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr, nullptr,
+                       nullptr, nullptr, nullptr);
+    c->inv_valid = c->keep_inv && c->n_inv_tasks > 0;
+    if (c->inv_valid) launch_inv(c, st, nullptr);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2562,10 +2763,13 @@ extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     const double* g = hb + 9 * c->nnzb_upper;
     if (hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess) return DPG_ERR_HIP;
     const double* di = c->use_dinv ? c->dinv : nullptr;   // inverted by the factorization's dpg_chol_solve
+    const double* li = c->inv_valid ? c->linv : nullptr;
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
-                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr);
+                       c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage, di, nullptr,
+                       li);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
-                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage, c->solve_maxseg, di, nullptr, nullptr, nullptr, nullptr);
+                       c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol, c->solve_stage,
+                       c->solve_maxseg, di, nullptr, nullptr, nullptr, nullptr, li);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
@@ -2594,16 +2798,50 @@ extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* ga
     if (!prezeroed && (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess ||
                        hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess))
         return DPG_ERR_HIP;
+    const bool inv = c->n_inv_tasks > 0;
+    if (inv) {   // this iteration's solves come after the previous iteration's inverse
+        if (!c->aux) {
+            if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_fac, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_inv[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->ev_inv[1], hipEventDisableTiming) != hipSuccess ||
+                hipEventRecord(c->ev_inv[0], c->aux) != hipSuccess || hipEventRecord(c->ev_inv[1], c->aux) != hipSuccess)
+                return DPG_ERR_HIP;
+        }
+        if (hipStreamWaitEvent(st, c->ev_inv[c->inv_par ^ 1], 0) != hipSuccess) return DPG_ERR_HIP;
+    }
     hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
                        c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
                        c->perm, c->fronts, c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, gate);
+    if (inv) {   // L11^-1 of a refactoring iteration beside its backward solve (which does not use it)
+        if (hipEventRecord(c->ev_fac, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->ev_fac, 0) != hipSuccess)
+            return DPG_ERR_HIP;
+        launch_inv(c, c->aux, gate);
+        if (hipEventRecord(c->ev_inv[c->inv_par], c->aux) != hipSuccess) return DPG_ERR_HIP;
+        c->inv_par ^= 1;
+    }
     hipLaunchKernelGGL(chol_forward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_fwd, c->sync, c->status,
                        c->sns, c->child_list, c->relmap, c->fronts, g, c->perm, c->ysol, c->acc, c->solve_stage,
-                       nullptr, gate);
+                       nullptr, gate, c->linv);
     hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                        c->sync + 1 + 2 * S.ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol,
-                       c->solve_stage, c->solve_maxseg, nullptr, gate, c->perm, X, max_out);
+                       c->solve_stage, c->solve_maxseg, nullptr, gate, c->perm, X, max_out, c->linv);
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
+// a Gauss-Newton graph's solver keeps L11^-1 for its chord steps (the incremental graph refactors
+// every update and does not)
+extern "C" void dpg_chol_keep_inverse(void* h, int on) {
+    if (h) reinterpret_cast<CholDev*>(h)->keep_inv = on != 0;
+}
+
+// the gated loop's control kernel rewrites the gate the inverse kernel reads: it must come after
+// this iteration's inverse (normally long finished: it ran beside the backward solve and assembly)
+extern "C" int dpg_chol_join_aux(void* h, void* stream) {
+    CholDev* c = reinterpret_cast<CholDev*>(h);
+    if (!c || !c->aux) return DPG_OK;
+    return hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), c->ev_inv[c->inv_par ^ 1], 0) == hipSuccess ? DPG_OK
+                                                                                                       : DPG_ERR_HIP;
 }
 
 extern "C" const int32_t* dpg_chol_pos_dev(void* h) { return reinterpret_cast<CholDev*>(h)->pos; }

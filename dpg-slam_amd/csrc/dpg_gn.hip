@@ -556,6 +556,7 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)pairs[(size_t)p].first; phi[(size_t)p] = (int32_t)pairs[(size_t)p].second; }
     rc = dpg_chol_create(&g->chol, n, plo.data(), phi.data(), P, opts);
     if (rc) g->chol = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
+    else dpg_chol_keep_inverse(g->chol, 1);   // chord steps reuse the factor: L11^-1 for their solves
     return DPG_OK;
 }
 
@@ -880,6 +881,7 @@ extern "C" int dpg_gn_pipe_issue_ctl(dpg_gn_dev* g, const dpg_gn_params* gp, dpg
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int32_t* sync;
     int64_t n_words;
+    if (dpg_chol_join_aux(g->chol, stream)) return DPG_ERR_HIP;
     dpg_chol_sync_dev(g->chol, &sync, &n_words);
     double* chi2 = g->hb_own + 9 * g->nnzb_upper + 3 * g->n_nodes;
     hipLaunchKernelGGL(pipe_ctl_kernel, dim3(1), dim3(1024), 0, s, ctl, g->partials + 6 * (size_t)g->n_blocks_rows,

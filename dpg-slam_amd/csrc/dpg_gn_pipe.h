@@ -65,6 +65,9 @@ int dpg_chol_gated_ok(void* chol);
 // max |x| in *max_out (retract_kernel's work)
 int dpg_chol_solve_gated(void* chol, const double* hb, const int32_t* gate, int prezeroed, double* X, double* max_out,
                          void* stream);
+// order `stream` after the L11^-1 kernel the last gated solve ran on its side stream (before the
+// control kernel rewrites the gate that kernel reads)
+int dpg_chol_join_aux(void* chol, void* stream);
 // the fused solve's synchronisation words (cleared before every solve)
 void dpg_chol_sync_dev(void* chol, int32_t** sync, int64_t* n_words);
 // set the control block for iteration 1 from the host state (g's chord bookkeeping) and the

@@ -158,6 +158,8 @@ void dpg_chol_destroy(void* chol);
 int dpg_chol_solve(void* chol, const double* hb, void* stream);
 /* solve H x = -g with the factorization of the last dpg_chol_solve (g from hb) */
 int dpg_chol_resolve(void* chol, const double* hb, void* stream);
+/* keep L11^-1 of the large fronts after each ungated factorization for dpg_chol_resolve (GN graphs) */
+void dpg_chol_keep_inverse(void* chol, int on);
 const int32_t* dpg_chol_pos_dev(void* chol);
 const double* dpg_chol_x_dev(void* chol);
 const int32_t* dpg_chol_status_dev(void* chol);

@@ -142,7 +142,7 @@ class SolverOptions(C.Structure):
     """dpg_solver_options -- the supernodal Cholesky's options (per context)."""
 
     _fields_ = [(n, C.c_int32) for n in ("order", "fused", "solve_stage", "solve_maxseg", "solve_dinv",
-                                          "merge_single", "max_supernode_cols", "pad")] + [("relax_fraction", C.c_double)]
+                                          "merge_single", "max_supernode_cols", "solve_inv_cols")] + [("relax_fraction", C.c_double)]
 
 
 class IncStats(C.Structure):

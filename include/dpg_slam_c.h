@@ -219,7 +219,12 @@ typedef struct dpg_solver_options {
     int32_t solve_dinv;          /* 1: the solves use inverted diagonal blocks (0: substitution chains) */
     int32_t merge_single;        /* 1: supernodes merge only along single-child chains (round 1's rule) */
     int32_t max_supernode_cols;  /* 64 block columns */
-    int32_t pad;
+    int32_t solve_inv_cols;      /* 0 (never): fronts with at least this many pivot columns get their
+                                    diagonal block's inverse L11^-1 after each factorization (beside
+                                    the backward solve in the pipelined loop), and the chord steps'
+                                    triangular solves apply it as one product instead of a
+                                    substitution chain -- 14 us off each solve, but the inversion and
+                                    its stream hand-offs cost more */
     double relax_fraction;       /* 0.3: explicit-zero budget of relaxed supernodes */
 } dpg_solver_options;
 void dpg_solver_options_default(dpg_solver_options* o);

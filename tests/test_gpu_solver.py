@@ -110,13 +110,14 @@ def test_orders_agree(ctx, workload, name):
 
 
 @pytest.mark.parametrize("opts", [{"solve_stage": 0}, {"solve_stage": 15000}, {"solve_maxseg": 0}, {"solve_maxseg": 1},
-                                  {"merge_single": 1}, {"solve_dinv": 1}])
+                                  {"merge_single": 1}, {"solve_dinv": 1}, {"solve_inv_cols": 48}])
 def test_solve_paths_agree(ctx, workload, opts):
     """The triangular solves' code paths give the same GN solution on config 4 (chord steps and
     fresh factorizations): no LDS staging, staging of whole fronts up to 15 000 doubles, the
     backward solve with every front waiting for its parent (no row segments) or with segments only
-    where there is one, the single-child supernode rule, and the inverted diagonal blocks --
-    against the defaults (dpg_solver_options)."""
+    where there is one, the single-child supernode rule, the inverted diagonal blocks, and the
+    large fronts' L11^-1 computed beside the pipelined loop's solves -- against the defaults
+    (dpg_solver_options)."""
     from dpgslam import _abi
     w = workload("config4")
     p = _abi.default_icp_params()

@@ -11,8 +11,9 @@
 #include <random>
 #include <vector>
 
+#include "../dpg-slam_amd/csrc/dpg_chol.h"
+
 extern "C" {
-struct dpg_chol_opts;
 int dpg_chol_create(void** chol, int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs,
                     const dpg_chol_opts* opts);
 void dpg_chol_destroy(void* chol);
@@ -44,7 +45,7 @@ void dpg_chol_tree(void* h, int32_t* parent, int32_t* m3, int32_t* k3);
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        fprintf(stderr, "usage: %s PAIRS.bin [iters]\n", argv[0]);
+        fprintf(stderr, "usage: %s PAIRS.bin [iters] [solve_inv_cols]\n", argv[0]);
         return 2;
     }
     const int iters = argc > 2 ? atoi(argv[2]) : 20;
@@ -83,7 +84,9 @@ int main(int argc, char** argv) {
     for (int64_t t = 0; t < 3 * n; ++t) g[t] = U(rng);
 
     void* ch = nullptr;
-    int rc = dpg_chol_create(&ch, n, lo.data(), hi.data(), P, nullptr);
+    dpg_chol_opts co;
+    if (argc > 3) co.solve_inv_cols = atoi(argv[3]);
+    int rc = dpg_chol_create(&ch, n, lo.data(), hi.data(), P, &co);
     if (rc) {
         fprintf(stderr, "dpg_chol_create failed %d\n", rc);
         return 1;
