@@ -346,6 +346,28 @@ __device__ __forceinline__ double ld_agent(double* p) {
     return __longlong_as_double(
         (long long)__hip_atomic_load(reinterpret_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
+// 16-B write-through (sc1) accesses of a front: a buffer descriptor over the whole front (front
+// offsets are even, so its base is 16-B aligned) and element pairs (e, e + 1), e even.  An 8-B sc1
+// access moves 0.54-0.70x the bytes of a 16-B one per instruction, an 8-B sc1 store ~1/2.7
+// (MI355X_MICROARCH.md, inter-workgroup visibility).  A column segment of a front is covered by the
+// aligned pairs that overlap it; the element a pair holds outside the segment is the row above it
+// in the same column or row 0 of the next column (both above the diagonal: never read as data) or
+// the front's padding.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t front_rsrc(const double* F, int m3) {
+    const uint64_t p = reinterpret_cast<uint64_t>(F);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane(((m3 * m3 + 1) & ~1) * 8);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ double2 ld2_sc1(__amdgpu_buffer_rsrc_t r, uint32_t e) {
+    return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, e * 8u, 0, 16));
+}
+__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t r, uint32_t e, double x, double y) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_double2(x, y)), r, e * 8u, 0, 16);
+}
+
 // Poll without the agent acquire: every handed-off byte the waiting workgroup reads is stored sc1
 // by its producer and loaded sc1 (ld_agent) here, so the L1 is never consulted for it (Guideline
 // 16, the sc1-load form); the wavefront fence only keeps the compiler from hoisting those loads.
@@ -747,6 +769,33 @@ __device__ __forceinline__ void stage_copy(double* dst, const double* src, int n
         }
     }
 }
+// L2 warm-up of the solves' unstaged reads: one load per 128-B line of every part of the front's
+// L a solve reads from global memory after its wait (everything but a fully staged front and L21's
+// first C columns), issued BEFORE the staging loads and retired with them -- so the front's lines
+// are in this XCD's L2 when the (often tens of us long) wait ends and the diagonal blocks' and the
+// column dots' loads, each a dependent round trip, hit there instead of the fabric.  The front was
+// written by an earlier launch (plain loads are coherent).  Rows j, j + 16, ... of column j, and
+// its last row (a 16-double step never skips a line).
+constexpr int kWarm = 16;
+__device__ __forceinline__ void warm_issue(const double* F, int m3, int k3, int C, double (&v)[kWarm]) {
+    const int per = ((m3 + 15) >> 4) + 1, n = k3 * per;
+#pragma unroll
+    for (int q = 0; q < kWarm; ++q) {
+        const int e = threadIdx.x + kT * q;
+        v[q] = 0.0;
+        if (e < n) {
+            const int j = e / per;
+            const int r = min(j + 16 * (e - j * per), m3 - 1);
+            if (!(j < C && r >= k3)) v[q] = F[(int64_t)j * m3 + r];
+        }
+    }
+}
+// the touches retire here (an empty asm using each value: the loads cannot be dropped)
+__device__ __forceinline__ void warm_retire(const double (&v)[kWarm]) {
+#pragma unroll
+    for (int q = 0; q < kWarm; ++q) asm volatile("" ::"v"(v[q]));
+}
+
 // the first C columns of L21 (rows k3..m3 of the front at F) -> dst [C][r3]
 __device__ __forceinline__ void stage_l21(double* dst, const double* F, int m3, int k3, int C) {
     const int r3 = m3 - k3, n = C * r3;
@@ -944,8 +993,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     if (Li) {
     } else if (dinv_f) load_dinv<false>(D, dinv_f, 0, min(kSB, k3));
     else load_diag(D, rd, F, m3, 0, min(kSB, k3));
-    if (P.full) stage_copy(Rg, F, m3 * k3);
-    else stage_l21(L21s, F, m3, k3, P.C);
+    if (P.full) {
+        stage_copy(Rg, F, m3 * k3);
+    } else {
+        double wv[kWarm];
+        if (!Li) warm_issue(F, m3, k3, P.C, wv);
+        stage_l21(L21s, F, m3, k3, P.C);
+        if (!Li) warm_retire(wv);
+    }
     if (S.nchild > 0) {
         if (tid == 0) wait_geq_sc1(sync + 1 + s, S.nchild, status);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1097,8 +1152,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
         if (dinv_f) load_dinv<true>(D, dinv_f, jb, k3 - jb);
         else load_diag(D, rd, F, m3, jb, k3 - jb);
     }
-    if (P.full) stage_copy(Rg, F, m3 * k3);
-    else stage_l21(L21s, F, m3, k3, P.C);
+    if (P.full) {
+        stage_copy(Rg, F, m3 * k3);
+    } else {
+        double wv[kWarm];
+        if (!Li) warm_issue(F, m3, k3, P.C, wv);
+        stage_l21(L21s, F, m3, k3, P.C);
+        if (!Li) warm_retire(wv);
+    }
     __syncthreads();
     if (P.full) bwd_front<true>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f, Li);
     else bwd_front<false>(s, S, nseg, sg, rp, sync, status, xsol, F, Rg, D, L21s, P.C, rd, z, xr, dinv_f, Li);
@@ -1319,10 +1380,16 @@ __device__ __forceinline__ void small_front(int s, const SnDev& S, int32_t* sync
         if (i >= j) F[(int64_t)j * m3 + i] = A[e];
     }
     for (int t = tid; t < k3; t += kFT) ysol[3 * (int64_t)S.c0 + t] = bv[t];
-    if (S.parent >= 0) {
-        for (int e = tid; e < r3 * r3; e += kFT) {
-            const int j = k3 + e / r3, i = k3 + e % r3;
-            if (i >= j) st_agent(F + (int64_t)j * m3 + i, A[j * m3 + i]);
+    if (S.parent >= 0) {   // the update matrix: 16-B sc1 stores of the aligned pairs over its columns
+        const auto rs = front_rsrc(F, m3);
+        const int npc = (r3 + 2) >> 1;
+        for (int e = tid; e < r3 * npc; e += kFT) {
+            const int jj = e / npc, k = e - jj * npc, j = k3 + jj;
+            const uint32_t a = (uint32_t)(j * m3 + k3);
+            const int i0 = 2 * k - (int)(a & 1u);   // rows k3 + i0, k3 + i0 + 1
+            if (i0 + 1 < jj || i0 >= r3) continue;
+            const double* Aj = A + j * m3 + k3;
+            st2_sc1(rs, (a & ~1u) + 2u * k, i0 >= jj ? Aj[i0] : 0.0, i0 + 1 < r3 ? Aj[i0 + 1] : 0.0);
         }
         for (int t = tid; t < r3; t += kFT) st_agent(acc + S.acc_off + t, -bv[k3 + t]);
     }
@@ -1462,9 +1529,15 @@ __device__ void publish_panel(int q, int s, const Tiles& T, double* F, const dou
     const int tid = threadIdx.x;
     const int j0 = kFNB * q, w = min(kFNB, T.k3 - j0), R = T.m3 - j0;
     const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
-    for (int e = tid; e < w * R; e += kFT) {
-        const int c = e / R, i = e - c * R;
-        if (i >= c) st_agent(F + (uint32_t)((j0 + c) * T.m3 + j0 + i), P[c * Rp + off + i]);
+    const auto rs = front_rsrc(F, T.m3);
+    const int npc = (R + 2) >> 1;   // aligned pairs per column segment (rows j0 .. m3)
+    for (int e = tid; e < w * npc; e += kFT) {
+        const int c = e / npc, k = e - c * npc;
+        const uint32_t a = (uint32_t)((j0 + c) * T.m3 + j0);
+        const int i0 = 2 * k - (int)(a & 1u);   // the pair's first row (segment frame)
+        if (i0 + 1 < c || i0 >= R) continue;   // wholly above the diagonal, or past the column
+        const double* pc = P + c * Rp + off;
+        st2_sc1(rs, (a & ~1u) + 2u * k, i0 >= c ? pc[i0] : 0.0, i0 + 1 < R ? pc[i0 + 1] : 0.0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1479,6 +1552,36 @@ __device__ void load_panel(int p, const Tiles& T, double* F, double* P) {
     const int tid = threadIdx.x;
     const int j0 = kFNB * p, w = min(kFNB, T.k3 - j0), R = T.m3 - j0;
     const int off = (4 - (w & 3)) & 3, Rp = fused_rp(R, off);
+    if (SC1) {   // 16-B sc1 loads of the aligned pairs (publish_panel's cover of each column segment)
+        const auto rs = front_rsrc(F, T.m3);
+        const int npc = (R + 2) >> 1, tot = w * npc;
+        constexpr int kB2 = 8;
+        for (int e0 = 0; e0 < tot; e0 += kFT * kB2) {
+            double2 v[kB2];
+#pragma unroll
+            for (int q = 0; q < kB2; ++q) {
+                const int e = e0 + tid + kFT * q;
+                const int c = e / npc, k = e - c * npc;
+                const uint32_t a = (uint32_t)((j0 + c) * T.m3 + j0);
+                const int i0 = 2 * k - (int)(a & 1u);
+                v[q] = make_double2(0.0, 0.0);
+                if (e < tot && i0 < R && i0 + 1 >= c) v[q] = ld2_sc1(rs, (a & ~1u) + 2u * k);
+            }
+#pragma unroll
+            for (int q = 0; q < kB2; ++q) {
+                const int e = e0 + tid + kFT * q;
+                const int c = e / npc, k = e - c * npc;
+                const uint32_t a = (uint32_t)((j0 + c) * T.m3 + j0);
+                const int i0 = 2 * k - (int)(a & 1u);
+                if (e < tot) {
+                    double* pc = P + c * Rp + off;
+                    if (i0 >= 0 && i0 < R) pc[i0] = i0 >= c ? v[q].x : 0.0;
+                    if (i0 + 1 < R) pc[i0 + 1] = i0 + 1 >= c ? v[q].y : 0.0;
+                }
+            }
+        }
+        return;
+    }
     constexpr int kB = 16;
     for (int e0 = 0; e0 < w * R; e0 += kFT * kB) {
         double v[kB];
@@ -1686,25 +1789,35 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
             __syncthreads();
             const FChild C = fchild[tk.ch_off + cq];
             const int n = 3 * C.r, m3c = 3 * (C.k + C.r), k3c = 3 * C.k, nj = C.jb - C.ja;
-            double* Fc = fronts + C.front_off + (int64_t)k3c * m3c + k3c;
+            // the child's update matrix: column j of it, rows i >= j, is front element
+            // (k3c + j) m3c + k3c + i -- 16-B sc1 loads of the aligned pairs over each column
+            const auto rs = front_rsrc(fronts + C.front_off, m3c);
             const int32_t* rm = relmap + C.rows_off;
-            for (int e0 = 0; e0 < nj * n; e0 += kFT * kPFL) {
-                double v[kPFL];
-                int dst[kPFL];
+            const int npc = (n + 2) >> 1, tot = nj * npc;
+            for (int e0 = 0; e0 < tot; e0 += kFT * kPFL) {
+                double2 v[kPFL];
+                int d0[kPFL], d1[kPFL];
 #pragma unroll
                 for (int q = 0; q < kPFL; ++q) {
                     const int e = e0 + tid + kFT * q;
-                    const int j = C.ja + e / n, i = e % n;
-                    dst[q] = -1;
-                    v[q] = 0.0;
-                    if (e < nj * n && i >= j) {
-                        v[q] = ld_agent(Fc + (int64_t)j * m3c + i);
-                        dst[q] = (3 * rm[j / 3] + j % 3 - cs) * m3 + 3 * rm[i / 3] + i % 3;
+                    const int jj = e / npc, k = e - jj * npc, j = C.ja + jj;
+                    const uint32_t a = (uint32_t)((k3c + j) * m3c + k3c);
+                    const int i0 = 2 * k - (int)(a & 1u);
+                    d0[q] = -1;
+                    d1[q] = -1;
+                    v[q] = make_double2(0.0, 0.0);
+                    if (e < tot && i0 + 1 >= j && i0 < n) {
+                        v[q] = ld2_sc1(rs, (a & ~1u) + 2u * k);
+                        const int cj = (3 * rm[j / 3] + j % 3 - cs) * m3;
+                        if (i0 >= j) d0[q] = cj + 3 * rm[i0 / 3] + i0 % 3;
+                        if (i0 + 1 < n) d1[q] = cj + 3 * rm[(i0 + 1) / 3] + (i0 + 1) % 3;
                     }
                 }
 #pragma unroll
-                for (int q = 0; q < kPFL; ++q)
-                    if (dst[q] >= 0) Tl[dst[q]] += v[q];
+                for (int q = 0; q < kPFL; ++q) {
+                    if (d0[q] >= 0) Tl[d0[q]] += v[q].x;
+                    if (d1[q] >= 0) Tl[d1[q]] += v[q].y;
+                }
             }
         }
         __syncthreads();

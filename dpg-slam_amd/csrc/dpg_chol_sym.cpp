@@ -786,7 +786,9 @@ static int sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const
         const int64_t k = sn_first[(size_t)s + 1] - sn_first[(size_t)s];
         const int64_t r = S->sn_rows_ptr[(size_t)s + 1] - S->sn_rows_ptr[(size_t)s];
         const int64_t m3 = 3 * (k + r);
-        S->front_off[(size_t)s + 1] = S->front_off[(size_t)s] + m3 * m3;
+        // rounded up to an even count: every front starts 16-B aligned (the fused factorization's
+        // 16-B sc1 hand-offs, dpg_chol.hip front_rsrc)
+        S->front_off[(size_t)s + 1] = S->front_off[(size_t)s] + ((m3 * m3 + 1) & ~(int64_t)1);
         maxm = std::max<int32_t>(maxm, (int32_t)(k + r));
         const double k3 = 3.0 * (double)k, r3 = 3.0 * (double)r;
         flops += k3 * k3 * k3 / 3.0 + k3 * k3 * r3 + k3 * r3 * r3;

@@ -172,23 +172,28 @@ int main(int argc, char** argv) {
             printf("fused factor span %.1f us (last front %d)\n", (t1 - t0) / 100.0, root);
             double sw = 0, sa = 0, sf = 0, so = 0, sl = 0;
             int depth = 0;
+            std::vector<int> crit;
             for (int q = root; q >= 0;) {
+                crit.push_back(q);
                 const unsigned long long* m = fm.data() + (size_t)q * 8;
                 int last = -1;
                 for (int c = 0; c < ns; ++c)
                     if (par[(size_t)c] == q && (last < 0 || fm[(size_t)c * 8 + 4] > fm[(size_t)last * 8 + 4])) last = c;
                 const double lat = last >= 0 ? ((double)m[1] - (double)fm[(size_t)last * 8 + 4]) / 100.0 : 0.0;
+                // large fronts: stamp 3 is the right-hand side owner's (a helper), stamp 4 the chain's
+                const double out = m[4] >= m[3] ? (m[4] - m[3]) / 100.0 : 0.0;
+                const double fac = ((double)(m[4] >= m[3] ? m[3] : m[4]) - (double)m[2]) / 100.0;
                 printf("  front %5d m3 %3d k3 %3d | claim %8.2f wait %7.2f (signal->ready %5.2f) asm %6.2f factor %7.2f out %6.2f\n", q,
                        m3v[(size_t)q], k3v[(size_t)q], (m[0] - t0) / 100.0, ((double)m[1] - (double)m[0]) / 100.0, lat,
-                       (m[2] - m[1]) / 100.0, (m[3] - m[2]) / 100.0, (m[4] - m[3]) / 100.0);
-                sw += lat; sa += (m[2] - m[1]) / 100.0; sf += (m[3] - m[2]) / 100.0; so += (m[4] - m[3]) / 100.0;
+                       (m[2] - m[1]) / 100.0, fac, out);
+                sw += lat; sa += (m[2] - m[1]) / 100.0; sf += fac; so += out;
                 sl += 0; ++depth;
                 q = last;
             }
             std::vector<unsigned long long> pm((size_t)ns * 16 * 8, 0ull);
             if (dpg_chol_panel_dump(pm.data(), ns) == 0) {
-                for (int q : {ns - 1, ns - 2, ns - 9}) {
-                    if (q < 0) continue;
+                for (int q : crit) {
+                    if (k3v[(size_t)q] <= 24) continue;
                     printf("  panels of front %d (k3 %d):", q, k3v[(size_t)q]);
                     for (int pp = 0; pp < 16; ++pp) {
                         const unsigned long long* m = pm.data() + ((size_t)q * 16 + pp) * 8;
@@ -204,8 +209,8 @@ int main(int argc, char** argv) {
                 }
             }
             std::vector<unsigned long long> sm2((size_t)ns * 16 * 8, 0ull);
-            if (dpg_chol_steps_dump(sm2.data(), ns) == 0) {
-                const int q = ns - 2;
+            if (dpg_chol_steps_dump(sm2.data(), ns) == 0 && crit.size() > 2 && k3v[(size_t)crit[2]] > 48) {
+                const int q = crit[2];
                 for (int pp = 1; pp < 3; ++pp) {
                     const unsigned long long* m = sm2.data() + ((size_t)q * 16 + pp) * 8;
                     const unsigned long long* pn = pm.data() + ((size_t)q * 16 + pp) * 8;
