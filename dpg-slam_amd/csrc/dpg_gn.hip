@@ -87,25 +87,14 @@ __device__ __forceinline__ void atwb_acc(const double* A, const double* w, const
 }
 
 // linearization by contribution-list entry: entry q of the upper blocks' lists (factor fi, role)
-// gets the 13 doubles its block adds, at rec[13 q] -- role 0 (diag i): A_i^T W A_i, the g_i term,
-// the chi2 term; role 1 (diag j, A_j = I): the diagonal of W, the g_j term; role 2 / 3 (the
-// (i, j) / (j, i) block): A_i^T W.  A factor is linearized once per entry (at most three times),
-// so the gather below reads one contiguous record per entry instead of chasing the factor.
+// contributes 13 doubles to its block -- role 0 (diag i): A_i^T W A_i, the g_i term, the chi2 term;
+// role 1 (diag j, A_j = I): the diagonal of W, the g_j term; role 2 / 3 (the (i, j) / (j, i) block):
+// A_i^T W.  A factor is linearized once per entry (at most three times).
 constexpr int kRec = 13;
-__global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X,
-                           const int32_t* __restrict__ clist, const int32_t* __restrict__ n_entries, int64_t fb,
-                           int64_t fe, const uint8_t* __restrict__ mine, double* __restrict__ rec, const int32_t* gate) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= *n_entries || (gate && !gate[0])) return;
-    const int32_t code = clist[q];
-    const int64_t fi = code >> 2;
-    const int role = code & 3;
-    if (mine ? !mine[fi] : (fi < fb || fi >= fe)) return;   // another rank's factor: the gather skips it
-    const dpg_factor f = F[fi];
+__device__ __forceinline__ void lin_record(const dpg_factor& f, const double* X, int role, double (&C)[kRec]) {
     double e[3], Ai[9];
     linearize(f, X, e, Ai);
     const double* w = f.info;
-    double C[kRec];
 #pragma unroll
     for (int k = 0; k < kRec; ++k) C[k] = 0.0;
     if (role == 0) {
@@ -120,67 +109,89 @@ __global__ void lin_kernel(const dpg_factor* __restrict__ F, const double* __res
         const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
         atwb_acc(Ai, w, I3, C);
     }
-    double* o = rec + kRec * q;
-#pragma unroll
-    for (int k = 0; k < kRec; ++k) o[k] = C[k];
 }
 
-// one lane per upper 3x3 block of H: adds its entries' records in list (= factor) order
-// (deterministic, no float atomics); kG records are loaded before the first is added
-template <int kG>
-__global__ __launch_bounds__(kRowThreads) void gather_kernel(const double* __restrict__ rec, const int32_t* __restrict__ cptr,
-                              const int32_t* __restrict__ clist, int64_t n_nodes, int64_t nnzb_upper,
-                              int64_t shard_begin, int64_t shard_end, const uint8_t* __restrict__ mine,
-                              double* __restrict__ hb, double* __restrict__ chi2_node, const int32_t* gate) {
-    const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nnzb_upper || (gate && !gate[0])) return;
-    const bool is_diag = u < n_nodes;
+// Linearization + assembly, ONE launch.  A 64-lane workgroup owns a run of upper blocks -- 8
+// diagonal ones (~8 entries each at config 4's degree) or 32 off-diagonal ones (~1 each), so
+// either way about one list entry per lane: the lanes linearize the run's entries into LDS (a
+// record per entry, kLgChunk at a time), then lane b adds block b's records in list (= factor)
+// order -- no float atomics, deterministic.  Round 4 ran this as two launches (a linearization
+// kernel writing the records to HBM, a gather kernel reading them back); same records, same order.
+constexpr int kLgLanes = 64, kLgDiag = 8, kLgOff = 32, kLgChunk = 128;
+__host__ __device__ inline int64_t lg_groups(int64_t n_nodes, int64_t nnzb_upper) {
+    return (n_nodes + kLgDiag - 1) / kLgDiag + (nnzb_upper - n_nodes + kLgOff - 1) / kLgOff;
+}
+__global__ __launch_bounds__(kLgLanes) void lin_gather_kernel(const dpg_factor* __restrict__ F, const double* __restrict__ X,
+                                                              const int32_t* __restrict__ cptr, const int32_t* __restrict__ clist,
+                                                              int64_t n_nodes, int64_t nnzb_upper, int64_t shard_begin,
+                                                              int64_t shard_end, const uint8_t* __restrict__ mine,
+                                                              double* __restrict__ hb, double* __restrict__ chi2_node,
+                                                              const int32_t* gate) {
+    __shared__ double rec[kLgChunk * kRec];
+    __shared__ int32_t code_s[kLgChunk];
+    if (gate && !gate[0]) return;
+    const int64_t nd = (n_nodes + kLgDiag - 1) / kLgDiag, wg = blockIdx.x;
+    const int64_t u0 = wg < nd ? wg * kLgDiag : n_nodes + (wg - nd) * kLgOff;
+    const int64_t u1 = wg < nd ? min(u0 + kLgDiag, n_nodes) : min(u0 + kLgOff, nnzb_upper);
+    const int lane = threadIdx.x;
+    const int64_t u = u0 + lane;
+    const bool own = u < u1;
+    const int32_t q0 = cptr[u0], q1 = cptr[u1];
+    const int32_t qa = own ? cptr[u] : 0, qb = own ? cptr[u + 1] : 0;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     double g[3] = {0, 0, 0};
     double chi2 = 0.0;
-    const int32_t q0 = cptr[u], q1 = cptr[u + 1];
-    for (int32_t qb = q0; qb < q1; qb += kG) {
-        int32_t code[kG];
-        double v[kG][kRec];
+    for (int32_t c0 = q0; c0 < q1; c0 += kLgChunk) {
+        const int32_t c1 = min(c0 + kLgChunk, q1);
+        for (int32_t q = c0 + lane; q < c1; q += kLgLanes) {
+            const int32_t code = clist[q], fi = code >> 2;
+            const bool skip = mine ? !mine[fi] : (fi < shard_begin || fi >= shard_end);   // another rank's factor
+            code_s[q - c0] = skip ? -1 : code;
+            if (skip) continue;
+            double C[kRec];
+            lin_record(F[fi], X, code & 3, C);
+            double* o = rec + kRec * (q - c0);
 #pragma unroll
-        for (int t = 0; t < kG; ++t) {
-            code[t] = qb + t < q1 ? clist[qb + t] : -1;
-            const double* r = rec + kRec * (int64_t)(qb + t < q1 ? qb + t : q0);
-#pragma unroll
-            for (int k = 0; k < kRec; ++k) v[t][k] = r[k];
+            for (int k = 0; k < kRec; ++k) o[k] = C[k];
         }
+        __syncthreads();
+        if (own) {
+            for (int32_t q = max(qa, c0); q < min(qb, c1); ++q) {
+                const int32_t code = code_s[q - c0];
+                if (code < 0) continue;
+                const double* v = rec + kRec * (q - c0);
+                const int role = code & 3;
+                if (role == 0) {          // diag i
 #pragma unroll
-        for (int t = 0; t < kG; ++t) {
-            const int32_t fi = code[t] >> 2, role = code[t] & 3;
-            if (code[t] < 0 || (mine ? !mine[fi] : (fi < shard_begin || fi >= shard_end))) continue;
-            if (role == 0) {          // diag i
+                    for (int k = 0; k < 9; ++k) H[k] += v[k];
 #pragma unroll
-                for (int k = 0; k < 9; ++k) H[k] += v[t][k];
+                    for (int r = 0; r < 3; ++r) g[r] += v[9 + r];
+                    chi2 += v[12];
+                } else if (role == 1) {   // diag j (A_j = I): W
 #pragma unroll
-                for (int r = 0; r < 3; ++r) g[r] += v[t][9 + r];
-                chi2 += v[t][12];
-            } else if (role == 1) {   // diag j (A_j = I): W
+                    for (int r = 0; r < 3; ++r)
 #pragma unroll
-                for (int r = 0; r < 3; ++r)
+                        for (int k = 0; k < 3; ++k) H[3 * r + k] += r == k ? v[r] : 0.0;
 #pragma unroll
-                    for (int k = 0; k < 3; ++k) H[3 * r + k] += r == k ? v[t][r] : 0.0;
+                    for (int r = 0; r < 3; ++r) g[r] += v[9 + r];
+                } else if (role == 2) {   // H(i, j) = A_i^T W, i < j
 #pragma unroll
-                for (int r = 0; r < 3; ++r) g[r] += v[t][9 + r];
-            } else if (role == 2) {   // H(i, j) = A_i^T W, i < j
+                    for (int k = 0; k < 9; ++k) H[k] += v[k];
+                } else {                  // H(j, i) = W A_i, j < i
 #pragma unroll
-                for (int k = 0; k < 9; ++k) H[k] += v[t][k];
-            } else {                  // H(j, i) = W A_i, j < i
+                    for (int r = 0; r < 3; ++r)
 #pragma unroll
-                for (int r = 0; r < 3; ++r)
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) H[3 * r + k] += v[t][3 * k + r];
+                        for (int k = 0; k < 3; ++k) H[3 * r + k] += v[3 * k + r];
+                }
             }
         }
+        __syncthreads();
     }
+    if (!own) return;
     double* o = hb + 9 * u;
 #pragma unroll
     for (int q = 0; q < 9; ++q) o[q] = H[q];
-    if (is_diag) {
+    if (u < n_nodes) {
         double* gb = hb + 9 * nnzb_upper + 3 * u;
         gb[0] = g[0]; gb[1] = g[1]; gb[2] = g[2];
         chi2_node[u] = chi2;
@@ -443,7 +454,7 @@ extern "C" int64_t dpg_gn_dev_hb_size(const dpg_gn_dev* g) { return dpg_gn_dev_v
 extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
     void* ptrs[] = {g->factors, g->up_row, g->up_col, g->up_cptr, g->up_clist, g->node_fptr, g->node_flist,
                     g->rowptr, g->colidx, g->src_up, g->bsr, g->minv, g->poses, g->x, g->r, g->z,
-                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own, g->contrib, g->scal3, g->mine, g->hb_part};
+                    g->p0, g->p1, g->q, g->partials, g->scal, g->hb_own, g->scal3, g->mine, g->hb_part};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (g->scal3_host) (void)hipHostFree(g->scal3_host);
@@ -540,7 +551,6 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     rc |= dev_alloc(&g->partials, 6 * (size_t)g->n_blocks_rows + (size_t)n);
     rc |= dev_alloc(&g->scal, 2 * (size_t)65536);
     rc |= dev_alloc(&g->hb_own, (size_t)dpg_gn_dev_hb_size(g));
-    rc |= dev_alloc(&g->contrib, 13 * std::max<size_t>(clist.size(), 1));   // lin_kernel's records
     rc |= dev_alloc(&g->scal3, 4);
     if (!rc && hipHostMalloc(reinterpret_cast<void**>(&g->scal3_host), 4 * sizeof(double)) != hipSuccess) rc = DPG_ERR_HIP;
     if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
@@ -571,18 +581,10 @@ extern "C" int dpg_gn_dev_icp_to_factors(dpg_gn_dev* g, const dpg_icp_result* re
 
 static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_t* gate, bool chi2 = true) {
     double* chi2_node = g->partials + 6 * (size_t)g->n_blocks_rows;
-    const int64_t nfs = g->mine ? g->n_factors : g->shard_end - g->shard_begin;
-    // upper bound of the list length (a Between factor has 3 entries); the kernel reads the length
-    if (nfs > 0)
-        hipLaunchKernelGGL(lin_kernel, dim3((unsigned)((3 * g->n_factors + 63) / 64)), dim3(64), 0, s, g->factors, g->poses,
-                           g->up_clist, g->up_cptr + g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, g->contrib,
-                           gate);
-    // 64-lane workgroups for both (the 30 k-lane gather filled under half the CUs at 256 threads:
-    // 0.487 -> 0.480 ms per GN iteration, identical final error), four records in flight per lane
-    // (at 256 threads 1 and 4 measured slower than 2; at 64 threads 4 ties 2 or wins by ~1 us)
-    hipLaunchKernelGGL(gather_kernel<4>, dim3((unsigned)((g->nnzb_upper + 63) / 64)), dim3(64), 0, s, g->contrib, g->up_cptr,
-                       g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, hb, chi2_node,
-                       gate);
+    const int64_t ng = lg_groups(g->n_nodes, g->nnzb_upper);
+    if (ng > 0)
+        hipLaunchKernelGGL(lin_gather_kernel, dim3((unsigned)ng), dim3(kLgLanes), 0, s, g->factors, g->poses, g->up_cptr,
+                           g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, hb, chi2_node, gate);
     if (chi2) {
         // the vote words go with the partial buffer only (the sum gives every device all of them)
         const bool vote = hb == g->hb_part && g->n_vote > 0 && g->chol;

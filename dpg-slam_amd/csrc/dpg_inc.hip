@@ -184,7 +184,7 @@ struct dpg_inc {
     int64_t reorders = 0;
     // device
     dpg_gn_dev g{};                            // assembly buffers + the Cholesky (g.chol)
-    size_t c_factors = 0, c_cptr = 0, c_clist = 0, c_hb = 0, c_contrib = 0, c_partials = 0;
+    size_t c_factors = 0, c_cptr = 0, c_clist = 0, c_hb = 0, c_partials = 0;
     double* theta = nullptr;                   // [V][3] linearization points (g.poses aliases it)
     double* est = nullptr;                     // [V][3] current estimate
     double* maxd = nullptr;                    // [V] max |delta_v| of the last update
@@ -225,7 +225,7 @@ struct dpg_inc {
 
 namespace {
 
-// contribution lists (gather_kernel) of every upper block, in factor order, and the device copies.
+// contribution lists (lin_gather_kernel) of every upper block, in factor order, and the device copies.
 // The factor list only grows between resets (a failed update truncates it again), so without Q1
 // scaling only the factors the device does not hold yet go up; the lists are rebuilt (a new factor
 // lands in the middle of the CSR) straight into a pinned staging buffer and copied without a
@@ -282,7 +282,6 @@ int inc_rebuild_lists(dpg_inc* q, hipStream_t s) {
     rc |= dgrow(&g.up_cptr, &q->c_cptr, (size_t)(nu + 1), s, 0);
     rc |= dgrow(&g.up_clist, &q->c_clist, (size_t)n_list, s, 0);
     rc |= dgrow(&g.hb_own, &q->c_hb, (size_t)(9 * nu + 3 * n + 2), s, 0);
-    rc |= dgrow(&g.contrib, &q->c_contrib, 13 * std::max<size_t>((size_t)n_list, 1), s, 0);   // lin_kernel's records
     rc |= dgrow(&g.partials, &q->c_partials, (size_t)(6 * g.n_blocks_rows + n), s, 0);
     if (!g.scal3) {
         rc |= hipMalloc(reinterpret_cast<void**>(&g.scal3), 4 * sizeof(double)) != hipSuccess;
@@ -423,7 +422,7 @@ void dpg_inc_destroy(dpg_inc* q) {
     if (!q) return;
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
     (void)hipStreamSynchronize(s);
-    void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.contrib, q->g.partials, q->g.scal3,
+    void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.partials, q->g.scal3,
                     q->theta, q->est, q->maxd, q->cnt, q->est_nxt, q->maxd_nxt, q->theta_bak, q->est_bak};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

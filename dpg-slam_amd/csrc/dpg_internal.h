@@ -124,7 +124,6 @@ typedef struct dpg_gn_dev {
     double* scal;                  /* PCG scalars */
     double* hb_own;                /* packed [H upper | b | chi2] buffer for single-GPU solves */
     void* chol;                    /* supernodal Cholesky (dpg_chol.hip), NULL if analysis failed */
-    double* contrib;               /* [n_factors][25] per-factor contributions (lin_kernel) */
     double* scal3;                 /* [4] device scalars: max |delta|, chi2, status, pad */
     double* scal3_host;            /* pinned mirror of scal3 */
     int32_t n_blocks_rows;         /* grid size for row kernels */
