@@ -1048,17 +1048,19 @@ __device__ __forceinline__ void bwd_z(const double* F, const double* Rg, const d
 
 template <bool kFull>
 __device__ __forceinline__ void bwd_diag(const double* F, const double* Rg, double* D, double* rd, int m3, int k3,
-                                         double* z, const double* dinv_f) {
+                                         double* z, const double* dinv_f, int s) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nblk = (k3 + kSB - 1) / kSB;
     for (int b = nblk - 1; b >= 0; --b) {
         const int jb = b * kSB, bw = min(kSB, k3 - jb);
+        ST_MARK(s, 8 + b, 0);   // timing builds: per block, load / chain / column dots
         if (b != nblk - 1) {   // the last block was loaded before the wait
             if (dinv_f) load_dinv<true>(D, dinv_f, jb, bw);
             else if constexpr (kFull) load_diag(D, rd, Rg, m3, jb, bw);
             else load_diag(D, rd, F, m3, jb, bw);
             __syncthreads();
         }
+        ST_MARK(s, 8 + b, 1);
         if (wave == 0) {
             if (dinv_f) {   // z_blk <- inv(B)^T z_blk
                 apply_dinv(D, z, jb, bw, lane);
@@ -1070,8 +1072,10 @@ __device__ __forceinline__ void bwd_diag(const double* F, const double* Rg, doub
             }
         }
         __syncthreads();
+        ST_MARK(s, 8 + b, 2);
         sub_coldots(z, (kFull ? Rg : F) + jb, m3, z + jb, jb, bw);
         __syncthreads();
+        ST_MARK(s, 8 + b, 3);
     }
 }
 
@@ -1107,7 +1111,7 @@ __device__ __forceinline__ void bwd_front(int s, const SnDev& S, int nseg, const
     __syncthreads();
     BW_MARK(s, 2);
     if (Li) inv_apply_upper(Li, k3, z, D);   // x_p <- L11^-T z_p: one product
-    else bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z, dinv_f);
+    else bwd_diag<kFull>(F, Rg, D, rd, m3, k3, z, dinv_f, s);
 }
 
 __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void chol_backward_dag(const int32_t* __restrict__ order, int32_t* sync,

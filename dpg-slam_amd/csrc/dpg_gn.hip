@@ -111,13 +111,14 @@ __device__ __forceinline__ void lin_record(const dpg_factor& f, const double* X,
     }
 }
 
-// Linearization + assembly, ONE launch.  A 64-lane workgroup owns a run of upper blocks -- 8
-// diagonal ones (~8 entries each at config 4's degree) or 32 off-diagonal ones (~1 each), so
-// either way about one list entry per lane: the lanes linearize the run's entries into LDS (a
+// Linearization + assembly, ONE launch.  A 64-lane workgroup owns a run of upper blocks -- 4
+// diagonal ones (~8.5 entries each at config 4's degree) or 32 off-diagonal ones (~1 each), so
+// either way at most one list entry per lane (8 diagonal blocks per workgroup: two rounds of
+// linearization on most lanes, 25 -> 14.5 us per launch at 4): the lanes linearize the run's entries into LDS (a
 // record per entry, kLgChunk at a time), then lane b adds block b's records in list (= factor)
 // order -- no float atomics, deterministic.  Round 4 ran this as two launches (a linearization
 // kernel writing the records to HBM, a gather kernel reading them back); same records, same order.
-constexpr int kLgLanes = 64, kLgDiag = 8, kLgOff = 32, kLgChunk = 128;
+constexpr int kLgLanes = 64, kLgDiag = 4, kLgOff = 32, kLgChunk = 128;
 __host__ __device__ inline int64_t lg_groups(int64_t n_nodes, int64_t nnzb_upper) {
     return (n_nodes + kLgDiag - 1) / kLgDiag + (nnzb_upper - n_nodes + kLgOff - 1) / kLgOff;
 }

@@ -208,20 +208,9 @@ int main(int argc, char** argv) {
                     printf("\n");
                 }
             }
-            std::vector<unsigned long long> sm2((size_t)ns * 16 * 8, 0ull);
-            if (dpg_chol_steps_dump(sm2.data(), ns) == 0 && crit.size() > 2 && k3v[(size_t)crit[2]] > 48) {
-                const int q = crit[2];
-                for (int pp = 1; pp < 3; ++pp) {
-                    const unsigned long long* m = sm2.data() + ((size_t)q * 16 + pp) * 8;
-                    const unsigned long long* pn = pm.data() + ((size_t)q * 16 + pp) * 8;
-                    printf("  front %d panel %d potrf steps (us from potrf start):", q, pp);
-                    for (int k = 0; k < 8; ++k) printf(" %.2f", ((double)m[k] - (double)pn[5]) / 100.0);
-                    printf(" end %.2f\n", ((double)pn[6] - (double)pn[5]) / 100.0);
-                }
-            }
             printf("critical path: %d fronts, hand-off %.1f + assembly %.1f + factor %.1f + out %.1f us\n", depth, sw, sa, sf, so);
         }
-        std::vector<unsigned long long> bm((size_t)ns * 8, 0ull);
+        std::vector<unsigned long long> bm((size_t)ns * 8, 0ull), sm2((size_t)ns * 16 * 8, 0ull);
         if (dpg_chol_bwd_dump(bm.data(), ns) == 0 && bm[4] != 0) {
             // backward: the last front to finish, then its parents up to the root
             unsigned long long t0 = ~0ull, t1 = 0;
@@ -241,6 +230,16 @@ int main(int argc, char** argv) {
                        m3v[(size_t)q], k3v[(size_t)q], (m[0] - t0) / 100.0, ((double)m[1] - (double)m[0]) / 100.0, lat,
                        (m[2] - m[1]) / 100.0, (m[3] - m[2]) / 100.0, (m[4] - m[3]) / 100.0);
                 sw += lat; sz += (m[2] - m[1]) / 100.0; sd += (m[3] - m[2]) / 100.0; so += (m[4] - m[3]) / 100.0;
+                if (k3v[(size_t)q] > 24 && dpg_chol_steps_dump(sm2.data(), ns) == 0) {   // per diagonal block: load, chain, column dots
+                    printf("      diag blocks:");
+                    for (int b = 3; b >= 0; --b) {
+                        const unsigned long long* d = sm2.data() + ((size_t)q * 16 + 8 + b) * 8;
+                        if (b * 64 >= k3v[(size_t)q] || !d[3]) continue;
+                        printf(" [b%d load %.2f chain %.2f dots %.2f]", b, ((double)d[1] - (double)d[0]) / 100.0,
+                               ((double)d[2] - (double)d[1]) / 100.0, ((double)d[3] - (double)d[2]) / 100.0);
+                    }
+                    printf("\n");
+                }
                 ++depth;
             }
             printf("backward critical path: %d fronts, hand-off %.1f + z %.1f + diag %.1f + out %.1f us\n", depth, sw, sz, sd, so);
