@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Why the ICP kernel times longer inside bench.py's step than in tools/icp_var_ab.py: the same
 launch (config 4, one context) timed (a) back to back, (b) right after the step's GN loop, (c) after
-the GN loop and a host sleep, (d) with the GN loop on but the covariance kernel off, interleaved."""
+the GN loop and a host sleep, (d) with the GN loop on but the covariance kernel off, (e) after GN
+and another ICP, (f, g) after the GN loop and a 0.1 / 1 ms host sleep, (h) after an ICP and a 5 ms
+sleep (idle without a GN before it), interleaved."""
 import os
 import sys
 import time
@@ -16,7 +18,8 @@ rounds = int(os.environ.get("AB_ROUNDS", "7"))
 w = synth.generate(os.environ.get("ICP_CONFIG", "config4"))
 p = _abi.default_icp_params()
 gp = _abi.default_gn_params()
-ms = {k: [] for k in ("a_back_to_back", "b_after_gn", "c_after_gn_sleep5ms", "d_after_gn_nocov", "e_after_gn_cov_icp")}
+ms = {k: [] for k in ("a_back_to_back", "b_after_gn", "c_after_gn_sleep5ms", "d_after_gn_nocov", "e_after_gn_cov_icp",
+                      "f_after_gn_sleep0.1ms", "g_after_gn_sleep1ms", "h_icp_sleep5ms")}
 with api.Context(0) as ctx:
     if os.environ.get("PROBE_TORCH_STREAM") == "1":   # bench.py's setting: torch's current stream
         import torch
@@ -43,6 +46,15 @@ with api.Context(0) as ctx:
             elif k == "c_after_gn_sleep5ms":
                 ctx.icp_run(compute_cov=True)
                 gn()
+                ctx.synchronize()
+                time.sleep(0.005)
+            elif k in ("f_after_gn_sleep0.1ms", "g_after_gn_sleep1ms"):
+                ctx.icp_run(compute_cov=True)
+                gn()
+                ctx.synchronize()
+                time.sleep(0.0001 if k.startswith("f") else 0.001)
+            elif k == "h_icp_sleep5ms":   # idle alone, no GN before it
+                ctx.icp_run(compute_cov=True)
                 ctx.synchronize()
                 time.sleep(0.005)
             elif k == "d_after_gn_nocov":
