@@ -1291,7 +1291,11 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
     if (n_edges <= 0) return DPG_OK;
     const int mode = max_points <= kModeMaxPts[0] ? 0 : max_points <= kModeMaxPts[1] ? 1 : 2;
     if (max_points > kp->lds_tgt || max_points > kModeMaxPts[2] || kp->lds_tgt > kModeMaxPts[mode]) return DPG_ERR_SIZE;
-    const size_t lds = ang_lds_layout(kp->lds_tgt, nullptr, mode);
+    // diagnostic forms 6 / 7: the same kernel with an LDS allocation that leaves room for only two /
+    // three workgroups per CU (the occupancy A/B of small shards, tools/icp_lpt_probe.py)
+    const int var0 = kp->kernel_variant;
+    const size_t lds = std::max(ang_lds_layout(kp->lds_tgt, nullptr, mode),
+                                var0 == 6 ? (size_t)80 * 1024 : var0 == 7 ? (size_t)54 * 1024 : (size_t)0);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const float2* ds = reinterpret_cast<const float2*>(ds_pts_dev);
     const float2* ip = reinterpret_cast<const float2*>(idx_pts_dev);

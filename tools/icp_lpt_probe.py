@@ -6,7 +6,7 @@ duration -- what that rank takes on its own GPU.  Both dispatch schedules: "call
 caller order) and "measured" (LPT over the last run's iterations x points, longest first).  The
 tail is then set against 1/N of the single-device launch and against the longest single
 alignment run alone (the floor no assignment can go below).
-usage: python tools/icp_lpt_probe.py [config] [reps]"""
+usage: python tools/icp_lpt_probe.py [config] [reps] [kernel variant]"""
 import os
 import sys
 
@@ -18,6 +18,7 @@ from dpgslam import _abi, api, synth  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "config4"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+kvar = int(sys.argv[3]) if len(sys.argv) > 3 else 0   # angular kernel form (6 / 7: two / three workgroups per CU)
 w = synth.generate(cfg)
 p = _abi.default_icp_params()
 
@@ -47,6 +48,7 @@ for n in (2, 4, 8):
     row = []
     for sched in ("caller", "measured"):
         with api.Context(0, virtual=n) as c:
+            c.set_icp_kernel_variant(kvar)
             c.set_icp_schedule(sched)
             c.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
             c.icp_prepare(w.edges, w.est, p)
