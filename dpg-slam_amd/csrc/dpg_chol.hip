@@ -971,6 +971,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     double* sm = smem_fw + 2;   // smem_fw[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
     if (gate_off(gate, 2)) return;
+    __builtin_amdgcn_s_setprio(2);   // as chol_factor_dag
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_fw));
     const SnDev S = sns[s];
     const int m3 = 3 * (S.k + S.r), k3 = 3 * S.k, r3 = 3 * S.r;
@@ -1128,6 +1129,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void ch
     double* sm = smem_b + 2;   // smem_b[0]: the claimed front (no static LDS)
     const int tid = threadIdx.x;
     if (gate_off(gate, 0)) return;
+    __builtin_amdgcn_s_setprio(2);   // as chol_factor_dag
     const int s = claim_lds(order, sync, reinterpret_cast<int*>(smem_b));
     const SnDev S = sns[s];
     BW_MARK(s, 0);
@@ -1953,6 +1955,9 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
     extern __shared__ __attribute__((aligned(16))) double smem_f[];
     double* sm = smem_f + 2;   // smem_f[0]: the claimed ticket (no static LDS: keeps the base 16-B aligned)
     if (gate_off(gate, 1)) return;
+    // issue priority over co-resident waves of other kernels (the batch covariance runs beside the
+    // first factorization of a step, dpg_icp_batch_run): this kernel is a chain of dependent steps
+    __builtin_amdgcn_s_setprio(2);
     const int code = claim_lds(order, sync, reinterpret_cast<int*>(smem_f));
     const int s = code >> 6, mem = code & 63;
     const SnDev S = sns[s];
