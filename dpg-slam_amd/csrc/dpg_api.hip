@@ -125,6 +125,7 @@ struct dpg_ctx {
     DevBuf<unsigned char> icp_scratch;   // angle variant, clouds above 4096 points: record slices
     std::vector<int64_t> full_off, ds_off;
     int64_t n_nodes = 0;
+    int64_t idx_valid = 0;         // angular variant: nodes [0, idx_valid) of the store have their index
     int32_t ratio = 1;
     int32_t max_ds = 0;
     // staged edge batch
@@ -245,12 +246,14 @@ int launch_batch(dpg_ctx* c, const float* ds_dev, const float* full_dev, const i
     if (c->icp_variant == DPG_ICP_KDTREE) {
         rc = dpg_launch_kdtree_build(ds_dev, ds_off_dev, n_tree_nodes, max_node_pts, tree_pts, tree_idx, c->stream);
         if (rc) return fail(rc, "k-d tree build launch failed (%d)", rc);
-    } else if (c->icp_variant == DPG_ICP_ANGULAR) {
+    } else if (c->icp_variant == DPG_ICP_ANGULAR && tree_from < n_tree_nodes) {
         rc = dpg_launch_angle_index(ds_dev, ds_off_dev + tree_from, n_tree_nodes - tree_from, max_node_pts, tree_pts,
                                     tree_idx, buckets + tree_from * (int64_t)(dpg_angle_buckets() + 1),
                                     c->kernel_variant == 2, c->stream);
         if (rc) return fail(rc, "angle index build launch failed (%d)", rc);
     }
+    if (ds_dev == c->ds.p)   // the store's own indexes: current for every node now, or (other variants) overwritten
+        c->idx_valid = c->icp_variant != DPG_ICP_ANGULAR ? 0 : tree_from <= c->idx_valid ? n_tree_nodes : c->idx_valid;
     if (timed) HIP_TRY(hipEventRecord(c->ev[0], c->stream));
     if (c->icp_variant == DPG_ICP_ANGULAR) {
         kp.lds_tgt = round_up(std::max<int32_t>(maxp, 1), 16);   // record capacity
@@ -690,6 +693,7 @@ static int scans_upload_1(dpg_ctx* c, const float* pts, const int64_t* off, int6
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_nodes = V;
+    c->idx_valid = 0;
     c->ratio = ratio;
     c->max_ds = (int32_t)mx;
     return DPG_OK;
@@ -773,6 +777,7 @@ int dpg_scans_index_all(dpg_ctx* c) {
     const int rc = dpg_launch_angle_index(c->ds.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
                                           c->buckets.p, c->kernel_variant == 2, c->stream);
     if (rc) return fail(rc, "angle index build failed");
+    c->idx_valid = c->n_nodes;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return DPG_OK;
 }
@@ -787,6 +792,7 @@ static void scans_truncate(dpg_ctx* c, int64_t V) {
         q->full_off.resize((size_t)V + 1);
         q->ds_off.resize((size_t)V + 1);
         q->n_nodes = V;
+        q->idx_valid = std::min(q->idx_valid, V);
     }
 }
 
@@ -940,9 +946,11 @@ static int batch_run_1(dpg_ctx* c, int32_t compute_cov, int32_t trace_iters) {
     }
     c->trace_iters = trace_iters > 0 ? trace_iters : 0;
     c->have_cov = compute_cov != 0;
+    // the angle index is a function of the stored scans alone: a batch run again on the same store
+    // (the next sweep, the bench's steps) reuses it and builds only the nodes appended since
     return launch_batch(c, c->ds.p, c->full.p, c->ds_off_dev.p, c->n_nodes, c->max_ds, c->tree_pts.p, c->tree_idx.p,
                         c->buckets.p, c->edges.p, c->n_edges, kp, c->max_src, c->max_tgt, c->res.p,
-                        compute_cov ? c->hess.p : nullptr, tr, true);
+                        compute_cov ? c->hess.p : nullptr, tr, true, std::min(c->idx_valid, c->n_nodes));
 }
 
 // ---- the rank form's cross-process steps (blocking; every rank makes them in the same order) ----
@@ -1055,7 +1063,10 @@ static int icp_batch_run_from(dpg_ctx* c, int64_t tree_from) {
 int dpg_ctx_set_icp_variant(dpg_ctx* c, int32_t variant) {
     if (!c || (variant != DPG_ICP_ANGULAR && variant != DPG_ICP_KDTREE && variant != DPG_ICP_GRID))
         return fail(DPG_ERR_ARG, "bad ICP variant");
-    for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->icp_variant = variant;
+    for (int k = 0; k < n_dev(c); ++k) {
+        if (dev_ctx(c, k)->icp_variant != variant) dev_ctx(c, k)->idx_valid = 0;
+        dev_ctx(c, k)->icp_variant = variant;
+    }
     return DPG_OK;
 }
 
@@ -1073,7 +1084,10 @@ int dpg_ctx_set_cov_workgroups(dpg_ctx* c, int32_t n) {
 
 int dpg_ctx_set_icp_kernel_variant(dpg_ctx* c, int32_t v) {
     if (!c || v < 0) return fail(DPG_ERR_ARG, "bad kernel variant");
-    for (int k = 0; k < n_dev(c); ++k) dev_ctx(c, k)->kernel_variant = v;
+    for (int k = 0; k < n_dev(c); ++k) {
+        if ((dev_ctx(c, k)->kernel_variant == 2) != (v == 2)) dev_ctx(c, k)->idx_valid = 0;   // form 2: the bitonic builder
+        dev_ctx(c, k)->kernel_variant = v;
+    }
     return DPG_OK;
 }
 
@@ -2237,6 +2251,7 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
                                     c->buckets.p + V * (int64_t)(dpg_angle_buckets() + 1), c->kernel_variant == 2,
                                     c->stream);
         if (rc) return fail(rc, "angle index build failed");
+        if (c->idx_valid == V) c->idx_valid = V + 1;
     }
     const double init[3] = {(double)init_pose[0], (double)init_pose[1], (double)init_pose[2]};
     if ((rc = dpg_inc_update(g, 1, init, F.data(), (int64_t)F.size(), &S.update))) return rc;   // rolled back itself
