@@ -733,18 +733,25 @@ __device__ __forceinline__ void clear_sync(int32_t* sync, int64_t n_words, int32
     if (threadIdx.x == 0) *status = 0;
 }
 
-// a report into host memory: the fields, a system-scope fence, then the tag the host polls
+// a report into host memory: the fields, then the tag the host polls.  The slot is fine-grained
+// (coherent, uncached) host memory (dpg_api.hip ensure_pipe): the fields go out as system-scope
+// stores, and the tag only after all of them have been acknowledged (s_waitcnt vmcnt(0)), so the
+// host never sees the tag before the fields -- without __threadfence_system's write-back of the
+// whole L2, which holds nothing of the slot's
+__device__ __forceinline__ void sys_st64(void* p, uint64_t v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+static_assert(offsetof(dpg_gn_slot, reuse) == 24 && offsetof(dpg_gn_slot, active) == 28 &&
+              offsetof(dpg_gn_slot, final_) == 32 && offsetof(dpg_gn_slot, it) == 36 && offsetof(dpg_gn_slot, tag) == 40,
+              "post_slot stores the int pairs as 8-byte words");
 __device__ __forceinline__ void post_slot(dpg_gn_slot* slot, const dpg_gn_slot& o, uint64_t tag) {
-    volatile dpg_gn_slot* v = slot;
-    v->dinf = o.dinf;
-    v->error = o.error;
-    v->status = o.status;
-    v->reuse = o.reuse;
-    v->active = o.active;
-    v->final_ = o.final_;
-    v->it = o.it;
-    __threadfence_system();
-    v->tag = tag;
+    sys_st64(&slot->dinf, (uint64_t)__double_as_longlong(o.dinf));
+    sys_st64(&slot->error, (uint64_t)__double_as_longlong(o.error));
+    sys_st64(&slot->status, (uint64_t)__double_as_longlong(o.status));
+    sys_st64(&slot->reuse, (uint64_t)(uint32_t)o.reuse | (uint64_t)(uint32_t)o.active << 32);
+    sys_st64(&slot->final_, (uint64_t)(uint32_t)o.final_ | (uint64_t)(uint32_t)o.it << 32);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sys_st64(&slot->tag, tag);
 }
 
 __global__ void pipe_init_kernel(dpg_gn_ctl* ctl, int32_t reuse, int32_t last_was_chord, int32_t have_factor,
