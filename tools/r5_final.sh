@@ -14,3 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err"
 rc=$?; echo "prof exit $rc"; [ $rc -eq 0 ] || exit $rc
 python3 tools/gn_timeline.py "$OUT/prof" 2 > "$OUT/timeline.txt" 2>&1; head -16 "$OUT/timeline.txt"
+timeout -k 10 300 python -u bench.py --workload incremental --cpu-nodes 0 > "$OUT/inc.json" 2> "$OUT/inc.err"
+rc=$?; echo "inc exit $rc"; tail -c 600 "$OUT/inc.json"; [ $rc -eq 0 ] || exit $rc
