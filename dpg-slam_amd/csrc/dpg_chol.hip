@@ -1827,6 +1827,17 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
             }
         }
         __syncthreads();
+        if (t == 0 && mem == 0 && db) {
+            // the chain's first panel straight from the assembled tile: LDS to LDS into the panel
+            // frame of PB (zeros above the diagonal, as load_panel), no round trip through the front
+            const int off = (4 - (nc & 3)) & 3, Rp = fused_rp(m3, off);
+            for (int e = tid; e < nc * m3; e += kFT) {
+                const int c = e / m3, i = e - c * m3;
+                PB[c * Rp + off + i] = i >= c ? Tl[e] : 0.0;
+            }
+            __syncthreads();
+            continue;
+        }
         const bool handoff = t == 1 && mem != 0;   // pivot tile 1 goes to the chain as assembled
         for (int e = tid; e < nc * m3; e += kFT) {
             const int col = cs + e / m3, row = e % m3;
@@ -1857,9 +1868,9 @@ __device__ __forceinline__ void large_front(int s, int mem, const SnDev& S, int3
     bool bad = false;
     if (mem == 0) {
         // ---- the panel chain
-        double* cur = PA;
+        double* cur = db ? PB : PA;   // db: panel 0 is in PB already (the assembly's relayout)
         if (tid < kFNB / 3) reinterpret_cast<int*>(scr + kFNB * kFNB + 8 * (kFNB / 3))[tid] = 0;   // POTRF step epochs
-        load_panel<false>(0, T, F, cur);   // tile 0: assembled by this workgroup
+        if (!db) load_panel<false>(0, T, F, cur);   // tile 0: assembled by this workgroup
         __syncthreads();
         factor_lds(0, s, T, cur, scr, bad);
         publish_panel(0, s, T, F, cur, pflag);
