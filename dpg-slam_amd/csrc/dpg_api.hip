@@ -161,6 +161,9 @@ struct dpg_ctx {
     // device 0 and holds the batch as the caller sees it; `peers` are full single-device contexts
     // of the other local devices.  Local device k is global rank rank0 + k of `world`.
     std::vector<dpg_ctx*> peers;
+    // incremental graphs and DPG stores created on this context: dpg_ctx_destroy destroys them
+    // first (their buffers, helper thread and events all use the context's stream)
+    std::vector<std::pair<void*, void (*)(void*)>> children;
     std::vector<ncclComm_t> comms;   // RCCL: one communicator per local device
     dpg_coll_ops host_ops{};         // kCollHost: the caller's host-memory collectives
     std::vector<double> host_hb;     // kCollHost: the packed system in host memory
@@ -584,8 +587,25 @@ int dpg_ctx_set_icp_schedule(dpg_ctx* c, int32_t schedule) {
     return DPG_OK;
 }
 
+void dpg_ctx_adopt(dpg_ctx* c, void* child, void (*destroy)(void*)) {
+    if (c && child) c->children.emplace_back(child, destroy);
+}
+void dpg_ctx_release_child(dpg_ctx* c, void* child) {
+    if (!c) return;
+    for (size_t k = 0; k < c->children.size(); ++k)
+        if (c->children[k].first == child) {
+            c->children.erase(c->children.begin() + (std::ptrdiff_t)k);
+            return;
+        }
+}
+
 void dpg_ctx_destroy(dpg_ctx* c) {
     if (!c) return;
+    while (!c->children.empty()) {   // each child's destroy releases itself from the list
+        const auto ch = c->children.back();
+        ch.second(ch.first);
+        if (!c->children.empty() && c->children.back().first == ch.first) c->children.pop_back();
+    }
     if (c->coll == kCollVirtual) (void)hipStreamSynchronize(c->stream);   // the peers' work is on it
     for (dpg_ctx* q : c->peers) dpg_ctx_destroy(q);
     c->peers.clear();
@@ -1129,7 +1149,12 @@ static int fetch_allgather(dpg_ctx* c, void* out, size_t rec_bytes, const void* 
 // the context's cost memory (the next plan of the same pairs); the per-node path, whose pairs are
 // never re-planned, does not learn (the memory grew by every node's pairs).
 static int batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess, bool learn);
-int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess) { return batch_fetch(c, results, hess, true); }
+int dpg_icp_batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess, int64_t cap) {
+    if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
+    if ((results || hess) && cap < (int64_t)c->batch.size())
+        return fail(DPG_ERR_SIZE, "result buffers hold fewer records than the staged batch (dpg_icp_batch_size)");
+    return batch_fetch(c, results, hess, true);
+}
 
 static int batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess, bool learn) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
@@ -1173,13 +1198,14 @@ static int batch_fetch(dpg_ctx* c, dpg_icp_result* results, double* hess, bool l
 // what dpg_icp_batch_fetch writes
 int64_t dpg_icp_batch_size(dpg_ctx* c) { return c ? (int64_t)c->batch.size() : fail(DPG_ERR_ARG, "ctx is NULL"); }
 
-int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t* max_src_out) {
+int dpg_icp_batch_fetch_trace(dpg_ctx* c, int32_t* trace, int64_t trace_cap, int64_t* max_src_out) {
     if (!c) return fail(DPG_ERR_ARG, "ctx is NULL");
     if (is_multi(c)) return fail(DPG_ERR_STATE, "the correspondence trace is a single-device diagnostic");
     if (max_src_out) *max_src_out = std::max(c->max_src, 1);
     if (!trace) return DPG_OK;
     if (c->trace_iters <= 0) return fail(DPG_ERR_STATE, "last batch ran without a trace");
     const size_t n = (size_t)c->n_edges * (size_t)c->trace_iters * (size_t)std::max(c->max_src, 1);
+    if (trace_cap < 0 || (size_t)trace_cap < n) return fail(DPG_ERR_SIZE, "trace buffer smaller than E * trace_iters * max_src");
     HIP_TRY(hipMemcpyAsync(trace, c->trace.p, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return DPG_OK;
@@ -1835,6 +1861,24 @@ static int gn_loop(dpg_ctx* c, const dpg_gn_params& P, double* poses, double t0,
                 else if (memcmp(sc, sc0, sizeof(sc)))
                     return fail(DPG_ERR_INTERNAL, "devices diverged at GN iteration %d (device %d)", it + 1, k);
             }
+            // world > 1: decide from the all-reduced vote words (every rank's max |delta| and
+            // status of this iteration, dpg_gn.hip chi2_kernel), never from the local scalars
+            // alone -- ranks that disagreed would issue different numbers of all-reduces and hang
+            if (multi && c->gn.n_vote > 0) {
+                const int W = c->gn.world;
+                std::vector<double> vw((size_t)(2 * W));
+                HIP_TRY(hipSetDevice(c->device));
+                HIP_TRY(hipMemcpyAsync(vw.data(), c->gn.hb_own + dpg_gn_dev_vote_offset(&c->gn), sizeof(double) * vw.size(),
+                                       hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(hipStreamSynchronize(c->stream));
+                for (int r = 0; r < W; ++r) {
+                    if (memcmp(&vw[(size_t)r], &vw[0], sizeof(double)))
+                        return fail(DPG_ERR_INTERNAL, "ranks diverged at GN iteration %d (rank %d: |d| %.17g, rank 0: %.17g)",
+                                    it + 1, r, vw[(size_t)r], vw[0]);
+                    sc0[2] = std::max(sc0[2], vw[(size_t)(W + r)]);
+                }
+                sc0[0] = vw[0];
+            }
             if (sc0[2] != 0.0) return fail(DPG_ERR_NUMERIC, "Cholesky failed (status %d)", (int)sc0[2]);
             S.pcg_iterations += c->gn.last_pcg_iters;
             ++it;
@@ -2093,7 +2137,7 @@ int dpg_reoptimize(dpg_ctx* c, int64_t V, const int32_t* pass, const float* est,
     // the sweep's own results (the caller may fetch them again: the batch stays staged) -- the
     // alignments end here, and their outcomes give the loop-closure count
     std::vector<dpg_icp_result> res((size_t)std::max<int64_t>(E, 1));
-    if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+    if ((rc = dpg_icp_batch_fetch(c, res.data(), nullptr, (int64_t)res.size()))) return rc;
     const double t2 = now_ms();
     // 5. batch Gauss-Newton from the estimated poses (optimizeGraph, dpg_slam.cc:111-119, 316-329);
     //    the ICP slots take the results where they were aligned (multi-device: on each device)
@@ -2136,7 +2180,7 @@ int dpg_reoptimize_inc(dpg_inc* g, int64_t V, const int32_t* pass, const float* 
     if (rc) return rc;
     const int64_t E = S.n_icp_edges;
     std::vector<dpg_icp_result> res((size_t)std::max<int64_t>(E, 1));
-    if (E > 0 && (rc = dpg_icp_batch_fetch(c, res.data(), nullptr))) return rc;
+    if (E > 0 && (rc = dpg_icp_batch_fetch(c, res.data(), nullptr, (int64_t)res.size()))) return rc;
     const double t2 = now_ms();
     // addObservationConstraint per aligned pair: the successive pairs always, a loop closure when
     // its alignment converged (dpg_slam.cc:85-104); the slots of dropped closures go away
@@ -2220,7 +2264,9 @@ int dpg_add_node_pairs(dpg_inc* g, const float* cloud, int64_t n_pts, const floa
     if (E > 0) {
         const double t0 = now_ms();
         if ((rc = dpg_icp_batch_prepare(c, edges.data(), E, pf.data(), &I))) return rc;
-        if ((rc = icp_batch_run_from(c, V))) return rc;
+        // nodes below V whose index is stale (a k-d tree / grid batch overwrote the buffers, or a
+        // fresh upload was not indexed) are rebuilt with the new node
+        if ((rc = icp_batch_run_from(c, std::min(V, c->idx_valid)))) return rc;
         // while the GPU aligns: the update's structure on the host, with every pair a factor may
         // come from (a loop closure that does not converge stays an explicit zero block)
         {

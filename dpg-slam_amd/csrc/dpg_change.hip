@@ -763,6 +763,7 @@ dpg_dpg* dpg_dpg_create(dpg_ctx* ctx, int64_t V, const int64_t* off, const float
         hipStreamSynchronize(s) != hipSuccess)
         return bad("upload of the node store failed");
     for (auto& e : d->ev) (void)hipEventCreate(&e);
+    dpg_ctx_adopt(ctx, d, [](void* x) { dpg_dpg_destroy(static_cast<dpg_dpg*>(x)); });
     return d;
 }
 
@@ -896,6 +897,7 @@ int dpg_dpg_append(dpg_dpg* d, int64_t n_new, const int64_t* off_rel, const floa
 
 void dpg_dpg_destroy(dpg_dpg* d) {
     if (!d) return;
+    dpg_ctx_release_child(d->ctx, d);
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     if (d->h_ctl) (void)hipHostFree(d->h_ctl);

@@ -411,10 +411,8 @@ __device__ __forceinline__ double group16_sum(double a) {
 // dependent substitution steps per 64-column block, each waiting on its block's loads (profiles/r05
 // chol timing: 59 of the backward's 122 us).  After each factorization this kernel inverts L11 of
 // every front with at least solve_inv_cols pivot columns; the solves then apply it as ONE product
-// (all loads in flight at once).  Task (s, j0): columns [j0, j0 + 16) of X = L11^-1 by column-parallel
-// forward substitution -- 16 lanes per column, lane l owning rows j0 + l + 16 q; step i broadcasts
-// x_i from its owner and every lane adds L(r, i) x_i to its rows r > i (ascending i: a fixed
-// summation order).  L11's columns are staged in LDS 16 at a time.
+// (all loads in flight at once).  Task (s, j0): columns [j0, j0 + kInvCols) of X = L11^-1 by
+// column-parallel forward substitution, ascending i (a fixed summation order).
 // One WAVE per column j of X = L11^-1 (four per workgroup): lane l owns rows j + l + 64 q (q < 3:
 // fronts up to 192 pivot columns); step i broadcasts x_i from its owner (one readlane) and every lane
 // adds L(r, i) x_i to its rows r > i.  L's columns come straight from the fronts (L2), 16 steps'
@@ -2349,7 +2347,6 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
         d.inv = (int32_t)c->linv_total;
         c->linv_total += (int64_t)k3 * k3;
         for (int32_t j0 = 0; j0 < k3; j0 += kInvCols) H.inv_t.push_back(make_int2(s, j0));
-        c->lds_inv = 0;
     }
     c->n_inv_tasks = (int64_t)H.inv_t.size();
     std::vector<SolveSeg>& segs = H.segs;

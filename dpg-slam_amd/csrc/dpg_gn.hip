@@ -239,7 +239,7 @@ __global__ void chi2_kernel(const double* __restrict__ chi2_node, int64_t n, dou
         *out = s;
         if (vote) {
             vote[rank] = *dinf;
-            vote[world + rank] = (double)*status;
+            vote[world + rank] = status ? (double)*status : 0.0;   // the PCG solver has no status word
         }
     }
 }
@@ -588,10 +588,10 @@ static int assemble_gated(dpg_gn_dev* g, double* hb, hipStream_t s, const int32_
                            g->up_clist, g->n_nodes, g->nnzb_upper, g->shard_begin, g->shard_end, g->mine, hb, chi2_node, gate);
     if (chi2) {
         // the vote words go with the partial buffer only (the sum gives every device all of them)
-        const bool vote = hb == g->hb_part && g->n_vote > 0 && g->chol;
+        const bool vote = hb == g->hb_part && g->n_vote > 0;
         hipLaunchKernelGGL(chi2_kernel, dim3(1), dim3(1024), 0, s, chi2_node, g->n_nodes,
                            hb + 9 * g->nnzb_upper + 3 * g->n_nodes, gate, vote ? hb + dpg_gn_dev_vote_offset(g) : nullptr,
-                           g->scal3, vote ? dpg_chol_status_dev(g->chol) : nullptr, g->world, g->rank);
+                           g->scal3, vote && g->chol ? dpg_chol_status_dev(g->chol) : nullptr, g->world, g->rank);
     }
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }

@@ -378,6 +378,7 @@ dpg_inc* dpg_inc_create(dpg_ctx* ctx, const dpg_inc_params* p) {
     if (q->P.reorder_lead < 0 || q->P.reorder_lead >= q->P.reorder_every) q->P.reorder_lead = 0;
     q->opts = *dpg_ctx_chol_opts(ctx);   // the context's solver options
     q->P.gn.linear_solver = DPG_SOLVER_CHOLESKY;
+    dpg_ctx_adopt(ctx, q, [](void* x) { dpg_inc_destroy(static_cast<dpg_inc*>(x)); });
     return q;
 }
 
@@ -420,6 +421,7 @@ int dpg_inc_abort_prepare(dpg_inc* q) {
 
 void dpg_inc_destroy(dpg_inc* q) {
     if (!q) return;
+    dpg_ctx_release_child(q->ctx, q);
     hipStream_t s = reinterpret_cast<hipStream_t>(dpg_ctx_stream_of(q->ctx));
     (void)hipStreamSynchronize(s);
     void* ptrs[] = {q->g.factors, q->g.up_cptr, q->g.up_clist, q->g.hb_own, q->g.partials, q->g.scal3,

@@ -27,6 +27,10 @@ int dpg_scans_export(dpg_ctx* c, int64_t* n_nodes, int32_t* ratio, int64_t* off,
 int dpg_scans_index_all(dpg_ctx* c);
 void* dpg_ctx_stream_of(dpg_ctx* c);
 int dpg_ctx_device_of(dpg_ctx* c);
+/* children of a context (incremental graphs, DPG stores): dpg_ctx_destroy destroys the ones still
+ * alive, newest first; a child's own destroy releases it from the list */
+void dpg_ctx_adopt(dpg_ctx* c, void* child, void (*destroy)(void*));
+void dpg_ctx_release_child(dpg_ctx* c, void* child);
 
 /* One ICP edge as the kernel sees it (64 B).  Offsets/counts are in points (float2). */
 typedef struct dpg_icp_edge {

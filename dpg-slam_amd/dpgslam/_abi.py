@@ -281,8 +281,8 @@ SIGNATURES = {
     "dpg_scans_upload": (C.c_int, [P, F32P, I64P, C.c_int64, C.c_int32]),
     "dpg_icp_batch_prepare": (C.c_int, [P, I32P, C.c_int64, F32P, C.POINTER(IcpParams)]),
     "dpg_icp_batch_run": (C.c_int, [P, C.c_int32, C.c_int32]),
-    "dpg_icp_batch_fetch": (C.c_int, [P, P, F64P]),
-    "dpg_icp_batch_fetch_trace": (C.c_int, [P, I32P, I64P]),
+    "dpg_icp_batch_fetch": (C.c_int, [P, P, F64P, C.c_int64]),
+    "dpg_icp_batch_fetch_trace": (C.c_int, [P, I32P, C.c_int64, I64P]),
     "dpg_icp_batch_size": (C.c_int64, [P]),
     "dpg_icp_batch_kernel_ms": (C.c_float, [P]),
     "dpg_cov_batch_kernel_ms": (C.c_float, [P]),

@@ -350,14 +350,14 @@ class Context:
         self.n_edges = n
         res = results_array(n)
         hess = np.zeros((n, 9), np.float64) if with_hessian else None
-        check(lib().dpg_icp_batch_fetch(self.handle, vptr(res), ptr(hess, C.c_double)), "dpg_icp_batch_fetch")
+        check(lib().dpg_icp_batch_fetch(self.handle, vptr(res), ptr(hess, C.c_double), n), "dpg_icp_batch_fetch")
         return res, (hess.reshape(-1, 3, 3) if hess is not None else None)
 
     def icp_fetch_trace(self, iters: int) -> np.ndarray:
         ms = C.c_int64(0)
-        check(lib().dpg_icp_batch_fetch_trace(self.handle, None, C.byref(ms)), "trace size")
+        check(lib().dpg_icp_batch_fetch_trace(self.handle, None, 0, C.byref(ms)), "trace size")
         tr = np.empty((self.n_edges, iters, ms.value), np.int32)
-        check(lib().dpg_icp_batch_fetch_trace(self.handle, ptr(tr, C.c_int32), C.byref(ms)), "trace fetch")
+        check(lib().dpg_icp_batch_fetch_trace(self.handle, ptr(tr, C.c_int32), tr.size, C.byref(ms)), "trace fetch")
         return tr
 
     def icp_batch(self, edges, poses, params=None, compute_cov=True, trace_iters=0):
@@ -499,9 +499,10 @@ class Context:
 def _ctx_gone(child) -> bool:
     """The context a DpgStore / IncGraph lives on is already destroyed.  Context.close closes its
     children first, but when both sit in one reference cycle the garbage collector clears the
-    context's weak child set before any finalizer runs, and may finalize the context first; the
-    child's native destroy would then touch freed context state, so it is skipped (the device
-    memory went with the context's)."""
+    context's weak child set before any finalizer runs, and may finalize the context first.
+    dpg_ctx_destroy has then already destroyed the child (a context destroys the incremental graphs
+    and DPG stores created on it: device buffers, pinned mirrors, events, helper thread), so the
+    handle is dangling and only dropped here."""
     ctx = getattr(child, "ctx", None)
     return ctx is not None and getattr(ctx, "handle", None) is None
 
@@ -531,7 +532,7 @@ class DpgStore:
 
     def close(self):
         if getattr(self, "handle", None):
-            if _ctx_gone(self):   # finalized after its context in one garbage cycle: nothing safe to free
+            if _ctx_gone(self):   # finalized after its context: dpg_ctx_destroy already destroyed it
                 self.handle = None
                 return
             lib().dpg_dpg_destroy(self.handle)
@@ -626,7 +627,7 @@ class IncGraph:
 
     def close(self):
         if getattr(self, "handle", None):
-            if _ctx_gone(self):   # finalized after its context in one garbage cycle: nothing safe to free
+            if _ctx_gone(self):   # finalized after its context: dpg_ctx_destroy already destroyed it
                 self.handle = None
                 return
             lib().dpg_inc_destroy(self.handle)

@@ -127,6 +127,8 @@ void dpg_icp_params_default(dpg_icp_params* p);
 void dpg_gn_params_default(dpg_gn_params* p);
 /* device = HIP device ordinal; returns NULL (and sets dpg_last_error) when no GPU is usable. */
 dpg_ctx* dpg_ctx_create(int device);
+/* Also destroys every incremental graph (dpg_inc_create / dpg_inc_load) and DPG store
+ * (dpg_dpg_create) still alive on ctx; their handles are invalid afterwards. */
 void dpg_ctx_destroy(dpg_ctx* ctx);
 /* Multi-GPU context (SURVEY 8b "dpg_ctx_create(int n_gpus)", 8e): ONE host process drives n_gpus
  * devices (devices[k], or 0 .. n_gpus-1 when devices is NULL), one stream per device and one RCCL
@@ -303,12 +305,17 @@ int dpg_icp_batch_prepare(dpg_ctx* ctx, const int32_t* edges, int64_t n_edges, c
  * context stream.  trace_iters > 0 records the per-iteration correspondence indices of every
  * edge (test mode; see dpg_icp_batch_fetch_trace). */
 int dpg_icp_batch_run(dpg_ctx* ctx, int32_t compute_cov, int32_t trace_iters);
-/* 4) copy results back (any pointer may be NULL). */
-int dpg_icp_batch_fetch(dpg_ctx* ctx, dpg_icp_result* results, double* hess /*[E][9]*/);
+/* 4) copy results back (any pointer may be NULL).  cap: the number of records results (and
+ * hess, [cap][9]) can hold; DPG_ERR_SIZE, with nothing written, when the staged batch is larger
+ * (dpg_icp_batch_size tells how many are staged -- a sweep or dpg_add_node may have staged more
+ * than the caller's own edges). */
+int dpg_icp_batch_fetch(dpg_ctx* ctx, dpg_icp_result* results, double* hess /*[cap][9]*/, int64_t cap);
 /* Edges of the staged batch -- dpg_icp_batch_prepare's, or the batch a sweep (dpg_reoptimize) or
  * dpg_add_node staged last: the number of records dpg_icp_batch_fetch writes. */
 int64_t dpg_icp_batch_size(dpg_ctx* ctx);
-int dpg_icp_batch_fetch_trace(dpg_ctx* ctx, int32_t* trace /*[E][trace_iters][max_src]*/,
+/* trace_cap: int32 elements trace can hold; DPG_ERR_SIZE when E * trace_iters * max_src exceeds it
+ * (call with trace = NULL first to learn max_src). */
+int dpg_icp_batch_fetch_trace(dpg_ctx* ctx, int32_t* trace /*[E][trace_iters][max_src]*/, int64_t trace_cap,
                               int64_t* max_src_out);
 /* Device time of the last ICP / covariance kernels (ms, HIP events on the context stream). */
 float dpg_icp_batch_kernel_ms(dpg_ctx* ctx);

@@ -50,3 +50,38 @@ def test_index_reused_and_rebuilt_when_needed(workload):
         inv[rev] = np.arange(V)
         ctx.icp_prepare(inv[w.edges].astype(w.edges.dtype), w.est[rev], p)
         assert _run(ctx).tobytes() == r0.tobytes()
+
+
+def test_add_node_rebuilds_stale_indexes_after_kdtree_run(workload):
+    """dpg_add_node_pairs after a k-d tree batch on the same scan store: the k-d tree
+    overwrote the index buffers of the older nodes, so the per-node run rebuilds every stale index,
+    not only the new node's -- the alignments equal those of a store that never left the angular
+    variant."""
+    from dpgslam import _abi, api
+    w = workload("config2")
+    p = _abi.default_icp_params()
+    prior = np.zeros(1, _abi.FACTOR_DTYPE)
+    prior["kind"], prior["i"], prior["info"] = _abi.DPG_FACTOR_PRIOR, 0, 1.0 / np.array([0.04, 0.04, 0.0225])
+
+    def run(detour):
+        ctx = api.Context(0)
+        g = api.IncGraph(ctx, mode="isam2")
+        g.add_node(w.cloud(0), np.zeros(1, np.int32), w.est[0], extra=prior, icp_params=p)
+        for v in (1, 2, 3):
+            g.add_node(w.cloud(v), np.zeros(v + 1, np.int32), w.est[v], icp_params=p)
+        if detour:
+            ctx.set_icp_variant("kdtree")
+            ctx.icp_prepare(np.array([[0, 1], [1, 2], [2, 3]], np.int32), w.est[:4], p)
+            _run(ctx)
+            ctx.set_icp_variant("angular")
+        g.add_node_pairs(w.cloud(4), w.est[4], np.array([[0, 4], [1, 4], [2, 4]], np.int32), icp_params=p)
+        res, _ = ctx.icp_fetch(with_hessian=False)
+        X = g.poses()
+        g.close()
+        ctx.close()
+        return res, X
+
+    r0, X0 = run(False)
+    r1, X1 = run(True)
+    assert len(r0) == 4 and r1.tobytes() == r0.tobytes()
+    assert np.array_equal(X0, X1)

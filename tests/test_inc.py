@@ -209,6 +209,55 @@ def test_gpu_add_node_failure_keeps_store_and_graph_in_step():
     ctx.close()
 
 
+@pytest.mark.gpu
+def test_gpu_fetch_capacity_checked_after_add_node():
+    """dpg_icp_batch_fetch takes the capacity of the caller's buffers: after
+    dpg_add_node_pairs stages a batch of several alignments inside C, a buffer one record short is
+    refused with DPG_ERR_SIZE and left untouched (no heap damage), and the exact size succeeds.
+    dpg_icp_batch_fetch_trace likewise refuses a short trace buffer."""
+    import ctypes as C
+    from dpgslam import api
+    from dpgslam._abi import lib
+    from dpgslam.api import results_array
+    w = synth.generate("config2")
+    p = _abi.default_icp_params()
+    ctx = api.Context(0)
+    g = api.IncGraph(ctx, mode="isam2")
+    prior = np.zeros(1, _abi.FACTOR_DTYPE)
+    prior["kind"], prior["i"], prior["info"] = _abi.DPG_FACTOR_PRIOR, 0, 1.0 / np.array([0.04, 0.04, 0.0225])
+    g.add_node(w.cloud(0), np.zeros(1, np.int32), w.est[0], extra=prior, icp_params=p)
+    g.add_node(w.cloud(1), np.zeros(2, np.int32), w.est[1], icp_params=p)
+    g.add_node_pairs(w.cloud(2), w.est[2], np.array([[0, 2]], np.int32), successive=True, icp_params=p)
+    n = int(lib().dpg_icp_batch_size(ctx.handle))
+    assert n == 2, n
+    short = results_array(n + 1)
+    sentinel = short.tobytes()
+    hess = np.full((n + 1, 9), -7.0)
+    rc = lib().dpg_icp_batch_fetch(ctx.handle, short.ctypes.data_as(C.c_void_p),
+                                   hess.ctypes.data_as(C.POINTER(C.c_double)), n - 1)
+    assert rc == -4 and short.tobytes() == sentinel and (hess == -7.0).all()   # DPG_ERR_SIZE
+    assert b"staged batch" in (lib().dpg_last_error() or b"")
+    res, _ = ctx.icp_fetch(with_hessian=False)     # the exact size: the two alignments
+    assert len(res) == n and all(int(r["iterations"]) > 0 for r in res)
+    # a NULL-pointer fetch needs no capacity (it only feeds the cost memory)
+    assert lib().dpg_icp_batch_fetch(ctx.handle, None, None, 0) == 0
+    g.close()
+    ctx.close()
+    # the trace: one int32 short of E * trace_iters * max_src is refused
+    ctx = api.Context(0)
+    ctx.upload_scans(w.pts, w.offsets, p.downsample_icp_points_ratio)
+    ctx.icp_prepare(w.edges[:3], w.est, p)
+    ctx.icp_run(compute_cov=False, trace_iters=2)
+    ms = C.c_int64(0)
+    assert lib().dpg_icp_batch_fetch_trace(ctx.handle, None, 0, C.byref(ms)) == 0
+    need = 3 * 2 * ms.value
+    tr = np.full(need, -5, np.int32)
+    rc = lib().dpg_icp_batch_fetch_trace(ctx.handle, tr.ctypes.data_as(C.POINTER(C.c_int32)), need - 1, C.byref(ms))
+    assert rc == -4 and (tr == -5).all()   # DPG_ERR_SIZE
+    assert ctx.icp_fetch_trace(2).shape == (3, 2, ms.value)
+    ctx.close()
+
+
 def test_checkpoint_rejects_foreign_files(tmp_path):
     """dpg_inc_load validates the file before it touches a device: a file that is not a graph
     checkpoint of this version (or is truncated) is rejected with DPG_ERR_ARG."""
