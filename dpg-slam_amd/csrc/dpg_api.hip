@@ -25,6 +25,10 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <string>
 #include <unordered_map>
@@ -167,6 +171,8 @@ struct dpg_ctx {
     std::vector<ncclComm_t> comms;   // RCCL: one communicator per local device
     dpg_coll_ops host_ops{};         // kCollHost: the caller's host-memory collectives
     std::vector<double> host_hb;     // kCollHost: the packed system in host memory
+    struct HostColl;                 // kCollHost, pipelined GN: the collective thread (below)
+    std::unique_ptr<HostColl> hc;
     int32_t coll = 0;                // kCollNone | kCollRccl | kCollVirtual | kCollHost
     int32_t world = 1, rank0 = 0;
     int32_t rank = 0;                // global rank of THIS device context (peers too)
@@ -185,6 +191,32 @@ struct dpg_ctx {
     DevBuf<int32_t> shard_idx;       // per device context: its shard's caller indices
     DevBuf<float> cost_dev;          // rank form: the all-reduced cost vector of a batch
     dpg_chol_opts copts;             // solver options (dpg_ctx_set_solver_options)
+};
+
+// The rank form over the caller's collectives (kCollHost) in the pipelined Gauss-Newton loop: the
+// packed system's all-reduce of iteration i runs on this thread, so the host can queue iteration
+// i + 1 before iteration i's report, as over RCCL.  Per iteration, on the context stream: the
+// assembly's partial system -> pinned host buffer, an event; then a one-lane kernel that waits
+// until the thread has stored the iteration's tag in a host-mapped word (system-scope loads); then
+// the summed system -> hb_own.  The thread waits for the event, calls the caller's all-reduce in
+// place and stores the tag.  Stream order serializes the buffer's uses (the next copy into it
+// follows this iteration's copy out of it).  A failed collective still stores the tag (the stream
+// moves on) and sets `failed`, which the loop checks at every report.
+struct dpg_ctx::HostColl {
+    double* buf = nullptr;           // pinned: the packed system, summed in place
+    size_t cap = 0;                  // doubles
+    uint32_t* flag = nullptr;        // host-mapped: the last tag the thread completed
+    uint32_t* timed_out = nullptr;   // host-mapped: the wait kernel gave up (no tag in 120 s)
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    uint32_t next_tag = 0;
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::pair<uint32_t, hipEvent_t>> jobs;
+    size_t count = 0;                // doubles of the current system
+    uint64_t posted = 0, done = 0;
+    bool stop = false;
+    std::atomic<int> failed{0};
 };
 
 namespace {
@@ -615,6 +647,18 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)join_cov(c);
     (void)hipStreamSynchronize(c->stream);
+    if (c->hc) {   // the collective thread: its queue is empty once the stream has drained
+        {
+            std::lock_guard<std::mutex> lk(c->hc->mu);
+            c->hc->stop = true;
+        }
+        c->hc->cv.notify_all();
+        if (c->hc->th.joinable()) c->hc->th.join();
+        if (c->hc->buf) (void)hipHostFree(c->hc->buf);
+        if (c->hc->flag) (void)hipHostFree(c->hc->flag);
+        for (auto& e : c->hc->ev) if (e) (void)hipEventDestroy(e);
+        c->hc.reset();
+    }
     if (c->aux) (void)hipStreamDestroy(c->aux);
     c->full.release(); c->ds.release(); c->edges.release(); c->res.release(); c->hess.release();
     c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
@@ -1652,6 +1696,77 @@ static int coll_sum_hb(dpg_ctx* c) {
     return DPG_OK;
 }
 
+// kCollHost, pipelined GN: the collective thread's loop (see dpg_ctx::HostColl)
+static void host_coll_thread(dpg_ctx* c) {
+    dpg_ctx::HostColl& h = *c->hc;
+    (void)hipSetDevice(c->device);
+    for (;;) {
+        std::pair<uint32_t, hipEvent_t> job;
+        {
+            std::unique_lock<std::mutex> lk(h.mu);
+            h.cv.wait(lk, [&] { return h.stop || !h.jobs.empty(); });
+            if (h.jobs.empty()) return;   // stop, nothing left
+            job = h.jobs.front();
+            h.jobs.pop_front();
+        }
+        int bad = hipEventSynchronize(job.second) != hipSuccess;
+        if (!bad && c->host_ops.allreduce_sum_f64(c->host_ops.user, h.buf, (int64_t)h.count)) bad = 1;
+        if (bad) h.failed.store(1);
+        std::atomic_thread_fence(std::memory_order_release);   // the sum before the tag
+        __atomic_store_n(h.flag, job.first, __ATOMIC_RELEASE);
+        {
+            std::lock_guard<std::mutex> lk(h.mu);
+            ++h.done;
+        }
+        h.cv.notify_all();
+    }
+}
+
+// queue iteration's all-reduce on the collective thread and make the stream wait for it
+static int coll_sum_hb_host_async(dpg_ctx* c) {
+    const size_t count = (size_t)dpg_gn_dev_hb_size(&c->gn);
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->hc) {
+        c->hc.reset(new dpg_ctx::HostColl());
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->hc->flag), 2 * sizeof(uint32_t),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        c->hc->flag[0] = 0;
+        c->hc->flag[1] = 0;
+        c->hc->timed_out = c->hc->flag + 1;
+        for (auto& e : c->hc->ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->hc->th = std::thread(host_coll_thread, c);
+    }
+    dpg_ctx::HostColl& h = *c->hc;
+    if (h.cap < count) {   // the thread is idle here: every posted job has completed (hc_drain)
+        if (h.buf) HIP_TRY(hipHostFree(h.buf));
+        h.buf = nullptr;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&h.buf), sizeof(double) * count, hipHostMallocDefault));
+        h.cap = count;
+    }
+    h.count = count;
+    const uint32_t tag = ++h.next_tag;
+    hipEvent_t ev = h.ev[tag & 1];
+    HIP_TRY(hipMemcpyAsync(h.buf, c->gn.hb_part, sizeof(double) * count, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(ev, c->stream));
+    {
+        std::lock_guard<std::mutex> lk(h.mu);
+        h.jobs.emplace_back(tag, ev);
+        ++h.posted;
+    }
+    h.cv.notify_all();
+    int rc = dpg_launch_host_wait(h.flag, tag, h.timed_out, c->stream);
+    if (rc) return fail(rc, "host-collective wait launch failed");
+    HIP_TRY(hipMemcpyAsync(c->gn.hb_own, h.buf, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+    return DPG_OK;
+}
+
+// every all-reduce posted to the collective thread has completed (its stream work may still run)
+static void hc_drain(dpg_ctx* c) {
+    if (!c->hc) return;
+    std::unique_lock<std::mutex> lk(c->hc->mu);
+    c->hc->cv.wait(lk, [&] { return c->hc->done == c->hc->posted; });
+}
+
 static int ensure_pipe(dpg_ctx* q) {
     if (q->pipe_ctl) return DPG_OK;
     HIP_TRY(hipSetDevice(q->device));
@@ -1694,7 +1809,18 @@ static int wait_slot(dpg_ctx* q, const dpg_gn_slot* slot, uint64_t tag) {
 // forms: every device solves the identical all-reduced system and decides for itself (its own
 // control block: the chord rule's bookkeeping stays per device); their reports must agree bit for
 // bit, which the loop checks every iteration.
+static int gn_loop_pipe_body(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it);
 static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it) {
+    int rc = gn_loop_pipe_body(c, P, S, nw, dinf, it);
+    if (c->coll == kCollHost && c->hc) {   // nothing of this loop left on the collective thread
+        hc_drain(c);
+        if (!rc && c->hc->failed.exchange(0)) rc = fail(DPG_ERR_HIP, "the caller's all-reduce of the packed system failed");
+        if (!rc && __atomic_load_n(c->hc->timed_out, __ATOMIC_ACQUIRE))
+            rc = fail(DPG_ERR_HIP, "GN pipeline: no all-reduce from the collective thread in 120 s");
+    }
+    return rc;
+}
+static int gn_loop_pipe_body(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, double& nw, double& dinf, int& it) {
     const int L = n_dev(c);
     const int part = is_multi(c) ? 1 : 0;
     int rc;
@@ -1714,7 +1840,7 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
             if ((r = dpg_gn_pipe_issue_solve(&q->gn, q->pipe_ctl, part, q->stream)))
                 return fail(r, "GN pipeline launch failed: %s", hipGetErrorString(hipGetLastError()));
         }
-        if (part && (r = coll_sum_hb(c))) return r;
+        if (part && (r = (c->coll == kCollHost ? coll_sum_hb_host_async(c) : coll_sum_hb(c)))) return r;
         for (int k = 0; k < L; ++k) {
             dpg_ctx* q = dev_ctx(c, k);
             HIP_TRY(hipSetDevice(q->device));
@@ -1775,6 +1901,10 @@ static int gn_loop_pipe(dpg_ctx* c, const dpg_gn_params& P, dpg_gn_stats& S, dou
             q->gn.prev_delta_inf = q->gn.last_delta_inf;
             q->gn.last_delta_inf = o.dinf;
             reuse_last[(size_t)k] = o.reuse;
+        }
+        if (c->hc && c->hc->failed.load()) {   // the caller's collective failed: the report is not a sum
+            for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);
+            return fail(DPG_ERR_HIP, "the caller's all-reduce of the packed system failed (GN iteration %d)", i);
         }
         if (o0.status != 0.0) {
             for (int j = 0; j < L; ++j) (void)hipStreamSynchronize(dev_ctx(c, j)->stream);

@@ -971,3 +971,25 @@ static int pcg_solve(dpg_gn_dev* g, const double* hb, const dpg_gn_params* gp, h
     }
     return it;
 }
+
+// the rank form's host collective (dpg_api.hip, dpg_ctx::HostColl): the stream waits here until the
+// collective thread has stored this iteration's tag.  One lane; vector loads at system scope (the
+// word is host memory), s_sleep between polls, a 120 s bound on the 100 MHz clock.
+__global__ void host_wait_kernel(const uint32_t* flag, uint32_t tag, uint32_t* timed_out) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = wall_clock64();
+    for (;;) {
+        const uint32_t v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((int32_t)(v - tag) >= 0) return;
+        if (wall_clock64() - t0 > 12000000000ull) {   // 120 s
+            __hip_atomic_store(timed_out, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+extern "C" int dpg_launch_host_wait(const uint32_t* flag, uint32_t tag, uint32_t* timed_out, void* stream) {
+    hipLaunchKernelGGL(host_wait_kernel, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream), flag, tag, timed_out);
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}

@@ -43,7 +43,11 @@
 // of all waves' trips (imbalance = 8 [14] / [15]).  DPG_ICP_TIMING
 // (per-wave s_memtime cycles summed over waves and iterations, last iteration excluded):
 // [8] search, [9] sums + fold, [10] arrival + fit + publish barrier, [11] move + barrier,
-// [12] wave-iterations, [45] queue phase (barrier, cooperative scans, barrier, finalize).
+// [12] wave-iterations, [45] queue phase (barrier, cooperative scans, barrier, finalize), [40]
+// set-up ticks, [41] / [42] shader / 100 MHz ticks from entry to the end of the loop, [43] waves,
+// DPG_ICP_SETUPCLK (no other diagnostics): wave 0 of every workgroup records its set-up steps in
+// g_icp_setup[dispatch slot][10]: shader ticks at entry, after the target records, source keys,
+// bucket tables, barrier, source transform, barrier, at the end; 100 MHz ticks at entry and end.
 // DPG_ICP_STATS also: [40] queued forward windows, [41] their candidates, [42] cooperative
 // reciprocal scans, [43] their candidates, [44] workgroup-iterations with a non-empty queue,
 // [46] float bits of max |moved - (F p + t)| over every moved source point (m, the incremental
@@ -51,8 +55,12 @@
 // float transform), [47] float bits of the max of that drift over the window margin the next
 // reciprocal test adds for it, 1e-4 + 5e-5 (k + 1) m (must stay below 1)
 #define DPG_ICP_DIAG 1
-__device__ unsigned long long g_icp_stats[48];
+__device__ unsigned long long g_icp_stats[64];
 #define ICP_STAT_ADD(k, v) atomicAdd(&g_icp_stats[k], (unsigned long long)(v))
+#endif
+#ifdef DPG_ICP_SETUPCLK
+constexpr int kSetupSlots = 65536;
+__device__ unsigned long long g_icp_setup[kSetupSlots * 10];
 #endif
 #ifdef DPG_ICP_STATS
 #define ICP_STAT(k, v) ICP_STAT_ADD(k, v)
@@ -324,12 +332,12 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 constexpr int kWaves = kT / 64;
 static_assert(kT == dpg_tree::kLanes, "one tree lane per thread");
 #ifndef DPG_ANG_KU
-#define DPG_ANG_KU 4
+#define DPG_ANG_KU 8
 #endif
 #ifndef DPG_ANG_WPE
 #define DPG_ANG_WPE 8
 #endif
-constexpr int kU = DPG_ANG_KU;   // candidates per trip
+constexpr int kU = DPG_ANG_KU;   // records repeated past each cloud: the longest candidate trip
 // an unmatched point searches kClear beyond r once; while the distance it has moved since stays
 // below the margin found, it provably has no target within r and skips its forward search
 constexpr float kClear = 0.1f;
@@ -426,17 +434,25 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 // kU consecutive records with four ds_read_b128 issued back to back and ONE wait (the compiler,
 // left alone, narrows an unused pad word to ds_read_b96 -- 8 LDS cycles instead of 4 -- or
 // serialises the loads behind per-load waits under the 64-VGPR budget)
-template <bool kLds>
-__device__ __forceinline__ void ld_recs(const Rec* p, uint4 (&r)[kU]) {
-    static_assert(kU == 4 || kU == 8, "ld_recs issues four or eight loads");
+template <bool kLds, int KN = kU>
+__device__ __forceinline__ void ld_recs(const Rec* p, uint4 (&r)[KN]) {
+    static_assert(KN == 2 || KN == 4 || KN == 8, "ld_recs issues two, four or eight loads");
     if constexpr (!kLds) {   // records in global scratch (large clouds): plain 16-byte loads
         const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-        for (int u = 0; u < kU; ++u) r[u] = q[u];
+        for (int u = 0; u < KN; ++u) r[u] = q[u];
         return;
     }
     const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(p);   // LDS byte offset
-    if constexpr (kU == 4) {
+    if constexpr (KN == 2) {
+        asm volatile(
+            "ds_read_b128 %0, %2\n\t"
+            "ds_read_b128 %1, %2 offset:16\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(r[0]), "=&v"(r[1])
+            : "v"(a)
+            : "memory");
+    } else if constexpr (KN == 4) {
         asm volatile(
             "ds_read_b128 %0, %4\n\t"
             "ds_read_b128 %1, %4 offset:16\n\t"
@@ -679,18 +695,32 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     const int vt = E.tgt_node, vs = E.src_node;
     const int cap = kp.lds_tgt;
     const int dcap = kp.defer_cap > 0 ? kp.defer_cap : 0x7fffffff;   // windows above it are queued
+#ifdef DPG_ICP_TIMING
+    // per wave: shader-clock ticks and constant 100 MHz ticks over the whole workgroup (their ratio is
+    // the shader clock the edge ran at), and the set-up's shader ticks (records into LDS)
+    const unsigned long long c_in = __builtin_amdgcn_s_memtime(), r_in = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef DPG_ICP_STATS
     __shared__ unsigned st_wmax;
     if (t == 0) st_wmax = 0;
 #endif
-    const int stepM = M > 0 ? kU % M : 0, stepN = N > 0 ? kU % N : 0;
+    // candidates per trip: 4 (form 5), 8 (form 6: fewer trips, more records past a lane's window)
+    constexpr int kTrip = VAR == 6 ? 8 : 4;
+    static_assert(kTrip <= kU, "a trip stays inside the kU repeated records");
+    const int stepM = M > 0 ? kTrip % M : 0, stepN = N > 0 ? kTrip % N : 0;
     Lds L = carve<MODE>(smem, cap, gscr);
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su0 = __builtin_amdgcn_s_memtime(), sr0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // sorted target + the kU repeated records after it
     for (int i = t; i < M + kU && M > 0; i += kT) {
         const int p = i < M ? i : (i - M) % M;
         const float2 q = idx_pts[E.tgt_ds_off + p];
         L.tp[i] = Rec{q.x, q.y, ((uint32_t)idx_orig[E.tgt_ds_off + p] << 16) | (uint32_t)p, 0u};
     }
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su1 = __builtin_amdgcn_s_memtime();
+#endif
     for (int s = t; s < N + kU && N > 0; s += kT) {
         const int p = s < N ? s : (s - N) % N;
         const uint16_t o = idx_orig[E.src_ds_off + p];
@@ -698,10 +728,16 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         L.scs[s].pad = 0u;
         if (s < N) L.spos[o] = (uint16_t)s;
     }
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su2 = __builtin_amdgcn_s_memtime();
+#endif
     for (int b = t; b <= kB; b += kT) {
         L.tb[b] = buckets[(size_t)vt * (kB + 1) + b];
         L.sb[b] = buckets[(size_t)vs * (kB + 1) + b];
     }
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su3 = __builtin_amdgcn_s_memtime();
+#endif
     float F[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) F[q] = uni(E.guess[q]);
@@ -725,6 +761,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
         *L.arrive = 0;
     }
     __syncthreads();
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su4 = __builtin_amdgcn_s_memtime();
+#endif
     float sx[PPT], sy[PPT];
     uint32_t st[PPT];
     // store the moved source point at its sorted position (and its repeat past n)
@@ -752,7 +791,13 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             put(m);
         }
     }
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su5 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();   // spos is dead from here on: its LDS holds the queue
+#ifdef DPG_ICP_SETUPCLK
+    const unsigned long long su6 = __builtin_amdgcn_s_memtime();
+#endif
 
     const float r2f = kp.r2_f;
     const float rmax = sqrtf(r2f) * 1.0001f + 1e-5f;
@@ -761,6 +806,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     int k = 0, converged = 0, status = DPG_ICP_OK;
 #ifdef DPG_ICP_TIMING
     unsigned long long ph[5] = {0, 0, 0, 0, 0}, nit = 0;
+    const unsigned long long c_setup = __builtin_amdgcn_s_memtime() - c_in;
 #endif
     // the forward result of a point (best key) -> its match position (-1: none) and next seed
     auto forward_done = [&](int m, uint64_t best, bool ext) -> int {
@@ -803,6 +849,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
             if constexpr (kWideQ) return (int)((qsl[m >> 2] >> (8 * (m & 3))) & 0xffu) - 1;
             else return (int)(m < 3 ? (okq >> (8 + 7 * m)) & 0x7fu : (qhi >> (7 * (m - 3))) & 0x7fu) - 1;
         };
+        {
 #pragma unroll
         for (int m = 0; m < PPT; ++m) {
             // every lane runs every trip (dead lanes included): the candidate loops are
@@ -831,17 +878,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
 #ifdef DPG_ICP_STATS
                 {
                     int trips = 0;
-                    for (int c = 0; __any(c < fc); c += kU) ++trips;
+                    for (int c = 0; __any(c < fc); c += kTrip) ++trips;
                     if (live) { ICP_STAT(0, 1); ICP_STAT(1, fc); if (fc >= M) ICP_STAT(7, 1); }
                     if (lane == 0) { ICP_STAT(2, trips); ICP_STAT(16 + trip_bin(trips), trips); }
                     wtrips += trips;
                 }
 #endif
                 auto ftrip = [&]() {
-                    uint4 r[kU];
-                    ld_recs<kTpL>(L.tp + s, r);
+                    uint4 r[kTrip];
+                    ld_recs<kTpL, kTrip>(L.tp + s, r);
 #pragma unroll
-                    for (int u = 0; u < kU; ++u) {
+                    for (int u = 0; u < kTrip; ++u) {
                         uint64_t kd;
                         if constexpr (VAR >= 1) kd = cand_key(r[u], qx, qy);
                         else kd = dkey(sqd(qx, qy, __uint_as_float(r[u].x), __uint_as_float(r[u].y)), r[u].z);
@@ -852,16 +899,19 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 if constexpr (VAR >= 2) {   // exact (d, original index) argmin
                     if (__any(0 < fc)) {
                         int c = 0;
-                        do { ftrip(); c += kU; } while (__any(c < fc));
+                        do { ftrip(); c += kTrip; } while (__any(c < fc));
                     }
                 } else {
-                    for (int c = 0; __any(c < fc); c += kU) ftrip();
+                    for (int c = 0; __any(c < fc); c += kTrip) ftrip();
                 }
 
             }
             int bp = -1;
             if (search && !pend) bp = forward_done(m, best, sd == -1);
             bool ok = live && bp >= 0;
+#ifdef DPG_ICP_STATS
+            int rtrips = 0;   // the reciprocal trips made (the loop ends once every lane is beaten)
+#endif
             // ---- reciprocal test in the static source index ----
             if (kp.reciprocal) {
                 const float bd = __uint_as_float((uint32_t)(best >> 32));
@@ -887,30 +937,29 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 // is closer to t_j (or tied with a lower index) and breaks reciprocity
                 const uint64_t mine = dkey(bd, ((uint32_t)i << 16) | (uint32_t)st_sp(st[m]));
 #ifdef DPG_ICP_STATS
-                {
-                    int trips = 0;
-                    for (int c = 0; __any(ok & (c < rc)); c += kU) ++trips;
-                    if (ok) { ICP_STAT(3, rc); if (rc >= N) ICP_STAT(13, 1); }
-                    if (live && !ok && !pend && slot < 0) ICP_STAT(6, 1);
-                    if (lane == 0) { ICP_STAT(4, trips); ICP_STAT(28 + trip_bin(trips), trips); }
-                    wtrips += trips;
-                }
+                if (ok) { ICP_STAT(3, rc); if (rc >= N) ICP_STAT(13, 1); }
+                if (live && !ok && !pend && slot < 0) ICP_STAT(6, 1);
 #endif
                 if constexpr (VAR >= 1) {
                     // the wave's still-reciprocal lanes as a mask: the beat tests are ballots
                     // folded by scalar ors, the loop condition one scalar and
                     uint64_t okm = __ballot(ok);
                     auto rtrip = [&]() {
-                        uint4 r[kU];
-                        ld_recs<kScsL>(L.scs + s, r);
+                        uint4 r[kTrip];
+                        ld_recs<kScsL, kTrip>(L.scs + s, r);
                         uint64_t beat = 0;
 #pragma unroll
-                        for (int u = 0; u < kU; ++u) beat |= __ballot(cand_key(r[u], tj.x, tj.y) < mine);
+                        for (int u = 0; u < kTrip; ++u) beat |= __ballot(cand_key(r[u], tj.x, tj.y) < mine);
                         okm &= ~beat;
                         s = advance(s, stepN, N);
                     };
                     int c = 0;
-                    for (; (okm & __ballot(c < rc)) != 0; c += kU) rtrip();
+                    for (; (okm & __ballot(c < rc)) != 0; c += kTrip) {
+                        rtrip();
+#ifdef DPG_ICP_STATS
+                        ++rtrips;
+#endif
+                    }
                     ok = ok && ((okm >> lane) & 1u);
                 } else {
                 for (int c = 0; __any(ok & (c < rc)); c += kU) {
@@ -928,9 +977,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
                 }
             }
 #ifdef DPG_ICP_STATS
+            if (kp.reciprocal && lane == 0) { ICP_STAT(4, rtrips); ICP_STAT(28 + trip_bin(rtrips), rtrips); }
+            if (kp.reciprocal) wtrips += rtrips;
             if (ok) ICP_STAT(5, 1);
 #endif
             okq |= (ok ? 1u : 0u) << m;
+        }
         }
         ICP_STAMP(c1);
         // ---- the cooperative queue: windows too wide for one lane, 64 candidates per trip ----
@@ -1227,6 +1279,17 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     if (lane == 0) {
         ICP_STAT_ADD(8, ph[0]); ICP_STAT_ADD(9, ph[1]); ICP_STAT_ADD(10, ph[2]); ICP_STAT_ADD(11, ph[3]);
         ICP_STAT_ADD(12, nit); ICP_STAT_ADD(45, ph[4]);
+        ICP_STAT_ADD(40, c_setup);
+        ICP_STAT_ADD(41, __builtin_amdgcn_s_memtime() - c_in);
+        ICP_STAT_ADD(42, __builtin_amdgcn_s_memrealtime() - r_in);
+        ICP_STAT_ADD(43, 1);
+    }
+#endif
+#ifdef DPG_ICP_SETUPCLK
+    if (t == 0 && blockIdx.x < kSetupSlots) {
+        unsigned long long* g = g_icp_setup + (size_t)blockIdx.x * 10;
+        g[0] = su0; g[1] = su1; g[2] = su2; g[3] = su3; g[4] = su4; g[5] = su5; g[6] = su6;
+        g[7] = __builtin_amdgcn_s_memtime(); g[8] = sr0; g[9] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
     if (t == 0) {
@@ -1255,11 +1318,19 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
 
 extern "C" int32_t dpg_angle_buckets(void) { return kB; }
 
+#ifdef DPG_ICP_SETUPCLK
+// diagnostics build: the per-workgroup set-up stamps of the last launch (n <= kSetupSlots records)
+extern "C" int dpg_icp_setup_clock(unsigned long long* out, int64_t n) {
+    if (n < 0 || n > kSetupSlots) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_setup), (size_t)n * 10 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #ifdef DPG_ICP_DIAG
 extern "C" int dpg_icp_stats(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 48 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_icp_stats), 64 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        unsigned long long z[48] = {0};
+        unsigned long long z[64] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_icp_stats), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
@@ -1325,11 +1396,15 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
         if (var == 1) DPG_ANG_K(P, M, 4);                                                                       \
         else DPG_ANG_K(P, M, 5)
+// variant 8 -> kernel form 6 (records in LDS only): eight-record candidate trips
+#define DPG_ANG_LAUNCH0(P)                                                                                       \
+        if (var == 8) DPG_ANG_K(P, 0, 6);                                                                       \
+        else DPG_ANG_LAUNCH(P, 0)
         if (mode == 0) {
-            if (ppt <= 1) DPG_ANG_LAUNCH(1, 0);
-            else if (ppt <= 2) DPG_ANG_LAUNCH(2, 0);
-            else if (ppt <= 4) DPG_ANG_LAUNCH(4, 0);
-            else DPG_ANG_LAUNCH(8, 0);
+            if (ppt <= 1) DPG_ANG_LAUNCH0(1);
+            else if (ppt <= 2) DPG_ANG_LAUNCH0(2);
+            else if (ppt <= 4) DPG_ANG_LAUNCH0(4);
+            else DPG_ANG_LAUNCH0(8);
         } else if (mode == 1) {
             DPG_ANG_LAUNCH(16, 1);
         } else {
@@ -1338,6 +1413,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
         if (hipGetLastError() != hipSuccess) return DPG_ERR_HIP;
     }
 #undef DPG_ANG_LAUNCH
+#undef DPG_ANG_LAUNCH0
 #undef DPG_ANG_K
     return DPG_OK;
 }

@@ -31,6 +31,9 @@ int dpg_ctx_device_of(dpg_ctx* c);
  * alive, newest first; a child's own destroy releases it from the list */
 void dpg_ctx_adopt(dpg_ctx* c, void* child, void (*destroy)(void*));
 void dpg_ctx_release_child(dpg_ctx* c, void* child);
+/* one lane waits (system-scope loads of a host-mapped word) until *flag - tag >= 0 as int32; after
+ * ~120 s it gives up and sets *timed_out (dpg_gn.hip; the rank form's host collective thread) */
+int dpg_launch_host_wait(const uint32_t* flag, uint32_t tag, uint32_t* timed_out, void* stream);
 
 /* One ICP edge as the kernel sees it (64 B).  Offsets/counts are in points (float2). */
 typedef struct dpg_icp_edge {

@@ -46,7 +46,8 @@ def run_step(ctx, w, p):
         ctx.gn_set_poses(w.est.astype(np.float64))
         sst, Xs = ctx.gn_run(w.V)
         out.update({f"rs{k}": rs.tobytes(), f"hs{k}": np.asarray(hs).tobytes(), f"Xs{k}": Xs,
-                    f"its{k}": sst["iterations"], f"nfs{k}": ctx.gn_factorizations(), f"err_s{k}": sst["final_error"]})
+                    f"its{k}": sst["iterations"], f"nfs{k}": ctx.gn_factorizations(), f"err_s{k}": sst["final_error"],
+                    f"gnms{k}": sst["ms_per_iteration"]})
     return out
 
 

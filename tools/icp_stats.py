@@ -31,7 +31,7 @@ if a.edges:
     w.edges = w.edges[:a.edges]
 L = _abi.lib()
 L.dpg_icp_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-st = (C.c_ulonglong * 48)()
+st = (C.c_ulonglong * 64)()
 with api.Context(0) as ctx:
     if os.environ.get("DPG_DEFER_CAP"):
         ctx.set_icp_defer_cap(int(os.environ["DPG_DEFER_CAP"]))

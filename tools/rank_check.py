@@ -70,7 +70,12 @@ def main():
     assert all(c == calls[0] for c in calls), calls
     assert coll.calls["allgather"] > 0 and coll.calls["allreduce_f64"] > 0 and coll.calls["allreduce_f32"] > 0, coll.calls
     dist.destroy_process_group()
-    print(f"rank check ok: rank {rank} of {world}, {cfg}, collectives {coll.calls}", flush=True)
+    # the pipelined GN of the rank form over the host collective (its all-reduce on libdpg's
+    # collective thread, no stream sync per iteration) beside the single-device loop; the two ranks
+    # share ONE card, so this is a correctness run's clock, not a scaling number
+    gn = {k: round(float(v["gnms1"]), 4) for k, v in (("rank_caller", outs["caller"]), ("rank_measured", outs["measured"]),
+                                                   ("single", ref))}
+    print(f"rank check ok: rank {rank} of {world}, {cfg}, collectives {coll.calls}, gn ms/iter {gn}", flush=True)
 
 
 if __name__ == "__main__":
