@@ -332,12 +332,12 @@ __device__ __forceinline__ uint64_t dkey(float d, uint32_t key) {
 constexpr int kWaves = kT / 64;
 static_assert(kT == dpg_tree::kLanes, "one tree lane per thread");
 #ifndef DPG_ANG_KU
-#define DPG_ANG_KU 8
+#define DPG_ANG_KU 4
 #endif
 #ifndef DPG_ANG_WPE
 #define DPG_ANG_WPE 8
 #endif
-constexpr int kU = DPG_ANG_KU;   // records repeated past each cloud: the longest candidate trip
+constexpr int kU = DPG_ANG_KU;   // candidates per trip
 // an unmatched point searches kClear beyond r once; while the distance it has moved since stays
 // below the margin found, it provably has no target within r and skips its forward search
 constexpr float kClear = 0.1f;
@@ -704,9 +704,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(ang_wpe(PPT,
     __shared__ unsigned st_wmax;
     if (t == 0) st_wmax = 0;
 #endif
-    // candidates per trip: 4 (form 5), 8 (form 6: fewer trips, more records past a lane's window)
-    constexpr int kTrip = VAR == 6 ? 8 : 4;
-    static_assert(kTrip <= kU, "a trip stays inside the kU repeated records");
+    constexpr int kTrip = kU;   // candidates per trip
     const int stepM = M > 0 ? kTrip % M : 0, stepN = N > 0 ? kTrip % N : 0;
     Lds L = carve<MODE>(smem, cap, gscr);
 #ifdef DPG_ICP_SETUPCLK
@@ -1396,10 +1394,7 @@ extern "C" int dpg_launch_icp_ang(const float* ds_pts_dev, const float* idx_pts_
 #define DPG_ANG_LAUNCH(P, M)                                                                                     \
         if (var == 1) DPG_ANG_K(P, M, 4);                                                                       \
         else DPG_ANG_K(P, M, 5)
-// variant 8 -> kernel form 6 (records in LDS only): eight-record candidate trips
-#define DPG_ANG_LAUNCH0(P)                                                                                       \
-        if (var == 8) DPG_ANG_K(P, 0, 6);                                                                       \
-        else DPG_ANG_LAUNCH(P, 0)
+#define DPG_ANG_LAUNCH0(P) DPG_ANG_LAUNCH(P, 0)
         if (mode == 0) {
             if (ppt <= 1) DPG_ANG_LAUNCH0(1);
             else if (ppt <= 2) DPG_ANG_LAUNCH0(2);
