@@ -722,7 +722,8 @@ def main():
     ctx.gn_setup(w.V, F, params=gp)
     ctx.synchronize()
     t3 = time.perf_counter()
-    setup = {"upload_ms": (t1 - t0) * 1e3, "icp_prepare_ms": (t2 - t1) * 1e3, "gn_setup_ms": (t3 - t2) * 1e3}
+    setup = {"upload_ms": (t1 - t0) * 1e3, "icp_prepare_ms": (t2 - t1) * 1e3, "gn_setup_ms": (t3 - t2) * 1e3,
+             "gn_setup_parts_ms": ctx.gn_setup_profile()}
     X0 = w.est.astype(np.float64)
 
     def step():
@@ -879,7 +880,7 @@ def main():
             "final_error": stats["final_error"],
             "icp_kernel_ms": stats["icp_kernel_ms"],
             **{k: v for k, v in cold_red.items()},
-            "setup_ms": sum(setup.values()), "setup": setup,
+            "setup_ms": setup["upload_ms"] + setup["icp_prepare_ms"] + setup["gn_setup_ms"], "setup": setup,
             **({"cold_single_solve_ms": cold_solve["total_ms"], "cold_single_solve": cold_solve} if cold_solve else {}),
             "cold_note": "icp_kernel_ms_first_run: the first warm-up step (no learnt costs: the caller's order, "
                          "the first launch after the upload); icp_kernel_ms_caller_order: the caller's order "

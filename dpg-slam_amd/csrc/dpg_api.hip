@@ -123,6 +123,7 @@ struct dpg_ctx {
     // scan store (batch form)
     DevBuf<float> full, ds;
     DevBuf<int64_t> ds_off_dev;
+    DevBuf<int64_t> full_off_dev;  // the full clouds' offsets (the upload's device-side downsampling)
     DevBuf<float> tree_pts;        // per-node index over the downsampled clouds (k-d tree or angle order)
     DevBuf<uint16_t> tree_idx;
     DevBuf<uint16_t> buckets;      // angle variant: [V][B+1] bucket starts
@@ -662,7 +663,7 @@ void dpg_ctx_destroy(dpg_ctx* c) {
     if (c->aux) (void)hipStreamDestroy(c->aux);
     c->full.release(); c->ds.release(); c->edges.release(); c->res.release(); c->hess.release();
     c->trace.release(); c->s_pts.release(); c->s_edge.release(); c->s_res.release(); c->s_hess.release();
-    c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release();
+    c->ds_off_dev.release(); c->tree_pts.release(); c->tree_idx.release(); c->full_off_dev.release();
     c->s_off.release(); c->s_tree_pts.release(); c->s_tree_idx.release();
     c->buckets.release(); c->s_buckets.release(); c->icp_scratch.release();
     c->shard_idx.release(); c->cost_dev.release();
@@ -724,6 +725,16 @@ int dpg_scans_append(dpg_ctx* c, const float* pts, const int64_t* off, int64_t k
     return hipSetDevice(c->device) == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
+// R2 downsamplePointCloud of every node on the device (dpg_slam.cc:346-360, dpg_host.c
+// dpg_downsample_cloud: every ratio-th point from the first, copied) -- one workgroup per node over
+// the full clouds already uploaded, instead of a host pass over all of them
+__global__ void downsample_kernel(const float2* __restrict__ full, const int64_t* __restrict__ full_off,
+                                  const int64_t* __restrict__ ds_off, int32_t ratio, float2* __restrict__ ds) {
+    const int64_t v = blockIdx.x;
+    const int64_t f0 = full_off[v], d0 = ds_off[v], nd = ds_off[v + 1] - d0;
+    for (int64_t k = threadIdx.x; k < nd; k += blockDim.x) ds[d0 + k] = full[f0 + k * ratio];
+}
+
 static int scans_upload_1(dpg_ctx* c, const float* pts, const int64_t* off, int64_t V, int32_t ratio) {
     if (!c || !pts || !off || V <= 0) return fail(DPG_ERR_ARG, "dpg_scans_upload: bad arguments");
     if (ratio < 1) ratio = 1;
@@ -741,20 +752,21 @@ static int scans_upload_1(dpg_ctx* c, const float* pts, const int64_t* off, int6
         if (n < 0) return fail(DPG_ERR_ARG, "node offsets must be non-decreasing");
         c->ds_off[(size_t)v + 1] = c->ds_off[(size_t)v] + (n + ratio - 1) / ratio;
     }
-    std::vector<float> ds((size_t)(2 * std::max<int64_t>(c->ds_off[(size_t)V], 1)));
-    for (int64_t v = 0; v < V; ++v)   // R2 downsamplePointCloud, per node
-        dpg_downsample_cloud(pts + 2 * off[v], off[v + 1] - off[v], ratio, ds.data() + 2 * c->ds_off[(size_t)v]);
+    const size_t n_ds = (size_t)(2 * std::max<int64_t>(c->ds_off[(size_t)V], 1));   // floats
     int64_t mx = 0;
     for (int64_t v = 0; v < V; ++v) mx = std::max(mx, c->ds_off[(size_t)v + 1] - c->ds_off[(size_t)v]);
     if (mx > 16384) return fail(DPG_ERR_SIZE, "a downsampled cloud has %lld points (max 16384)", (long long)mx);
-    if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(ds.size()) ||
-        c->ds_off_dev.reserve((size_t)V + 1) || c->tree_pts.reserve(ds.size()) || c->tree_idx.reserve(ds.size() / 2) ||
-        c->buckets.reserve((size_t)V * (size_t)(dpg_angle_buckets() + 1)))
+    if (c->full.reserve((size_t)(2 * std::max<int64_t>(total, 1))) || c->ds.reserve(n_ds) ||
+        c->ds_off_dev.reserve((size_t)V + 1) || c->full_off_dev.reserve((size_t)V + 1) || c->tree_pts.reserve(n_ds) ||
+        c->tree_idx.reserve(n_ds / 2) || c->buckets.reserve((size_t)V * (size_t)(dpg_angle_buckets() + 1)))
         return fail(DPG_ERR_HIP, "out of device memory for scans");
     HIP_TRY(hipMemcpyAsync(c->full.p, pts, sizeof(float) * 2 * (size_t)total, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->ds.p, ds.data(), sizeof(float) * ds.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->full_off_dev.p, off, sizeof(int64_t) * ((size_t)V + 1), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->ds_off_dev.p, c->ds_off.data(), sizeof(int64_t) * ((size_t)V + 1), hipMemcpyHostToDevice,
                            c->stream));
+    hipLaunchKernelGGL(downsample_kernel, dim3((unsigned)V), dim3(256), 0, c->stream, reinterpret_cast<const float2*>(c->full.p),
+                       c->full_off_dev.p, c->ds_off_dev.p, ratio, reinterpret_cast<float2*>(c->ds.p));
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->n_nodes = V;
     c->idx_valid = 0;
@@ -1479,11 +1491,13 @@ int icp_cov_sandwich(dpg_ctx* c, const float* data, int64_t nd, const float* mod
 static int gn_setup_1(dpg_ctx* c, int64_t V, const dpg_factor* F, int64_t nf, int64_t b, int64_t e,
                       const dpg_gn_params* gp) {
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->gn_ready) dpg_gn_dev_free(&c->gn);
-    c->gn_ready = false;
-    int rc = dpg_gn_dev_alloc(&c->gn, V, F, nf, b, e, &c->copts);
+    // the new graph's host work overlaps what still runs on the stream (a batch's ICP); the
+    // stream is drained before the device allocations, and the previous graph freed after them
+    dpg_gn_dev ng;
+    int rc = dpg_gn_dev_alloc(&ng, V, F, nf, b, e, &c->copts, c->stream);
     if (rc) return fail(rc, "pose-graph setup failed (invalid factor or out of memory)");
+    if (c->gn_ready) dpg_gn_dev_free(&c->gn);
+    c->gn = ng;
     c->gn_ready = true;
     if (gp) c->gp = *gp;
     else dpg_gn_params_default(&c->gp);
@@ -1537,6 +1551,12 @@ int dpg_gn_take_icp_measurements(dpg_ctx* c, int64_t first, int64_t count, int64
 }
 
 int64_t dpg_gn_hb_size(dpg_ctx* c) { return (c && c->gn_ready) ? dpg_gn_dev_hb_size(&c->gn) : -1; }
+
+int dpg_gn_setup_profile(dpg_ctx* c, double out[5]) {
+    if (!c || !c->gn_ready || !out) return fail(DPG_ERR_STATE, "graph not set up");
+    for (int k = 0; k < 5; ++k) out[k] = c->gn.setup_ms[k];
+    return DPG_OK;
+}
 
 static int gn_set_poses_1(dpg_ctx* c, const double* poses) {
     if (!c->gn_ready) return fail(DPG_ERR_STATE, "graph not set up");

@@ -61,7 +61,7 @@ int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
 // cover: the chosen cut's separator as a minimum vertex cover of its crossing edges)
 int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                           int32_t starts, int32_t bal, int32_t score, bool cover, std::vector<int32_t>& perm,
-                          std::vector<std::vector<int32_t>>& pat);
+                          std::vector<std::vector<int32_t>>& pat, bool par = false);
 int dpg_chol_sym_from_patterns(int64_t n, const std::vector<int32_t>& perm, const std::vector<std::vector<int32_t>>& pat,
                                const dpg_chol_opts* opts, dpg_chol_sym* S);
 // the fused factorization's critical-path estimate (us) of an analysis (the chol_plan ticket model)

@@ -19,6 +19,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <atomic>
 #include <functional>
 #include <future>
 #include <queue>
@@ -117,30 +118,42 @@ void min_degree(int64_t n, const std::vector<int64_t>& aptr, const std::vector<i
 struct NdParams {
     int32_t starts = 0, bal = 5, score = 0;
     bool cover = false;   // the chosen cut's separator as a minimum vertex cover of its crossing edges
+    bool par = false;     // the two halves of a large part ordered on two threads (same order)
+};
+// Per-vertex scratch shared by the parallel halves of a split (the parts are disjoint: a part only
+// writes its own vertices; it reads a neighbour's stamp, which another part may be writing, only
+// to compare it with its own id -- relaxed atomic accesses for the stamps, the levels and the
+// cover marks are only touched for the part's own vertices)
+struct NdShared {
+    std::vector<int32_t> stamp, lvl, aux;
+    std::atomic<int32_t> next_id{0};
 };
 struct NdState {
     const int64_t* aptr;
     const int32_t* adj;
     int32_t leaf;
     NdParams prm;
-    int32_t next_id = 0;
-    std::vector<int32_t> stamp, lvl, queue, aux;
+    NdShared* sh;
+    std::vector<int32_t> queue;
     std::vector<int32_t>* out;
 };
+inline int32_t stamp_of(const NdState& st, int32_t v) { return __atomic_load_n(&st.sh->stamp[(size_t)v], __ATOMIC_RELAXED); }
+inline void stamp_set(NdState& st, int32_t v, int32_t id) { __atomic_store_n(&st.sh->stamp[(size_t)v], id, __ATOMIC_RELAXED); }
+inline int32_t nd_new_id(NdState& st) { return st.sh->next_id.fetch_add(1, std::memory_order_relaxed) + 1; }
 
 // BFS over the nodes stamped `id` from `src`; fills lvl and queue (visit order); returns the height
 int32_t nd_bfs(NdState& st, int32_t id, int32_t src) {
     st.queue.clear();
     st.queue.push_back(src);
-    st.lvl[(size_t)src] = 0;
+    st.sh->lvl[(size_t)src] = 0;
     int32_t h = 0;
     for (size_t qi = 0; qi < st.queue.size(); ++qi) {
         const int32_t v = st.queue[qi];
-        h = std::max(h, st.lvl[(size_t)v]);
+        h = std::max(h, st.sh->lvl[(size_t)v]);
         for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
             const int32_t u = st.adj[(size_t)t];
-            if (st.stamp[(size_t)u] == id && st.lvl[(size_t)u] < 0) {
-                st.lvl[(size_t)u] = st.lvl[(size_t)v] + 1;
+            if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] < 0) {
+                st.sh->lvl[(size_t)u] = st.sh->lvl[(size_t)v] + 1;
                 st.queue.push_back(u);
             }
         }
@@ -150,19 +163,19 @@ int32_t nd_bfs(NdState& st, int32_t id, int32_t src) {
 
 int32_t nd_degree(const NdState& st, int32_t id, int32_t v) {
     int32_t d = 0;
-    for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) d += st.stamp[(size_t)st.adj[(size_t)t]] == id;
+    for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) d += stamp_of(st, st.adj[(size_t)t]) == id;
     return d;
 }
 
 void nd_min_degree(NdState& st, const std::vector<int32_t>& sub) {
-    const int32_t id = ++st.next_id;
-    for (size_t i = 0; i < sub.size(); ++i) { st.stamp[(size_t)sub[i]] = id; st.lvl[(size_t)sub[i]] = (int32_t)i; }
+    const int32_t id = nd_new_id(st);
+    for (size_t i = 0; i < sub.size(); ++i) { stamp_set(st, sub[i], id); st.sh->lvl[(size_t)sub[i]] = (int32_t)i; }
     std::vector<int64_t> ap(sub.size() + 1, 0);
     std::vector<int32_t> aj;
     for (size_t i = 0; i < sub.size(); ++i) {
         const int32_t v = sub[i];
         for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t)
-            if (st.stamp[(size_t)st.adj[(size_t)t]] == id) aj.push_back(st.lvl[(size_t)st.adj[(size_t)t]]);
+            if (stamp_of(st, st.adj[(size_t)t]) == id) aj.push_back(st.sh->lvl[(size_t)st.adj[(size_t)t]]);
         ap[i + 1] = (int64_t)aj.size();
     }
     std::vector<int32_t> lp;
@@ -173,6 +186,31 @@ void nd_min_degree(NdState& st, const std::vector<int32_t>& sub) {
 
 void nd_rec(NdState& st, std::vector<int32_t>& sub);
 
+// after a split: A's order, B's order, then the separator.  With prm.par a large part's two halves
+// are ordered at once, B into its own list on a second thread -- the same order as one thread
+// (each half's recursion sees only its own vertices; the ids only need to be distinct)
+constexpr size_t kNdParMin = 1024;
+void nd_halves(NdState& st, std::vector<int32_t>& A, std::vector<int32_t>& B, const std::vector<int32_t>& S) {
+    if (st.prm.par && A.size() + B.size() >= kNdParMin) {
+        std::vector<int32_t> outB;
+        NdState sb;
+        sb.aptr = st.aptr;
+        sb.adj = st.adj;
+        sb.leaf = st.leaf;
+        sb.prm = st.prm;
+        sb.sh = st.sh;
+        sb.out = &outB;
+        std::future<void> fb = std::async(std::launch::async, [&sb, &B] { nd_rec(sb, B); });
+        nd_rec(st, A);
+        fb.get();
+        st.out->insert(st.out->end(), outB.begin(), outB.end());
+    } else {
+        nd_rec(st, A);
+        nd_rec(st, B);
+    }
+    for (int32_t v : S) st.out->push_back(v);
+}
+
 // the separator search with several level structures (NdParams, starts > 0); src is the part's
 // pseudo-peripheral node, `id` its stamp
 void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t src) {
@@ -180,7 +218,7 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
     const int T = N >= 256 ? st.prm.starts : 1;
     std::vector<int32_t> starts{src};
     {
-        for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
         nd_bfs(st, id, src);
         const std::vector<int32_t> order(st.queue.begin(), st.queue.end());
         for (int t = 1; t < T; ++t) starts.push_back(order[(size_t)((int64_t)t * (N - 1) / T)]);
@@ -192,21 +230,21 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
     int64_t bimb = 0;
     std::vector<int64_t> slo, shi, cnt;
     for (int32_t s0 : starts) {
-        for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
         const int32_t hh = nd_bfs(st, id, s0);
         if (hh < 3) continue;
         cnt.assign((size_t)hh, 0);
         slo.assign((size_t)hh, 0);
         shi.assign((size_t)hh, 0);
         for (int32_t v : sub) {
-            const int32_t l = st.lvl[(size_t)v];
+            const int32_t l = st.sh->lvl[(size_t)v];
             cnt[(size_t)l]++;
             bool up = false, dn = false;
             for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
                 const int32_t u = st.adj[(size_t)t];
-                if (st.stamp[(size_t)u] != id) continue;
-                up |= st.lvl[(size_t)u] == l + 1;
-                dn |= st.lvl[(size_t)u] == l - 1;
+                if (stamp_of(st, u) != id) continue;
+                up |= st.sh->lvl[(size_t)u] == l + 1;
+                dn |= st.sh->lvl[(size_t)u] == l - 1;
             }
             slo[(size_t)l] += up;                    // on level l, touching l + 1
             if (l > 0) shi[(size_t)l - 1] += dn;     // on level l, touching l - 1
@@ -228,12 +266,12 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         }
     }
     if (bm < 0) { nd_min_degree(st, sub); return; }
-    for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+    for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
     nd_bfs(st, id, bsrc);
     auto touches = [&](int32_t v, int32_t l) {
         for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
             const int32_t u = st.adj[(size_t)t];
-            if (st.stamp[(size_t)u] == id && st.lvl[(size_t)u] == l) return true;
+            if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] == l) return true;
         }
         return false;
     };
@@ -244,9 +282,9 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         // smallest separator this cut admits -- never larger than either side's boundary
         std::vector<int32_t> X, Y;
         for (int32_t v : sub) {
-            const int32_t l = st.lvl[(size_t)v];
-            if (l == bm && touches(v, bm + 1)) { st.aux[(size_t)v] = (int32_t)X.size(); X.push_back(v); }
-            else if (l == bm + 1 && touches(v, bm)) { st.aux[(size_t)v] = (int32_t)Y.size(); Y.push_back(v); }
+            const int32_t l = st.sh->lvl[(size_t)v];
+            if (l == bm && touches(v, bm + 1)) { st.sh->aux[(size_t)v] = (int32_t)X.size(); X.push_back(v); }
+            else if (l == bm + 1 && touches(v, bm)) { st.sh->aux[(size_t)v] = (int32_t)Y.size(); Y.push_back(v); }
         }
         std::vector<int64_t> xp(X.size() + 1, 0);
         std::vector<int32_t> xa;
@@ -254,7 +292,7 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
             const int32_t v = X[i];
             for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
                 const int32_t u = st.adj[(size_t)t];
-                if (st.stamp[(size_t)u] == id && st.lvl[(size_t)u] == bm + 1) xa.push_back(st.aux[(size_t)u]);
+                if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] == bm + 1) xa.push_back(st.sh->aux[(size_t)u]);
             }
             xp[i + 1] = (int64_t)xa.size();
         }
@@ -300,18 +338,18 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
                 if (x2 >= 0 && !zx[(size_t)x2]) { zx[(size_t)x2] = 1; q.push_back(x2); }
             }
         }
-        for (size_t i = 0; i < X.size(); ++i) st.aux[(size_t)X[i]] = zx[i] ? -1 : -2;   // -2: in the cover
-        for (size_t j = 0; j < Y.size(); ++j) st.aux[(size_t)Y[j]] = zy[j] ? -2 : -1;
+        for (size_t i = 0; i < X.size(); ++i) st.sh->aux[(size_t)X[i]] = zx[i] ? -1 : -2;   // -2: in the cover
+        for (size_t j = 0; j < Y.size(); ++j) st.sh->aux[(size_t)Y[j]] = zy[j] ? -2 : -1;
         for (int32_t v : sub) {
-            const int32_t l = st.lvl[(size_t)v];
-            const bool in_cover = (l == bm || l == bm + 1) && st.aux[(size_t)v] == -2;
+            const int32_t l = st.sh->lvl[(size_t)v];
+            const bool in_cover = (l == bm || l == bm + 1) && st.sh->aux[(size_t)v] == -2;
             (in_cover ? S : l <= bm ? A : B).push_back(v);
         }
-        for (int32_t v : X) st.aux[(size_t)v] = -1;
-        for (int32_t v : Y) st.aux[(size_t)v] = -1;
+        for (int32_t v : X) st.sh->aux[(size_t)v] = -1;
+        for (int32_t v : Y) st.sh->aux[(size_t)v] = -1;
     } else {
         for (int32_t v : sub) {
-            const int32_t l = st.lvl[(size_t)v];
+            const int32_t l = st.sh->lvl[(size_t)v];
             if (!bupper) {
                 if (l < bm) A.push_back(v);
                 else if (l > bm) B.push_back(v);
@@ -323,19 +361,17 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
             }
         }
     }
-    nd_rec(st, A);
-    nd_rec(st, B);
-    for (int32_t v : S) st.out->push_back(v);
+    nd_halves(st, A, B, S);
 }
 
 void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     if ((int32_t)sub.size() <= st.leaf) { nd_min_degree(st, sub); return; }
-    const int32_t id = ++st.next_id;
-    for (int32_t v : sub) { st.stamp[(size_t)v] = id; st.lvl[(size_t)v] = -1; }
+    const int32_t id = nd_new_id(st);
+    for (int32_t v : sub) { stamp_set(st, v, id); st.sh->lvl[(size_t)v] = -1; }
     // connected components, each ordered on its own
     std::vector<std::vector<int32_t>> comps;
     for (int32_t v : sub)
-        if (st.lvl[(size_t)v] < 0) {
+        if (st.sh->lvl[(size_t)v] < 0) {
             nd_bfs(st, id, v);
             comps.emplace_back(st.queue.begin(), st.queue.end());
         }
@@ -350,13 +386,13 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     // height grows
     int32_t src = sub[0], h = 0;
     for (int it = 0; it < 4; ++it) {
-        for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
         const int32_t hh = nd_bfs(st, id, src);
         if (hh <= h) break;
         h = hh;
         int32_t best = -1, bd = 1 << 30;
         for (int32_t v : st.queue)
-            if (st.lvl[(size_t)v] == h - 1) {
+            if (st.sh->lvl[(size_t)v] == h - 1) {
                 const int32_t d = nd_degree(st, id, v);
                 if (d < bd || (d == bd && v < best)) { bd = d; best = v; }
             }
@@ -364,12 +400,12 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
         src = best;
     }
     if (st.prm.starts > 0) { nd_split_multi(st, sub, id, src); return; }
-    for (int32_t v : sub) st.lvl[(size_t)v] = -1;
+    for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
     h = nd_bfs(st, id, src);
     const int64_t N = (int64_t)sub.size();
     if (h < 3) { nd_min_degree(st, sub); return; }
     std::vector<int64_t> cnt((size_t)h, 0);
-    for (int32_t v : sub) cnt[(size_t)st.lvl[(size_t)v]]++;
+    for (int32_t v : sub) cnt[(size_t)st.sh->lvl[(size_t)v]]++;
     // separator level: the smallest in the middle (both sides >= N/5), ties -> the most balanced
     int32_t m = -1;
     int64_t below = 0, best_sz = 0, best_imb = 0;
@@ -396,20 +432,20 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     auto touches = [&](int32_t v, int32_t l) {
         for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
             const int32_t u = st.adj[(size_t)t];
-            if (st.stamp[(size_t)u] == id && st.lvl[(size_t)u] == l) return true;
+            if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] == l) return true;
         }
         return false;
     };
     int64_t s_lo = 0, s_hi = 0;
     for (int32_t v : sub) {
-        const int32_t l = st.lvl[(size_t)v];
+        const int32_t l = st.sh->lvl[(size_t)v];
         if (l == m) s_lo += touches(v, m + 1);
         else if (l == m + 1) s_hi += touches(v, m);
     }
     const bool upper = s_hi < s_lo;
     std::vector<int32_t> A, B, S;
     for (int32_t v : sub) {
-        const int32_t l = st.lvl[(size_t)v];
+        const int32_t l = st.sh->lvl[(size_t)v];
         if (!upper) {
             if (l < m) A.push_back(v);
             else if (l > m) B.push_back(v);
@@ -420,9 +456,7 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
             else (touches(v, m) ? S : B).push_back(v);
         }
     }
-    nd_rec(st, A);
-    nd_rec(st, B);
-    for (int32_t v : S) st.out->push_back(v);
+    nd_halves(st, A, B, S);
 }
 
 // column patterns of L (positions, sorted) for a given order: each column's later neighbours and
@@ -462,7 +496,7 @@ int dpg_chol_order_nd(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
 
 int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, int64_t n_pairs, int32_t leaf,
                           int32_t starts, int32_t bal, int32_t score, bool cover, std::vector<int32_t>& perm,
-                          std::vector<std::vector<int32_t>>& pat) {
+                          std::vector<std::vector<int32_t>>& pat, bool par) {
     if (n <= 0) return -1;
     std::vector<int64_t> aptr((size_t)n + 1, 0);
     for (int64_t p = 0; p < n_pairs; ++p) { aptr[(size_t)pair_lo[p] + 1]++; aptr[(size_t)pair_hi[p] + 1]++; }
@@ -483,9 +517,12 @@ int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair
     st.prm.bal = std::max<int32_t>(bal, 2);
     st.prm.score = score;
     st.prm.cover = cover && starts > 0;
-    st.aux.assign((size_t)n, -1);
-    st.stamp.assign((size_t)n, 0);
-    st.lvl.assign((size_t)n, -1);
+    st.prm.par = par;
+    NdShared sh;
+    sh.aux.assign((size_t)n, -1);
+    sh.stamp.assign((size_t)n, 0);
+    sh.lvl.assign((size_t)n, -1);
+    st.sh = &sh;
     perm.clear();
     perm.reserve((size_t)n);
     st.out = &perm;
@@ -578,7 +615,7 @@ int dpg_chol_symbolic(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi,
         std::vector<int32_t> pm;
         std::vector<std::vector<int32_t>> pt;
         if (dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, cands[k].starts, cands[k].bal, cands[k].score, true,
-                                  pm, pt) ||
+                                  pm, pt, true) ||
             dpg_chol_sym_from_patterns(n, pm, pt, opts, &r.T))
             r.rc = -1;
         else

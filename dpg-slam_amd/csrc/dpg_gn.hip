@@ -22,10 +22,12 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <algorithm>
 #include <vector>
 
+#include "dpg_chol.h"
 #include "dpg_internal.h"
 #include "dpg_gn_pipe.h"
 
@@ -463,13 +465,22 @@ extern "C" void dpg_gn_dev_free(dpg_gn_dev* g) {
     memset(g, 0, sizeof(*g));
 }
 
+static double gn_wall_ms() {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e3 + (double)ts.tv_nsec * 1e-6;
+}
+
 extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, int64_t nf,
-                                int64_t shard_begin, int64_t shard_end, const dpg_chol_opts* opts) {
+                                int64_t shard_begin, int64_t shard_end, const dpg_chol_opts* opts, void* sync_stream) {
     memset(g, 0, sizeof(*g));
     if (n <= 0 || nf < 0 || n > (int64_t)1 << 28) return DPG_ERR_ARG;
-    // unique pairs (lo, hi) of Between factors
-    std::vector<std::pair<int64_t, int64_t>> pairs;
-    pairs.reserve((size_t)nf);
+    const double t0 = gn_wall_ms();
+    // unique pairs (lo, hi) of Between factors, as sorted 64-bit keys lo << 32 | hi; every
+    // factor's pair index found once
+    std::vector<uint64_t> fkey((size_t)nf, ~0ull);
+    std::vector<uint64_t> pk;
+    pk.reserve((size_t)nf);
     for (int64_t k = 0; k < nf; ++k) {
         const dpg_factor& f = F[k];
         if (f.kind == DPG_FACTOR_PRIOR) {
@@ -478,15 +489,17 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
         }
         if (f.kind != DPG_FACTOR_BETWEEN || f.i < 0 || f.j < 0 || f.i >= n || f.j >= n || f.i == f.j)
             return DPG_ERR_ARG;
-        pairs.emplace_back(std::min<int64_t>(f.i, f.j), std::max<int64_t>(f.i, f.j));
+        fkey[(size_t)k] = (uint64_t)std::min(f.i, f.j) << 32 | (uint64_t)std::max(f.i, f.j);
+        pk.push_back(fkey[(size_t)k]);
     }
-    std::sort(pairs.begin(), pairs.end());
-    pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
-    const int64_t P = (int64_t)pairs.size();
+    std::sort(pk.begin(), pk.end());
+    pk.erase(std::unique(pk.begin(), pk.end()), pk.end());
+    const int64_t P = (int64_t)pk.size();
     const int64_t nu = n + P;
-    auto pair_id = [&](int64_t lo, int64_t hi) {
-        return (int64_t)(std::lower_bound(pairs.begin(), pairs.end(), std::make_pair(lo, hi)) - pairs.begin());
-    };
+    std::vector<int32_t> fpair((size_t)nf, -1);
+    for (int64_t k = 0; k < nf; ++k)
+        if (fkey[(size_t)k] != ~0ull)
+            fpair[(size_t)k] = (int32_t)(std::lower_bound(pk.begin(), pk.end(), fkey[(size_t)k]) - pk.begin());
     // contribution lists per upper block (factor order)
     std::vector<int32_t> cnt((size_t)nu + 1, 0);
     for (int64_t k = 0; k < nf; ++k) {
@@ -494,7 +507,7 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
         cnt[(size_t)f.i + 1]++;
         if (f.kind == DPG_FACTOR_BETWEEN) {
             cnt[(size_t)f.j + 1]++;
-            cnt[(size_t)(n + pair_id(std::min<int64_t>(f.i, f.j), std::max<int64_t>(f.i, f.j))) + 1]++;
+            cnt[(size_t)(n + fpair[(size_t)k]) + 1]++;
         }
     }
     for (int64_t u = 0; u < nu; ++u) cnt[(size_t)u + 1] += cnt[(size_t)u];
@@ -505,26 +518,51 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
         clist[(size_t)cur[(size_t)f.i]++] = (int32_t)(k << 2 | 0);
         if (f.kind == DPG_FACTOR_BETWEEN) {
             clist[(size_t)cur[(size_t)f.j]++] = (int32_t)(k << 2 | 1);
-            const int64_t u = n + pair_id(std::min<int64_t>(f.i, f.j), std::max<int64_t>(f.i, f.j));
-            clist[(size_t)cur[(size_t)u]++] = (int32_t)(k << 2 | (f.i < f.j ? 2 : 3));
+            clist[(size_t)cur[(size_t)(n + fpair[(size_t)k])]++] = (int32_t)(k << 2 | (f.i < f.j ? 2 : 3));
         }
     }
-    // full BSR rows
-    std::vector<std::vector<std::pair<int32_t, int32_t>>> rows((size_t)n);
-    for (int64_t v = 0; v < n; ++v) rows[(size_t)v].emplace_back((int32_t)v, (int32_t)v);
-    for (int64_t p = 0; p < P; ++p) {
-        const int64_t lo = pairs[(size_t)p].first, hi = pairs[(size_t)p].second;
-        rows[(size_t)lo].emplace_back((int32_t)hi, (int32_t)(n + p));
-        rows[(size_t)hi].emplace_back((int32_t)lo, (int32_t)(-1 - (n + p)));
+    // full BSR rows, by column: row v is the pairs (u, v) with u < v in ascending u (the key order
+    // deals them so, bucketed by v), the diagonal block, then the pairs (v, w) in ascending w
+    std::vector<int32_t> rowptr((size_t)n + 1, 0);
+    for (int64_t v = 0; v < n; ++v) rowptr[(size_t)v + 1] = 1;
+    for (uint64_t key : pk) { rowptr[(size_t)(key >> 32) + 1]++; rowptr[(size_t)(key & 0xffffffffu) + 1]++; }
+    for (int64_t v = 0; v < n; ++v) rowptr[(size_t)v + 1] += rowptr[(size_t)v];
+    std::vector<int32_t> colidx((size_t)rowptr[(size_t)n]), srcup((size_t)rowptr[(size_t)n]);
+    {
+        std::vector<int32_t> at(rowptr.begin(), rowptr.end() - 1);
+        for (int64_t p = 0; p < P; ++p) {   // row hi: (lo, pair), ascending lo
+            const int32_t lo = (int32_t)(pk[(size_t)p] >> 32), hi = (int32_t)(pk[(size_t)p] & 0xffffffffu);
+            colidx[(size_t)at[(size_t)hi]] = lo;
+            srcup[(size_t)at[(size_t)hi]++] = (int32_t)(-1 - (n + p));
+        }
+        for (int64_t v = 0; v < n; ++v) {   // the diagonal block after them
+            colidx[(size_t)at[(size_t)v]] = (int32_t)v;
+            srcup[(size_t)at[(size_t)v]++] = (int32_t)v;
+        }
+        for (int64_t p = 0; p < P; ++p) {   // row lo: (hi, pair), ascending hi
+            const int32_t lo = (int32_t)(pk[(size_t)p] >> 32), hi = (int32_t)(pk[(size_t)p] & 0xffffffffu);
+            colidx[(size_t)at[(size_t)lo]] = hi;
+            srcup[(size_t)at[(size_t)lo]++] = (int32_t)(n + p);
+        }
     }
-    std::vector<int32_t> rowptr((size_t)n + 1, 0), colidx, srcup;
-    colidx.reserve((size_t)(n + 2 * P));
-    srcup.reserve((size_t)(n + 2 * P));
-    for (int64_t v = 0; v < n; ++v) {
-        auto& rw = rows[(size_t)v];
-        std::sort(rw.begin(), rw.end());
-        for (auto& cs : rw) { colidx.push_back(cs.first); srcup.push_back(cs.second); }
-        rowptr[(size_t)v + 1] = (int32_t)colidx.size();
+    // the Cholesky's symbolic analysis and host plan (no device call): all of the setup's host
+    // work runs before the wait below, so a caller's kernels still running on sync_stream (the
+    // batch's ICP) overlap it
+    const double t1 = gn_wall_ms();
+    void* chol = nullptr;
+    {
+        std::vector<int32_t> plo((size_t)P), phi((size_t)P);
+        for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)(pk[(size_t)p] >> 32); phi[(size_t)p] = (int32_t)(pk[(size_t)p] & 0xffffffffu); }
+        dpg_chol_opts o = opts ? *opts : dpg_chol_opts{};
+        dpg_chol_sym S;
+        if (dpg_chol_symbolic(n, plo.data(), phi.data(), P, &o, &S) ||
+            dpg_chol_create_sym_plan(&chol, n, plo.data(), phi.data(), P, &S, &o))
+            chol = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
+    }
+    const double t2 = gn_wall_ms();
+    if (sync_stream && hipStreamSynchronize(reinterpret_cast<hipStream_t>(sync_stream)) != hipSuccess) {
+        if (chol) dpg_chol_destroy(chol);
+        return DPG_ERR_HIP;
     }
     g->n_nodes = n;
     g->n_factors = nf;
@@ -554,20 +592,26 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     rc |= dev_alloc(&g->hb_own, (size_t)dpg_gn_dev_hb_size(g));
     rc |= dev_alloc(&g->scal3, 4);
     if (!rc && hipHostMalloc(reinterpret_cast<void**>(&g->scal3_host), 4 * sizeof(double)) != hipSuccess) rc = DPG_ERR_HIP;
-    if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
+    if (rc) { if (chol) dpg_chol_destroy(chol); dpg_gn_dev_free(g); return DPG_ERR_HIP; }
     if (nf && hipMemcpy(g->factors, F, (size_t)nf * sizeof(dpg_factor), hipMemcpyHostToDevice) != hipSuccess) rc = DPG_ERR_HIP;
     rc |= up(g->up_cptr, cptr);
     rc |= up(g->up_clist, clist);
     rc |= up(g->rowptr, rowptr);
     rc |= up(g->colidx, colidx);
     rc |= up(g->src_up, srcup);
-    if (rc) { dpg_gn_dev_free(g); return DPG_ERR_HIP; }
-    // symbolic analysis + device structures of the supernodal Cholesky (once per pattern)
-    std::vector<int32_t> plo((size_t)P), phi((size_t)P);
-    for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)pairs[(size_t)p].first; phi[(size_t)p] = (int32_t)pairs[(size_t)p].second; }
-    rc = dpg_chol_create(&g->chol, n, plo.data(), phi.data(), P, opts);
-    if (rc) g->chol = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
-    else dpg_chol_keep_inverse(g->chol, 1);   // chord steps reuse the factor: L11^-1 for their solves
+    if (rc) { if (chol) dpg_chol_destroy(chol); dpg_gn_dev_free(g); return DPG_ERR_HIP; }
+    // the supernodal Cholesky's device structures (once per pattern)
+    g->chol = chol;
+    if (g->chol && dpg_chol_create_sym_upload(&g->chol)) g->chol = nullptr;   // (destroyed on error)
+    if (g->chol) dpg_chol_keep_inverse(g->chol, 1);   // chord steps reuse the factor: L11^-1 for their solves
+    const double t3 = gn_wall_ms();
+    double bt[2] = {0.0, 0.0};
+    if (g->chol) dpg_chol_build_times(g->chol, bt);
+    g->setup_ms[0] = t1 - t0;
+    g->setup_ms[1] = std::max(0.0, (t2 - t1) - bt[0]);   // the symbolic analysis (ordering, supernodes)
+    g->setup_ms[2] = bt[0];                               // its host plan
+    g->setup_ms[3] = std::max(0.0, (t3 - t2) - bt[1]);   // waiting for the stream, allocations, uploads
+    g->setup_ms[4] = bt[1];                               // the Cholesky's upload
     return DPG_OK;
 }
 

@@ -152,6 +152,10 @@ typedef struct dpg_gn_dev {
        (dpg_gn_pipe.h): the ranks cannot disagree on the iteration count, and with it on the number
        of collectives they issue */
     int32_t n_vote;
+    /* host clock of the last dpg_gn_dev_alloc (ms): pattern + contribution lists + BSR rows, the
+       Cholesky's symbolic analysis, its host plan (these three before the stream wait), the wait +
+       device allocations + uploads, the Cholesky's upload */
+    double setup_ms[5];
 } dpg_gn_dev;
 
 /* Supernodal multifrontal Cholesky of the block system (dpg_chol.hip); opts (dpg_chol.h, NULL =
@@ -171,8 +175,10 @@ const double* dpg_chol_x_dev(void* chol);
 const int32_t* dpg_chol_status_dev(void* chol);
 void dpg_chol_stats(void* chol, double out[6]);
 
+/* host work first (pattern, lists, the Cholesky's analysis and plan), then -- after
+   hipStreamSynchronize(sync_stream) when given -- the device allocations and uploads */
 int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n_nodes, const dpg_factor* factors, int64_t n_factors,
-                     int64_t shard_begin, int64_t shard_end, const struct dpg_chol_opts* opts);
+                     int64_t shard_begin, int64_t shard_end, const struct dpg_chol_opts* opts, void* sync_stream);
 /* the context's solver options (dpg_ctx_set_solver_options) */
 const struct dpg_chol_opts* dpg_ctx_chol_opts(dpg_ctx* c);
 void dpg_gn_dev_free(dpg_gn_dev* g);

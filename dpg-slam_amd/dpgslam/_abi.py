@@ -298,6 +298,7 @@ SIGNATURES = {
     "dpg_gn_setup": (C.c_int, [P, C.c_int64, P, C.c_int64, C.c_int64, C.c_int64, C.POINTER(GnParams)]),
     "dpg_gn_take_icp_measurements": (C.c_int, [P, C.c_int64, C.c_int64, C.c_int64, C.POINTER(IcpParams)]),
     "dpg_gn_hb_size": (C.c_int64, [P]),
+    "dpg_gn_setup_profile": (C.c_int, [P, F64P]),
     "dpg_gn_set_poses": (C.c_int, [P, F64P]),
     "dpg_gn_get_poses": (C.c_int, [P, F64P]),
     "dpg_gn_assemble": (C.c_int, [P, P]),

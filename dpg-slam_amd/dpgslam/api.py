@@ -406,6 +406,13 @@ class Context:
         X = _f64(poses).reshape(-1, 3)
         check(lib().dpg_gn_set_poses(self.handle, ptr(X, C.c_double)), "dpg_gn_set_poses")
 
+    def gn_setup_profile(self) -> dict:
+        """dpg_gn_setup_profile: host ms of the last gn_setup's parts."""
+        out = np.zeros(5, np.float64)
+        check(lib().dpg_gn_setup_profile(self.handle, ptr(out, C.c_double)), "dpg_gn_setup_profile")
+        return dict(zip(("pattern_lists_bsr", "chol_symbolic", "chol_plan", "wait_alloc_upload", "chol_upload"),
+                        (float(x) for x in out)))
+
     def gn_run(self, V: int | None = None):
         """The whole GN loop natively (dpg_gn_run) from the poses of gn_set_poses; returns
         (stats dict, poses [V, 3] or None when V is None)."""
