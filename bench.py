@@ -152,9 +152,10 @@ def main_incremental(args):
     import ctypes as C
     L = _abi.lib()
     prof, pbuf = [], (C.c_double * 8)()
-    lat, icp_ms, sym_ms, num_ms, reord, relin = [], [], [], [], 0, 0
+    lat, icp_ms, sym_ms, num_ms, reord, relin, kept = [], [], [], [], 0, 0, []
     with api.Context(0) as ctx:
-        g = api.IncGraph(ctx, mode=args.inc_mode, reorder_every=args.inc_reorder_every)
+        g = api.IncGraph(ctx, mode=args.inc_mode, reorder_every=args.inc_reorder_every,
+                         full_refactor=args.inc_full_refactor)
         for v in range(V):
             extra = w.base_factors[v:v + 1]
             ts = time.perf_counter()
@@ -166,6 +167,7 @@ def main_incremental(args):
             num_ms.append(st.update.ms_numeric)
             reord += st.update.reordered
             relin += st.update.relinearized
+            kept.append(int(st.update.fronts_kept))
             L.dpg_inc_last_profile(C.c_void_p(g.handle), pbuf, 8)
             prof.append(list(pbuf)[:6])
             if v % 1000 == 999:
@@ -191,6 +193,11 @@ def main_incremental(args):
                                                           "chol_host", "chol_upload"],
                                                          np.mean(np.asarray(prof[-500:]), 0).round(4).tolist()))},
         "reorders": reord, "relinearized_total": relin, "nnz_L_blocks": nnz, "factors": n_fac,
+        # isam_->update's partial re-elimination: updates of the last 500 that kept fronts of the
+        # previous factorization, and how many (the others refactored every front: reorders,
+        # relinearizations, grown buffers)
+        "partial_refactor": {"updates_keeping_fronts_tail": int(np.sum(np.asarray(kept[-500:]) > 0)),
+                             "fronts_kept_median_tail": float(np.median(kept[-500:]))},
         "round1_per_node_from_scratch_ms": scratch_ms, "round1_from_scratch_gn_iterations": int(gst.iterations),
     }
 
@@ -636,6 +643,7 @@ def main():
     ap.add_argument("--inc-mode", default="isam2", choices=["isam2", "batch"])
     ap.add_argument("--inc-nodes", type=int, default=5000)
     ap.add_argument("--inc-reorder-every", type=int, default=32, help="incremental: a fresh order every this many nodes")
+    ap.add_argument("--inc-full-refactor", action="store_true", help="incremental: refactor every front every update")
     ap.add_argument("--cpu-nodes", type=int, default=8, help="nodes in the incremental CPU-baseline sample")
     args = ap.parse_args()
     if args.workload == "incremental":

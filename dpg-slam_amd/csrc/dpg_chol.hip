@@ -1960,7 +1960,7 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
                                                        const double* __restrict__ hb, const double* __restrict__ g,
                                                        const int32_t* __restrict__ perm, double* fronts,
                                                        double* __restrict__ ysol, double* acc, int ns, int db,
-                                                       const int32_t* gate) {
+                                                       const int32_t* gate, const uint8_t* __restrict__ keep) {
     extern __shared__ __attribute__((aligned(16))) double smem_f[];
     double* sm = smem_f + 2;   // smem_f[0]: the claimed ticket (no static LDS: keeps the base 16-B aligned)
     if (gate_off(gate, 1)) return;
@@ -1970,12 +1970,32 @@ __global__ __launch_bounds__(kFT, 2) void chol_factor_dag(const int32_t* __restr
     const int code = claim_lds(order, sync, reinterpret_cast<int*>(smem_f));
     const int s = code >> 6, mem = code & 63;
     const SnDev S = sns[s];
+    if (keep && keep[s]) {   // partial refactorization: the front keeps its factored values (and its
+                             // update matrix, which the parent reads as from a finished member)
+        if (threadIdx.x == 0 && S.parent >= 0)
+            __hip_atomic_fetch_add(sync + 1 + S.parent, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (mem == 0) FT_MARK(s, 0);
     if (S.G == 1 && 3 * (S.k + S.r) <= kSmall && S.nchild <= kMaxCh)
         small_front(s, S, sync + 1, status, sns, omap, relmap, child_list, hb, g, perm, fronts, ysol, acc, sm);
     else
         large_front(s, mem, S, sync + 1, sync + 1 + ns, sync + 2 + 3 * ns, status, sns, omap, relmap, child_list,
                     ftasks, fchild, hb, g, perm, fronts, ysol, acc, sm, db);
+}
+
+// partial refactorization: the kept fronts (and their pending forward-solve updates) the new layout
+// moved, as runs {src, dst, doubles, buffer} (one run per blockIdx.y; buffer 0: fronts, 1: the
+// pending updates), through a scratch buffer (gather, then scatter: old and new places overlap)
+__global__ __launch_bounds__(256) void chol_copy_runs(const double* __restrict__ src0, const double* __restrict__ src1,
+                                                      double* __restrict__ dst0, double* __restrict__ dst1,
+                                                      const int64_t* __restrict__ runs) {
+    const int64_t* r = runs + 4 * blockIdx.y;
+    const int64_t s0 = r[0], d0 = r[1], n = r[2];
+    const double* src = r[3] ? src1 : src0;
+    double* dst = r[3] ? dst1 : dst0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[d0 + i] = src[s0 + i];
 }
 
 // device buffers are kept between rebuilds of the same solver (an incremental graph re-derives its
@@ -2060,11 +2080,43 @@ struct CholDev {
     size_t c_stage = 0;
     char* arena = nullptr;        // device: every structure array above (sns .. upd_tasks), one copy
     size_t c_arena = 0;
+    // partial refactorization (dpg_chol_track_factor): `fac_sym` is the analysis the values in
+    // `fronts` were factored under (valid while fac_valid and fronts == fac_ptr), fac_G its team
+    // sizes; sym_is_fac: the current analysis is that one (it moves to fac_sym with the next plan)
+    bool track = false, fac_valid = false, sym_is_fac = false, fac_db = false;
+    double* fac_ptr = nullptr;         // fronts, y and the pending updates of that factorization
+    double* fac_ysol = nullptr;
+    double* fac_acc = nullptr;
+    dpg_chol_sym fac_sym;
+    std::vector<int32_t> cur_G, fac_G;
+    std::vector<uint8_t> h_keep;
+    std::vector<int32_t> h_old;
+    std::vector<int64_t> h_runs;
+    double* scratch = nullptr;    // the moved fronts between the gather and the scatter
+    size_t c_scratch = 0;
+    char* pstage = nullptr;       // pinned: keep flags + runs, one copy up
+    size_t c_pstage = 0;
+    char* dpart = nullptr;
+    size_t c_dpart = 0;
+    hipEvent_t pev = nullptr;     // after that copy (the staging buffer's next rewrite waits for it)
+    bool pev_set = false;
+    int64_t pstats[3] = {0, 0, 0};   // last solve: fronts refactored, kept, doubles moved
     void* host = nullptr;         // CholHost of the build in progress (a plan and its upload may run
                                   // on different threads, one after the other)
 };
 
 void free_host(void* p);
+
+// a new analysis in; *S gets back one whose buffers the caller reuses.  With tracking, the analysis
+// of the last factorization moves to fac_sym instead (the partial refactorization compares with it)
+void take_sym(CholDev* c, dpg_chol_sym* S) {
+    if (c->track && c->sym_is_fac) {
+        std::swap(c->fac_sym, c->sym);
+        c->fac_G.swap(c->cur_G);
+        c->sym_is_fac = false;
+    }
+    std::swap(c->sym, *S);
+}
 
 }  // namespace
 
@@ -2073,7 +2125,9 @@ extern "C" void dpg_chol_destroy(void* h) {
     if (!c) return;
     // (the structure arrays live in c->arena)
     if (c->aux) (void)hipStreamSynchronize(c->aux);
-    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync, c->dinv, c->linv};
+    void* ptrs[] = {c->arena, c->fronts, c->acc, c->ysol, c->xsol, c->status, c->sync, c->dinv, c->linv, c->scratch, c->dpart};
+    if (c->pev) (void)hipEventDestroy(c->pev);
+    if (c->pstage) (void)hipHostFree(c->pstage);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (c->stage) (void)hipHostFree(c->stage);
@@ -2110,7 +2164,7 @@ int dpg_chol_create_sym(void** h, int64_t n, const int32_t* pair_lo, const int32
                         dpg_chol_sym* S, const dpg_chol_opts* opts) {
     CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
     if (opts) c->opts = *opts;
-    std::swap(c->sym, *S);   // *S gets the previous analysis (its buffers are reused by the next derive)
+    take_sym(c, S);   // *S gets an earlier analysis (its buffers are reused by the next derive)
     const int rc = chol_build(c, n, pair_lo, pair_hi, n_pairs);
     if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
     *h = c;
@@ -2333,6 +2387,10 @@ int chol_plan(CholDev* c, int64_t n, const int32_t* pair_lo, const int32_t* pair
     }
     for (int32_t s = 0; s < S.ns; ++s)
         if (sns[(size_t)s].parent >= 0) sns[(size_t)sns[(size_t)s].parent].need += sns[(size_t)s].G;
+    if (c->track) {
+        c->cur_G.resize((size_t)S.ns);
+        for (int32_t s = 0; s < S.ns; ++s) c->cur_G[(size_t)s] = sns[(size_t)s].G;
+    }
     // L11^-1 of the fronts with at least solve_inv_cols pivot columns (and at most 64 kInvMaxQ = 192)
     H.inv_t.clear();
     c->linv_total = 0;
@@ -2719,10 +2777,14 @@ int chol_upload(CholDev* c, int64_t n, const CholHost& H) {
         off += al(std::max<size_t>(pieces[i].bytes, 1));
     }
     int rc = hipMemcpyAsync(c->arena, c->stage, total, hipMemcpyHostToDevice, nullptr) != hipSuccess;
+    // a re-allocated front, y or pending-update buffer has lost the tracked factorization (a new
+    // allocation may come back at the old address: the capacities tell)
+    const size_t cap0[3] = {c->c_fronts, c->c_acc, c->c_ysol};
     rc |= dreserve(&c->sync, &c->c_sync, c->sync_bytes / sizeof(int32_t));
     rc |= dreserve(&c->fronts, &c->c_fronts, (size_t)S.front_off[(size_t)S.ns]);
     rc |= dreserve(&c->acc, &c->c_acc, (size_t)H.acc_total);
     rc |= dreserve(&c->ysol, &c->c_ysol, (size_t)(3 * n));
+    if (rc || cap0[0] != c->c_fronts || cap0[1] != c->c_acc || cap0[2] != c->c_ysol) c->fac_valid = false;
     rc |= dreserve(&c->xsol, &c->c_xsol, (size_t)(3 * n));
     rc |= dreserve(&c->status, &c->c_status, 1);
     rc |= dreserve(&c->dinv, &c->c_dinv, (size_t)(3 * n) * kSB);
@@ -2764,7 +2826,7 @@ int dpg_chol_create_sym_plan(void** h, int64_t n, const int32_t* pair_lo, const 
                              dpg_chol_sym* S, const dpg_chol_opts* opts) {
     CholDev* c = *h ? reinterpret_cast<CholDev*>(*h) : new CholDev();
     if (opts) c->opts = *opts;
-    std::swap(c->sym, *S);
+    take_sym(c, S);
     const int rc = chol_build_plan(c, n, pair_lo, pair_hi, n_pairs);
     if (rc) { dpg_chol_destroy(c); *h = nullptr; return rc; }
     *h = c;
@@ -2831,8 +2893,23 @@ static void launch_inv(CholDev* c, hipStream_t st, const int32_t* gate) {
                            c->fronts, c->linv, gate);
 }
 
+// the values in fronts now belong to the current analysis
+static void note_factored(CholDev* c, int64_t refactored, int64_t kept, int64_t moved) {
+    c->pstats[0] = refactored;
+    c->pstats[1] = kept;
+    c->pstats[2] = moved;
+    if (!c->track) return;
+    c->fac_valid = true;
+    c->fac_ptr = c->fronts;
+    c->fac_ysol = c->ysol;
+    c->fac_acc = c->acc;
+    c->sym_is_fac = true;
+    c->fac_db = c->fused_db;
+}
+
 extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
+    note_factored(c, c->sym.ns, 0, 0);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dpg_chol_sym& S = c->sym;
     const double* g = hb + 9 * c->nnzb_upper;
@@ -2842,7 +2919,7 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
         hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
                            c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
                            c->perm, c->fronts,
-                           c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, nullptr);
+                           c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, nullptr, nullptr);
         if (c->use_dinv && c->n_dblocks > 0)
             hipLaunchKernelGGL(chol_inv_diag, dim3((unsigned)c->n_dblocks), dim3(64), 0, st, c->dblocks, c->sns, c->fronts, c->dinv);
         hipLaunchKernelGGL(chol_backward_dag, dim3(S.ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
@@ -2885,6 +2962,177 @@ extern "C" int dpg_chol_solve(void* h, const double* hb, void* stream) {
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }
 
+extern "C" void dpg_chol_track_factor(void* h, int on) {
+    CholDev* c = reinterpret_cast<CholDev*>(h);
+    if (!c || c->track == (on != 0)) return;
+    c->track = on != 0;
+    c->fac_valid = false;
+    c->sym_is_fac = false;
+    c->cur_G.clear();   // the current analysis was planned untracked: its team sizes are unknown
+}
+extern "C" void dpg_chol_forget_factor(void* h) {
+    if (h) reinterpret_cast<CholDev*>(h)->fac_valid = false;
+}
+extern "C" void dpg_chol_partial_stats(void* h, int64_t out[3]) {
+    const CholDev* c = reinterpret_cast<const CholDev*>(h);
+    for (int k = 0; k < 3; ++k) out[k] = c ? c->pstats[k] : 0;
+}
+
+// ISAM2's partial re-elimination (isam_->update, dpg_slam.cc:320, re-eliminates only the cliques
+// the new factors touch and their ancestors), as a multifrontal refactorization that keeps every
+// front whose values cannot have changed since the tracked factorization:
+//   * the same columns (same first column, same count: positions are stable between reorders, the
+//     caller checks the order is unchanged -- here: the old order is a prefix of the new), the same
+//     rows, the same children (by first column, in order: the extend-add order), the same team
+//     size and panel buffering (the arithmetic order of the factorization kernel);
+//   * no dirty node's column in it (its H blocks are then the same sums of the same factors at the
+//     same linearization point: the caller's contract);
+//   * no dirty front below it (its children's update matrices are unchanged).
+// The forward solve folded into the factorization keeps its values too: a kept front's nodes have
+// the same gradient (no new factor on them, same theta) and its children are kept, so its part of y
+// (at its column positions: unchanged between reorders) and its pending row updates for the parent
+// are what a full refactorization would compute again.  A kept front the new layout moved -- its
+// values and its pending updates -- goes through the scratch buffer (gather, scatter), then the
+// factorization runs with the kept fronts only signalling their parents, then the backward solve
+// over every front.  The result is bit-identical to dpg_chol_solve's.
+extern "C" int dpg_chol_solve_partial(void* h, const double* hb, const int32_t* dirty_nodes, int64_t n_dirty,
+                                      void* stream) {
+    CholDev* c = reinterpret_cast<CholDev*>(h);
+    const dpg_chol_sym& S = c->sym;
+    const dpg_chol_sym& O = c->fac_sym;
+    const bool usable = c->track && c->fac_valid && !c->sym_is_fac && c->fac_ptr == c->fronts &&
+                        c->fac_ysol == c->ysol && c->fac_acc == c->acc && c->fused &&
+                        !(c->use_dinv && c->n_dblocks > 0) && c->fac_db == c->fused_db && O.ns > 0 && O.n <= S.n &&
+                        (int64_t)c->fac_G.size() == (int64_t)O.ns && (int64_t)c->cur_G.size() == (int64_t)S.ns &&
+                        std::equal(O.perm.begin(), O.perm.end(), S.perm.begin());
+    if (!usable) return dpg_chol_solve(h, hb, stream);
+    const int32_t ns = S.ns;
+    std::vector<uint8_t>& keep = c->h_keep;
+    std::vector<int32_t>& old = c->h_old;
+    keep.assign((size_t)ns, 1);
+    old.assign((size_t)ns, -1);
+    for (int64_t q = 0; q < n_dirty; ++q) {
+        const int32_t v = dirty_nodes[q];
+        if (v < 0 || v >= S.n) return dpg_chol_solve(h, hb, stream);
+        keep[(size_t)S.sn_of[(size_t)S.pos[(size_t)v]]] = 0;
+    }
+    int64_t kept = 0;
+    for (int32_t sn = 0; sn < ns; ++sn) {   // children before parents (a parent's first column is later)
+        if (keep[(size_t)sn]) {
+            const int32_t c0 = S.sn_c0[(size_t)sn], c1 = S.sn_c0[(size_t)sn + 1];
+            bool same = c1 <= O.n;
+            int32_t os = -1;
+            if (same) {
+                os = O.sn_of[(size_t)c0];
+                same = O.sn_c0[(size_t)os] == c0 && O.sn_c0[(size_t)os + 1] == c1 && c->fac_G[(size_t)os] == c->cur_G[(size_t)sn];
+            }
+            if (same) {
+                const int64_t r0 = S.sn_rows_ptr[(size_t)sn], r1 = S.sn_rows_ptr[(size_t)sn + 1];
+                const int64_t q0 = O.sn_rows_ptr[(size_t)os], q1 = O.sn_rows_ptr[(size_t)os + 1];
+                same = r1 - r0 == q1 - q0 && std::equal(S.sn_rows.begin() + r0, S.sn_rows.begin() + r1, O.sn_rows.begin() + q0);
+            }
+            if (same) {
+                const int64_t a0 = S.child_ptr[(size_t)sn], a1 = S.child_ptr[(size_t)sn + 1];
+                const int64_t b0 = O.child_ptr[(size_t)os], b1 = O.child_ptr[(size_t)os + 1];
+                same = a1 - a0 == b1 - b0;
+                for (int64_t t = 0; same && t < a1 - a0; ++t)
+                    same = S.sn_c0[(size_t)S.child_list[(size_t)(a0 + t)]] == O.sn_c0[(size_t)O.child_list[(size_t)(b0 + t)]];
+            }
+            if (same) {
+                old[(size_t)sn] = os;
+                ++kept;
+            } else {
+                keep[(size_t)sn] = 0;
+            }
+        }
+        if (!keep[(size_t)sn] && S.sn_parent[(size_t)sn] >= 0) keep[(size_t)S.sn_parent[(size_t)sn]] = 0;
+    }
+    if (kept == 0) return dpg_chol_solve(h, hb, stream);
+    // runs of kept fronts the layout moved: gather {old, scratch}, scatter {scratch, new}; the
+    // pending updates of front s sit at 3 sn_rows_ptr[s] (chol_plan's acc_off)
+    std::vector<int64_t>& runs = c->h_runs;
+    runs.clear();
+    int64_t moved = 0, max_run = 0;
+    auto add_run = [&](int64_t src, int64_t dst, int64_t len, int64_t buf) {
+        if (src == dst || len == 0) return;
+        const size_t nr = runs.size();
+        if (nr >= 4 && runs[nr - 1] == buf && runs[nr - 4] + runs[nr - 2] == src && runs[nr - 3] + runs[nr - 2] == dst) {
+            runs[nr - 2] += len;
+        } else {
+            runs.push_back(src);
+            runs.push_back(dst);
+            runs.push_back(len);
+            runs.push_back(buf);
+        }
+        max_run = std::max(max_run, runs[runs.size() - 2]);
+        moved += len;
+    };
+    for (int32_t sn = 0; sn < ns; ++sn)
+        if (keep[(size_t)sn])
+            add_run(O.front_off[(size_t)old[(size_t)sn]], S.front_off[(size_t)sn],
+                    S.front_off[(size_t)sn + 1] - S.front_off[(size_t)sn], 0);
+    for (int32_t sn = 0; sn < ns; ++sn)
+        if (keep[(size_t)sn])
+            add_run(3 * O.sn_rows_ptr[(size_t)old[(size_t)sn]], 3 * S.sn_rows_ptr[(size_t)sn],
+                    3 * (S.sn_rows_ptr[(size_t)sn + 1] - S.sn_rows_ptr[(size_t)sn]), 1);
+    const int64_t nruns = (int64_t)runs.size() / 4;
+    if (nruns > 65535) return dpg_chol_solve(h, hb, stream);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // keep flags + gather runs + scatter runs: one pinned buffer, one copy up
+    const size_t keep_bytes = ((size_t)ns + 15) & ~size_t(15);
+    const size_t run_bytes = sizeof(int64_t) * 4 * (size_t)nruns;
+    const size_t bytes = keep_bytes + 2 * run_bytes;
+    if (c->pev_set && hipEventSynchronize(c->pev) != hipSuccess) return DPG_ERR_HIP;
+    if (bytes > c->c_pstage) {
+        if (c->pstage) (void)hipHostFree(c->pstage);
+        c->pstage = nullptr;
+        const size_t want = std::max(bytes, c->c_pstage + c->c_pstage / 2);
+        c->c_pstage = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&c->pstage), want) != hipSuccess) return DPG_ERR_HIP;
+        c->c_pstage = want;
+    }
+    if (dreserve(&c->dpart, &c->c_dpart, bytes) || (moved > 0 && dreserve(&c->scratch, &c->c_scratch, (size_t)moved)))
+        return DPG_ERR_HIP;
+    memcpy(c->pstage, keep.data(), (size_t)ns);
+    int64_t* gat = reinterpret_cast<int64_t*>(c->pstage + keep_bytes);
+    int64_t* sca = gat + 4 * nruns;
+    for (int64_t r = 0, off = 0; r < nruns; ++r) {
+        const int64_t* q = runs.data() + 4 * r;
+        const int64_t g4[4] = {q[0], off, q[2], q[3]}, s4[4] = {off, q[1], q[2], q[3]};
+        std::copy(g4, g4 + 4, gat + 4 * r);
+        std::copy(s4, s4 + 4, sca + 4 * r);
+        off += q[2];
+    }
+    if (!c->pev && hipEventCreateWithFlags(&c->pev, hipEventDisableTiming) != hipSuccess) return DPG_ERR_HIP;
+    if (hipMemcpyAsync(c->dpart, c->pstage, bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipEventRecord(c->pev, st) != hipSuccess)
+        return DPG_ERR_HIP;
+    c->pev_set = true;
+    const uint8_t* keep_dev = reinterpret_cast<const uint8_t*>(c->dpart);
+    const int64_t* gat_dev = reinterpret_cast<const int64_t*>(c->dpart + keep_bytes);
+    const int64_t* sca_dev = gat_dev + 4 * nruns;
+    if (nruns > 0) {
+        const unsigned gx = (unsigned)std::min<int64_t>(64, std::max<int64_t>(1, (max_run + 2047) / 2048));
+        hipLaunchKernelGGL(chol_copy_runs, dim3(gx, (unsigned)nruns), dim3(256), 0, st, c->fronts, c->acc, c->scratch,
+                           c->scratch, gat_dev);
+        hipLaunchKernelGGL(chol_copy_runs, dim3(gx, (unsigned)nruns), dim3(256), 0, st, c->scratch, c->scratch, c->fronts,
+                           c->acc, sca_dev);
+    }
+    const double* g = hb + 9 * c->nnzb_upper;
+    if (hipMemsetAsync(c->status, 0, sizeof(int32_t), st) != hipSuccess ||
+        hipMemsetAsync(c->sync, 0, c->sync_bytes, st) != hipSuccess)
+        return DPG_ERR_HIP;
+    hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
+                       c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
+                       c->perm, c->fronts, c->ysol, c->acc, ns, c->fused_db ? 1 : 0, nullptr, keep_dev);
+    hipLaunchKernelGGL(chol_backward_dag, dim3(ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
+                       c->sync + 1 + 2 * ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol,
+                       c->solve_stage, c->solve_maxseg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+    note_factored(c, ns - kept, kept, moved);
+    c->inv_valid = false;
+    return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
+}
+
 // forward + backward solves with the fronts of the last factorization (the right-hand side from hb)
 extern "C" int dpg_chol_resolve(void* h, const double* hb, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
@@ -2922,6 +3170,7 @@ extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* ga
                                     double* max_out, void* stream) {
     CholDev* c = reinterpret_cast<CholDev*>(h);
     if (!dpg_chol_gated_ok(h)) return DPG_ERR_STATE;
+    c->fac_valid = false;   // (a Gauss-Newton loop's refactorizations are not tracked)
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const dpg_chol_sym& S = c->sym;
     const double* g = hb + 9 * c->nnzb_upper;
@@ -2942,7 +3191,7 @@ extern "C" int dpg_chol_solve_gated(void* h, const double* hb, const int32_t* ga
     }
     hipLaunchKernelGGL(chol_factor_dag, dim3((unsigned)c->n_tickets), dim3(kFT), c->lds_fused, st, c->order_fac,
                        c->sync, c->status, c->sns, c->omap, c->relmap, c->child_list, c->ftasks, c->fchild, hb, g,
-                       c->perm, c->fronts, c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, gate);
+                       c->perm, c->fronts, c->ysol, c->acc, S.ns, c->fused_db ? 1 : 0, gate, nullptr);
     if (inv) {   // L11^-1 of a refactoring iteration beside its backward solve (which does not use it)
         if (hipEventRecord(c->ev_fac, st) != hipSuccess || hipStreamWaitEvent(c->aux, c->ev_fac, 0) != hipSuccess)
             return DPG_ERR_HIP;

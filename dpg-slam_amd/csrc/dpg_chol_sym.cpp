@@ -22,6 +22,7 @@
 #include <atomic>
 #include <functional>
 #include <future>
+#include <memory>
 #include <queue>
 #include <vector>
 
@@ -129,6 +130,7 @@ struct NdShared {
     std::atomic<int32_t> next_id{0};
 };
 struct NdState {
+    int64_t n;
     const int64_t* aptr;
     const int32_t* adj;
     int32_t leaf;
@@ -141,25 +143,27 @@ inline int32_t stamp_of(const NdState& st, int32_t v) { return __atomic_load_n(&
 inline void stamp_set(NdState& st, int32_t v, int32_t id) { __atomic_store_n(&st.sh->stamp[(size_t)v], id, __ATOMIC_RELAXED); }
 inline int32_t nd_new_id(NdState& st) { return st.sh->next_id.fetch_add(1, std::memory_order_relaxed) + 1; }
 
-// BFS over the nodes stamped `id` from `src`; fills lvl and queue (visit order); returns the height
-int32_t nd_bfs(NdState& st, int32_t id, int32_t src) {
-    st.queue.clear();
-    st.queue.push_back(src);
-    st.sh->lvl[(size_t)src] = 0;
+// BFS over the nodes stamped `id` from `src` into the level array `lvl` (-1 = not reached) and
+// `queue` (visit order); returns the height
+int32_t nd_bfs_into(const NdState& st, int32_t id, int32_t src, int32_t* lvl, std::vector<int32_t>& queue) {
+    queue.clear();
+    queue.push_back(src);
+    lvl[src] = 0;
     int32_t h = 0;
-    for (size_t qi = 0; qi < st.queue.size(); ++qi) {
-        const int32_t v = st.queue[qi];
-        h = std::max(h, st.sh->lvl[(size_t)v]);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int32_t v = queue[qi];
+        h = std::max(h, lvl[v]);
         for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
             const int32_t u = st.adj[(size_t)t];
-            if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] < 0) {
-                st.sh->lvl[(size_t)u] = st.sh->lvl[(size_t)v] + 1;
-                st.queue.push_back(u);
+            if (stamp_of(st, u) == id && lvl[u] < 0) {
+                lvl[u] = lvl[v] + 1;
+                queue.push_back(u);
             }
         }
     }
     return h + 1;
 }
+int32_t nd_bfs(NdState& st, int32_t id, int32_t src) { return nd_bfs_into(st, id, src, st.sh->lvl.data(), st.queue); }
 
 int32_t nd_degree(const NdState& st, int32_t id, int32_t v) {
     int32_t d = 0;
@@ -194,6 +198,7 @@ void nd_halves(NdState& st, std::vector<int32_t>& A, std::vector<int32_t>& B, co
     if (st.prm.par && A.size() + B.size() >= kNdParMin) {
         std::vector<int32_t> outB;
         NdState sb;
+        sb.n = st.n;
         sb.aptr = st.aptr;
         sb.adj = st.adj;
         sb.leaf = st.leaf;
@@ -211,6 +216,54 @@ void nd_halves(NdState& st, std::vector<int32_t>& A, std::vector<int32_t>& B, co
     for (int32_t v : S) st.out->push_back(v);
 }
 
+// the best cut between consecutive levels of the level structure from s0 (bm < 0: none admissible)
+struct NdCut {
+    int32_t bm = -1;
+    bool up = false;
+    double sc = 0.0;
+    int64_t imb = 0;
+};
+constexpr size_t kNdStartsParMin = 2048;
+constexpr size_t kNdStartsThreads = 4;
+NdCut nd_best_cut(const NdState& st, const std::vector<int32_t>& sub, int32_t id, int32_t s0, int32_t* lvl,
+                  std::vector<int32_t>& queue) {
+    NdCut best;
+    const int64_t N = (int64_t)sub.size();
+    for (int32_t v : sub) lvl[v] = -1;
+    const int32_t hh = nd_bfs_into(st, id, s0, lvl, queue);
+    if (hh < 3) return best;
+    std::vector<int64_t> cnt((size_t)hh, 0), slo((size_t)hh, 0), shi((size_t)hh, 0);
+    for (int32_t v : sub) {
+        const int32_t l = lvl[v];
+        cnt[(size_t)l]++;
+        bool up = false, dn = false;
+        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
+            const int32_t u = st.adj[(size_t)t];
+            if (stamp_of(st, u) != id) continue;
+            up |= lvl[u] == l + 1;
+            dn |= lvl[u] == l - 1;
+        }
+        slo[(size_t)l] += up;                    // on level l, touching l + 1
+        if (l > 0) shi[(size_t)l - 1] += dn;     // on level l, touching l - 1
+    }
+    int64_t below = 0;
+    for (int32_t l = 0; l + 1 < hh; ++l) {   // the cut between levels l and l + 1
+        const bool up = shi[(size_t)l] < slo[(size_t)l];
+        const int64_t sz = up ? shi[(size_t)l] : slo[(size_t)l];
+        const int64_t a_sz = below + cnt[(size_t)l] - (up ? 0 : sz), b_sz = N - a_sz - sz;
+        below += cnt[(size_t)l];
+        if (l == 0 || (int64_t)st.prm.bal * a_sz < N || (int64_t)st.prm.bal * b_sz < N) continue;
+        const double mn = (double)std::min(a_sz, b_sz);
+        const double sc = st.prm.score == 2 ? (double)sz * sqrt((double)N / mn)
+                          : st.prm.score == 1 ? (double)sz * (double)N / mn : (double)sz;
+        const int64_t imb = a_sz > b_sz ? a_sz - b_sz : b_sz - a_sz;
+        if (best.bm < 0 || sc < best.sc || (sc == best.sc && imb < best.imb)) {
+            best.bm = l; best.up = up; best.sc = sc; best.imb = imb;
+        }
+    }
+    return best;
+}
+
 // the separator search with several level structures (NdParams, starts > 0); src is the part's
 // pseudo-peripheral node, `id` its stamp
 void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t src) {
@@ -224,45 +277,32 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         for (int t = 1; t < T; ++t) starts.push_back(order[(size_t)((int64_t)t * (N - 1) / T)]);
         starts.push_back(order.back());
     }
+    // every start's best cut (the first of the smallest (score, imbalance) along its levels), then
+    // the first best over the starts in order -- the same pick as one scan over all (start, cut);
+    // a large part's starts are searched on several threads, each with its own level array
+    std::vector<NdCut> cuts(starts.size());
+    const int W = st.prm.par && (size_t)N >= kNdStartsParMin ? (int)std::min<size_t>(kNdStartsThreads, starts.size()) : 1;
+    if (W == 1) {
+        for (size_t k = 0; k < starts.size(); ++k) cuts[k] = nd_best_cut(st, sub, id, starts[k], st.sh->lvl.data(), st.queue);
+    } else {
+        auto work = [&](int w) {
+            std::unique_ptr<int32_t[]> lv(new int32_t[(size_t)st.n]);
+            std::vector<int32_t> q;
+            for (size_t k = (size_t)w; k < starts.size(); k += (size_t)W) cuts[k] = nd_best_cut(st, sub, id, starts[k], lv.get(), q);
+        };
+        std::vector<std::future<void>> fs;
+        for (int w = 1; w < W; ++w) fs.push_back(std::async(std::launch::async, work, w));
+        work(0);
+        for (auto& f : fs) f.get();
+    }
     int32_t bsrc = -1, bm = -1;
     bool bupper = false;
     double bsc = 0.0;
     int64_t bimb = 0;
-    std::vector<int64_t> slo, shi, cnt;
-    for (int32_t s0 : starts) {
-        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
-        const int32_t hh = nd_bfs(st, id, s0);
-        if (hh < 3) continue;
-        cnt.assign((size_t)hh, 0);
-        slo.assign((size_t)hh, 0);
-        shi.assign((size_t)hh, 0);
-        for (int32_t v : sub) {
-            const int32_t l = st.sh->lvl[(size_t)v];
-            cnt[(size_t)l]++;
-            bool up = false, dn = false;
-            for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
-                const int32_t u = st.adj[(size_t)t];
-                if (stamp_of(st, u) != id) continue;
-                up |= st.sh->lvl[(size_t)u] == l + 1;
-                dn |= st.sh->lvl[(size_t)u] == l - 1;
-            }
-            slo[(size_t)l] += up;                    // on level l, touching l + 1
-            if (l > 0) shi[(size_t)l - 1] += dn;     // on level l, touching l - 1
-        }
-        int64_t below = 0;
-        for (int32_t l = 0; l + 1 < hh; ++l) {   // the cut between levels l and l + 1
-            const bool up = shi[(size_t)l] < slo[(size_t)l];
-            const int64_t sz = up ? shi[(size_t)l] : slo[(size_t)l];
-            const int64_t a_sz = below + cnt[(size_t)l] - (up ? 0 : sz), b_sz = N - a_sz - sz;
-            below += cnt[(size_t)l];
-            if (l == 0 || (int64_t)st.prm.bal * a_sz < N || (int64_t)st.prm.bal * b_sz < N) continue;
-            const double mn = (double)std::min(a_sz, b_sz);
-            const double sc = st.prm.score == 2 ? (double)sz * sqrt((double)N / mn)
-                              : st.prm.score == 1 ? (double)sz * (double)N / mn : (double)sz;
-            const int64_t imb = a_sz > b_sz ? a_sz - b_sz : b_sz - a_sz;
-            if (bm < 0 || sc < bsc || (sc == bsc && imb < bimb)) {
-                bsrc = s0; bm = l; bupper = up; bsc = sc; bimb = imb;
-            }
+    for (size_t k = 0; k < starts.size(); ++k) {
+        const NdCut& c = cuts[k];
+        if (c.bm >= 0 && (bm < 0 || c.sc < bsc || (c.sc == bsc && c.imb < bimb))) {
+            bsrc = starts[k]; bm = c.bm; bupper = c.up; bsc = c.sc; bimb = c.imb;
         }
     }
     if (bm < 0) { nd_min_degree(st, sub); return; }
@@ -510,6 +550,7 @@ int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair
         }
     }
     NdState st;
+    st.n = n;
     st.aptr = aptr.data();
     st.adj = adj.data();
     st.leaf = std::max<int32_t>(leaf, 4);

@@ -218,9 +218,11 @@ struct dpg_inc {
     const char* prep_msg = "";                 // its failure message
     double prep_ms[3] = {};                    // its incsym, derive, chol plan times
     std::unique_ptr<dpg_inc_helper> helper;    // the plan's H-block buckets beside the derivation
+    std::vector<int32_t> dirty;                // the update's dirty nodes (partial refactorization)
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
                                                // chol upload (ms); factor Mflop, largest front (blocks),
-                                               // fused DAG path (1) or level path (0), supernodes
+                                               // fused DAG path (1) or level path (0), supernodes, levels,
+                                               // doubles of kept fronts moved (partial refactorization)
 };
 
 namespace {
@@ -399,6 +401,7 @@ int dpg_inc_reset(dpg_inc* q) {
     q->prepared = false;
     q->prep_new = 0;
     q->prep_pairs0 = 0;
+    if (q->g.chol) dpg_chol_forget_factor(q->g.chol);
     return DPG_OK;
 }
 
@@ -416,6 +419,7 @@ int dpg_inc_abort_prepare(dpg_inc* q) {
     q->V_at_order = q->nnz_at_order = 0;
     q->prepared = false;
     q->prep_new = 0;
+    if (q->g.chol) dpg_chol_forget_factor(q->g.chol);
     return DPG_OK;
 }
 
@@ -667,6 +671,7 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     bool theta_saved = false, est_saved = false;
     auto rollback = [&](int code, const char* msg) -> int {
         (void)hipStreamSynchronize(s);
+        if (q->g.chol) dpg_chol_forget_factor(q->g.chol);
         q->F.resize((size_t)nF0);
         q->n_dev_f = std::min(q->n_dev_f, nF0);
         q->f_created.resize((size_t)nF0);
@@ -683,6 +688,9 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
     if ((rc = inc_rebuild_lists(q, s))) return rollback(rc, "dpg_inc_update: contribution lists failed");
     q->prof[2] = now_ms() - t1b;
     if ((rc = inc_rebuild_chol(q))) return rollback(rc, "dpg_inc_update: solver rebuild failed");
+    // the solver remembers its factorization's analysis for the next update's partial refactorization
+    // (ISAM2 updates without the Q1 information scaling, which changes every block every update)
+    dpg_chol_track_factor(q->g.chol, q->P.mode == DPG_INC_ISAM2 && q->P.full_refactor == 0 && !q->P.duplicate_factors);
     const double t2 = now_ms();
     dpg_inc_stats S;
     memset(&S, 0, sizeof(S));
@@ -704,7 +712,34 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
             return rollback(DPG_ERR_HIP, "dpg_inc_update: out of device memory");
         q->g.poses = q->theta;
         if ((rc = dpg_gn_dev_assemble(&q->g, q->g.hb_own, s))) return rollback(rc, "assembly failed");
-        if ((rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s))) return rollback(rc, "Cholesky launch failed");
+        // isam_->update's partial re-elimination: between reorders and relinearizations every H
+        // block is the same sum at the same theta unless a new factor or pair touches its nodes, so
+        // the fronts off the new nodes' and factors' paths to the root keep their factors
+        // (dpg_chol_solve_partial; bit-identical to refactoring every front)
+        const bool partial = q->P.full_refactor == 0 && !relin && !q->prep_reordered && V0 > 0;
+        if (partial) {
+            std::vector<int32_t>& dirty = q->dirty;
+            dirty.clear();
+            for (int64_t v = V0; v < V1; ++v) dirty.push_back((int32_t)v);
+            for (int64_t k = 0; k < n_factors; ++k) {
+                dirty.push_back(factors[k].i);
+                if (factors[k].kind == DPG_FACTOR_BETWEEN) dirty.push_back(factors[k].j);
+            }
+            for (size_t k = (size_t)q->prep_pairs0; k < q->plo.size(); ++k) {
+                dirty.push_back(q->plo[k]);
+                dirty.push_back(q->phi[k]);
+            }
+            rc = dpg_chol_solve_partial(q->g.chol, q->g.hb_own, dirty.data(), (int64_t)dirty.size(), s);
+        } else {
+            rc = dpg_chol_solve(q->g.chol, q->g.hb_own, s);
+        }
+        if (rc) return rollback(rc, "Cholesky launch failed");
+        {
+            int64_t pst[3];
+            dpg_chol_partial_stats(q->g.chol, pst);
+            S.fronts_kept = (int32_t)pst[1];
+            q->prof[11] = (double)pst[2];
+        }
         if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return rollback(DPG_ERR_HIP, "memset");
         hipLaunchKernelGGL(inc_estimate_kernel, dim3(nblk(V1)), dim3(kThreads), 0, s, q->theta, dpg_chol_x_dev(q->g.chol),
                            dpg_chol_pos_dev(q->g.chol), V1, q->est_nxt, q->maxd_nxt, q->g.scal3);

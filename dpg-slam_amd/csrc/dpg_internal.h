@@ -170,6 +170,19 @@ int dpg_chol_solve(void* chol, const double* hb, void* stream);
 int dpg_chol_resolve(void* chol, const double* hb, void* stream);
 /* keep L11^-1 of the large fronts after each ungated factorization for dpg_chol_resolve (GN graphs) */
 void dpg_chol_keep_inverse(void* chol, int on);
+/* Partial refactorization (the incremental graph's ISAM2 updates, dpg_inc.hip): with tracking on,
+   the solver remembers the analysis its fronts were last factored under.  dpg_chol_solve_partial
+   then refactors only the fronts that hold a dirty node's column (a new node, an endpoint of a new
+   factor or pair), whose structure changed, or that lie above such a front; the others keep their
+   factored values (moved to the new layout where it shifted them), then the forward and backward
+   solves run over every front.  Falls back to dpg_chol_solve when nothing can be kept.  Valid only
+   when the H blocks of the kept fronts are unchanged since that factorization (same linearization
+   point, same factors). */
+void dpg_chol_track_factor(void* chol, int on);
+void dpg_chol_forget_factor(void* chol);
+int dpg_chol_solve_partial(void* chol, const double* hb, const int32_t* dirty_nodes, int64_t n_dirty, void* stream);
+/* the last solve: fronts refactored, fronts kept, doubles moved (all fronts refactored: kept = 0) */
+void dpg_chol_partial_stats(void* chol, int64_t out[3]);
 const int32_t* dpg_chol_pos_dev(void* chol);
 const double* dpg_chol_x_dev(void* chol);
 const int32_t* dpg_chol_status_dev(void* chol);

@@ -133,7 +133,7 @@ class IncParams(C.Structure):
         ("duplicate_factors", C.c_int32),
         ("reorder_every", C.c_int32),
         ("reorder_lead", C.c_int32),
-        ("pad", C.c_int32),
+        ("full_refactor", C.c_int32),
         ("gn", GnParams),
     ]
 
@@ -153,7 +153,7 @@ class IncStats(C.Structure):
         ("reordered", C.c_int32),
         ("relinearized", C.c_int32),
         ("gn_iterations", C.c_int32),
-        ("pad", C.c_int32),
+        ("fronts_kept", C.c_int32),
         ("error", C.c_double),
         ("last_delta_inf", C.c_double),
         ("ms_total", C.c_double),

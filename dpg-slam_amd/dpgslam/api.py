@@ -615,15 +615,18 @@ class DpgStore:
 class IncGraph:
     """The incremental per-node pose graph (dpg_inc): isam_->update once per new node
     (dpg_slam.cc:255-329), device-resident, growing in place.  mode: "isam2" (ISAM2 defaults: partial
-    relinearization, threshold 0.1, skip 10) or "batch" (Gauss-Newton to convergence per update)."""
+    relinearization, threshold 0.1, skip 10) or "batch" (Gauss-Newton to convergence per update).
+    full_refactor: every ISAM2 update refactors every Cholesky front (default: only the fronts the
+    update touches and their ancestors -- isam_->update's partial re-elimination, same numbers)."""
 
     def __init__(self, ctx: Context, mode: str = "isam2", duplicate_factors: bool = False, reorder_every: int = 32,
-                 gn_params=None):
+                 gn_params=None, full_refactor: bool = False):
         self.ctx = ctx
         p = _abi.default_inc_params()
         p.mode = {"isam2": _abi.DPG_INC_ISAM2, "batch": _abi.DPG_INC_BATCH}[mode]
         p.duplicate_factors = 1 if duplicate_factors else 0
         p.reorder_every = int(reorder_every)
+        p.full_refactor = 1 if full_refactor else 0
         if gn_params is not None:
             p.gn = gn_params
         self.params = p

@@ -484,7 +484,11 @@ typedef struct dpg_inc_params {
     int32_t reorder_lead;            /* 8: that order is computed on a worker thread from a snapshot of
                                         the graph this many nodes before it is due, then extended by the
                                         nodes and edges that arrived since; 0: on the calling thread */
-    int32_t pad;
+    int32_t full_refactor;           /* 0: ISAM2 updates refactor only the fronts the update touches
+                                        (new nodes, new factors' and pairs' nodes, structure changes,
+                                        and everything above them) -- isam_->update's partial
+                                        re-elimination, bit-identical to a full refactorization;
+                                        1: every front, every update */
     dpg_gn_params gn;                /* DPG_INC_BATCH: the Gauss-Newton loop (Cholesky) */
 } dpg_inc_params;
 
@@ -494,7 +498,8 @@ typedef struct dpg_inc_stats {
     int32_t reordered;               /* 1: this update computed a fresh order */
     int32_t relinearized;            /* ISAM2: variables relinearized by this update */
     int32_t gn_iterations;           /* ISAM2: 1 */
-    int32_t pad;
+    int32_t fronts_kept;             /* ISAM2: Cholesky fronts this update kept from the last one
+                                        (0: a full refactorization) */
     double error;                    /* 0.5 chi2 at the last linearization point */
     double last_delta_inf;
     double ms_total, ms_symbolic, ms_numeric;

@@ -145,6 +145,38 @@ def test_gpu_incremental_matches_oracle(ctx, mode, dup):
     g.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("reorder_every", [32, 64])
+def test_gpu_partial_refactor_is_bit_identical(ctx, reorder_every):
+    """ISAM2's partial re-elimination (isam_->update, dpg_slam.cc:320): an update refactors only the
+    Cholesky fronts its new nodes, factors and pairs touch and their ancestors, and keeps the rest.
+    Every estimate, error and delta equals the full refactorization's bit for bit -- through
+    loop closures, relinearizations (updates 10, 20, ...), reorders and updates without new nodes --
+    and most updates keep most fronts."""
+    from dpgslam import api
+    X0, F = _sequence("config3", 400)
+    key = _per_node(F)
+    gp = api.IncGraph(ctx, reorder_every=reorder_every)
+    gf = api.IncGraph(ctx, reorder_every=reorder_every, full_refactor=True)
+    kept_updates = 0
+    n_upd = 0
+    for v in range(len(X0) + 12):
+        x = X0[v:v + 1] if v < len(X0) else np.zeros((0, 3))
+        f = F[key == v] if v < len(X0) else F[:0]
+        sp = gp.update(x, f)
+        sf = gf.update(x, f)
+        n_upd += 1
+        assert sf.fronts_kept == 0
+        kept_updates += sp.fronts_kept > 0
+        assert (sp.error, sp.last_delta_inf, sp.relinearized) == (sf.error, sf.last_delta_inf, sf.relinearized), v
+        if v % 20 == 0 or v >= len(X0) - 2:
+            assert np.array_equal(gp.poses(), gf.poses()), v
+    assert np.array_equal(gp.export_state()["theta"], gf.export_state()["theta"])
+    assert kept_updates > n_upd // 2, (kept_updates, n_upd)
+    gp.close()
+    gf.close()
+
+
 def test_oracle_isam2_first_relinearization_is_update_10():
     """ISAM2::update counts the update before relinarizationNeeded(update_count_) (GTSAM 4.0), so
     with relinearizeSkip 10 the linearization points first move on the 10th update, then the 20th
