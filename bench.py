@@ -151,7 +151,7 @@ def main_incremental(args):
 
     import ctypes as C
     L = _abi.lib()
-    prof, pbuf = [], (C.c_double * 8)()
+    prof, pbuf = [], (C.c_double * 12)()
     lat, icp_ms, sym_ms, num_ms, reord, relin, kept = [], [], [], [], 0, 0, []
     with api.Context(0) as ctx:
         g = api.IncGraph(ctx, mode=args.inc_mode, reorder_every=args.inc_reorder_every,
@@ -168,8 +168,8 @@ def main_incremental(args):
             reord += st.update.reordered
             relin += st.update.relinearized
             kept.append(int(st.update.fronts_kept))
-            L.dpg_inc_last_profile(C.c_void_p(g.handle), pbuf, 8)
-            prof.append(list(pbuf)[:6])
+            L.dpg_inc_last_profile(C.c_void_p(g.handle), pbuf, 12)
+            prof.append(list(pbuf)[:6] + [pbuf[11]])
             if v % 1000 == 999:
                 print(f"node {v + 1}: last latency {lat[-1]:.2f} ms", file=sys.stderr, flush=True)
         X_inc = g.poses()
@@ -190,7 +190,7 @@ def main_incremental(args):
         "tail_breakdown_ms": {"icp": float(np.mean(icp_ms[-500:])), "symbolic_host": float(np.mean(sym_ms[-500:])),
                               "numeric": float(np.mean(num_ms[-500:])),
                               "symbolic_parts": dict(zip(["incsym", "derive", "lists_upload", "chol_build",
-                                                          "chol_host", "chol_upload"],
+                                                          "chol_host", "chol_upload", "numeric_partial_pick"],
                                                          np.mean(np.asarray(prof[-500:]), 0).round(4).tolist()))},
         "reorders": reord, "relinearized_total": relin, "nnz_L_blocks": nnz, "factors": n_fac,
         # isam_->update's partial re-elimination: updates of the last 500 that kept fronts of the

@@ -2100,7 +2100,7 @@ struct CholDev {
     size_t c_dpart = 0;
     hipEvent_t pev = nullptr;     // after that copy (the staging buffer's next rewrite waits for it)
     bool pev_set = false;
-    int64_t pstats[3] = {0, 0, 0};   // last solve: fronts refactored, kept, doubles moved
+    int64_t pstats[4] = {0, 0, 0, 0};   // last solve: fronts refactored, kept, doubles moved, host ns of the pick
     void* host = nullptr;         // CholHost of the build in progress (a plan and its upload may run
                                   // on different threads, one after the other)
 };
@@ -2894,10 +2894,11 @@ static void launch_inv(CholDev* c, hipStream_t st, const int32_t* gate) {
 }
 
 // the values in fronts now belong to the current analysis
-static void note_factored(CholDev* c, int64_t refactored, int64_t kept, int64_t moved) {
+static void note_factored(CholDev* c, int64_t refactored, int64_t kept, int64_t moved, int64_t pick_ns = 0) {
     c->pstats[0] = refactored;
     c->pstats[1] = kept;
     c->pstats[2] = moved;
+    c->pstats[3] = pick_ns;
     if (!c->track) return;
     c->fac_valid = true;
     c->fac_ptr = c->fronts;
@@ -2973,9 +2974,9 @@ extern "C" void dpg_chol_track_factor(void* h, int on) {
 extern "C" void dpg_chol_forget_factor(void* h) {
     if (h) reinterpret_cast<CholDev*>(h)->fac_valid = false;
 }
-extern "C" void dpg_chol_partial_stats(void* h, int64_t out[3]) {
+extern "C" void dpg_chol_partial_stats(void* h, int64_t out[4]) {
     const CholDev* c = reinterpret_cast<const CholDev*>(h);
-    for (int k = 0; k < 3; ++k) out[k] = c ? c->pstats[k] : 0;
+    for (int k = 0; k < 4; ++k) out[k] = c ? c->pstats[k] : 0;
 }
 
 // ISAM2's partial re-elimination (isam_->update, dpg_slam.cc:320, re-eliminates only the cliques
@@ -3006,6 +3007,7 @@ extern "C" int dpg_chol_solve_partial(void* h, const double* hb, const int32_t* 
                         (int64_t)c->fac_G.size() == (int64_t)O.ns && (int64_t)c->cur_G.size() == (int64_t)S.ns &&
                         std::equal(O.perm.begin(), O.perm.end(), S.perm.begin());
     if (!usable) return dpg_chol_solve(h, hb, stream);
+    const double t_pick = wall_ms();
     const int32_t ns = S.ns;
     std::vector<uint8_t>& keep = c->h_keep;
     std::vector<int32_t>& old = c->h_old;
@@ -3128,7 +3130,7 @@ extern "C" int dpg_chol_solve_partial(void* h, const double* hb, const int32_t* 
     hipLaunchKernelGGL(chol_backward_dag, dim3(ns), dim3(kT), c->lds_solve_max, st, c->order_bwd,
                        c->sync + 1 + 2 * ns, c->status, c->sns, c->rows, c->segs, c->fronts, c->ysol, c->xsol,
                        c->solve_stage, c->solve_maxseg, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
-    note_factored(c, ns - kept, kept, moved);
+    note_factored(c, ns - kept, kept, moved, (int64_t)((wall_ms() - t_pick) * 1e6));
     c->inv_valid = false;
     return hipGetLastError() == hipSuccess ? DPG_OK : DPG_ERR_HIP;
 }

@@ -222,7 +222,7 @@ struct dpg_inc {
     double prof[12] = {};                      // last update: incsym, derive, lists, chol build, chol host,
                                                // chol upload (ms); factor Mflop, largest front (blocks),
                                                // fused DAG path (1) or level path (0), supernodes, levels,
-                                               // doubles of kept fronts moved (partial refactorization)
+                                               // host ms of the partial refactorization's pick + launches
 };
 
 namespace {
@@ -735,10 +735,10 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         }
         if (rc) return rollback(rc, "Cholesky launch failed");
         {
-            int64_t pst[3];
+            int64_t pst[4];
             dpg_chol_partial_stats(q->g.chol, pst);
             S.fronts_kept = (int32_t)pst[1];
-            q->prof[11] = (double)pst[2];
+            q->prof[11] = (double)pst[3] * 1e-6;
         }
         if (hipMemsetAsync(q->g.scal3, 0, sizeof(double), s) != hipSuccess) return rollback(DPG_ERR_HIP, "memset");
         hipLaunchKernelGGL(inc_estimate_kernel, dim3(nblk(V1)), dim3(kThreads), 0, s, q->theta, dpg_chol_x_dev(q->g.chol),

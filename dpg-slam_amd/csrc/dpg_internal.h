@@ -181,8 +181,9 @@ void dpg_chol_keep_inverse(void* chol, int on);
 void dpg_chol_track_factor(void* chol, int on);
 void dpg_chol_forget_factor(void* chol);
 int dpg_chol_solve_partial(void* chol, const double* hb, const int32_t* dirty_nodes, int64_t n_dirty, void* stream);
-/* the last solve: fronts refactored, fronts kept, doubles moved (all fronts refactored: kept = 0) */
-void dpg_chol_partial_stats(void* chol, int64_t out[3]);
+/* the last solve: fronts refactored, fronts kept, doubles moved (all fronts refactored: kept = 0),
+   host ns of the partial solve's pick + launches */
+void dpg_chol_partial_stats(void* chol, int64_t out[4]);
 const int32_t* dpg_chol_pos_dev(void* chol);
 const double* dpg_chol_x_dev(void* chol);
 const int32_t* dpg_chol_status_dev(void* chol);
