@@ -368,9 +368,10 @@ int dpg_gn_setup(dpg_ctx* ctx, int64_t n_nodes, const dpg_factor* factors, int64
 int dpg_gn_take_icp_measurements(dpg_ctx* ctx, int64_t first_factor, int64_t count, int64_t n_always,
                                  const dpg_icp_params* params);
 int64_t dpg_gn_hb_size(dpg_ctx* ctx);   /* doubles in the packed buffer */
-/* Host clock (ms) of the last dpg_gn_setup's parts: the pattern, contribution lists and BSR rows;
- * the device allocations and uploads; the Cholesky's symbolic analysis (ordering, supernodes); its
- * plan; its upload. */
+/* Host clock (ms) of the last dpg_gn_setup's parts, in this order: the pattern, contribution lists
+ * and BSR rows; the Cholesky's symbolic analysis (ordering, supernodes); its plan (these three
+ * before the setup waits for the context's stream); the wait + device allocations + uploads; the
+ * Cholesky's upload. */
 int dpg_gn_setup_profile(dpg_ctx* ctx, double out[5]);
 int dpg_gn_set_poses(dpg_ctx* ctx, const double* poses);
 int dpg_gn_get_poses(dpg_ctx* ctx, double* poses);
