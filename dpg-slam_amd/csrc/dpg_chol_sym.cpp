@@ -957,8 +957,10 @@ int dpg_incsym_order(int64_t n, const int32_t* pair_lo, const int32_t* pair_hi, 
         };
         auto run = [&](int k) {
             Cand c;
-            c.rc = k == 0 ? dpg_chol_order(n, pair_lo, pair_hi, n_pairs, c.pm, c.pt)
-                          : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, c.pm, c.pt);
+            // (dpg_chol_order's nested dissection; a waiting caller's orders also split their
+            // large parts over threads -- the same orders)
+            c.rc = k == 0 ? dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 0, 5, 0, false, c.pm, c.pt, concurrent)
+                          : dpg_chol_order_nd_sep(n, pair_lo, pair_hi, n_pairs, 16, 8, 4, 2, true, c.pm, c.pt, concurrent);
             if (c.rc == 0) {
                 dpg_chol_sym T;
                 if (dpg_chol_sym_from_patterns(n, c.pm, c.pt, &o, &T)) c.rc = -1;
