@@ -225,12 +225,16 @@ struct NdCut {
 };
 constexpr size_t kNdStartsParMin = 2048;
 constexpr size_t kNdStartsThreads = 4;
+// (have_h > 0: lvl already holds the level structure from s0, of height have_h)
 NdCut nd_best_cut(const NdState& st, const std::vector<int32_t>& sub, int32_t id, int32_t s0, int32_t* lvl,
-                  std::vector<int32_t>& queue) {
+                  std::vector<int32_t>& queue, int32_t have_h = 0) {
     NdCut best;
     const int64_t N = (int64_t)sub.size();
-    for (int32_t v : sub) lvl[v] = -1;
-    const int32_t hh = nd_bfs_into(st, id, s0, lvl, queue);
+    int32_t hh = have_h;
+    if (hh <= 0) {
+        for (int32_t v : sub) lvl[v] = -1;
+        hh = nd_bfs_into(st, id, s0, lvl, queue);
+    }
     if (hh < 3) return best;
     std::vector<int64_t> cnt((size_t)hh, 0), slo((size_t)hh, 0), shi((size_t)hh, 0);
     for (int32_t v : sub) {
@@ -265,14 +269,20 @@ NdCut nd_best_cut(const NdState& st, const std::vector<int32_t>& sub, int32_t id
 }
 
 // the separator search with several level structures (NdParams, starts > 0); src is the part's
-// pseudo-peripheral node, `id` its stamp
-void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t src) {
+// pseudo-peripheral node, `id` its stamp; have_h > 0: the shared level array and queue hold the
+// level structure from src already (of height have_h: the pseudo-peripheral search's last BFS).
+// A level structure already in the shared array is not recomputed -- src's for the first start,
+// the last start's for the chosen cut -- with the same result.
+void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t src, int32_t have_h) {
     const int64_t N = (int64_t)sub.size();
     const int T = N >= 256 ? st.prm.starts : 1;
     std::vector<int32_t> starts{src};
+    int32_t h_src = have_h;
     {
-        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
-        nd_bfs(st, id, src);
+        if (h_src <= 0) {
+            for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
+            h_src = nd_bfs(st, id, src);
+        }
         const std::vector<int32_t> order(st.queue.begin(), st.queue.end());
         for (int t = 1; t < T; ++t) starts.push_back(order[(size_t)((int64_t)t * (N - 1) / T)]);
         starts.push_back(order.back());
@@ -282,9 +292,16 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
     // a large part's starts are searched on several threads, each with its own level array
     std::vector<NdCut> cuts(starts.size());
     const int W = st.prm.par && (size_t)N >= kNdStartsParMin ? (int)std::min<size_t>(kNdStartsThreads, starts.size()) : 1;
-    if (W == 1) {
-        for (size_t k = 0; k < starts.size(); ++k) cuts[k] = nd_best_cut(st, sub, id, starts[k], st.sh->lvl.data(), st.queue);
-    } else {
+    // worker 0 (this thread) works in the shared array: its first start is src (already there)
+    size_t k_shared = 0;   // the start whose level structure the shared array holds at the end
+    for (size_t k = 0; k < starts.size(); k += (size_t)W) {
+        cuts[k] = nd_best_cut(st, sub, id, starts[k], st.sh->lvl.data(), st.queue, k == 0 ? h_src : 0);
+        k_shared = k;
+        if (k == 0 && W > 1) {   // the other workers start once src's cut is taken
+            break;
+        }
+    }
+    if (W > 1) {
         auto work = [&](int w) {
             std::unique_ptr<int32_t[]> lv(new int32_t[(size_t)st.n]);
             std::vector<int32_t> q;
@@ -292,7 +309,10 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         };
         std::vector<std::future<void>> fs;
         for (int w = 1; w < W; ++w) fs.push_back(std::async(std::launch::async, work, w));
-        work(0);
+        for (size_t k = (size_t)W; k < starts.size(); k += (size_t)W) {
+            cuts[k] = nd_best_cut(st, sub, id, starts[k], st.sh->lvl.data(), st.queue);
+            k_shared = k;
+        }
         for (auto& f : fs) f.get();
     }
     int32_t bsrc = -1, bm = -1;
@@ -306,8 +326,10 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         }
     }
     if (bm < 0) { nd_min_degree(st, sub); return; }
-    for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
-    nd_bfs(st, id, bsrc);
+    if (bsrc != starts[k_shared]) {
+        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
+        nd_bfs(st, id, bsrc);
+    }
     auto touches = [&](int32_t v, int32_t l) {
         for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
             const int32_t u = st.adj[(size_t)t];
@@ -410,9 +432,10 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     for (int32_t v : sub) { stamp_set(st, v, id); st.sh->lvl[(size_t)v] = -1; }
     // connected components, each ordered on its own
     std::vector<std::vector<int32_t>> comps;
+    int32_t comp_h = 0;   // one component: the level structure from sub[0] is in the shared array
     for (int32_t v : sub)
         if (st.sh->lvl[(size_t)v] < 0) {
-            nd_bfs(st, id, v);
+            comp_h = nd_bfs(st, id, v);
             comps.emplace_back(st.queue.begin(), st.queue.end());
         }
     if (comps.size() > 1) {
@@ -425,9 +448,15 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     // pseudo-peripheral start: repeat BFS from a least-degree node of the last level while the
     // height grows
     int32_t src = sub[0], h = 0;
+    int32_t bfs_src = -1, bfs_h = 0;   // the level structure the shared array holds
     for (int it = 0; it < 4; ++it) {
-        for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
-        const int32_t hh = nd_bfs(st, id, src);
+        int32_t hh = it == 0 ? comp_h : 0;   // the components' BFS was from sub[0] = src
+        if (hh <= 0) {
+            for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
+            hh = nd_bfs(st, id, src);
+        }
+        bfs_src = src;
+        bfs_h = hh;
         if (hh <= h) break;
         h = hh;
         int32_t best = -1, bd = 1 << 30;
@@ -439,7 +468,7 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
         if (best == src) break;
         src = best;
     }
-    if (st.prm.starts > 0) { nd_split_multi(st, sub, id, src); return; }
+    if (st.prm.starts > 0) { nd_split_multi(st, sub, id, src, bfs_src == src ? bfs_h : 0); return; }
     for (int32_t v : sub) st.sh->lvl[(size_t)v] = -1;
     h = nd_bfs(st, id, src);
     const int64_t N = (int64_t)sub.size();
