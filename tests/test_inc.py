@@ -41,6 +41,19 @@ def test_background_order_extended_matches_elimination(incsym_bin, n0, steps, se
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("n,seed", [(3000, 1), (6000, 2), (9000, 3)])
+def test_threaded_nested_dissection_gives_the_serial_order(tmp_path, n, seed):
+    """The orderings' threaded forms (a large part's halves on two threads, its separator starts on
+    up to four, level structures reused) give the serial permutation and column patterns, for both
+    candidate rules and the incremental reorder (dpg_chol_sym.cpp), on route-like graphs of 1-3
+    components."""
+    out = str(tmp_path / "nd_par_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-pthread", "-o", out, os.path.join(ROOT, "tools", "nd_par_check.cpp"),
+                    os.path.join(ROOT, "dpg-slam_amd", "csrc", "dpg_chol_sym.cpp")], check=True)
+    r = subprocess.run([out, str(n), str(seed)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
 def test_solver_plan_matches_straightforward_construction(tmp_path):
     """The GPU solver's host plan (dpg_chol.hip chol_plan: H-block -> front map by column buckets,
     child column ranges by binary search, critical-path front order) equals the straightforward
