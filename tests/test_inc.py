@@ -190,6 +190,33 @@ def test_gpu_partial_refactor_is_bit_identical(ctx, reorder_every):
     gf.close()
 
 
+@pytest.mark.gpu
+def test_gpu_partial_refactor_through_failed_updates(ctx):
+    """Failed updates (a node without factors: H singular) roll the graph back; the partial path
+    forgets its tracked factorization and the next updates still equal the full refactorization's
+    bit for bit, including updates that keep fronts again afterwards."""
+    from dpgslam import api
+    X0, F = _sequence("config3", 160)
+    key = _per_node(F)
+    gp = api.IncGraph(ctx, reorder_every=64)
+    gf = api.IncGraph(ctx, reorder_every=64, full_refactor=True)
+    kept_after = 0
+    for v in range(len(X0)):
+        if v in (41, 42, 97):
+            for g in (gp, gf):
+                with pytest.raises(_abi.DpgError):
+                    g.update(X0[v:v + 1], F[:0])
+        sp = gp.update(X0[v:v + 1], F[key == v])
+        sf = gf.update(X0[v:v + 1], F[key == v])
+        if v > 97:
+            kept_after += sp.fronts_kept > 0
+        assert (sp.error, sp.last_delta_inf) == (sf.error, sf.last_delta_inf), v
+    assert np.array_equal(gp.poses(), gf.poses())
+    assert kept_after > 20, kept_after
+    gp.close()
+    gf.close()
+
+
 def test_oracle_isam2_first_relinearization_is_update_10():
     """ISAM2::update counts the update before relinarizationNeeded(update_count_) (GTSAM 4.0), so
     with relinearizeSkip 10 the linearization points first move on the 10th update, then the 20th
