@@ -125,14 +125,20 @@ struct NdParams {
 // writes its own vertices; it reads a neighbour's stamp, which another part may be writing, only
 // to compare it with its own id -- relaxed atomic accesses for the stamps, the levels and the
 // cover marks are only touched for the part's own vertices)
+// fptr / fcnt: each vertex's neighbours inside its current part, a range of that part's filtered
+// adjacency (NdState.fadj; built once per part, in the graph's adjacency order, so every traversal
+// visits what the unfiltered one with the stamp test would, in the same order)
 struct NdShared {
     std::vector<int32_t> stamp, lvl, aux;
+    std::vector<int64_t> fptr;
+    std::vector<int32_t> fcnt;
     std::atomic<int32_t> next_id{0};
 };
 struct NdState {
     int64_t n;
     const int64_t* aptr;
     const int32_t* adj;
+    const int32_t* fadj = nullptr;   // the current part's filtered adjacency
     int32_t leaf;
     NdParams prm;
     NdShared* sh;
@@ -143,20 +149,43 @@ inline int32_t stamp_of(const NdState& st, int32_t v) { return __atomic_load_n(&
 inline void stamp_set(NdState& st, int32_t v, int32_t id) { __atomic_store_n(&st.sh->stamp[(size_t)v], id, __ATOMIC_RELAXED); }
 inline int32_t nd_new_id(NdState& st) { return st.sh->next_id.fetch_add(1, std::memory_order_relaxed) + 1; }
 
-// BFS over the nodes stamped `id` from `src` into the level array `lvl` (-1 = not reached) and
-// `queue` (visit order); returns the height
+inline const int32_t* nbr_begin(const NdState& st, int32_t v) { return st.fadj + st.sh->fptr[(size_t)v]; }
+inline const int32_t* nbr_end(const NdState& st, int32_t v) { return st.fadj + st.sh->fptr[(size_t)v] + st.sh->fcnt[(size_t)v]; }
+
+// the part's filtered adjacency (its vertices are stamped `id`): into `fadj`, which must outlive
+// the part's own traversals (its sub-parts build their own)
+void nd_filter(NdState& st, const std::vector<int32_t>& sub, int32_t id, std::vector<int32_t>& fadj) {
+    size_t tot = 0;
+    for (int32_t v : sub) tot += (size_t)(st.aptr[v + 1] - st.aptr[v]);
+    fadj.clear();
+    fadj.reserve(tot);
+    for (int32_t v : sub) {
+        st.sh->fptr[(size_t)v] = (int64_t)fadj.size();
+        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
+            const int32_t u = st.adj[(size_t)t];
+            if (stamp_of(st, u) == id) fadj.push_back(u);
+        }
+        st.sh->fcnt[(size_t)v] = (int32_t)((int64_t)fadj.size() - st.sh->fptr[(size_t)v]);
+    }
+    st.fadj = fadj.data();
+}
+
+// BFS over the current part from `src` into the level array `lvl` (-1 = not reached) and `queue`
+// (visit order); returns the height
 int32_t nd_bfs_into(const NdState& st, int32_t id, int32_t src, int32_t* lvl, std::vector<int32_t>& queue) {
+    (void)id;
     queue.clear();
     queue.push_back(src);
     lvl[src] = 0;
     int32_t h = 0;
     for (size_t qi = 0; qi < queue.size(); ++qi) {
         const int32_t v = queue[qi];
-        h = std::max(h, lvl[v]);
-        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
-            const int32_t u = st.adj[(size_t)t];
-            if (stamp_of(st, u) == id && lvl[u] < 0) {
-                lvl[u] = lvl[v] + 1;
+        const int32_t lv = lvl[v];
+        h = std::max(h, lv);
+        for (const int32_t *p = nbr_begin(st, v), *e = nbr_end(st, v); p != e; ++p) {
+            const int32_t u = *p;
+            if (lvl[u] < 0) {
+                lvl[u] = lv + 1;
                 queue.push_back(u);
             }
         }
@@ -166,14 +195,53 @@ int32_t nd_bfs_into(const NdState& st, int32_t id, int32_t src, int32_t* lvl, st
 int32_t nd_bfs(NdState& st, int32_t id, int32_t src) { return nd_bfs_into(st, id, src, st.sh->lvl.data(), st.queue); }
 
 int32_t nd_degree(const NdState& st, int32_t id, int32_t v) {
-    int32_t d = 0;
-    for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) d += stamp_of(st, st.adj[(size_t)t]) == id;
-    return d;
+    (void)id;
+    return st.sh->fcnt[(size_t)v];
+}
+
+// min_degree's order (no patterns) of a part of at most 64 nodes: one bitmask row per node, the
+// same choices -- the uneliminated node of least (degree, index), its neighbourhood made a clique
+// in ascending index order -- without min_degree's allocations (the nested dissection orders a
+// thousand such parts per order)
+void min_degree_small(int32_t n, uint64_t* row, int32_t* perm) {
+    int32_t deg[64];
+    uint64_t left = n == 64 ? ~0ull : ((1ull << n) - 1);
+    for (int32_t v = 0; v < n; ++v) deg[v] = __builtin_popcountll(row[v]);
+    for (int32_t p = 0; p < n; ++p) {
+        int32_t v = -1;
+        for (uint64_t m = left; m; m &= m - 1) {
+            const int32_t u = __builtin_ctzll(m);
+            if (v < 0 || deg[u] < deg[v]) v = u;
+        }
+        left &= ~(1ull << v);
+        perm[p] = v;
+        const uint64_t bv = row[v];
+        for (uint64_t m = bv; m; m &= m - 1) {
+            const int32_t u = __builtin_ctzll(m);
+            row[u] = (row[u] | bv) & ~(1ull << u) & ~(1ull << v);
+            deg[u] = __builtin_popcountll(row[u]);
+        }
+        row[v] = 0;
+    }
 }
 
 void nd_min_degree(NdState& st, const std::vector<int32_t>& sub) {
     const int32_t id = nd_new_id(st);
     for (size_t i = 0; i < sub.size(); ++i) { stamp_set(st, sub[i], id); st.sh->lvl[(size_t)sub[i]] = (int32_t)i; }
+    if (sub.size() <= 64) {
+        uint64_t row[64];
+        int32_t lp[64];
+        const int32_t n = (int32_t)sub.size();
+        for (int32_t i = 0; i < n; ++i) {
+            const int32_t v = sub[(size_t)i];
+            row[i] = 0;
+            for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t)
+                if (stamp_of(st, st.adj[(size_t)t]) == id) row[i] |= 1ull << st.sh->lvl[(size_t)st.adj[(size_t)t]];
+        }
+        min_degree_small(n, row, lp);
+        for (int32_t k = 0; k < n; ++k) st.out->push_back(sub[(size_t)lp[k]]);
+        return;
+    }
     std::vector<int64_t> ap(sub.size() + 1, 0);
     std::vector<int32_t> aj;
     for (size_t i = 0; i < sub.size(); ++i) {
@@ -241,11 +309,10 @@ NdCut nd_best_cut(const NdState& st, const std::vector<int32_t>& sub, int32_t id
         const int32_t l = lvl[v];
         cnt[(size_t)l]++;
         bool up = false, dn = false;
-        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
-            const int32_t u = st.adj[(size_t)t];
-            if (stamp_of(st, u) != id) continue;
-            up |= lvl[u] == l + 1;
-            dn |= lvl[u] == l - 1;
+        for (const int32_t *p = nbr_begin(st, v), *e = nbr_end(st, v); p != e; ++p) {
+            const int32_t lu = lvl[*p];
+            up |= lu == l + 1;
+            dn |= lu == l - 1;
         }
         slo[(size_t)l] += up;                    // on level l, touching l + 1
         if (l > 0) shi[(size_t)l - 1] += dn;     // on level l, touching l - 1
@@ -331,10 +398,8 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         nd_bfs(st, id, bsrc);
     }
     auto touches = [&](int32_t v, int32_t l) {
-        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
-            const int32_t u = st.adj[(size_t)t];
-            if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] == l) return true;
-        }
+        for (const int32_t *p = nbr_begin(st, v), *e = nbr_end(st, v); p != e; ++p)
+            if (st.sh->lvl[(size_t)*p] == l) return true;
         return false;
     };
     std::vector<int32_t> A, B, S;
@@ -352,10 +417,8 @@ void nd_split_multi(NdState& st, std::vector<int32_t>& sub, int32_t id, int32_t 
         std::vector<int32_t> xa;
         for (size_t i = 0; i < X.size(); ++i) {
             const int32_t v = X[i];
-            for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
-                const int32_t u = st.adj[(size_t)t];
-                if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] == bm + 1) xa.push_back(st.sh->aux[(size_t)u]);
-            }
+            for (const int32_t *p = nbr_begin(st, v), *e = nbr_end(st, v); p != e; ++p)
+                if (st.sh->lvl[(size_t)*p] == bm + 1) xa.push_back(st.sh->aux[(size_t)*p]);
             xp[i + 1] = (int64_t)xa.size();
         }
         std::vector<int32_t> mx(X.size(), -1), my(Y.size(), -1), seen(Y.size(), -1);
@@ -430,6 +493,8 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     if ((int32_t)sub.size() <= st.leaf) { nd_min_degree(st, sub); return; }
     const int32_t id = nd_new_id(st);
     for (int32_t v : sub) { stamp_set(st, v, id); st.sh->lvl[(size_t)v] = -1; }
+    std::vector<int32_t> fadj;   // this part's filtered adjacency (st.fadj while the part splits)
+    nd_filter(st, sub, id, fadj);
     // connected components, each ordered on its own
     std::vector<std::vector<int32_t>> comps;
     int32_t comp_h = 0;   // one component: the level structure from sub[0] is in the shared array
@@ -499,10 +564,8 @@ void nd_rec(NdState& st, std::vector<int32_t>& sub) {
     // side), or the level-(m + 1) nodes with a neighbour on level m (the others join the upper
     // side), whichever is smaller
     auto touches = [&](int32_t v, int32_t l) {
-        for (int64_t t = st.aptr[v]; t < st.aptr[v + 1]; ++t) {
-            const int32_t u = st.adj[(size_t)t];
-            if (stamp_of(st, u) == id && st.sh->lvl[(size_t)u] == l) return true;
-        }
+        for (const int32_t *p = nbr_begin(st, v), *e = nbr_end(st, v); p != e; ++p)
+            if (st.sh->lvl[(size_t)*p] == l) return true;
         return false;
     };
     int64_t s_lo = 0, s_hi = 0;
@@ -592,6 +655,8 @@ int dpg_chol_order_nd_sep(int64_t n, const int32_t* pair_lo, const int32_t* pair
     sh.aux.assign((size_t)n, -1);
     sh.stamp.assign((size_t)n, 0);
     sh.lvl.assign((size_t)n, -1);
+    sh.fptr.assign((size_t)n, 0);
+    sh.fcnt.assign((size_t)n, 0);
     st.sh = &sh;
     perm.clear();
     perm.reserve((size_t)n);
