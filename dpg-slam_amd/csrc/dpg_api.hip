@@ -427,6 +427,9 @@ dpg_ctx* dpg_ctx_create(int device) {
         return nullptr;
     }
     c->own_stream = true;
+    // the side stream of the timed batch's covariance (beside the pose graph) is the context's too:
+    // created with it, not inside the first solve (a stream creation costs ~7 ms on this stack)
+    if (hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess) c->aux = nullptr;
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     dpg_gn_params_default(&c->gp);
     return c;
