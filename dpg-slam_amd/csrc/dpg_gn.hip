@@ -25,6 +25,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <future>
 #include <vector>
 
 #include "dpg_chol.h"
@@ -496,6 +497,25 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     pk.erase(std::unique(pk.begin(), pk.end()), pk.end());
     const int64_t P = (int64_t)pk.size();
     const int64_t nu = n + P;
+    // the Cholesky's symbolic analysis and host plan (no device call) need only the pairs: on a
+    // thread of their own while this one builds the contribution lists and the BSR rows; all of
+    // the setup's host work runs before the wait below, so a caller's kernels still running on
+    // sync_stream (the batch's ICP) overlap it
+    std::vector<int32_t> plo((size_t)P), phi((size_t)P);
+    for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)(pk[(size_t)p] >> 32); phi[(size_t)p] = (int32_t)(pk[(size_t)p] & 0xffffffffu); }
+    const dpg_chol_opts copt = opts ? *opts : dpg_chol_opts{};
+    double sym_ms = 0.0;
+    std::future<void*> sym_job = std::async(std::launch::async, [&]() -> void* {
+        const double ts = gn_wall_ms();
+        void* ch = nullptr;
+        dpg_chol_opts o = copt;
+        dpg_chol_sym S;
+        if (dpg_chol_symbolic(n, plo.data(), phi.data(), P, &o, &S) ||
+            dpg_chol_create_sym_plan(&ch, n, plo.data(), phi.data(), P, &S, &o))
+            ch = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
+        sym_ms = gn_wall_ms() - ts;
+        return ch;
+    });
     std::vector<int32_t> fpair((size_t)nf, -1);
     for (int64_t k = 0; k < nf; ++k)
         if (fkey[(size_t)k] != ~0ull)
@@ -545,20 +565,8 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
             srcup[(size_t)at[(size_t)lo]++] = (int32_t)(n + p);
         }
     }
-    // the Cholesky's symbolic analysis and host plan (no device call): all of the setup's host
-    // work runs before the wait below, so a caller's kernels still running on sync_stream (the
-    // batch's ICP) overlap it
     const double t1 = gn_wall_ms();
-    void* chol = nullptr;
-    {
-        std::vector<int32_t> plo((size_t)P), phi((size_t)P);
-        for (int64_t p = 0; p < P; ++p) { plo[(size_t)p] = (int32_t)(pk[(size_t)p] >> 32); phi[(size_t)p] = (int32_t)(pk[(size_t)p] & 0xffffffffu); }
-        dpg_chol_opts o = opts ? *opts : dpg_chol_opts{};
-        dpg_chol_sym S;
-        if (dpg_chol_symbolic(n, plo.data(), phi.data(), P, &o, &S) ||
-            dpg_chol_create_sym_plan(&chol, n, plo.data(), phi.data(), P, &S, &o))
-            chol = nullptr;   // the PCG solver still works; dpg_gn_dev_solve reports which ran
-    }
+    void* chol = sym_job.get();
     const double t2 = gn_wall_ms();
     if (sync_stream && hipStreamSynchronize(reinterpret_cast<hipStream_t>(sync_stream)) != hipSuccess) {
         if (chol) dpg_chol_destroy(chol);
@@ -607,8 +615,8 @@ extern "C" int dpg_gn_dev_alloc(dpg_gn_dev* g, int64_t n, const dpg_factor* F, i
     const double t3 = gn_wall_ms();
     double bt[2] = {0.0, 0.0};
     if (g->chol) dpg_chol_build_times(g->chol, bt);
-    g->setup_ms[0] = t1 - t0;
-    g->setup_ms[1] = std::max(0.0, (t2 - t1) - bt[0]);   // the symbolic analysis (ordering, supernodes)
+    g->setup_ms[0] = t1 - t0;                             // (beside the next two from the pairs on)
+    g->setup_ms[1] = std::max(0.0, sym_ms - bt[0]);       // the symbolic analysis (ordering, supernodes)
     g->setup_ms[2] = bt[0];                               // its host plan
     g->setup_ms[3] = std::max(0.0, (t3 - t2) - bt[1]);   // waiting for the stream, allocations, uploads
     g->setup_ms[4] = bt[1];                               // the Cholesky's upload

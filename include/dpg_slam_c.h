@@ -370,8 +370,8 @@ int dpg_gn_take_icp_measurements(dpg_ctx* ctx, int64_t first_factor, int64_t cou
 int64_t dpg_gn_hb_size(dpg_ctx* ctx);   /* doubles in the packed buffer */
 /* Host clock (ms) of the last dpg_gn_setup's parts, in this order: the pattern, contribution lists
  * and BSR rows; the Cholesky's symbolic analysis (ordering, supernodes); its plan (these three
- * before the setup waits for the context's stream); the wait + device allocations + uploads; the
- * Cholesky's upload. */
+ * before the setup waits for the context's stream; the lists and rows are built beside the other
+ * two once the pairs are known); the wait + device allocations + uploads; the Cholesky's upload. */
 int dpg_gn_setup_profile(dpg_ctx* ctx, double out[5]);
 int dpg_gn_set_poses(dpg_ctx* ctx, const double* poses);
 int dpg_gn_get_poses(dpg_ctx* ctx, double* poses);
