@@ -684,10 +684,26 @@ int dpg_inc_update(dpg_inc* q, int64_t n_new, const double* init, const dpg_fact
         if (est_saved) (void)hipMemcpy(q->est, q->est_bak, sizeof(double) * 3 * (size_t)V0, hipMemcpyDeviceToDevice);
         return set_err(code, msg);
     };
+    // the contribution lists (and their copies on s) on the graph's helper thread while this one
+    // uploads the Cholesky's plan: disjoint state (the lists and assembly buffers / g.chol)
     const double t1b = now_ms();
-    if ((rc = inc_rebuild_lists(q, s))) return rollback(rc, "dpg_inc_update: contribution lists failed");
-    q->prof[2] = now_ms() - t1b;
-    if ((rc = inc_rebuild_chol(q))) return rollback(rc, "dpg_inc_update: solver rebuild failed");
+    int lrc = DPG_OK;
+    double lists_ms = 0.0;
+    if (q->helper) {
+        q->helper->post([q, s, &lrc, &lists_ms] {
+            const double t = now_ms();
+            lrc = inc_rebuild_lists(q, s);
+            lists_ms = now_ms() - t;
+        });
+    } else {
+        lrc = inc_rebuild_lists(q, s);
+        lists_ms = now_ms() - t1b;
+    }
+    rc = inc_rebuild_chol(q);
+    if (q->helper) q->helper->wait();
+    q->prof[2] = lists_ms;
+    if (lrc) return rollback(lrc, "dpg_inc_update: contribution lists failed");
+    if (rc) return rollback(rc, "dpg_inc_update: solver rebuild failed");
     // the solver remembers its factorization's analysis for the next update's partial refactorization
     // (ISAM2 updates without the Q1 information scaling, which changes every block every update)
     dpg_chol_track_factor(q->g.chol, q->P.mode == DPG_INC_ISAM2 && q->P.full_refactor == 0 && !q->P.duplicate_factors);
