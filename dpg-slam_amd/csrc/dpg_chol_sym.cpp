@@ -174,22 +174,29 @@ void nd_filter(NdState& st, const std::vector<int32_t>& sub, int32_t id, std::ve
 // (visit order); returns the height
 int32_t nd_bfs_into(const NdState& st, int32_t id, int32_t src, int32_t* lvl, std::vector<int32_t>& queue) {
     (void)id;
-    queue.clear();
-    queue.push_back(src);
+    // branch-free visit (the new-or-not test of a neighbour is data-dependent, mispredicted about
+    // half the time): every neighbour is written at the queue's tail, which advances only when it
+    // is new -- the same visit order as a test-and-push
+    if (queue.size() < (size_t)st.n + 1) queue.resize((size_t)st.n + 1);
+    int32_t* q = queue.data();
+    size_t qh = 0, qt = 1;
+    q[0] = src;
     lvl[src] = 0;
     int32_t h = 0;
-    for (size_t qi = 0; qi < queue.size(); ++qi) {
-        const int32_t v = queue[qi];
+    while (qh < qt) {
+        const int32_t v = q[qh++];
         const int32_t lv = lvl[v];
         h = std::max(h, lv);
         for (const int32_t *p = nbr_begin(st, v), *e = nbr_end(st, v); p != e; ++p) {
             const int32_t u = *p;
-            if (lvl[u] < 0) {
-                lvl[u] = lv + 1;
-                queue.push_back(u);
-            }
+            const int32_t lu = lvl[u];
+            const bool fresh = lu < 0;
+            lvl[u] = fresh ? lv + 1 : lu;
+            q[qt] = u;
+            qt += fresh;
         }
     }
+    queue.resize(qt);
     return h + 1;
 }
 int32_t nd_bfs(NdState& st, int32_t id, int32_t src) { return nd_bfs_into(st, id, src, st.sh->lvl.data(), st.queue); }
