@@ -876,15 +876,16 @@ static int sym_from_csr(int64_t n, const int32_t* perm, const int64_t* cp, const
         const int32_t c0 = sn_first[(size_t)s], c1 = sn_first[(size_t)s + 1];
         // sorted union of the columns' rows >= c1, merged from the last column down (the last
         // column's rows all qualify; in a fundamental supernode every merge adds nothing)
-        rowbuf.assign(prow + cp[c1 - 1], prow + cp[c1]);
 #ifndef DPG_PLAN_VERIFY
-        if (exact) {
-            S->sn_rows.insert(S->sn_rows.end(), rowbuf.begin(), rowbuf.end());
+        if (exact) {   // straight from the last column's pattern
+            const int32_t *b = prow + cp[c1 - 1], *e = prow + cp[c1];
+            S->sn_rows.insert(S->sn_rows.end(), b, e);
             S->sn_rows_ptr[(size_t)s + 1] = (int64_t)S->sn_rows.size();
-            if (!rowbuf.empty()) S->sn_parent[(size_t)s] = S->sn_of[(size_t)rowbuf[0]];
+            if (e > b) S->sn_parent[(size_t)s] = S->sn_of[(size_t)*b];
             continue;
         }
 #endif
+        rowbuf.assign(prow + cp[c1 - 1], prow + cp[c1]);
         for (int32_t c = c1 - 2; c >= c0; --c) {
             const int32_t* b = std::lower_bound(prow + cp[c], prow + cp[c + 1], c1);
             const int32_t* e = prow + cp[c + 1];
